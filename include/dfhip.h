@@ -1,0 +1,246 @@
+/*
+ * dfhip.h — C-ABI of the MI355X (gfx950) NeRF hot-path kernels.
+ *
+ * This is the drop-in boundary that replaces the four pybind11 extension
+ * modules of the reference (torch-ngp style): `_raymarching`, `_gridencoder`,
+ * `_freqencoder`, `_shencoder`.  Every entry point below names the reference
+ * binding it replaces (file:line, relative to the reference repo root).
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + sizes; no torch / HIP types in signatures.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).
+ *     The reference launches on the legacy default stream
+ *     (raymarching/src/raymarching.cu:154); our Python shims pass torch's
+ *     current stream.
+ *   - all buffers contiguous, row-major, AoS exactly as the reference.
+ *   - the caller owns and allocates every buffer (reference ownership rule,
+ *     raymarching/raymarching.py:205-218).  Entry points marked [scratch]
+ *     take an explicit caller-provided scratch buffer; the reference-signature
+ *     form allocates stream-ordered scratch itself (hipMallocAsync).
+ *   - return 0 on success, a DFHIP_E* code otherwise; dfhip_last_error()
+ *     returns a thread-local message for the last failing call on that thread.
+ *     (Reference: TORCH_CHECK / std::runtime_error -> Python RuntimeError,
+ *     gridencoder/src/gridencoder.cu:354,372,425-441.)
+ *   - `dtype` selects the floating storage type of the `void*` float buffers
+ *     (reference: AT_DISPATCH_FLOATING_TYPES_AND_HALF).  Arithmetic inside the
+ *     kernels is f32 as in the reference (f64 for the f64 storage variant of
+ *     the compositing accumulators).
+ */
+#ifndef DFHIP_H
+#define DFHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *dfhip_stream_t; /* hipStream_t */
+
+enum dfhip_dtype { DFHIP_F32 = 0, DFHIP_F16 = 1, DFHIP_F64 = 2 };
+
+enum dfhip_status {
+    DFHIP_OK = 0,
+    DFHIP_EINVAL = 1,     /* bad size / null pointer / unsupported D,C */
+    DFHIP_EDTYPE = 2,     /* unsupported dtype */
+    DFHIP_ELAUNCH = 3,    /* HIP launch / runtime error */
+    DFHIP_ENOMEM = 4      /* stream-ordered scratch allocation failed */
+};
+
+int dfhip_abi_version(void);
+const char *dfhip_last_error(void);
+
+/* ---------------------------------------------------------------- raymarching
+ * Reference: raymarching/src/raymarching.h:7-18, bindings.cpp:5-18. */
+
+/* raymarching.cu:148 near_far_from_aabb(rays_o, rays_d, aabb, N, min_near, nears, fars) */
+int dfhip_near_far_from_aabb(int dtype, const void *rays_o, const void *rays_d,
+                             const void *aabb, uint32_t N, float min_near,
+                             void *nears, void *fars, dfhip_stream_t stream);
+
+/* raymarching.cu:201 sph_from_ray(rays_o, rays_d, radius, N, coords) */
+int dfhip_sph_from_ray(int dtype, const void *rays_o, const void *rays_d,
+                       float radius, uint32_t N, void *coords,
+                       dfhip_stream_t stream);
+
+/* raymarching.cu:229 morton3D(coords, N, indices) */
+int dfhip_morton3D(const int32_t *coords, uint32_t N, int32_t *indices,
+                   dfhip_stream_t stream);
+
+/* raymarching.cu:257 morton3D_invert(indices, N, coords) */
+int dfhip_morton3D_invert(const int32_t *indices, uint32_t N, int32_t *coords,
+                          dfhip_stream_t stream);
+
+/* raymarching.cu:292 packbits(grid, N, density_thresh, bitfield) */
+int dfhip_packbits(int dtype, const void *grid, uint32_t N, float density_thresh,
+                   uint8_t *bitfield, dfhip_stream_t stream);
+
+/* raymarching.cu:482 march_rays_train(rays_o, rays_d, grid, bound, dt_gamma,
+ *   max_steps, N, C, H, M, nears, fars, xyzs, dirs, deltas, rays, counter, noises)
+ * Reference-signature form.  Deterministic: rays[i] = (i, offset_i, count_i)
+ * with offsets the exclusive prefix sum of counts in ray order (the reference
+ * assigns offsets by atomicAdd arrival order, raymarching.cu:405-406; per-ray
+ * contents are identical).  counter[0] += total points, counter[1] += N. */
+int dfhip_march_rays_train(int dtype, const void *rays_o, const void *rays_d,
+                           const uint8_t *grid, float bound, float dt_gamma,
+                           uint32_t max_steps, uint32_t N, uint32_t C, uint32_t H,
+                           uint32_t M, const void *nears, const void *fars,
+                           void *xyzs, void *dirs, void *deltas, int32_t *rays,
+                           int32_t *counter, const void *noises,
+                           dfhip_stream_t stream);
+
+/* [scratch] Split form used by the native Python path.
+ * Pass 1 (count): rays[i] = (i, -, count_i); block_sums[ceil(N/64)];
+ *   counter[0] += total, counter[1] += N.
+ * Pass 2 (emit): offsets from block_sums + in-block scan; writes samples.
+ *   Let W = end of the rows actually written (total, or the offset of the first
+ *   ray that does not fit in M).  zero_tail < 0: rows [W, M) are zeroed;
+ *   zero_tail = a > 0: rows [W, min(align_up(total), M)) are zeroed, with the
+ *   reference's align rule align_up(m) = m + a - m % a (raymarching.py:225-226);
+ *   zero_tail = 0: nothing is zeroed.  Either way the caller can allocate the
+ *   outputs uninitialised (no N*max_steps memset). */
+uint32_t dfhip_march_rays_train_scratch_ints(uint32_t N);
+int dfhip_march_rays_train_count(int dtype, const void *rays_o, const void *rays_d,
+                                 const uint8_t *grid, float bound, float dt_gamma,
+                                 uint32_t max_steps, uint32_t N, uint32_t C,
+                                 uint32_t H, const void *nears, const void *fars,
+                                 int32_t *rays, int32_t *counter,
+                                 const void *noises, int32_t *block_sums,
+                                 dfhip_stream_t stream);
+int dfhip_march_rays_train_emit(int dtype, const void *rays_o, const void *rays_d,
+                                const uint8_t *grid, float bound, float dt_gamma,
+                                uint32_t max_steps, uint32_t N, uint32_t C,
+                                uint32_t H, uint32_t M, const void *nears,
+                                const void *fars, void *xyzs, void *dirs,
+                                void *deltas, int32_t *rays, const void *noises,
+                                const int32_t *block_sums, int zero_tail,
+                                dfhip_stream_t stream);
+
+/* raymarching.cu:580 composite_rays_train_forward(sigmas, rgbs, deltas, rays,
+ *   M, N, T_thresh, weights_sum, depth, image) */
+int dfhip_composite_rays_train_forward(int dtype, const void *sigmas,
+                                       const void *rgbs, const void *deltas,
+                                       const int32_t *rays, uint32_t M, uint32_t N,
+                                       float T_thresh, void *weights_sum,
+                                       void *depth, void *image,
+                                       dfhip_stream_t stream);
+
+/* raymarching.cu:685 composite_rays_train_backward(grad_weights_sum, grad_image,
+ *   sigmas, rgbs, deltas, rays, weights_sum, image, M, N, T_thresh,
+ *   grad_sigmas, grad_rgbs).  Rows past a ray's early break are left untouched
+ *   (the caller zero-fills, raymarching.py:283-284). */
+int dfhip_composite_rays_train_backward(int dtype, const void *grad_weights_sum,
+                                        const void *grad_image, const void *sigmas,
+                                        const void *rgbs, const void *deltas,
+                                        const int32_t *rays, const void *weights_sum,
+                                        const void *image, uint32_t M, uint32_t N,
+                                        float T_thresh, void *grad_sigmas,
+                                        void *grad_rgbs, dfhip_stream_t stream);
+
+/* Native variant: also writes zeros into rows that the reference leaves
+ * untouched (past the early break, empty / overflowing rays), so grad_sigmas /
+ * grad_rgbs may be allocated uninitialised.  Requires ray-ordered, contiguous
+ * rays (as produced by dfhip_march_rays_train*): row ranges of consecutive
+ * rays tile [0, total).  Rows in [total, M) are zeroed by the last block. */
+int dfhip_composite_rays_train_backward_dense(int dtype, const void *grad_weights_sum,
+                                              const void *grad_image,
+                                              const void *sigmas, const void *rgbs,
+                                              const void *deltas, const int32_t *rays,
+                                              const void *weights_sum,
+                                              const void *image, uint32_t M,
+                                              uint32_t N, float T_thresh,
+                                              void *grad_sigmas, void *grad_rgbs,
+                                              dfhip_stream_t stream);
+
+/* raymarching.cu:808 march_rays(n_alive, n_step, rays_alive, rays_t, rays_o,
+ *   rays_d, bound, dt_gamma, max_steps, C, H, grid, near, far, xyzs, dirs,
+ *   deltas, noises).  Every one of a ray's n_step slots is written (zeros past
+ *   the last occupied step), so the caller only needs to zero its align tail. */
+int dfhip_march_rays(int dtype, uint32_t n_alive, uint32_t n_step,
+                     const int32_t *rays_alive, const void *rays_t,
+                     const void *rays_o, const void *rays_d, float bound,
+                     float dt_gamma, uint32_t max_steps, uint32_t C, uint32_t H,
+                     const uint8_t *grid, const void *nears, const void *fars,
+                     void *xyzs, void *dirs, void *deltas, const void *noises,
+                     dfhip_stream_t stream);
+
+/* raymarching.cu:908 composite_rays(n_alive, n_step, T_thresh, rays_alive,
+ *   rays_t, sigmas, rgbs, deltas, weights, depth, image) — in place. */
+int dfhip_composite_rays(int dtype, uint32_t n_alive, uint32_t n_step,
+                         float T_thresh, int32_t *rays_alive, void *rays_t,
+                         const void *sigmas, const void *rgbs, const void *deltas,
+                         void *weights_sum, void *depth, void *image,
+                         dfhip_stream_t stream);
+
+/* ---------------------------------------------------------------- gridencoder
+ * Reference: gridencoder/src/gridencoder.h:12-13, bindings.cpp.
+ * `dtype` is the embeddings / outputs / grad dtype (F32, F16, F64); `inputs`
+ * are always f32 (gridencoder.cu:445).  gridtype: 0 = hash, 1 = tiled. */
+
+/* gridencoder.cu:424 grid_encode_forward(inputs, embeddings, offsets, outputs,
+ *   B, D, C, L, S, H, dy_dx?, gridtype, align_corners); outputs [L, B, C],
+ *   dy_dx (nullable) [B, L*D*C]. */
+int dfhip_grid_encode_forward(int dtype, const float *inputs, const void *embeddings,
+                              const int32_t *offsets, void *outputs, uint32_t B,
+                              uint32_t D, uint32_t C, uint32_t L, float S,
+                              uint32_t H, void *dy_dx, uint32_t gridtype,
+                              int align_corners, dfhip_stream_t stream);
+
+/* gridencoder.cu:449 grid_encode_backward(grad [L,B,C], inputs, embeddings,
+ *   offsets, grad_embeddings, B, D, C, L, S, H, dy_dx?, grad_inputs?, gridtype,
+ *   align_corners).  grad_embeddings is accumulated into (caller zero-fills). */
+int dfhip_grid_encode_backward(int dtype, const void *grad, const float *inputs,
+                               const void *embeddings, const int32_t *offsets,
+                               void *grad_embeddings, uint32_t B, uint32_t D,
+                               uint32_t C, uint32_t L, float S, uint32_t H,
+                               const void *dy_dx, void *grad_inputs,
+                               uint32_t gridtype, int align_corners,
+                               dfhip_stream_t stream);
+
+/* Native layout variants: outputs / grad in [B, L*C] (the layout the caller
+ * wants after the reference's permute, grid.py:42,70), which removes the two
+ * permute copies per call.  Same numerics as the [L,B,C] forms. */
+int dfhip_grid_encode_forward_blc(int dtype, const float *inputs,
+                                  const void *embeddings, const int32_t *offsets,
+                                  void *outputs, uint32_t B, uint32_t D, uint32_t C,
+                                  uint32_t L, float S, uint32_t H, void *dy_dx,
+                                  uint32_t gridtype, int align_corners,
+                                  dfhip_stream_t stream);
+/* grad_dtype: dtype of `grad` ([B, L*C]); acc_dtype: dtype of grad_embeddings
+ * (F32 accumulation is allowed with F16 grads: more accurate than the
+ * reference's half2 atomics, same request count). */
+/* dy_dx ([B, L*D*C], grad_dtype) and grad_inputs ([B, D], grad_dtype) are
+ * nullable: when both are given, grad_inputs = sum_l,c grad * dy_dx
+ * (gridencoder.cu:316-342). */
+int dfhip_grid_encode_backward_blc(int grad_dtype, int acc_dtype, const void *grad,
+                                   const float *inputs, const int32_t *offsets,
+                                   void *grad_embeddings, uint32_t B, uint32_t D,
+                                   uint32_t C, uint32_t L, float S, uint32_t H,
+                                   const void *dy_dx, void *grad_inputs,
+                                   uint32_t gridtype, int align_corners,
+                                   dfhip_stream_t stream);
+
+/* ---------------------------------------------------------------- freqencoder
+ * Reference: freqencoder/src/freqencoder.h:6-9 (f32 only, freqencoder.cu:109). */
+int dfhip_freq_encode_forward(const float *inputs, uint32_t B, uint32_t D,
+                              uint32_t deg, uint32_t C, float *outputs,
+                              dfhip_stream_t stream);
+int dfhip_freq_encode_backward(const float *grad, const float *outputs, uint32_t B,
+                               uint32_t D, uint32_t deg, uint32_t C,
+                               float *grad_inputs, dfhip_stream_t stream);
+
+/* ---------------------------------------------------------------- shencoder
+ * Reference: shencoder/src/shencoder.h:8-9.  C = degree (1..8), D = 3. */
+int dfhip_sh_encode_forward(int dtype, const void *inputs, void *outputs,
+                            uint32_t B, uint32_t D, uint32_t C, void *dy_dx,
+                            dfhip_stream_t stream);
+/* grad_inputs is accumulated into (caller zero-fills, sphere_harmonics.py). */
+int dfhip_sh_encode_backward(int dtype, const void *grad, const void *inputs,
+                             uint32_t B, uint32_t D, uint32_t C, const void *dy_dx,
+                             void *grad_inputs, dfhip_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DFHIP_H */

@@ -1,0 +1,199 @@
+"""ctypes binding of the gfx950 kernel library (lib/libdfhip.so, include/dfhip.h).
+
+This is the only place that touches the C-ABI.  The per-extension shim modules
+(`_raymarching`, `_gridencoder`, `_freqencoder`, `_shencoder`) sit on top of it
+and expose the reference's pybind11 signatures.
+
+There is deliberately no CPU / eager fallback: if the library is missing, or a
+tensor is not on the GPU, calls raise.  `import torch` happens before the
+library is opened, so its HIP runtime dependency (SONAME libamdhip64.so.7)
+binds to the runtime torch already loaded and pointers / streams are shared.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+LIB_PATH = Path(os.environ.get("DFHIP_LIB", Path(__file__).resolve().parent / "lib" / "libdfhip.so"))
+
+F32, F16, F64 = 0, 1, 2
+_DTYPE = {torch.float32: F32, torch.float16: F16, torch.float64: F64}
+
+_vp, _u32, _i32, _f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
+
+# name -> argtypes (stream is always the trailing c_void_p)
+_SIGS = {
+    "dfhip_near_far_from_aabb": [_i32, _vp, _vp, _vp, _u32, _f32, _vp, _vp, _vp],
+    "dfhip_sph_from_ray": [_i32, _vp, _vp, _f32, _u32, _vp, _vp],
+    "dfhip_morton3D": [_vp, _u32, _vp, _vp],
+    "dfhip_morton3D_invert": [_vp, _u32, _vp, _vp],
+    "dfhip_packbits": [_i32, _vp, _u32, _f32, _vp, _vp],
+    "dfhip_march_rays_train": [_i32, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _u32, _u32,
+                               _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_march_rays_train_count": [_i32, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _u32,
+                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_march_rays_train_emit": [_i32, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _u32,
+                                    _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dfhip_composite_rays_train_forward": [_i32, _vp, _vp, _vp, _vp, _u32, _u32, _f32, _vp, _vp,
+                                           _vp, _vp],
+    "dfhip_composite_rays_train_backward": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32,
+                                            _u32, _f32, _vp, _vp, _vp],
+    "dfhip_composite_rays_train_backward_dense": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                  _u32, _u32, _f32, _vp, _vp, _vp],
+    "dfhip_march_rays": [_i32, _u32, _u32, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _vp,
+                         _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_composite_rays": [_i32, _u32, _u32, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_grid_encode_forward": [_i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _f32, _u32,
+                                  _vp, _u32, _i32, _vp],
+    "dfhip_grid_encode_forward_blc": [_i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _f32,
+                                      _u32, _vp, _u32, _i32, _vp],
+    "dfhip_grid_encode_backward": [_i32, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _f32,
+                                   _u32, _vp, _vp, _u32, _i32, _vp],
+    "dfhip_grid_encode_backward_blc": [_i32, _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
+                                       _f32, _u32, _vp, _vp, _u32, _i32, _vp],
+    "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
+    "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
+    "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],
+    "dfhip_sh_encode_backward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp],
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Open libdfhip.so once and declare every entry point's signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"gfx950 kernel library not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    lib.dfhip_last_error.restype = ctypes.c_char_p
+    lib.dfhip_abi_version.restype = ctypes.c_int
+    lib.dfhip_march_rays_train_scratch_ints.restype = _u32
+    lib.dfhip_march_rays_train_scratch_ints.argtypes = [_u32]
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return ["dfhip_abi_version", "dfhip_last_error", "dfhip_march_rays_train_scratch_ints",
+            *_SIGS.keys()]
+
+
+# ---------------------------------------------------------------- kernel timing
+# Opt-in (bench.py): HIP events recorded on the launching stream around a
+# region of the hot path, with the algorithmic bytes of that launch.
+
+class _KernelTimer:
+    def __init__(self):
+        self.records = []  # (name, start_event, end_event, bytes)
+
+    def region(self, name, nbytes):
+        return _Region(self, name, nbytes)
+
+
+class _Region:
+    __slots__ = ("timer", "name", "nbytes", "e0")
+
+    def __init__(self, timer, name, nbytes):
+        self.timer, self.name, self.nbytes = timer, name, nbytes
+
+    def __enter__(self):
+        self.e0 = torch.cuda.Event(enable_timing=True)
+        self.e0.record()
+
+    def __exit__(self, *exc):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.timer.records.append((self.name, self.e0, e1, self.nbytes))
+
+
+class _NoRegion:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_REGION = _NoRegion()
+_timer = None
+
+
+def set_kernel_timer(timer):
+    """Install (or remove with None) a _KernelTimer; returns the previous one."""
+    global _timer
+    prev, _timer = _timer, timer
+    return prev
+
+
+def new_kernel_timer():
+    return _KernelTimer()
+
+
+def timed(name, nbytes):
+    """Context manager timing one launch region when a timer is installed."""
+    return _NO_REGION if _timer is None else _timer.region(name, nbytes)
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        msg = load().dfhip_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+# ---------------------------------------------------------------- tensor helpers
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(t: torch.Tensor, what: str) -> int:
+    try:
+        return _DTYPE[t.dtype]
+    except KeyError:
+        raise RuntimeError(f"{what} must be a floating tensor (float32/float16/float64), got {t.dtype}")
+
+
+def check_cuda(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{what} must be a CUDA tensor")
+
+
+def check_contig(t: torch.Tensor, what: str) -> None:
+    if not t.is_contiguous():
+        raise RuntimeError(f"{what} must be a contiguous tensor")
+
+
+def check_int(t: torch.Tensor, what: str) -> None:
+    if t.dtype != torch.int32:
+        raise RuntimeError(f"{what} must be an int tensor")
+
+
+def checked(t: torch.Tensor, what: str, kind: str = "float") -> torch.Tensor:
+    """CHECK_CUDA + CHECK_CONTIGUOUS + dtype check (reference gridencoder.cu:15-18)."""
+    check_cuda(t, what)
+    check_contig(t, what)
+    if kind == "int":
+        check_int(t, what)
+    elif kind == "u8":
+        if t.dtype != torch.uint8:
+            raise RuntimeError(f"{what} must be a uint8 tensor")
+    else:
+        dtype_code(t, what)
+    return t

@@ -1,0 +1,54 @@
+"""`_gridencoder` backend module: the reference pybind11 surface
+(gridencoder/src/bindings.cpp, gridencoder.h:12-13) over the gfx950 C-ABI,
+plus the native [B, L*C]-layout entry points.  Checks mirror
+gridencoder.cu:425-441 (CHECK_CUDA / CHECK_CONTIGUOUS / dtype) and raise
+RuntimeError."""
+import _dfhip as _d
+from _dfhip import call, ptr, stream, checked
+
+
+def _common(inputs, embeddings, offsets):
+    checked(inputs, "inputs")
+    if inputs.dtype.itemsize != 4 or not inputs.is_floating_point():
+        raise RuntimeError("inputs must be a float32 tensor")
+    checked(embeddings, "embeddings")
+    checked(offsets, "offsets", "int")
+    return _d.dtype_code(embeddings, "embeddings")
+
+
+def grid_encode_forward(inputs, embeddings, offsets, outputs, B, D, C, L, S, H, dy_dx, gridtype,
+                        align_corners):
+    dt = _common(inputs, embeddings, offsets)
+    checked(outputs, "outputs")
+    call("dfhip_grid_encode_forward", dt, ptr(inputs), ptr(embeddings), ptr(offsets), ptr(outputs),
+         B, D, C, L, S, H, ptr(dy_dx), gridtype, int(bool(align_corners)), stream())
+
+
+def grid_encode_backward(grad, inputs, embeddings, offsets, grad_embeddings, B, D, C, L, S, H,
+                         dy_dx, grad_inputs, gridtype, align_corners):
+    dt = _common(inputs, embeddings, offsets)
+    checked(grad, "grad")
+    checked(grad_embeddings, "grad_embeddings")
+    call("dfhip_grid_encode_backward", dt, ptr(grad), ptr(inputs), ptr(embeddings), ptr(offsets),
+         ptr(grad_embeddings), B, D, C, L, S, H, ptr(dy_dx), ptr(grad_inputs), gridtype,
+         int(bool(align_corners)), stream())
+
+
+def grid_encode_forward_blc(inputs, embeddings, offsets, outputs, B, D, C, L, S, H, dy_dx, gridtype,
+                            align_corners):
+    dt = _common(inputs, embeddings, offsets)
+    checked(outputs, "outputs")
+    call("dfhip_grid_encode_forward_blc", dt, ptr(inputs), ptr(embeddings), ptr(offsets),
+         ptr(outputs), B, D, C, L, S, H, ptr(dy_dx), gridtype, int(bool(align_corners)), stream())
+
+
+def grid_encode_backward_blc(grad, inputs, offsets, grad_embeddings, B, D, C, L, S, H, dy_dx,
+                             grad_inputs, gridtype, align_corners):
+    checked(grad, "grad")
+    checked(inputs, "inputs")
+    checked(offsets, "offsets", "int")
+    checked(grad_embeddings, "grad_embeddings")
+    call("dfhip_grid_encode_backward_blc", _d.dtype_code(grad, "grad"),
+         _d.dtype_code(grad_embeddings, "grad_embeddings"), ptr(grad), ptr(inputs), ptr(offsets),
+         ptr(grad_embeddings), B, D, C, L, S, H, ptr(dy_dx), ptr(grad_inputs), gridtype,
+         int(bool(align_corners)), stream())

@@ -1,0 +1,566 @@
+// Multi-resolution tiled / hashed grid encoding for gfx950 (MI355X).
+//
+// Behavioural spec: reference gridencoder/src/gridencoder.cu (cited per kernel)
+// and gridencoder/grid.py.  Numerics: explicit fmaf() where nvcc contracts
+// (gridencoder.cu:134,165), half accumulators rounded per corner exactly as
+// c10::Half arithmetic does (gridencoder.cu:142,165: the product w*g is rounded
+// to half, then added in half), compiled with -ffp-contract=off.
+//
+// MI355X design:
+//  * One thread per sample loops over all levels: at every gather instruction
+//    the 64 lanes of a wave sit on the SAME level (level-major gathers, good L2
+//    line reuse at the coarse levels) while the thread keeps 16 independent
+//    level chains in flight (ILP for the ~500-cycle L2/MALL latency).
+//  * Per-level constants (scale, resolution) are computed once on the host and
+//    passed as kernel arguments, with a correctly rounded exp2 (exact at the
+//    integer exponents of levels 0 and L-1).
+//  * Levels whose tiled index drops a trailing dimension (stride overflow,
+//    gridtype.cu:60) gather each shared corner once and reuse it; the backward
+//    merges those corners' weights into one atomic per shared table row.
+//  * The native [B, L*C] output / grad layout removes the reference's two
+//    permute copies (grid.py:42,70).
+#include "common.h"
+
+#include <math.h>
+
+namespace dfhip {
+namespace ge {
+
+constexpr uint32_t kMaxLevels = 64;
+
+struct Levels {
+    float scale[kMaxLevels];
+    uint32_t res[kMaxLevels];
+};
+
+// gridencoder.cu:125-126, evaluated on the host.
+static Levels make_levels(uint32_t L, float S, uint32_t H) {
+    Levels lv;
+    for (uint32_t l = 0; l < L; ++l) {
+        const float ls = (float)l * S;
+        const float e = (float)exp2((double)ls);
+        const float scale = fmaf(e, (float)H, -1.0f);
+        lv.scale[l] = scale;
+        lv.res[l] = (uint32_t)ceilf(scale) + 1u;
+    }
+    return lv;
+}
+
+// gridencoder.cu:35-51 — instant-ngp spatial hash.
+template <uint32_t D>
+__device__ __forceinline__ uint32_t spatial_hash(const uint32_t p[D]) {
+    constexpr uint32_t kPrimes[7] = {1u, 2654435761u, 805459861u, 3674653429u,
+                                     2097192037u, 1434869437u, 2165219737u};
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) h ^= p[d] * kPrimes[d];
+    return h;
+}
+
+// Wave-uniform per-level context.
+struct LevelCtx {
+    uint32_t base;     // first table row of the level (offsets[l])
+    uint32_t hsize;    // rows in the level
+    uint32_t smul;     // stride multiplier: res (align_corners) or res + 1
+    uint32_t used;     // dims consumed by the tiled index before stride > hsize
+    bool hashed;       // gridtype == hash and stride overflowed -> spatial_hash
+    bool pow2;         // hsize is a power of two -> modulo is a mask
+    float scale;
+};
+
+template <uint32_t D>
+__device__ __forceinline__ LevelCtx level_ctx(const int32_t *__restrict__ offsets,
+                                              const Levels &lv, uint32_t l,
+                                              uint32_t gridtype, bool align) {
+    LevelCtx c;
+    c.base = (uint32_t)offsets[l];
+    c.hsize = (uint32_t)offsets[l + 1] - c.base;
+    c.scale = lv.scale[l];
+    c.smul = align ? lv.res[l] : lv.res[l] + 1u;
+    // gridencoder.cu:56-63: for (d < D && stride <= hashmap_size)
+    uint32_t stride = 1, used = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) {
+        if (stride <= c.hsize) { stride *= c.smul; ++used; }
+    }
+    c.used = used;
+    c.hashed = (gridtype == 0) && (stride > c.hsize);
+    c.pow2 = (c.hsize & (c.hsize - 1)) == 0;
+    return c;
+}
+
+// gridencoder.cu:54-72 (row index; the caller multiplies by C).
+template <uint32_t D>
+__device__ __forceinline__ uint32_t row_index(const LevelCtx &c, const uint32_t p[D]) {
+    uint32_t idx;
+    if (c.hashed) {
+        idx = spatial_hash<D>(p);
+    } else {
+        idx = 0;
+        uint32_t stride = 1;
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) {
+            if (d < c.used) { idx += p[d] * stride; stride *= c.smul; }
+        }
+    }
+    return c.pow2 ? (idx & (c.hsize - 1)) : (idx % c.hsize);
+}
+
+// ------------------------------------------------------------ storage helpers
+// Accumulate one corner contribution into a per-channel register, following
+// the reference's scalar_t arithmetic exactly (gridencoder.cu:142,165).
+__device__ __forceinline__ void acc_corner(float &r, float w, float g) { r = fmaf(w, g, r); }
+__device__ __forceinline__ void acc_corner(double &r, float w, double g) {
+    r = fma((double)w, g, r);
+}
+__device__ __forceinline__ void acc_corner(half_t &r, float w, half_t g) {
+    // c10::Half: Half += float  ==>  Half(float(r) + float(Half(w * float(g))))
+    const half_t p = (half_t)(w * (float)g);
+    r = (half_t)((float)r + (float)p);
+}
+
+// ------------------------------------------------------------ forward
+
+// gridencoder.cu:75-223.  BLC: outputs [B, L*C] (native) else [L, B, C].
+template <typename scalar_t, uint32_t D, uint32_t C, bool BLC>
+__global__ __launch_bounds__(256) void k_grid_fwd(const float *__restrict__ inputs,
+                                                  const scalar_t *__restrict__ grid,
+                                                  const int32_t *__restrict__ offsets,
+                                                  scalar_t *__restrict__ outputs, uint32_t B,
+                                                  uint32_t L, Levels lv,
+                                                  scalar_t *__restrict__ dy_dx,
+                                                  uint32_t gridtype, int align_corners) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const bool align = align_corners != 0;
+
+    float x[D];
+    bool oob = false;
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) {
+        x[d] = inputs[(size_t)b * D + d];
+        if (x[d] < 0.0f || x[d] > 1.0f) oob = true;
+    }
+
+    for (uint32_t l = 0; l < L; ++l) {
+        scalar_t *out = BLC ? outputs + (size_t)b * L * C + (size_t)l * C
+                            : outputs + (size_t)l * B * C + (size_t)b * C;
+        if (oob) {
+#pragma unroll
+            for (uint32_t ch = 0; ch < C; ++ch) out[ch] = (scalar_t)0.0f;
+            if (dy_dx) {
+                scalar_t *g = dy_dx + (size_t)b * D * L * C + (size_t)l * D * C;
+                for (uint32_t i = 0; i < D * C; ++i) g[i] = (scalar_t)0.0f;
+            }
+            continue;
+        }
+        const LevelCtx c = level_ctx<D>(offsets, lv, l, gridtype, align);
+        const scalar_t *tab = grid + (size_t)c.base * C;
+
+        float frac[D];
+        uint32_t cell[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) {
+            const float p = fmaf(x[d], c.scale, align ? 0.0f : 0.5f);
+            cell[d] = (uint32_t)floorf(p);
+            frac[d] = p - (float)cell[d];
+        }
+
+        scalar_t acc[C];
+#pragma unroll
+        for (uint32_t ch = 0; ch < C; ++ch) acc[ch] = (scalar_t)0.0f;
+
+        // Tiled levels whose index ignores the trailing dims: every corner with
+        // the same leading-dim bits reads the same row; gather it once.
+        const uint32_t lead = (!c.hashed) ? c.used : D;
+        const uint32_t lead_mask = (1u << lead) - 1u;
+        scalar_t cached[1u << D][C];
+#pragma unroll
+        for (uint32_t k = 0; k < (1u << D); ++k) {
+            float w = 1.0f;
+            uint32_t p[D];
+#pragma unroll
+            for (uint32_t d = 0; d < D; ++d) {
+                if (k & (1u << d)) { w *= frac[d]; p[d] = cell[d] + 1u; }
+                else { w *= 1.0f - frac[d]; p[d] = cell[d]; }
+            }
+            if ((k & ~lead_mask) == 0 || dy_dx) {
+                const uint32_t row = row_index<D>(c, p);
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch) cached[k][ch] = tab[(size_t)row * C + ch];
+            } else {
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch) cached[k][ch] = cached[k & lead_mask][ch];
+            }
+#pragma unroll
+            for (uint32_t ch = 0; ch < C; ++ch) acc_corner(acc[ch], w, cached[k][ch]);
+        }
+#pragma unroll
+        for (uint32_t ch = 0; ch < C; ++ch) out[ch] = acc[ch];
+
+        if (dy_dx) {
+            // gridencoder.cu:179-222: d(out)/d(x_gd) = scale * sum over the
+            // other dims' corners of w * (right - left).
+            scalar_t *g = dy_dx + (size_t)b * D * L * C + (size_t)l * D * C;
+#pragma unroll
+            for (uint32_t gd = 0; gd < D; ++gd) {
+                scalar_t rg[C];
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch) rg[ch] = (scalar_t)0.0f;
+#pragma unroll
+                for (uint32_t k = 0; k < (1u << (D - 1)); ++k) {
+                    float w = c.scale;
+                    uint32_t kl = 0;
+#pragma unroll
+                    for (uint32_t nd = 0; nd < D - 1; ++nd) {
+                        const uint32_t d = (nd >= gd) ? nd + 1 : nd;
+                        if (k & (1u << nd)) { w *= frac[d]; kl |= 1u << d; }
+                        else { w *= 1.0f - frac[d]; }
+                    }
+                    const uint32_t kr = kl | (1u << gd);
+#pragma unroll
+                    for (uint32_t ch = 0; ch < C; ++ch) {
+                        // scalar_t subtraction (c10::Half - Half -> Half)
+                        const scalar_t diff = (scalar_t)(cached[kr][ch] - cached[kl][ch]);
+                        acc_corner(rg[ch], w, diff);
+                    }
+                }
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch) g[gd * C + ch] = rg[ch];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------ backward
+
+// No-return atomic adds of one table row's C channels.
+template <uint32_t C>
+__device__ __forceinline__ void row_atomic_add(float *dst, const float v[C]) {
+#pragma unroll
+    for (uint32_t ch = 0; ch < C; ++ch) unsafeAtomicAdd(dst + ch, v[ch]);
+}
+template <uint32_t C>
+__device__ __forceinline__ void row_atomic_add(double *dst, const float v[C]) {
+#pragma unroll
+    for (uint32_t ch = 0; ch < C; ++ch) unsafeAtomicAdd(dst + ch, (double)v[ch]);
+}
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+template <uint32_t C>
+__device__ __forceinline__ void row_atomic_add(half_t *dst, const float v[C]) {
+    // gridencoder.cu:298-304: each product rounded to half, packed pairs added
+    // with one global_atomic_pk_add_f16.
+#pragma unroll
+    for (uint32_t ch = 0; ch < C; ch += 2) {
+        half2_t p;
+        p.x = (half_t)v[ch];
+        p.y = (half_t)v[ch + 1];
+        typedef __attribute__((address_space(1))) half2_t global_half2_t;
+        __builtin_amdgcn_global_atomic_fadd_v2f16((global_half2_t *)(dst + ch), p);
+    }
+}
+
+// gridencoder.cu:226-313.  Grad layout: BLC [B, L*C] (native) or [L, B, C].
+// Corners that share a row (tiled levels with dropped trailing dims) are merged
+// into one atomic with the summed weight.
+template <typename grad_t, typename acc_t, uint32_t D, uint32_t C, bool BLC>
+__global__ __launch_bounds__(256) void k_grid_bwd(const grad_t *__restrict__ grad,
+                                                  const float *__restrict__ inputs,
+                                                  const int32_t *__restrict__ offsets,
+                                                  acc_t *__restrict__ grad_grid, uint32_t B,
+                                                  uint32_t L, Levels lv, uint32_t gridtype,
+                                                  int align_corners) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const bool align = align_corners != 0;
+    float x[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) {
+        x[d] = inputs[(size_t)b * D + d];
+        if (x[d] < 0.0f || x[d] > 1.0f) return;  // grads stay zero
+    }
+    for (uint32_t l = 0; l < L; ++l) {
+        const grad_t *gp = BLC ? grad + (size_t)b * L * C + (size_t)l * C
+                               : grad + (size_t)l * B * C + (size_t)b * C;
+        float g[C];
+#pragma unroll
+        for (uint32_t ch = 0; ch < C; ++ch) g[ch] = (float)gp[ch];
+
+        const LevelCtx c = level_ctx<D>(offsets, lv, l, gridtype, align);
+        acc_t *tab = grad_grid + (size_t)c.base * C;
+        float frac[D];
+        uint32_t cell[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) {
+            const float p = fmaf(x[d], c.scale, align ? 0.0f : 0.5f);
+            cell[d] = (uint32_t)floorf(p);
+            frac[d] = p - (float)cell[d];
+        }
+        const uint32_t lead = (!c.hashed) ? c.used : D;
+        // Leading-dim corners, each carrying the summed weight of the trailing
+        // corners that map to the same row.
+        float tw = 1.0f;  // sum over trailing-dim corners = prod(1 - f + f)
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d)
+            if (d >= lead) tw *= (1.0f - frac[d]) + frac[d];
+#pragma unroll
+        for (uint32_t k = 0; k < (1u << D); ++k) {
+            if (k >> lead) continue;  // uniform per level
+            float w = tw;
+            uint32_t p[D];
+#pragma unroll
+            for (uint32_t d = 0; d < D; ++d) {
+                if (d < lead) {
+                    if (k & (1u << d)) { w *= frac[d]; p[d] = cell[d] + 1u; }
+                    else { w *= 1.0f - frac[d]; p[d] = cell[d]; }
+                } else {
+                    p[d] = cell[d];
+                }
+            }
+            const uint32_t row = row_index<D>(c, p);
+            float v[C];
+#pragma unroll
+            for (uint32_t ch = 0; ch < C; ++ch) v[ch] = w * g[ch];
+            row_atomic_add<C>(tab + (size_t)row * C, v);
+        }
+    }
+}
+
+// gridencoder.cu:316-342.  BLC: grad in [B, L*C] (native) else [L, B, C].
+template <typename scalar_t, uint32_t D, uint32_t C, bool BLC>
+__global__ __launch_bounds__(256) void k_grid_input_bwd(const scalar_t *__restrict__ grad,
+                                                        const scalar_t *__restrict__ dy_dx,
+                                                        scalar_t *__restrict__ grad_inputs,
+                                                        uint32_t B, uint32_t L) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * D) return;
+    const uint32_t b = t / D, d = t - b * D;
+    const scalar_t *j = dy_dx + (size_t)b * L * D * C;
+    scalar_t r = (scalar_t)0.0f;
+    for (uint32_t l = 0; l < L; ++l) {
+#pragma unroll
+        for (uint32_t ch = 0; ch < C; ++ch) {
+            const scalar_t a = BLC ? grad[(size_t)b * L * C + (size_t)l * C + ch]
+                                   : grad[(size_t)l * B * C + (size_t)b * C + ch];
+            const scalar_t m = j[l * D * C + d * C + ch];
+            if constexpr (sizeof(scalar_t) == 2) {
+                const half_t p = (half_t)((float)a * (float)m);
+                r = (half_t)((float)r + (float)p);
+            } else {
+                r = fma(a, m, r);
+            }
+        }
+    }
+    grad_inputs[t] = r;
+}
+
+// ------------------------------------------------------------ dispatch
+
+template <typename scalar_t, uint32_t D, bool BLC>
+static void launch_fwd_c(uint32_t C, dim3 g, dim3 blk, hipStream_t s, const float *in,
+                         const scalar_t *emb, const int32_t *off, scalar_t *out, uint32_t B,
+                         uint32_t L, const Levels &lv, scalar_t *dy, uint32_t gt, int ac) {
+    switch (C) {
+    case 1: k_grid_fwd<scalar_t, D, 1, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 2: k_grid_fwd<scalar_t, D, 2, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 4: k_grid_fwd<scalar_t, D, 4, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 8: k_grid_fwd<scalar_t, D, 8, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    }
+}
+
+template <typename scalar_t, bool BLC>
+static void launch_fwd(uint32_t D, uint32_t C, dim3 g, dim3 blk, hipStream_t s, const float *in,
+                       const scalar_t *emb, const int32_t *off, scalar_t *out, uint32_t B,
+                       uint32_t L, const Levels &lv, scalar_t *dy, uint32_t gt, int ac) {
+    switch (D) {
+    case 1: launch_fwd_c<scalar_t, 1, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 2: launch_fwd_c<scalar_t, 2, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 3: launch_fwd_c<scalar_t, 3, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 4: launch_fwd_c<scalar_t, 4, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 5: launch_fwd_c<scalar_t, 5, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    }
+}
+
+template <typename grad_t, typename acc_t, uint32_t D, bool BLC>
+static void launch_bwd_c(uint32_t C, dim3 g, dim3 blk, hipStream_t s, const grad_t *grad,
+                         const float *in, const int32_t *off, acc_t *gg, uint32_t B, uint32_t L,
+                         const Levels &lv, uint32_t gt, int ac) {
+    switch (C) {
+    case 1:
+        if constexpr (sizeof(acc_t) != 2)
+            k_grid_bwd<grad_t, acc_t, D, 1, BLC><<<g, blk, 0, s>>>(grad, in, off, gg, B, L, lv, gt, ac);
+        break;
+    case 2: k_grid_bwd<grad_t, acc_t, D, 2, BLC><<<g, blk, 0, s>>>(grad, in, off, gg, B, L, lv, gt, ac); break;
+    case 4: k_grid_bwd<grad_t, acc_t, D, 4, BLC><<<g, blk, 0, s>>>(grad, in, off, gg, B, L, lv, gt, ac); break;
+    case 8: k_grid_bwd<grad_t, acc_t, D, 8, BLC><<<g, blk, 0, s>>>(grad, in, off, gg, B, L, lv, gt, ac); break;
+    }
+}
+
+template <typename grad_t, typename acc_t, bool BLC>
+static void launch_bwd(uint32_t D, uint32_t C, dim3 g, dim3 blk, hipStream_t s, const grad_t *grad,
+                       const float *in, const int32_t *off, acc_t *gg, uint32_t B, uint32_t L,
+                       const Levels &lv, uint32_t gt, int ac) {
+    switch (D) {
+    case 1: launch_bwd_c<grad_t, acc_t, 1, BLC>(C, g, blk, s, grad, in, off, gg, B, L, lv, gt, ac); break;
+    case 2: launch_bwd_c<grad_t, acc_t, 2, BLC>(C, g, blk, s, grad, in, off, gg, B, L, lv, gt, ac); break;
+    case 3: launch_bwd_c<grad_t, acc_t, 3, BLC>(C, g, blk, s, grad, in, off, gg, B, L, lv, gt, ac); break;
+    case 4: launch_bwd_c<grad_t, acc_t, 4, BLC>(C, g, blk, s, grad, in, off, gg, B, L, lv, gt, ac); break;
+    case 5: launch_bwd_c<grad_t, acc_t, 5, BLC>(C, g, blk, s, grad, in, off, gg, B, L, lv, gt, ac); break;
+    }
+}
+
+template <typename scalar_t, bool BLC>
+static void launch_input_bwd(uint32_t D, uint32_t C, hipStream_t s, const scalar_t *grad,
+                             const scalar_t *dy, scalar_t *gi, uint32_t B, uint32_t L) {
+    const dim3 g(ceil_div(B * D, 256u)), blk(256);
+#define DFHIP_IB(DD)                                                                           \
+    switch (C) {                                                                               \
+    case 1: k_grid_input_bwd<scalar_t, DD, 1, BLC><<<g, blk, 0, s>>>(grad, dy, gi, B, L); break; \
+    case 2: k_grid_input_bwd<scalar_t, DD, 2, BLC><<<g, blk, 0, s>>>(grad, dy, gi, B, L); break; \
+    case 4: k_grid_input_bwd<scalar_t, DD, 4, BLC><<<g, blk, 0, s>>>(grad, dy, gi, B, L); break; \
+    case 8: k_grid_input_bwd<scalar_t, DD, 8, BLC><<<g, blk, 0, s>>>(grad, dy, gi, B, L); break; \
+    }
+    switch (D) {
+    case 1: DFHIP_IB(1) break;
+    case 2: DFHIP_IB(2) break;
+    case 3: DFHIP_IB(3) break;
+    case 4: DFHIP_IB(4) break;
+    case 5: DFHIP_IB(5) break;
+    }
+#undef DFHIP_IB
+}
+
+static bool check_dc(const char *what, uint32_t D, uint32_t C, uint32_t L) {
+    if (D < 1 || D > 5) {  // gridencoder.cu:372
+        set_error("%s: GridEncoding: D must be 1, 2, 3, 4, or 5.", what);
+        return false;
+    }
+    if (C != 1 && C != 2 && C != 4 && C != 8) {  // gridencoder.cu:354
+        set_error("%s: GridEncoding: C must be 1, 2, 4, or 8.", what);
+        return false;
+    }
+    if (L > kMaxLevels) {
+        set_error("%s: at most %u levels supported (got %u)", what, kMaxLevels, L);
+        return false;
+    }
+    return true;
+}
+
+}  // namespace ge
+}  // namespace dfhip
+
+using namespace dfhip;
+using namespace dfhip::ge;
+
+template <bool BLC>
+static int grid_fwd_impl(const char *name, int dtype, const float *inputs,
+                         const void *embeddings, const int32_t *offsets, void *outputs,
+                         uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                         void *dy_dx, uint32_t gridtype, int align_corners,
+                         dfhip_stream_t stream) {
+    if (!check_dc(name, D, C, L)) return DFHIP_EINVAL;
+    if (B == 0 || L == 0) return DFHIP_OK;
+    const Levels lv = make_levels(L, S, H);
+    const dim3 g(ceil_div(B, 256u)), blk(256);
+    DFHIP_DISPATCH(dtype, name,
+        launch_fwd<scalar_t, BLC>(D, C, g, blk, as_stream(stream), inputs,
+                                  (const scalar_t *)embeddings, offsets, (scalar_t *)outputs, B,
+                                  L, lv, (scalar_t *)dy_dx, gridtype, align_corners));
+    return check_launch(name);
+}
+
+extern "C" int dfhip_grid_encode_forward(int dtype, const float *inputs, const void *embeddings,
+                                         const int32_t *offsets, void *outputs, uint32_t B,
+                                         uint32_t D, uint32_t C, uint32_t L, float S,
+                                         uint32_t H, void *dy_dx, uint32_t gridtype,
+                                         int align_corners, dfhip_stream_t stream) {
+    return grid_fwd_impl<false>("grid_encode_forward", dtype, inputs, embeddings, offsets,
+                                outputs, B, D, C, L, S, H, dy_dx, gridtype, align_corners,
+                                stream);
+}
+
+extern "C" int dfhip_grid_encode_forward_blc(int dtype, const float *inputs,
+                                             const void *embeddings, const int32_t *offsets,
+                                             void *outputs, uint32_t B, uint32_t D, uint32_t C,
+                                             uint32_t L, float S, uint32_t H, void *dy_dx,
+                                             uint32_t gridtype, int align_corners,
+                                             dfhip_stream_t stream) {
+    return grid_fwd_impl<true>("grid_encode_forward_blc", dtype, inputs, embeddings, offsets,
+                               outputs, B, D, C, L, S, H, dy_dx, gridtype, align_corners,
+                               stream);
+}
+
+template <bool BLC>
+static int grid_bwd_impl(const char *name, int grad_dtype, int acc_dtype, const void *grad,
+                         const float *inputs, const int32_t *offsets, void *grad_embeddings,
+                         uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                         uint32_t gridtype, int align_corners, dfhip_stream_t stream) {
+    if (!check_dc(name, D, C, L)) return DFHIP_EINVAL;
+    if (acc_dtype == DFHIP_F16 && (C % 2) != 0) {
+        // The reference's half atomicAdd for odd C is an empty stub
+        // (gridencoder.cu:22-26); refuse instead of silently dropping grads.
+        set_error("%s: f16 accumulation needs an even C (got C=%u)", name, C);
+        return DFHIP_EDTYPE;
+    }
+    if (B == 0 || L == 0) return DFHIP_OK;
+    const Levels lv = make_levels(L, S, H);
+    const dim3 g(ceil_div(B, 256u)), blk(256);
+    hipStream_t s = as_stream(stream);
+#define DFHIP_BWD_ACC(GT)                                                                    \
+    switch (acc_dtype) {                                                                     \
+    case DFHIP_F32: launch_bwd<GT, float, BLC>(D, C, g, blk, s, (const GT *)grad, inputs,     \
+                                               offsets, (float *)grad_embeddings, B, L, lv,   \
+                                               gridtype, align_corners); break;               \
+    case DFHIP_F16: launch_bwd<GT, half_t, BLC>(D, C, g, blk, s, (const GT *)grad, inputs,    \
+                                                offsets, (half_t *)grad_embeddings, B, L, lv, \
+                                                gridtype, align_corners); break;              \
+    case DFHIP_F64: launch_bwd<GT, double, BLC>(D, C, g, blk, s, (const GT *)grad, inputs,    \
+                                                offsets, (double *)grad_embeddings, B, L, lv, \
+                                                gridtype, align_corners); break;              \
+    default: set_error("%s: unsupported accumulation dtype %d", name, acc_dtype);            \
+             return DFHIP_EDTYPE;                                                            \
+    }
+    switch (grad_dtype) {
+    case DFHIP_F32: DFHIP_BWD_ACC(float) break;
+    case DFHIP_F16: DFHIP_BWD_ACC(half_t) break;
+    case DFHIP_F64: DFHIP_BWD_ACC(double) break;
+    default: set_error("%s: unsupported grad dtype %d", name, grad_dtype); return DFHIP_EDTYPE;
+    }
+#undef DFHIP_BWD_ACC
+    return check_launch(name);
+}
+
+extern "C" int dfhip_grid_encode_backward(int dtype, const void *grad, const float *inputs,
+                                          const void *embeddings, const int32_t *offsets,
+                                          void *grad_embeddings, uint32_t B, uint32_t D,
+                                          uint32_t C, uint32_t L, float S, uint32_t H,
+                                          const void *dy_dx, void *grad_inputs,
+                                          uint32_t gridtype, int align_corners,
+                                          dfhip_stream_t stream) {
+    (void)embeddings;  // only its dtype matters (gridencoder.cu:475)
+    int rc = grid_bwd_impl<false>("grid_encode_backward", dtype, dtype, grad, inputs, offsets,
+                                  grad_embeddings, B, D, C, L, S, H, gridtype, align_corners,
+                                  stream);
+    if (rc != DFHIP_OK || dy_dx == nullptr || grad_inputs == nullptr || B == 0) return rc;
+    DFHIP_DISPATCH(dtype, "grid_encode_backward",
+        (launch_input_bwd<scalar_t, false>)(D, C, as_stream(stream), (const scalar_t *)grad,
+                                   (const scalar_t *)dy_dx, (scalar_t *)grad_inputs, B, L));
+    return check_launch("grid_encode_backward(inputs)");
+}
+
+extern "C" int dfhip_grid_encode_backward_blc(int grad_dtype, int acc_dtype, const void *grad,
+                                              const float *inputs, const int32_t *offsets,
+                                              void *grad_embeddings, uint32_t B, uint32_t D,
+                                              uint32_t C, uint32_t L, float S, uint32_t H,
+                                              const void *dy_dx, void *grad_inputs,
+                                              uint32_t gridtype, int align_corners,
+                                              dfhip_stream_t stream) {
+    int rc = grid_bwd_impl<true>("grid_encode_backward_blc", grad_dtype, acc_dtype, grad, inputs,
+                                 offsets, grad_embeddings, B, D, C, L, S, H, gridtype,
+                                 align_corners, stream);
+    if (rc != DFHIP_OK || dy_dx == nullptr || grad_inputs == nullptr || B == 0) return rc;
+    DFHIP_DISPATCH(grad_dtype, "grid_encode_backward_blc",
+        (launch_input_bwd<scalar_t, true>)(D, C, as_stream(stream), (const scalar_t *)grad,
+                                           (const scalar_t *)dy_dx, (scalar_t *)grad_inputs, B, L));
+    return check_launch("grid_encode_backward_blc(inputs)");
+}

@@ -1,0 +1,783 @@
+// Occupancy-grid ray marching + volume compositing for gfx950 (MI355X).
+//
+// Behavioural spec: reference raymarching/src/raymarching.cu (cited per kernel).
+// Numerics follow the reference's nvcc build: every multiply-add that nvcc
+// contracts by default (-fmad=true) is an explicit fmaf() here, and the file is
+// compiled with -ffp-contract=off so nothing else is contracted.  The CPU oracle
+// (oracle/oracle.c) makes the same choices, which makes per-ray sample counts and
+// sample contents bit-exact between the two.
+//
+// MI355X design notes:
+//  * march_rays_train is deterministic: a count pass (one wave per 64 rays,
+//    wave-reduced block totals, integer atomics only for the API counter), then
+//    an emit pass that derives each ray's offset from the block totals plus a
+//    wave64 inclusive scan.  Samples land in ray order, contiguous per ray, so
+//    compositing and the encoders read each ray's samples as one run.
+//  * No N*max_steps zero-fill: the emit pass zeroes only the align tail.
+//  * One wave per workgroup for the per-ray kernels: 16k rays = 256 workgroups
+//    = one per CU, instead of 64 CUs with 256-thread blocks.
+#include "common.h"
+
+#include <float.h>
+#include <math.h>
+
+namespace dfhip {
+namespace rm {
+
+constexpr float kSqrt3 = 1.7320508075688772f;
+constexpr float kInvPi = 0.3183098861837907f;
+
+__device__ __forceinline__ float clampf(float x, float lo, float hi) {
+    return fminf(hi, fmaxf(lo, x));
+}
+
+// raymarching.cu:56-71 (expand_bits / morton3D) — same integer semantics for
+// every uint32 input (the multiplies are written as shift-adds).
+__host__ __device__ __forceinline__ uint32_t spread3(uint32_t v) {
+    v = (v + (v << 16)) & 0xFF0000FFu;
+    v = (v + (v << 8)) & 0x0F00F00Fu;
+    v = (v + (v << 4)) & 0xC30C30C3u;
+    v = (v + (v << 2)) & 0x49249249u;
+    return v;
+}
+__host__ __device__ __forceinline__ uint32_t morton3(uint32_t x, uint32_t y, uint32_t z) {
+    return spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
+}
+// raymarching.cu:73-81
+__host__ __device__ __forceinline__ uint32_t compact3(uint32_t v) {
+    v &= 0x49249249u;
+    v = (v | (v >> 2)) & 0xC30C30C3u;
+    v = (v | (v >> 4)) & 0x0F00F00Fu;
+    v = (v | (v >> 8)) & 0xFF0000FFu;
+    v = (v | (v >> 16)) & 0x0000FFFFu;
+    return v;
+}
+
+// Per-launch constants of the marcher (raymarching.cu:337-346).
+struct MarchConsts {
+    float bound, dt_gamma, dt_min, dt_max, rH, H3, Hf, Cf, Hm1;
+    uint32_t H;
+};
+
+static MarchConsts make_consts(float bound, float dt_gamma, uint32_t max_steps,
+                               uint32_t C, uint32_t H) {
+    MarchConsts k;
+    k.bound = bound;
+    k.dt_gamma = dt_gamma;
+    k.dt_min = (2.0f * kSqrt3) / (float)max_steps;
+    k.dt_max = (2.0f * kSqrt3 * (float)(1u << (C - 1))) / (float)H;
+    k.rH = 1.0f / (float)H;
+    k.H3 = (float)(H * H * H);
+    k.Hf = (float)H;
+    k.Cf = (float)C;
+    k.Hm1 = (float)(H - 1);
+    k.H = H;
+    return k;
+}
+
+// Cascade level of a point (raymarching.cu:42-54, max over position and dt).
+__device__ __forceinline__ int mip_level(const MarchConsts &k, float x, float y, float z,
+                                         float dt) {
+    int ep, ed;
+    const float mx = fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z)));
+    frexpf(mx, &ep);
+    const float lp = fminf(k.Cf - 1.0f, fmaxf(0.0f, (float)ep));
+    const float md = (float)((double)(dt * k.Hf) * 0.5);
+    frexpf(md, &ed);
+    const float ld = fminf(k.Cf - 1.0f, fmaxf(0.0f, (float)ed));
+    return max((int)lp, (int)ld);
+}
+
+// Grid cell of a clamped coordinate (raymarching.cu:374-376: the product is
+// formed in double, then narrowed to float by the float clamp()).
+__device__ __forceinline__ int cell_of(const MarchConsts &k, float c, float rbound) {
+    const float u = fmaf(c, rbound, 1.0f);
+    const float v = (float)(0.5 * (double)u * (double)k.H);
+    return (int)clampf(v, 0.0f, k.Hm1);
+}
+
+// Distance (in t) to the far face of the current cell along one axis
+// (raymarching.cu:390-392, nvcc contraction model).
+__device__ __forceinline__ float face_dist(const MarchConsts &k, int n, float d, float rd,
+                                           float c, float mip_bound) {
+    const float a = fmaf(0.5f, copysignf(1.0f, d), (float)n + 0.5f);
+    const float b = fmaf(a * k.rH, 2.0f, -1.0f);
+    return fmaf(b, mip_bound, -c) * rd;
+}
+
+struct Ray {
+    float ox, oy, oz, dx, dy, dz, rdx, rdy, rdz;
+};
+
+template <typename scalar_t>
+__device__ __forceinline__ Ray load_ray(const scalar_t *o, const scalar_t *d) {
+    Ray r;
+    r.ox = to_f(o[0]); r.oy = to_f(o[1]); r.oz = to_f(o[2]);
+    r.dx = to_f(d[0]); r.dy = to_f(d[1]); r.dz = to_f(d[2]);
+    r.rdx = 1.0f / r.dx; r.rdy = 1.0f / r.dy; r.rdz = 1.0f / r.dz;
+    return r;
+}
+
+// The march loop shared by the count pass, the emit pass and the inference
+// marcher (raymarching.cu:359-400, 427-479, 750-804).  Visits the same
+// t-sequence in every mode.  WRITE: store each occupied sample at out[step].
+// Returns the number of occupied samples taken (<= limit).
+template <bool WRITE, typename scalar_t>
+__device__ __forceinline__ uint32_t march(const MarchConsts &k, const Ray &r,
+                                          const uint8_t *__restrict__ grid, float t,
+                                          float far, uint32_t limit, scalar_t *xyzs,
+                                          scalar_t *dirs, scalar_t *deltas,
+                                          float *t_out) {
+    uint32_t step = 0;
+    float last_t = t;
+    while (t < far && step < limit) {
+        const float x = clampf(fmaf(t, r.dx, r.ox), -k.bound, k.bound);
+        const float y = clampf(fmaf(t, r.dy, r.oy), -k.bound, k.bound);
+        const float z = clampf(fmaf(t, r.dz, r.oz), -k.bound, k.bound);
+        const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
+        const int level = mip_level(k, x, y, z, dt);
+        const float mip_bound = fminf(scalbnf(1.0f, level), k.bound);
+        const float rbound = 1.0f / mip_bound;
+        const int nx = cell_of(k, x, rbound);
+        const int ny = cell_of(k, y, rbound);
+        const int nz = cell_of(k, z, rbound);
+        const uint32_t idx =
+            (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
+        const bool occ = (grid[idx >> 3] >> (idx & 7)) & 1;
+        if (occ) {
+            if (WRITE) {
+                scalar_t *px = xyzs + 3 * step;
+                scalar_t *pd = dirs + 3 * step;
+                scalar_t *pl = deltas + 2 * step;
+                px[0] = from_f<scalar_t>(x);
+                px[1] = from_f<scalar_t>(y);
+                px[2] = from_f<scalar_t>(z);
+                pd[0] = from_f<scalar_t>(r.dx);
+                pd[1] = from_f<scalar_t>(r.dy);
+                pd[2] = from_f<scalar_t>(r.dz);
+                t += dt;
+                pl[0] = from_f<scalar_t>(dt);
+                pl[1] = from_f<scalar_t>(t - last_t);
+                last_t = t;
+            } else {
+                t += dt;
+            }
+            ++step;
+        } else {
+            const float tx = face_dist(k, nx, r.dx, r.rdx, x, mip_bound);
+            const float ty = face_dist(k, ny, r.dy, r.rdy, y, mip_bound);
+            const float tz = face_dist(k, nz, r.dz, r.rdz, z, mip_bound);
+            const float tt = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+            do {
+                t += clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
+            } while (t < tt);
+        }
+    }
+    if (t_out) *t_out = t;
+    return step;
+}
+
+// ------------------------------------------------------------------ utils
+
+// numeric_limits<scalar_t>::max() of the reference's miss value (raymarching.cu:122)
+template <typename T> __device__ __forceinline__ T max_value();
+template <> __device__ __forceinline__ float max_value<float>() { return FLT_MAX; }
+template <> __device__ __forceinline__ double max_value<double>() { return DBL_MAX; }
+template <> __device__ __forceinline__ half_t max_value<half_t>() { return (half_t)65504.0f; }
+
+// raymarching.cu:91-145
+template <typename scalar_t>
+__global__ __launch_bounds__(256) void k_near_far(const scalar_t *__restrict__ rays_o,
+                                                  const scalar_t *__restrict__ rays_d,
+                                                  const scalar_t *__restrict__ aabb,
+                                                  uint32_t N, float min_near,
+                                                  scalar_t *nears, scalar_t *fars) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
+    const float b0 = to_f(aabb[0]), b1 = to_f(aabb[1]), b2 = to_f(aabb[2]);
+    const float b3 = to_f(aabb[3]), b4 = to_f(aabb[4]), b5 = to_f(aabb[5]);
+
+    float lo = (b0 - r.ox) * r.rdx, hi = (b3 - r.ox) * r.rdx;
+    if (lo > hi) { float s = lo; lo = hi; hi = s; }
+    float lo_y = (b1 - r.oy) * r.rdy, hi_y = (b4 - r.oy) * r.rdy;
+    if (lo_y > hi_y) { float s = lo_y; lo_y = hi_y; hi_y = s; }
+    const scalar_t miss = max_value<scalar_t>();
+    if (lo > hi_y || lo_y > hi) {
+        nears[n] = fars[n] = miss;
+        return;
+    }
+    if (lo_y > lo) lo = lo_y;
+    if (hi_y < hi) hi = hi_y;
+    float lo_z = (b2 - r.oz) * r.rdz, hi_z = (b5 - r.oz) * r.rdz;
+    if (lo_z > hi_z) { float s = lo_z; lo_z = hi_z; hi_z = s; }
+    if (lo > hi_z || lo_z > hi) {
+        nears[n] = fars[n] = miss;
+        return;
+    }
+    if (lo_z > lo) lo = lo_z;
+    if (hi_z < hi) hi = hi_z;
+    if (lo < min_near) lo = min_near;
+    nears[n] = from_f<scalar_t>(lo);
+    fars[n] = from_f<scalar_t>(hi);
+}
+
+// raymarching.cu:162-198
+template <typename scalar_t>
+__global__ __launch_bounds__(256) void k_sph_from_ray(const scalar_t *__restrict__ rays_o,
+                                                      const scalar_t *__restrict__ rays_d,
+                                                      float radius, uint32_t N,
+                                                      scalar_t *coords) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
+    // Contraction model (LLVM DAG combine, as nvcc): a*b + c*d -> fma(a, b, c*d).
+    const float A = fmaf(r.dz, r.dz, fmaf(r.dx, r.dx, r.dy * r.dy));
+    const float Bh = fmaf(r.oz, r.dz, fmaf(r.ox, r.dx, r.oy * r.dy));
+    const float Cc = fmaf(-radius, radius, fmaf(r.oz, r.oz, fmaf(r.ox, r.ox, r.oy * r.oy)));
+    const float t = (-Bh + sqrtf(fmaf(Bh, Bh, -(A * Cc)))) / A;
+    const float x = fmaf(t, r.dx, r.ox), y = fmaf(t, r.dy, r.oy), z = fmaf(t, r.dz, r.oz);
+    const float theta = atan2f(sqrtf(fmaf(x, x, z * z)), y);
+    const float phi = atan2f(z, x);
+    coords[2 * n + 0] = from_f<scalar_t>(fmaf(2.0f * theta, kInvPi, -1.0f));
+    coords[2 * n + 1] = from_f<scalar_t>(phi * kInvPi);
+}
+
+// raymarching.cu:214-226
+__global__ __launch_bounds__(256) void k_morton3D(const int32_t *__restrict__ coords,
+                                                  uint32_t N, int32_t *indices) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const int32_t *c = coords + 3 * n;
+    indices[n] = (int32_t)morton3((uint32_t)c[0], (uint32_t)c[1], (uint32_t)c[2]);
+}
+
+// raymarching.cu:237-254
+__global__ __launch_bounds__(256) void k_morton3D_invert(const int32_t *__restrict__ indices,
+                                                         uint32_t N, int32_t *coords) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const uint32_t v = (uint32_t)indices[n];
+    coords[3 * n + 0] = (int32_t)compact3(v);
+    coords[3 * n + 1] = (int32_t)compact3(v >> 1);
+    coords[3 * n + 2] = (int32_t)compact3(v >> 2);
+}
+
+// raymarching.cu:267-289 — one thread per output byte; the 8 grid values of a
+// byte are read as two 16-B vectors when the storage is f32.
+template <typename scalar_t>
+__global__ __launch_bounds__(256) void k_packbits(const scalar_t *__restrict__ grid,
+                                                  uint32_t N, float thresh,
+                                                  uint8_t *bitfield) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const scalar_t *g = grid + 8 * (size_t)n;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bits |= (to_f(g[i]) > thresh ? 1u : 0u) << i;
+    bitfield[n] = (uint8_t)bits;
+}
+
+// 16-B aligned f32 storage: the 8 values of a byte as two float4 loads.
+__global__ __launch_bounds__(256) void k_packbits_f32v(const float *__restrict__ grid,
+                                                         uint32_t N, float thresh,
+                                                         uint8_t *bitfield) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const float4 *g = reinterpret_cast<const float4 *>(grid) + 2 * (size_t)n;
+    const float4 a = g[0], b = g[1];
+    const uint32_t bits = (a.x > thresh) | ((a.y > thresh) << 1) | ((a.z > thresh) << 2) |
+                          ((a.w > thresh) << 3) | ((b.x > thresh) << 4) |
+                          ((b.y > thresh) << 5) | ((b.z > thresh) << 6) | ((b.w > thresh) << 7);
+    bitfield[n] = (uint8_t)bits;
+}
+
+// ------------------------------------------------------------------ training march
+
+// Pass 1 (raymarching.cu:341-400): count occupied samples per ray.
+template <typename scalar_t>
+__global__ __launch_bounds__(64) void k_march_train_count(
+    const scalar_t *__restrict__ rays_o, const scalar_t *__restrict__ rays_d,
+    const uint8_t *__restrict__ grid, MarchConsts k, uint32_t max_steps, uint32_t N,
+    const scalar_t *__restrict__ nears, const scalar_t *__restrict__ fars,
+    int32_t *rays, int32_t *counter, const scalar_t *__restrict__ noises,
+    int32_t *block_sums) {
+    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    int cnt = 0;
+    if (n < N) {
+        const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
+        const float near = to_f(nears[n]), far = to_f(fars[n]);
+        const float t0 = fmaf(clampf(near * k.dt_gamma, k.dt_min, k.dt_max),
+                              to_f(noises[n]), near);
+        cnt = (int)march<false, scalar_t>(k, r, grid, t0, far, max_steps, nullptr,
+                                          nullptr, nullptr, nullptr);
+        rays[3 * n + 0] = (int32_t)n;
+        rays[3 * n + 2] = cnt;
+    }
+    const int tot = wave_reduce_add(cnt);
+    if (threadIdx.x == 0) {
+        block_sums[blockIdx.x] = tot;
+        atomicAdd(counter, tot);
+        atomicAdd(counter + 1, (int)min(64u, N - blockIdx.x * 64));
+    }
+}
+
+template <typename scalar_t>
+__device__ __forceinline__ void zero_rows(scalar_t *xyzs, scalar_t *dirs, scalar_t *deltas,
+                                          uint64_t begin, uint64_t end, uint32_t first,
+                                          uint32_t stride) {
+    const scalar_t zero = from_f<scalar_t>(0.0f);
+    for (uint64_t row = begin + first; row < end; row += stride) {
+        xyzs[3 * row] = zero; xyzs[3 * row + 1] = zero; xyzs[3 * row + 2] = zero;
+        dirs[3 * row] = zero; dirs[3 * row + 1] = zero; dirs[3 * row + 2] = zero;
+        deltas[2 * row] = zero; deltas[2 * row + 1] = zero;
+    }
+}
+
+// Pass 2 (raymarching.cu:405-479): offsets = block prefix + wave scan, then
+// re-march and write.  Rays whose range would cross M are not written
+// (raymarching.cu:416).
+template <typename scalar_t>
+__global__ __launch_bounds__(64) void k_march_train_emit(
+    const scalar_t *__restrict__ rays_o, const scalar_t *__restrict__ rays_d,
+    const uint8_t *__restrict__ grid, MarchConsts k, uint32_t N, uint32_t M,
+    const scalar_t *__restrict__ nears, const scalar_t *__restrict__ fars,
+    scalar_t *xyzs, scalar_t *dirs, scalar_t *deltas, int32_t *rays,
+    const scalar_t *__restrict__ noises, const int32_t *__restrict__ block_sums,
+    int zero_tail) {
+    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    int part = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 64) part += block_sums[i];
+    const int prefix = wave_reduce_add(part);
+    const int cnt = (n < N) ? rays[3 * n + 2] : 0;
+    const int incl = wave_inclusive_scan(cnt);
+    const uint32_t off = (uint32_t)(prefix + incl - cnt);
+    if (n < N) {
+        rays[3 * n + 1] = (int32_t)off;
+        if (cnt > 0 && off + (uint32_t)cnt <= M) {
+            const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
+            const float near = to_f(nears[n]), far = to_f(fars[n]);
+            const float t0 = fmaf(clampf(near * k.dt_gamma, k.dt_min, k.dt_max),
+                                  to_f(noises[n]), near);
+            march<true, scalar_t>(k, r, grid, t0, far, (uint32_t)cnt, xyzs + 3 * (size_t)off,
+                                  dirs + 3 * (size_t)off, deltas + 2 * (size_t)off, nullptr);
+        } else if (zero_tail != 0 && cnt > 0 && off < M) {
+            // first ray that does not fit: rows [off, M) stay unwritten -> zero
+            // (end clipped by the align limit, like the tail below)
+            uint64_t end = M;
+            if (zero_tail > 0) {
+                uint64_t total = (uint64_t)prefix;  // global total, rare path
+                for (uint32_t i = blockIdx.x; i < gridDim.x; ++i) total += (uint32_t)block_sums[i];
+                end = min(end, total + (uint64_t)zero_tail - total % (uint64_t)zero_tail);
+            }
+            zero_rows(xyzs, dirs, deltas, off, end, 0, 1);
+        }
+    }
+    if (zero_tail != 0 && blockIdx.x == gridDim.x - 1) {
+        const uint64_t total = (uint64_t)prefix + (uint32_t)__shfl(incl, 63, 64);
+        uint64_t end = M;
+        if (zero_tail > 0) end = min(end, total + (uint64_t)zero_tail - total % (uint64_t)zero_tail);
+        zero_rows(xyzs, dirs, deltas, total, end, threadIdx.x, 64);
+    }
+}
+
+// ------------------------------------------------------------------ compositing
+
+template <typename scalar_t> struct Acc { typedef float type; };
+template <> struct Acc<double> { typedef double type; };
+
+// raymarching.cu:500-577
+template <typename scalar_t>
+__global__ __launch_bounds__(64) void k_composite_train_fwd(
+    const scalar_t *__restrict__ sigmas, const scalar_t *__restrict__ rgbs,
+    const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays, uint32_t M,
+    uint32_t N, float T_thresh, scalar_t *weights_sum, scalar_t *depth, scalar_t *image) {
+    typedef typename Acc<scalar_t>::type acc_t;
+    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    if (n >= N) return;
+    const uint32_t index = (uint32_t)rays[3 * n];
+    const uint32_t offset = (uint32_t)rays[3 * n + 1];
+    const uint32_t num = (uint32_t)rays[3 * n + 2];
+    acc_t T = 1, r = 0, g = 0, b = 0, ws = 0, t = 0, d = 0;
+    if (num != 0 && offset + num <= M) {
+        const scalar_t *s = sigmas + offset;
+        const scalar_t *c = rgbs + 3 * (size_t)offset;
+        const scalar_t *dl = deltas + 2 * (size_t)offset;
+        for (uint32_t i = 0; i < num; ++i) {
+            const acc_t alpha = (acc_t)1.0f - (acc_t)__expf(-to_f(s[i]) * to_f(dl[2 * i]));
+            const acc_t w = alpha * T;
+            r = fma(w, (acc_t)to_f(c[3 * i + 0]), r);
+            g = fma(w, (acc_t)to_f(c[3 * i + 1]), g);
+            b = fma(w, (acc_t)to_f(c[3 * i + 2]), b);
+            t += (acc_t)to_f(dl[2 * i + 1]);
+            d = fma(w, t, d);
+            ws += w;
+            T *= (acc_t)1.0f - alpha;
+            if (T < (acc_t)T_thresh) break;
+        }
+    }
+    weights_sum[index] = (scalar_t)ws;
+    depth[index] = (scalar_t)d;
+    image[3 * index + 0] = (scalar_t)r;
+    image[3 * index + 1] = (scalar_t)g;
+    image[3 * index + 2] = (scalar_t)b;
+}
+
+// raymarching.cu:601-682.  DENSE: also zero rows the reference leaves untouched.
+template <typename scalar_t, bool DENSE>
+__global__ __launch_bounds__(64) void k_composite_train_bwd(
+    const scalar_t *__restrict__ grad_ws, const scalar_t *__restrict__ grad_image,
+    const scalar_t *__restrict__ sigmas, const scalar_t *__restrict__ rgbs,
+    const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays,
+    const scalar_t *__restrict__ weights_sum, const scalar_t *__restrict__ image,
+    uint32_t M, uint32_t N, float T_thresh, scalar_t *grad_sigmas, scalar_t *grad_rgbs) {
+    typedef typename Acc<scalar_t>::type acc_t;
+    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    if (n >= N) return;
+    const uint32_t index = (uint32_t)rays[3 * n];
+    const uint32_t offset = (uint32_t)rays[3 * n + 1];
+    const uint32_t num = (uint32_t)rays[3 * n + 2];
+    const scalar_t zero = (scalar_t)0.0f;
+    uint32_t i = 0;
+    if (num != 0 && offset + num <= M) {
+        const scalar_t *s = sigmas + offset;
+        const scalar_t *c = rgbs + 3 * (size_t)offset;
+        const scalar_t *dl = deltas + 2 * (size_t)offset;
+        scalar_t *gs = grad_sigmas + offset;
+        scalar_t *gc = grad_rgbs + 3 * (size_t)offset;
+        const acc_t gr = to_f(grad_image[3 * index + 0]);
+        const acc_t gg = to_f(grad_image[3 * index + 1]);
+        const acc_t gb = to_f(grad_image[3 * index + 2]);
+        const acc_t gw = to_f(grad_ws[index]);
+        const acc_t rf = to_f(image[3 * index + 0]);
+        const acc_t gf = to_f(image[3 * index + 1]);
+        const acc_t bf = to_f(image[3 * index + 2]);
+        const acc_t wsf = to_f(weights_sum[index]);
+        acc_t T = 1, r = 0, g = 0, b = 0, ws = 0;
+        for (; i < num; ++i) {
+            const acc_t sg = to_f(s[i]), dt = to_f(dl[2 * i]);
+            const acc_t cr = to_f(c[3 * i]), cg = to_f(c[3 * i + 1]), cb = to_f(c[3 * i + 2]);
+            const acc_t alpha = (acc_t)1.0f - (acc_t)__expf(-(float)sg * (float)dt);
+            const acc_t w = alpha * T;
+            r = fma(w, cr, r);
+            g = fma(w, cg, g);
+            b = fma(w, cb, b);
+            ws += w;
+            T *= (acc_t)1.0f - alpha;
+            gc[3 * i + 0] = (scalar_t)(gr * w);
+            gc[3 * i + 1] = (scalar_t)(gg * w);
+            gc[3 * i + 2] = (scalar_t)(gb * w);
+            // ((gr*A + gg*B) + gb*C) + gw*D, nvcc contraction: fuse the left product.
+            acc_t acc = fma(gr, fma(T, cr, -(rf - r)), gg * fma(T, cg, -(gf - g)));
+            acc = fma(gb, fma(T, cb, -(bf - b)), acc);
+            acc = fma(gw, (acc_t)1 - wsf, acc);
+            gs[i] = (scalar_t)(dt * acc);
+            if (T < (acc_t)T_thresh) { ++i; break; }
+        }
+    }
+    if (DENSE) {
+        // Zero rows [offset + i, offset + num) of this ray, clipped to M.
+        const uint64_t end = min((uint64_t)offset + num, (uint64_t)M);
+        for (uint64_t row = (uint64_t)offset + i; row < end; ++row) {
+            grad_sigmas[row] = zero;
+            grad_rgbs[3 * row] = zero; grad_rgbs[3 * row + 1] = zero; grad_rgbs[3 * row + 2] = zero;
+        }
+        if (n == N - 1) {
+            for (uint64_t row = (uint64_t)offset + num; row < M; ++row) {
+                grad_sigmas[row] = zero;
+                grad_rgbs[3 * row] = zero; grad_rgbs[3 * row + 1] = zero; grad_rgbs[3 * row + 2] = zero;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ inference
+
+// raymarching.cu:700-804; also writes zeros into the slots it does not fill.
+template <typename scalar_t>
+__global__ __launch_bounds__(64) void k_march_infer(
+    uint32_t n_alive, uint32_t n_step, const int32_t *__restrict__ rays_alive,
+    const scalar_t *__restrict__ rays_t, const scalar_t *__restrict__ rays_o,
+    const scalar_t *__restrict__ rays_d, MarchConsts k, const uint8_t *__restrict__ grid,
+    const scalar_t *__restrict__ fars, scalar_t *xyzs, scalar_t *dirs, scalar_t *deltas,
+    const scalar_t *__restrict__ noises) {
+    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    if (n >= n_alive) return;
+    const int index = rays_alive[n];
+    const Ray r = load_ray(rays_o + 3 * (size_t)index, rays_d + 3 * (size_t)index);
+    float t = to_f(rays_t[index]);
+    const float far = to_f(fars[index]);
+    t = fmaf(clampf(t * k.dt_gamma, k.dt_min, k.dt_max), to_f(noises[n]), t);
+    scalar_t *px = xyzs + 3 * (size_t)n * n_step;
+    scalar_t *pd = dirs + 3 * (size_t)n * n_step;
+    scalar_t *pl = deltas + 2 * (size_t)n * n_step;
+    const uint32_t got = march<true, scalar_t>(k, r, grid, t, far, n_step, px, pd, pl, nullptr);
+    const scalar_t zero = from_f<scalar_t>(0.0f);
+    for (uint32_t s = got; s < n_step; ++s) {
+        px[3 * s] = zero; px[3 * s + 1] = zero; px[3 * s + 2] = zero;
+        pd[3 * s] = zero; pd[3 * s + 1] = zero; pd[3 * s + 2] = zero;
+        pl[2 * s] = zero; pl[2 * s + 1] = zero;
+    }
+}
+
+// raymarching.cu:818-905
+template <typename scalar_t>
+__global__ __launch_bounds__(64) void k_composite_infer(
+    uint32_t n_alive, uint32_t n_step, float T_thresh, int32_t *rays_alive,
+    scalar_t *rays_t, const scalar_t *__restrict__ sigmas,
+    const scalar_t *__restrict__ rgbs, const scalar_t *__restrict__ deltas,
+    scalar_t *weights_sum, scalar_t *depth, scalar_t *image) {
+    typedef typename Acc<scalar_t>::type acc_t;
+    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    if (n >= n_alive) return;
+    const int index = rays_alive[n];
+    const scalar_t *s = sigmas + (size_t)n * n_step;
+    const scalar_t *c = rgbs + 3 * (size_t)n * n_step;
+    const scalar_t *dl = deltas + 2 * (size_t)n * n_step;
+    acc_t t = to_f(rays_t[index]);
+    acc_t wsum = to_f(weights_sum[index]);
+    acc_t d = to_f(depth[index]);
+    acc_t r = to_f(image[3 * index]), g = to_f(image[3 * index + 1]), b = to_f(image[3 * index + 2]);
+    uint32_t step = 0;
+    while (step < n_step) {
+        const acc_t dt = to_f(dl[2 * step]);
+        if (dt == (acc_t)0) break;
+        const acc_t alpha = (acc_t)1.0f - (acc_t)__expf(-to_f(s[step]) * (float)dt);
+        const acc_t T = (acc_t)1 - wsum;
+        const acc_t w = alpha * T;
+        wsum += w;
+        t += (acc_t)to_f(dl[2 * step + 1]);
+        d = fma(w, t, d);
+        r = fma(w, (acc_t)to_f(c[3 * step]), r);
+        g = fma(w, (acc_t)to_f(c[3 * step + 1]), g);
+        b = fma(w, (acc_t)to_f(c[3 * step + 2]), b);
+        if (T < (acc_t)T_thresh) break;
+        ++step;
+    }
+    if (step < n_step) rays_alive[n] = -1;
+    else rays_t[index] = (scalar_t)t;
+    weights_sum[index] = (scalar_t)wsum;
+    depth[index] = (scalar_t)d;
+    image[3 * index] = (scalar_t)r;
+    image[3 * index + 1] = (scalar_t)g;
+    image[3 * index + 2] = (scalar_t)b;
+}
+
+static bool march_args_ok(const char *what, uint32_t C, uint32_t H, uint32_t max_steps) {
+    if (C < 1 || C > 16 || H < 2 || H > 1024 || max_steps == 0) {
+        set_error("%s: invalid C=%u H=%u max_steps=%u", what, C, H, max_steps);
+        return false;
+    }
+    return true;
+}
+
+}  // namespace rm
+}  // namespace dfhip
+
+using namespace dfhip;
+using namespace dfhip::rm;
+
+// ====================================================================== C ABI
+
+extern "C" int dfhip_near_far_from_aabb(int dtype, const void *rays_o, const void *rays_d,
+                                        const void *aabb, uint32_t N, float min_near,
+                                        void *nears, void *fars, dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    DFHIP_DISPATCH(dtype, "near_far_from_aabb",
+        k_near_far<scalar_t><<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(
+            (const scalar_t *)rays_o, (const scalar_t *)rays_d, (const scalar_t *)aabb, N,
+            min_near, (scalar_t *)nears, (scalar_t *)fars));
+    return check_launch("near_far_from_aabb");
+}
+
+extern "C" int dfhip_sph_from_ray(int dtype, const void *rays_o, const void *rays_d,
+                                  float radius, uint32_t N, void *coords,
+                                  dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    DFHIP_DISPATCH(dtype, "sph_from_ray",
+        k_sph_from_ray<scalar_t><<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(
+            (const scalar_t *)rays_o, (const scalar_t *)rays_d, radius, N,
+            (scalar_t *)coords));
+    return check_launch("sph_from_ray");
+}
+
+extern "C" int dfhip_morton3D(const int32_t *coords, uint32_t N, int32_t *indices,
+                              dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    k_morton3D<<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(coords, N, indices);
+    return check_launch("morton3D");
+}
+
+extern "C" int dfhip_morton3D_invert(const int32_t *indices, uint32_t N, int32_t *coords,
+                                     dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    k_morton3D_invert<<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(indices, N, coords);
+    return check_launch("morton3D_invert");
+}
+
+extern "C" int dfhip_packbits(int dtype, const void *grid, uint32_t N, float density_thresh,
+                              uint8_t *bitfield, dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    if (dtype == DFHIP_F32 && ((uintptr_t)grid & 15) == 0) {
+        k_packbits_f32v<<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(
+            (const float *)grid, N, density_thresh, bitfield);
+        return check_launch("packbits");
+    }
+    DFHIP_DISPATCH(dtype, "packbits",
+        k_packbits<scalar_t><<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(
+            (const scalar_t *)grid, N, density_thresh, bitfield));
+    return check_launch("packbits");
+}
+
+extern "C" uint32_t dfhip_march_rays_train_scratch_ints(uint32_t N) {
+    return ceil_div(N, 64u) > 0 ? ceil_div(N, 64u) : 1u;
+}
+
+extern "C" int dfhip_march_rays_train_count(int dtype, const void *rays_o, const void *rays_d,
+                                            const uint8_t *grid, float bound, float dt_gamma,
+                                            uint32_t max_steps, uint32_t N, uint32_t C,
+                                            uint32_t H, const void *nears, const void *fars,
+                                            int32_t *rays, int32_t *counter,
+                                            const void *noises, int32_t *block_sums,
+                                            dfhip_stream_t stream) {
+    if (!march_args_ok("march_rays_train_count", C, H, max_steps)) return DFHIP_EINVAL;
+    if (N == 0) return DFHIP_OK;
+    const MarchConsts k = make_consts(bound, dt_gamma, max_steps, C, H);
+    DFHIP_DISPATCH(dtype, "march_rays_train_count",
+        k_march_train_count<scalar_t><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+            (const scalar_t *)rays_o, (const scalar_t *)rays_d, grid, k, max_steps, N,
+            (const scalar_t *)nears, (const scalar_t *)fars, rays, counter,
+            (const scalar_t *)noises, block_sums));
+    return check_launch("march_rays_train_count");
+}
+
+extern "C" int dfhip_march_rays_train_emit(int dtype, const void *rays_o, const void *rays_d,
+                                           const uint8_t *grid, float bound, float dt_gamma,
+                                           uint32_t max_steps, uint32_t N, uint32_t C,
+                                           uint32_t H, uint32_t M, const void *nears,
+                                           const void *fars, void *xyzs, void *dirs,
+                                           void *deltas, int32_t *rays, const void *noises,
+                                           const int32_t *block_sums, int zero_tail,
+                                           dfhip_stream_t stream) {
+    if (!march_args_ok("march_rays_train_emit", C, H, max_steps)) return DFHIP_EINVAL;
+    if (N == 0) return DFHIP_OK;
+    const MarchConsts k = make_consts(bound, dt_gamma, max_steps, C, H);
+    DFHIP_DISPATCH(dtype, "march_rays_train_emit",
+        k_march_train_emit<scalar_t><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+            (const scalar_t *)rays_o, (const scalar_t *)rays_d, grid, k, N, M,
+            (const scalar_t *)nears, (const scalar_t *)fars, (scalar_t *)xyzs,
+            (scalar_t *)dirs, (scalar_t *)deltas, rays, (const scalar_t *)noises,
+            block_sums, zero_tail));
+    return check_launch("march_rays_train_emit");
+}
+
+extern "C" int dfhip_march_rays_train(int dtype, const void *rays_o, const void *rays_d,
+                                      const uint8_t *grid, float bound, float dt_gamma,
+                                      uint32_t max_steps, uint32_t N, uint32_t C, uint32_t H,
+                                      uint32_t M, const void *nears, const void *fars,
+                                      void *xyzs, void *dirs, void *deltas, int32_t *rays,
+                                      int32_t *counter, const void *noises,
+                                      dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    int32_t *scratch = nullptr;
+    const size_t bytes = sizeof(int32_t) * dfhip_march_rays_train_scratch_ints(N);
+    if (hipMallocAsync((void **)&scratch, bytes, as_stream(stream)) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("march_rays_train: scratch allocation of %zu bytes failed", bytes);
+        return DFHIP_ENOMEM;
+    }
+    int rc = dfhip_march_rays_train_count(dtype, rays_o, rays_d, grid, bound, dt_gamma,
+                                          max_steps, N, C, H, nears, fars, rays, counter,
+                                          noises, scratch, stream);
+    if (rc == DFHIP_OK)
+        rc = dfhip_march_rays_train_emit(dtype, rays_o, rays_d, grid, bound, dt_gamma,
+                                         max_steps, N, C, H, M, nears, fars, xyzs, dirs,
+                                         deltas, rays, noises, scratch, 0, stream);
+    (void)hipFreeAsync(scratch, as_stream(stream));
+    return rc;
+}
+
+extern "C" int dfhip_composite_rays_train_forward(int dtype, const void *sigmas,
+                                                  const void *rgbs, const void *deltas,
+                                                  const int32_t *rays, uint32_t M, uint32_t N,
+                                                  float T_thresh, void *weights_sum,
+                                                  void *depth, void *image,
+                                                  dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    DFHIP_DISPATCH(dtype, "composite_rays_train_forward",
+        k_composite_train_fwd<scalar_t><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+            (const scalar_t *)sigmas, (const scalar_t *)rgbs, (const scalar_t *)deltas, rays,
+            M, N, T_thresh, (scalar_t *)weights_sum, (scalar_t *)depth, (scalar_t *)image));
+    return check_launch("composite_rays_train_forward");
+}
+
+template <bool DENSE>
+static int composite_bwd_impl(const char *name, int dtype, const void *grad_weights_sum,
+                              const void *grad_image, const void *sigmas, const void *rgbs,
+                              const void *deltas, const int32_t *rays,
+                              const void *weights_sum, const void *image, uint32_t M,
+                              uint32_t N, float T_thresh, void *grad_sigmas,
+                              void *grad_rgbs, dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    DFHIP_DISPATCH(dtype, name,
+        (k_composite_train_bwd<scalar_t, DENSE><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+            (const scalar_t *)grad_weights_sum, (const scalar_t *)grad_image,
+            (const scalar_t *)sigmas, (const scalar_t *)rgbs, (const scalar_t *)deltas, rays,
+            (const scalar_t *)weights_sum, (const scalar_t *)image, M, N, T_thresh,
+            (scalar_t *)grad_sigmas, (scalar_t *)grad_rgbs)));
+    return check_launch(name);
+}
+
+extern "C" int dfhip_composite_rays_train_backward(
+    int dtype, const void *grad_weights_sum, const void *grad_image, const void *sigmas,
+    const void *rgbs, const void *deltas, const int32_t *rays, const void *weights_sum,
+    const void *image, uint32_t M, uint32_t N, float T_thresh, void *grad_sigmas,
+    void *grad_rgbs, dfhip_stream_t stream) {
+    return composite_bwd_impl<false>("composite_rays_train_backward", dtype, grad_weights_sum,
+                                     grad_image, sigmas, rgbs, deltas, rays, weights_sum, image,
+                                     M, N, T_thresh, grad_sigmas, grad_rgbs, stream);
+}
+
+extern "C" int dfhip_composite_rays_train_backward_dense(
+    int dtype, const void *grad_weights_sum, const void *grad_image, const void *sigmas,
+    const void *rgbs, const void *deltas, const int32_t *rays, const void *weights_sum,
+    const void *image, uint32_t M, uint32_t N, float T_thresh, void *grad_sigmas,
+    void *grad_rgbs, dfhip_stream_t stream) {
+    return composite_bwd_impl<true>("composite_rays_train_backward_dense", dtype,
+                                    grad_weights_sum, grad_image, sigmas, rgbs, deltas, rays,
+                                    weights_sum, image, M, N, T_thresh, grad_sigmas, grad_rgbs,
+                                    stream);
+}
+
+extern "C" int dfhip_march_rays(int dtype, uint32_t n_alive, uint32_t n_step,
+                                const int32_t *rays_alive, const void *rays_t,
+                                const void *rays_o, const void *rays_d, float bound,
+                                float dt_gamma, uint32_t max_steps, uint32_t C, uint32_t H,
+                                const uint8_t *grid, const void *nears, const void *fars,
+                                void *xyzs, void *dirs, void *deltas, const void *noises,
+                                dfhip_stream_t stream) {
+    (void)nears;  // read but unused by the reference kernel (raymarching.cu:737)
+    if (!march_args_ok("march_rays", C, H, max_steps)) return DFHIP_EINVAL;
+    if (n_alive == 0 || n_step == 0) return DFHIP_OK;
+    const MarchConsts k = make_consts(bound, dt_gamma, max_steps, C, H);
+    DFHIP_DISPATCH(dtype, "march_rays",
+        k_march_infer<scalar_t><<<ceil_div(n_alive, 64u), 64, 0, as_stream(stream)>>>(
+            n_alive, n_step, rays_alive, (const scalar_t *)rays_t, (const scalar_t *)rays_o,
+            (const scalar_t *)rays_d, k, grid, (const scalar_t *)fars, (scalar_t *)xyzs,
+            (scalar_t *)dirs, (scalar_t *)deltas, (const scalar_t *)noises));
+    return check_launch("march_rays");
+}
+
+extern "C" int dfhip_composite_rays(int dtype, uint32_t n_alive, uint32_t n_step,
+                                    float T_thresh, int32_t *rays_alive, void *rays_t,
+                                    const void *sigmas, const void *rgbs, const void *deltas,
+                                    void *weights_sum, void *depth, void *image,
+                                    dfhip_stream_t stream) {
+    if (n_alive == 0 || n_step == 0) return DFHIP_OK;
+    DFHIP_DISPATCH(dtype, "composite_rays",
+        k_composite_infer<scalar_t><<<ceil_div(n_alive, 64u), 64, 0, as_stream(stream)>>>(
+            n_alive, n_step, T_thresh, rays_alive, (scalar_t *)rays_t,
+            (const scalar_t *)sigmas, (const scalar_t *)rgbs, (const scalar_t *)deltas,
+            (scalar_t *)weights_sum, (scalar_t *)depth, (scalar_t *)image));
+    return check_launch("composite_rays");
+}

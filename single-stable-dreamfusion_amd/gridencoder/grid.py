@@ -1,0 +1,157 @@
+"""Multi-resolution grid encoder (mirror of reference gridencoder/grid.py).
+
+Public surface identical to the reference: `grid_encode` (autograd Function)
+and `GridEncoder(input_dim, num_levels, level_dim, per_level_scale,
+base_resolution, log2_hashmap_size, desired_resolution, gridtype,
+align_corners)` with the same parameter layout (`offsets`, `embeddings`,
+grid.py:91-133) and the same autocast rule (half embeddings when C is even,
+grid.py:38-39).
+
+GPU-side differences (invisible to callers): outputs are produced directly in
+the [B, L*C] layout the caller consumes (no [L, B, C] buffer + permute copy,
+grid.py:42,52,70), and the backward reads the [B, L*C] gradient as is.
+`DFHIP_GRID_GRAD_ACC=float` accumulates the embedding gradient in f32 instead
+of the reference's half2 atomics (same atomic request count, no fp16 rounding
+of partial sums); the default keeps the reference's half accumulation.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.autograd import Function
+from torch.amp import custom_bwd, custom_fwd
+
+import _dfhip
+import _gridencoder as _backend
+
+_gridtype_to_id = {"hash": 0, "tiled": 1}
+
+
+def _grad_acc_dtype(emb_dtype):
+    mode = os.environ.get("DFHIP_GRID_GRAD_ACC", "native").lower()
+    if mode == "float" and emb_dtype == torch.float16:
+        return torch.float32
+    return emb_dtype
+
+
+class _grid_encode(Function):
+    @staticmethod
+    @custom_fwd(device_type="cuda")
+    def forward(ctx, inputs, embeddings, offsets, per_level_scale, base_resolution,
+                calc_grad_inputs=False, gridtype=0, align_corners=False):
+        """inputs [B, D] in [0, 1] (f32), embeddings [sum_l rows_l, C],
+        offsets [L+1] int32 -> [B, L*C] (half under autocast when C is even)."""
+        inputs = inputs.contiguous()
+        B, D = inputs.shape
+        L = offsets.shape[0] - 1
+        C = embeddings.shape[1]
+        S = float(np.log2(per_level_scale))
+        H = int(base_resolution)
+        table = embeddings
+        if torch.is_autocast_enabled("cuda") and C % 2 == 0:
+            table = embeddings.to(torch.half)
+        table = table.contiguous()
+        outputs = torch.empty(B, L * C, device=inputs.device, dtype=table.dtype)
+        dy_dx = (torch.empty(B, L * D * C, device=inputs.device, dtype=table.dtype)
+                 if calc_grad_inputs else None)
+        # algorithmic bytes: inputs + outputs per sample, table once
+        nbytes = B * (4 * D + L * C * table.element_size()) + table.numel() * table.element_size()
+        with _dfhip.timed("grid_encode_forward", nbytes):
+            _backend.grid_encode_forward_blc(inputs, table, offsets, outputs, B, D, C, L, S, H,
+                                             dy_dx, gridtype, align_corners)
+        ctx.save_for_backward(inputs, offsets, dy_dx)
+        ctx.dims = (B, D, C, L, S, H, gridtype, bool(align_corners))
+        ctx.table_meta = (table.shape[0], table.dtype)
+        return outputs
+
+    @staticmethod
+    @custom_bwd(device_type="cuda")
+    def backward(ctx, grad):
+        inputs, offsets, dy_dx = ctx.saved_tensors
+        B, D, C, L, S, H, gridtype, align_corners = ctx.dims
+        rows, table_dtype = ctx.table_meta
+        grad = grad.to(table_dtype).contiguous()  # [B, L*C], no permute
+        grad_embeddings = torch.zeros(rows, C, device=grad.device,
+                                      dtype=_grad_acc_dtype(table_dtype))
+        grad_inputs = None
+        if dy_dx is not None:
+            grad_inputs = torch.empty(B, D, device=grad.device, dtype=table_dtype)
+        # HBM algorithmic bytes: grad + inputs per sample (the 2^D*L*C atomic
+        # adds per sample are L2/atomic-unit traffic, accounted separately)
+        nbytes = B * (4 * D + L * C * grad.element_size())
+        with _dfhip.timed("grid_encode_backward", nbytes):
+            _backend.grid_encode_backward_blc(grad, inputs, offsets, grad_embeddings, B, D, C, L, S,
+                                              H, dy_dx, grad_inputs, gridtype, align_corners)
+        if grad_inputs is not None:
+            grad_inputs = grad_inputs.to(inputs.dtype)
+        return grad_inputs, grad_embeddings, None, None, None, None, None, None
+
+
+grid_encode = _grid_encode.apply
+
+
+def level_offsets(num_levels, level_dim, input_dim, base_resolution, per_level_scale,
+                  log2_hashmap_size, align_corners):
+    """Row offsets of each level's table (reference grid.py:110-124): rows of
+    level l = min(2^log2_hashmap_size, (res_l [+1])^D) rounded up to 8, with
+    res_l = ceil(base_resolution * per_level_scale^l)."""
+    cap = 2 ** log2_hashmap_size
+    starts, total = [], 0
+    for lvl in range(num_levels):
+        res = int(np.ceil(base_resolution * per_level_scale ** lvl))
+        side = res if align_corners else res + 1
+        rows = int(np.ceil(min(cap, side ** input_dim) / 8) * 8)
+        starts.append(total)
+        total += rows
+    starts.append(total)
+    return np.asarray(starts, dtype=np.int32)
+
+
+class GridEncoder(nn.Module):
+    def __init__(self, input_dim=3, num_levels=16, level_dim=2, per_level_scale=2,
+                 base_resolution=16, log2_hashmap_size=19, desired_resolution=None,
+                 gridtype="hash", align_corners=False):
+        super().__init__()
+        if desired_resolution is not None:
+            # finest level hits desired_resolution (grid.py:96-97)
+            per_level_scale = np.exp2(np.log2(desired_resolution / base_resolution) / (num_levels - 1))
+        self.input_dim = input_dim
+        self.num_levels = num_levels
+        self.level_dim = level_dim
+        self.per_level_scale = per_level_scale
+        self.log2_hashmap_size = log2_hashmap_size
+        self.base_resolution = base_resolution
+        self.output_dim = num_levels * level_dim
+        self.gridtype = gridtype
+        self.gridtype_id = _gridtype_to_id[gridtype]
+        self.align_corners = align_corners
+        self.max_params = 2 ** log2_hashmap_size
+
+        offsets = level_offsets(num_levels, level_dim, input_dim, base_resolution,
+                                per_level_scale, log2_hashmap_size, align_corners)
+        self.register_buffer("offsets", torch.from_numpy(offsets))
+        self.n_params = self.offsets[-1] * level_dim
+        self.embeddings = nn.Parameter(torch.empty(int(offsets[-1]), level_dim))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        std = 1e-4
+        self.embeddings.data.uniform_(-std, std)
+
+    def __repr__(self):
+        top = int(round(self.base_resolution * self.per_level_scale ** (self.num_levels - 1)))
+        return (f"GridEncoder: input_dim={self.input_dim} num_levels={self.num_levels} "
+                f"level_dim={self.level_dim} resolution={self.base_resolution} -> {top} "
+                f"per_level_scale={self.per_level_scale:.4f} params={tuple(self.embeddings.shape)} "
+                f"gridtype={self.gridtype} align_corners={self.align_corners}")
+
+    def forward(self, inputs, bound=1):
+        """inputs [..., input_dim] in [-bound, bound] -> [..., num_levels*level_dim]."""
+        x = (inputs + bound) / (2 * bound)
+        lead = list(x.shape[:-1])
+        x = x.view(-1, self.input_dim)
+        out = grid_encode(x, self.embeddings, self.offsets, self.per_level_scale,
+                          self.base_resolution, x.requires_grad, self.gridtype_id,
+                          self.align_corners)
+        return out.view(lead + [self.output_dim])

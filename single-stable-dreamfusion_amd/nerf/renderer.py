@@ -1,0 +1,313 @@
+"""NeRF renderer (behavioural mirror of reference nerf/renderer.py).
+
+`NeRFRenderer(opt)` keeps the reference's buffers (`aabb_train`, `aabb_infer`,
+`density_grid`, `density_bitfield`, `step_counter` — checkpoint keys
+unchanged), attributes (`bound`, `cascade`, `grid_size`, `mean_density`,
+`mean_count`, `local_step`, ...) and methods (`run`, `run_cuda`,
+`update_extra_state`, `render`, `reset_extra_state`), so a field written
+against the reference (e.g. its nerf/network_grid.py) subclasses it unchanged.
+
+The ray-marching ops it calls are the gfx950 kernels behind `raymarching`.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+import raymarching
+from .utils import custom_meshgrid, safe_normalize
+
+
+def sample_pdf(bins, weights, n_samples, det=False):
+    """Inverse-CDF importance sampling (reference renderer.py:15-49).
+    bins [B, T], weights [B, T-1] -> new z values [B, n_samples]."""
+    w = weights + 1e-5
+    pdf = w / w.sum(-1, keepdim=True)
+    cdf = torch.cat([torch.zeros_like(pdf[..., :1]), torch.cumsum(pdf, -1)], -1)
+    if det:
+        u = torch.linspace(0.5 / n_samples, 1.0 - 0.5 / n_samples, n_samples, device=w.device)
+        u = u.expand(list(cdf.shape[:-1]) + [n_samples])
+    else:
+        u = torch.rand(list(cdf.shape[:-1]) + [n_samples], device=w.device)
+    u = u.contiguous()
+    hi_idx = torch.searchsorted(cdf, u, right=True)
+    lo = (hi_idx - 1).clamp(min=0)
+    hi = hi_idx.clamp(max=cdf.shape[-1] - 1)
+    pair = torch.stack([lo, hi], -1)  # [B, n, 2]
+    shape = [pair.shape[0], pair.shape[1], cdf.shape[-1]]
+    cdf_g = torch.gather(cdf.unsqueeze(1).expand(shape), 2, pair)
+    bins_g = torch.gather(bins.unsqueeze(1).expand(shape), 2, pair)
+    span = cdf_g[..., 1] - cdf_g[..., 0]
+    span = torch.where(span < 1e-5, torch.ones_like(span), span)
+    frac = (u - cdf_g[..., 0]) / span
+    return bins_g[..., 0] + frac * (bins_g[..., 1] - bins_g[..., 0])
+
+
+class NeRFRenderer(nn.Module):
+    def __init__(self, opt):
+        super().__init__()
+        self.opt = opt
+        self.bound = opt.bound
+        self.cascade = 1 + math.ceil(math.log2(opt.bound))
+        self.grid_size = 128
+        self.cuda_ray = opt.cuda_ray
+        self.min_near = opt.min_near
+        self.density_thresh = opt.density_thresh
+        self.bg_radius = opt.bg_radius
+
+        b = opt.bound
+        aabb = torch.FloatTensor([-b, -b, -b, b, b, b])
+        self.register_buffer("aabb_train", aabb)
+        self.register_buffer("aabb_infer", aabb.clone())
+
+        if self.cuda_ray:
+            cells = self.grid_size ** 3
+            self.register_buffer("density_grid", torch.zeros([self.cascade, cells]))
+            self.register_buffer("density_bitfield",
+                                 torch.zeros(self.cascade * cells // 8, dtype=torch.uint8))
+            self.mean_density = 0
+            self.iter_density = 0
+            self.register_buffer("step_counter", torch.zeros(16, 2, dtype=torch.int32))
+            self.mean_count = 0
+            self.local_step = 0
+
+    # field interface, implemented by the network subclass
+    def forward(self, x, d):
+        raise NotImplementedError()
+
+    def density(self, x):
+        raise NotImplementedError()
+
+    def color(self, x, d, mask=None, **kwargs):
+        raise NotImplementedError()
+
+    def reset_extra_state(self):
+        if not self.cuda_ray:
+            return
+        self.density_grid.zero_()
+        self.mean_density = 0
+        self.iter_density = 0
+        self.step_counter.zero_()
+        self.mean_count = 0
+        self.local_step = 0
+
+    @torch.no_grad()
+    def export_mesh(self, path, resolution=None, S=128):
+        # renderer.py:121-299 needs mcubes / xatlas / nvdiffrast, none of
+        # which exist on this platform.
+        raise NotImplementedError("export_mesh needs mcubes/xatlas/nvdiffrast (not available)")
+
+    def _bg(self, rays_d, bg_color):
+        if self.bg_radius > 0:
+            return self.background(rays_d.reshape(-1, 3))
+        return 1 if bg_color is None else bg_color
+
+    # ------------------------------------------------------------------ run()
+    def run(self, rays_o, rays_d, num_steps=128, upsample_steps=128, light_d=None,
+            ambient_ratio=1.0, shading="albedo", bg_color=None, perturb=False, **kwargs):
+        """Coarse (uniform) + importance sampled rendering in plain torch
+        (reference renderer.py:301-443).  rays_o, rays_d: [B, N, 3]."""
+        prefix = rays_o.shape[:-1]
+        rays_o = rays_o.contiguous().view(-1, 3)
+        rays_d = rays_d.contiguous().view(-1, 3)
+        N = rays_o.shape[0]
+        device = rays_o.device
+        results = {}
+        aabb = self.aabb_train if self.training else self.aabb_infer
+
+        nears, fars = raymarching.near_far_from_aabb(rays_o, rays_d, aabb, self.min_near)
+        nears = nears.unsqueeze(-1)
+        fars = fars.unsqueeze(-1)
+        if light_d is None:
+            light_d = safe_normalize(rays_o[0] + torch.randn(3, device=device, dtype=torch.float))
+
+        z = torch.linspace(0.0, 1.0, num_steps, device=device).unsqueeze(0).expand((N, num_steps))
+        z = nears + (fars - nears) * z
+        sample_dist = (fars - nears) / num_steps
+        if perturb:
+            z = z + (torch.rand(z.shape, device=device) - 0.5) * sample_dist
+        xyzs = rays_o.unsqueeze(-2) + rays_d.unsqueeze(-2) * z.unsqueeze(-1)
+        xyzs = torch.min(torch.max(xyzs, aabb[:3]), aabb[3:])
+
+        dens = {k: v.view(N, num_steps, -1) for k, v in self.density(xyzs.reshape(-1, 3)).items()}
+
+        if upsample_steps > 0:
+            with torch.no_grad():
+                dz = z[..., 1:] - z[..., :-1]
+                dz = torch.cat([dz, sample_dist * torch.ones_like(dz[..., :1])], dim=-1)
+                alphas = 1 - torch.exp(-dz * dens["sigma"].squeeze(-1))
+                trans = torch.cumprod(torch.cat([torch.ones_like(alphas[..., :1]),
+                                                 1 - alphas + 1e-15], dim=-1), dim=-1)[..., :-1]
+                weights = alphas * trans
+                z_mid = z[..., :-1] + 0.5 * dz[..., :-1]
+                new_z = sample_pdf(z_mid, weights[:, 1:-1], upsample_steps,
+                                   det=not self.training).detach()
+                new_xyzs = rays_o.unsqueeze(-2) + rays_d.unsqueeze(-2) * new_z.unsqueeze(-1)
+                new_xyzs = torch.min(torch.max(new_xyzs, aabb[:3]), aabb[3:])
+            new_dens = {k: v.view(N, upsample_steps, -1)
+                        for k, v in self.density(new_xyzs.reshape(-1, 3)).items()}
+            z, order = torch.sort(torch.cat([z, new_z], dim=1), dim=1)
+            xyzs = torch.cat([xyzs, new_xyzs], dim=1)
+            xyzs = torch.gather(xyzs, 1, order.unsqueeze(-1).expand_as(xyzs))
+            for k in dens:
+                both = torch.cat([dens[k], new_dens[k]], dim=1)
+                dens[k] = torch.gather(both, 1, order.unsqueeze(-1).expand_as(both))
+
+        dz = z[..., 1:] - z[..., :-1]
+        dz = torch.cat([dz, sample_dist * torch.ones_like(dz[..., :1])], dim=-1)
+        alphas = 1 - torch.exp(-dz * dens["sigma"].squeeze(-1))
+        trans = torch.cumprod(torch.cat([torch.ones_like(alphas[..., :1]), 1 - alphas + 1e-15],
+                                        dim=-1), dim=-1)[..., :-1]
+        weights = alphas * trans
+
+        dirs = rays_d.view(-1, 1, 3).expand_as(xyzs)
+        sigmas, rgbs, normals = self(xyzs.reshape(-1, 3), dirs.reshape(-1, 3), light_d,
+                                     ratio=ambient_ratio, shading=shading)
+        rgbs = rgbs.view(N, -1, 3)
+        if normals is not None:
+            normals = normals.view(N, -1, 3)
+            orient = weights.detach() * (normals * dirs).sum(-1).clamp(min=0) ** 2
+            results["loss_orient"] = orient.sum(-1).mean()
+            jitter = self.normal(xyzs + torch.randn_like(xyzs) * 1e-2).view(N, -1, 3)
+            results["loss_smooth"] = (normals - jitter).abs().mean()
+
+        weights_sum = weights.sum(dim=-1)
+        depth = torch.sum(weights * ((z - nears) / (fars - nears)).clamp(0, 1), dim=-1)
+        image = torch.sum(weights.unsqueeze(-1) * rgbs, dim=-2)
+        image = image + (1 - weights_sum).unsqueeze(-1) * self._bg(rays_d, bg_color)
+
+        results["image"] = image.view(*prefix, 3)
+        results["depth"] = depth.view(*prefix)
+        results["weights_sum"] = weights_sum
+        results["mask"] = (nears < fars).reshape(*prefix)
+        return results
+
+    # ------------------------------------------------------------- run_cuda()
+    def run_cuda(self, rays_o, rays_d, dt_gamma=0, light_d=None, ambient_ratio=1.0,
+                 shading="albedo", bg_color=None, perturb=False, force_all_rays=False,
+                 max_steps=1024, T_thresh=1e-4, **kwargs):
+        """Occupancy-grid rendering (reference renderer.py:446-559)."""
+        prefix = rays_o.shape[:-1]
+        rays_o = rays_o.contiguous().view(-1, 3)
+        rays_d = rays_d.contiguous().view(-1, 3)
+        N = rays_o.shape[0]
+        device = rays_o.device
+
+        # the train path passes no min_near -> the op's default 0.2 (renderer.py:458)
+        nears, fars = raymarching.near_far_from_aabb(
+            rays_o, rays_d, self.aabb_train if self.training else self.aabb_infer)
+        if light_d is None:
+            light_d = safe_normalize(rays_o[0] + torch.randn(3, device=device, dtype=torch.float))
+
+        results = {}
+        if self.training:
+            counter = self.step_counter[self.local_step % 16]
+            counter.zero_()
+            self.local_step += 1
+            xyzs, dirs, deltas, rays = raymarching.march_rays_train(
+                rays_o, rays_d, self.bound, self.density_bitfield, self.cascade, self.grid_size,
+                nears, fars, counter, self.mean_count, perturb, 128, force_all_rays, dt_gamma,
+                max_steps)
+            sigmas, rgbs, normals = self(xyzs, dirs, light_d, ratio=ambient_ratio, shading=shading)
+            weights_sum, depth, image = raymarching.composite_rays_train(sigmas, rgbs, deltas, rays,
+                                                                         T_thresh)
+            if normals is not None:
+                w = 1 - torch.exp(-sigmas)
+                results["loss_orient"] = (w.detach() * (normals * dirs).sum(-1).clamp(min=0) ** 2).mean()
+                jitter = self.normal(xyzs + torch.randn_like(xyzs) * 1e-2)
+                results["loss_smooth"] = (normals - jitter).abs().mean()
+        else:
+            weights_sum, depth, image = self._infer_loop(rays_o, rays_d, nears, fars, light_d,
+                                                         ambient_ratio, shading, perturb,
+                                                         dt_gamma, max_steps, T_thresh)
+
+        image = image + (1 - weights_sum).unsqueeze(-1) * self._bg(rays_d, bg_color)
+        results["image"] = image.view(*prefix, 3)
+        # depth relative to the ray's near plane, normalised (renderer.py:547)
+        results["depth"] = (torch.clamp(depth - nears, min=0) / (fars - nears)).view(*prefix)
+        results["weights_sum"] = weights_sum.reshape(*prefix)
+        results["mask"] = (nears < fars).reshape(*prefix)
+        return results
+
+    def _infer_loop(self, rays_o, rays_d, nears, fars, light_d, ambient_ratio, shading, perturb,
+                    dt_gamma, max_steps, T_thresh):
+        """Alive-ray compaction loop of the inference render (renderer.py:496-532)."""
+        N = rays_o.shape[0]
+        device = rays_o.device
+        weights_sum = torch.zeros(N, dtype=torch.float32, device=device)
+        depth = torch.zeros(N, dtype=torch.float32, device=device)
+        image = torch.zeros(N, 3, dtype=torch.float32, device=device)
+        rays_alive = torch.arange(N, dtype=torch.int32, device=device)
+        rays_t = nears.clone()
+        step = 0
+        while step < max_steps:
+            n_alive = rays_alive.shape[0]
+            if n_alive <= 0:
+                break
+            n_step = max(min(N // n_alive, 8), 1)
+            xyzs, dirs, deltas = raymarching.march_rays(
+                n_alive, n_step, rays_alive, rays_t, rays_o, rays_d, self.bound,
+                self.density_bitfield, self.cascade, self.grid_size, nears, fars, 128,
+                perturb if step == 0 else False, dt_gamma, max_steps)
+            sigmas, rgbs, _ = self(xyzs, dirs, light_d, ratio=ambient_ratio, shading=shading)
+            raymarching.composite_rays(n_alive, n_step, rays_alive, rays_t, sigmas, rgbs, deltas,
+                                       weights_sum, depth, image, T_thresh)
+            rays_alive = rays_alive[rays_alive >= 0]
+            step += n_step
+        return weights_sum, depth, image
+
+    # ------------------------------------------------------ occupancy grid
+    @torch.no_grad()
+    def update_extra_state(self, decay=0.95, S=128):
+        """Refresh the density grid (EMA-max of jittered density queries) and
+        re-pack the occupancy bitfield (reference renderer.py:562-615)."""
+        if not self.cuda_ray:
+            return
+        tmp_grid = -torch.ones_like(self.density_grid)
+        dev = self.density_bitfield.device
+        axis = torch.arange(self.grid_size, dtype=torch.int32, device=dev).split(S)
+        for xs in axis:
+            for ys in axis:
+                for zs in axis:
+                    xx, yy, zz = custom_meshgrid(xs, ys, zs)
+                    coords = torch.cat([xx.reshape(-1, 1), yy.reshape(-1, 1), zz.reshape(-1, 1)],
+                                       dim=-1)
+                    indices = raymarching.morton3D(coords).long()
+                    xyzs = 2 * coords.float() / (self.grid_size - 1) - 1
+                    for cas in range(self.cascade):
+                        bound = min(2 ** cas, self.bound)
+                        half = bound / self.grid_size
+                        cas_xyzs = xyzs * (bound - half)
+                        cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * half
+                        sig = self.density(cas_xyzs)["sigma"].reshape(-1).detach()
+                        tmp_grid[cas, indices] = sig.to(tmp_grid.dtype)
+        valid = self.density_grid >= 0
+        self.density_grid[valid] = torch.maximum(self.density_grid[valid] * decay, tmp_grid[valid])
+        self.mean_density = torch.mean(self.density_grid[valid]).item()
+        self.iter_density += 1
+        thresh = min(self.mean_density, self.density_thresh)
+        self.density_bitfield = raymarching.packbits(self.density_grid, thresh,
+                                                     self.density_bitfield)
+        total_step = min(16, self.local_step)
+        if total_step > 0:
+            self.mean_count = int(self.step_counter[:total_step, 0].sum().item() / total_step)
+        self.local_step = 0
+
+    def render(self, rays_o, rays_d, staged=False, max_ray_batch=4096, **kwargs):
+        """rays_o, rays_d: [B, N, 3] -> dict(image [B, N, 3], depth, weights_sum, ...)."""
+        _run = self.run_cuda if self.cuda_ray else self.run
+        B, N = rays_o.shape[:2]
+        device = rays_o.device
+        if not (staged and not self.cuda_ray):
+            return _run(rays_o, rays_d, **kwargs)
+        depth = torch.empty((B, N), device=device)
+        image = torch.empty((B, N, 3), device=device)
+        weights_sum = torch.empty((B, N), device=device)
+        for b in range(B):
+            for head in range(0, N, max_ray_batch):
+                tail = min(head + max_ray_batch, N)
+                r = _run(rays_o[b:b + 1, head:tail], rays_d[b:b + 1, head:tail], **kwargs)
+                depth[b:b + 1, head:tail] = r["depth"]
+                weights_sum[b:b + 1, head:tail] = r["weights_sum"]
+                image[b:b + 1, head:tail] = r["image"]
+        return {"depth": depth, "image": image, "weights_sum": weights_sum}

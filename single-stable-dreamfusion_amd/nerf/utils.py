@@ -1,0 +1,431 @@
+"""Camera rays, seeding and the SDS training loop (behavioural mirror of the
+train-step parts of reference nerf/utils.py: get_rays :42-106, Trainer
+:151-968 restricted to train_step / train_one_epoch / train / checkpoints).
+
+Training-loop differences from the reference, each switchable:
+
+* fused_backward (default on): the SDS latent gradient and the scaled
+  regulariser loss are back-propagated in ONE autograd pass
+  (`torch.autograd.backward([latents, scaler.scale(loss)], [grad, None])`).
+  The reference runs two passes over the whole render graph
+  (`latents.backward(grad, retain_graph=True)` in sd.py:115, then
+  `scaler.scale(loss).backward()` in utils.py:708); the parameter gradients
+  are the same sum, computed with one grid-backward scatter instead of two.
+  The reference quirk that the SDS gradient is not multiplied by the scaler's
+  scale (then divided by it in scaler.step) is kept in both modes.
+* multi-GPU: one process per GPU; the trainable gradients are flattened into
+  one buffer and all-reduced (RCCL over xGMI) before scaler.step, so every
+  rank takes the same GradScaler skip decision.  No DDP wrapper (the
+  reference's DDP path, utils.py:200-202, is dead code).
+* loss.item() is not read every step (it is a host sync); losses are summed on
+  the device and read once per epoch.
+"""
+import glob
+import math
+import os
+import random
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def custom_meshgrid(*args):
+    return torch.meshgrid(*args, indexing="ij")
+
+
+def safe_normalize(x, eps=1e-20):
+    return x / torch.sqrt(torch.clamp(torch.sum(x * x, -1, keepdim=True), min=eps))
+
+
+@torch.autocast("cuda", enabled=False)
+def get_rays(poses, intrinsics, H, W, N=-1, error_map=None):
+    """Pinhole rays through pixel centres (reference utils.py:42-106).
+    poses [B, 4, 4] cam2world, intrinsics (fx, fy, cx, cy) -> rays_o, rays_d [B, H*W, 3]
+    (or N random pixels when N > 0)."""
+    device = poses.device
+    B = poses.shape[0]
+    fx, fy, cx, cy = intrinsics
+    i, j = custom_meshgrid(torch.linspace(0, W - 1, W, device=device),
+                           torch.linspace(0, H - 1, H, device=device))
+    i = i.t().reshape([1, H * W]).expand([B, H * W]) + 0.5
+    j = j.t().reshape([1, H * W]).expand([B, H * W]) + 0.5
+    results = {}
+    if N > 0:
+        N = min(N, H * W)
+        if error_map is None:
+            inds = torch.randint(0, H * W, size=[N], device=device).expand([B, N])
+        else:
+            coarse = torch.multinomial(error_map.to(device), N, replacement=False)
+            ix, iy = coarse // 128, coarse % 128
+            sx, sy = H / 128, W / 128
+            ix = (ix * sx + torch.rand(B, N, device=device) * sx).long().clamp(max=H - 1)
+            iy = (iy * sy + torch.rand(B, N, device=device) * sy).long().clamp(max=W - 1)
+            inds = ix * W + iy
+            results["inds_coarse"] = coarse
+        i = torch.gather(i, -1, inds)
+        j = torch.gather(j, -1, inds)
+        results["inds"] = inds
+    zs = torch.ones_like(i)
+    xs = (i - cx) / fx * zs
+    ys = (j - cy) / fy * zs
+    dirs = safe_normalize(torch.stack((xs, ys, zs), dim=-1))
+    rays_d = dirs @ poses[:, :3, :3].transpose(-1, -2)
+    rays_o = poses[..., :3, 3][..., None, :].expand_as(rays_d)
+    results["rays_o"] = rays_o
+    results["rays_d"] = rays_d
+    return results
+
+
+def seed_everything(seed):
+    random.seed(seed)
+    os.environ["PYTHONHASHSEED"] = str(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed(seed)
+
+
+# ----------------------------------------------------------------------------
+# data-parallel gradient exchange
+# ----------------------------------------------------------------------------
+
+def flat_allreduce_(params, world_size, group=None):
+    """Average the .grad of `params` over all ranks with ONE all-reduce of a
+    flat buffer (7.27 MB for the grid network: one RCCL ring / tree over xGMI
+    instead of one collective per tensor).  Missing grads count as zeros."""
+    params = [p for p in params if p.requires_grad]
+    if world_size <= 1 or not params:
+        return
+    dev = params[0].device
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).float()
+                      for p in params])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.div_(world_size)
+    off = 0
+    for p in params:
+        n = p.numel()
+        chunk = flat[off:off + n].view_as(p).to(p.dtype)
+        if p.grad is None:
+            p.grad = chunk.clone()
+        else:
+            p.grad.copy_(chunk)
+        off += n
+    assert off == flat.numel() and flat.device == dev
+
+
+class _EMA:
+    """Exponential moving average of parameters (stand-in for torch_ema)."""
+
+    def __init__(self, params, decay):
+        self.params = [p for p in params if p.requires_grad]
+        self.decay = decay
+        self.shadow = [p.detach().clone() for p in self.params]
+
+    @torch.no_grad()
+    def update(self):
+        for s, p in zip(self.shadow, self.params):
+            s.mul_(self.decay).add_(p.detach(), alpha=1 - self.decay)
+
+    def state_dict(self):
+        return {"decay": self.decay, "shadow": self.shadow}
+
+    def load_state_dict(self, state):
+        self.decay = state["decay"]
+        for s, v in zip(self.shadow, state["shadow"]):
+            s.copy_(v)
+
+
+class Trainer(object):
+    def __init__(self, name, opt, model, guidance, criterion=None, optimizer=None, ema_decay=None,
+                 lr_scheduler=None, metrics=[], local_rank=0, world_size=1, device=None,
+                 mute=False, fp16=False, eval_interval=1, max_keep_ckpt=2, workspace="workspace",
+                 best_mode="min", use_loss_as_metric=True, report_metric_at_train=False,
+                 use_checkpoint="latest", use_tensorboardX=True, scheduler_update_every_step=False,
+                 fused_backward=True):
+        self.name = name
+        self.opt = opt
+        self.mute = mute
+        self.metrics = metrics
+        self.local_rank = local_rank
+        self.world_size = world_size
+        self.workspace = workspace
+        self.ema_decay = ema_decay
+        self.fp16 = fp16
+        self.best_mode = best_mode
+        self.use_loss_as_metric = use_loss_as_metric
+        self.report_metric_at_train = report_metric_at_train
+        self.max_keep_ckpt = max_keep_ckpt
+        self.eval_interval = eval_interval
+        self.use_checkpoint = use_checkpoint
+        self.use_tensorboardX = use_tensorboardX
+        self.time_stamp = time.strftime("%Y-%m-%d_%H-%M-%S")
+        self.scheduler_update_every_step = scheduler_update_every_step
+        self.fused_backward = fused_backward
+        self.device = device if device is not None else torch.device(
+            f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu")
+
+        model.to(self.device)
+        self.model = model
+        self.guidance = guidance
+        if self.guidance is not None:
+            for p in self.guidance.parameters():
+                p.requires_grad = False
+            self.prepare_text_embeddings()
+        else:
+            self.text_z = None
+        if isinstance(criterion, nn.Module):
+            criterion.to(self.device)
+        self.criterion = criterion
+
+        if optimizer is None:
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=0.001, weight_decay=5e-4)
+        else:
+            self.optimizer = optimizer(self.model)
+        if lr_scheduler is None:
+            self.lr_scheduler = torch.optim.lr_scheduler.LambdaLR(self.optimizer, lambda e: 1)
+        else:
+            self.lr_scheduler = lr_scheduler(self.optimizer)
+        self.ema = _EMA(self.model.parameters(), ema_decay) if ema_decay is not None else None
+        self.scaler = torch.amp.GradScaler("cuda", enabled=self.fp16)
+
+        self.epoch = 0
+        self.global_step = 0
+        self.local_step = 0
+        self.stats = {"loss": [], "valid_loss": [], "results": [], "checkpoints": [],
+                      "best_result": None}
+        if len(metrics) == 0 or self.use_loss_as_metric:
+            self.best_mode = "min"
+        self._pending_sds = None
+
+        self.log_ptr = None
+        if self.workspace is not None:
+            os.makedirs(self.workspace, exist_ok=True)
+            self.log_path = os.path.join(workspace, f"log_{self.name}.txt")
+            self.log_ptr = open(self.log_path, "a+")
+            self.ckpt_path = os.path.join(self.workspace, "checkpoints")
+            self.best_path = f"{self.ckpt_path}/{self.name}.pth"
+            os.makedirs(self.ckpt_path, exist_ok=True)
+        self.log(f"[INFO] Trainer: {self.name} | {self.time_stamp} | {self.device} | "
+                 f"{'fp16' if self.fp16 else 'fp32'} | {self.workspace}")
+        self.log(f"[INFO] #parameters: {sum(p.numel() for p in model.parameters() if p.requires_grad)}")
+        if self.workspace is not None and self.use_checkpoint not in (None, "scratch"):
+            if self.use_checkpoint == "latest":
+                self.load_checkpoint()
+            elif self.use_checkpoint == "latest_model":
+                self.load_checkpoint(model_only=True)
+            elif self.use_checkpoint == "best":
+                self.load_checkpoint(self.best_path if os.path.exists(self.best_path) else None)
+            else:
+                self.load_checkpoint(self.use_checkpoint)
+
+    # ------------------------------------------------------------------ misc
+    def prepare_text_embeddings(self):
+        if self.opt.text is None:
+            self.log("[WARN] text prompt is not provided.")
+            self.text_z = None
+            return
+        if not self.opt.dir_text:
+            self.text_z = self.guidance.get_text_embeds([self.opt.text], [self.opt.negative])
+            return
+        self.text_z = []
+        for d in ["front", "side", "back", "side", "overhead", "bottom"]:
+            negative = f"{self.opt.negative}"
+            if self.opt.suppress_face and d != "front":
+                negative = (negative + ", " if negative else "") + "face"
+            self.text_z.append(self.guidance.get_text_embeds([f"{self.opt.text}, {d} view"],
+                                                             [negative]))
+
+    def __del__(self):
+        if getattr(self, "log_ptr", None):
+            self.log_ptr.close()
+
+    def log(self, *args, **kwargs):
+        if self.local_rank != 0:
+            return
+        if not self.mute:
+            print(*args)
+        if self.log_ptr:
+            print(*args, file=self.log_ptr)
+            self.log_ptr.flush()
+
+    # ------------------------------------------------------------ train step
+    def train_step(self, data):
+        """Render one random view, take the SDS step and assemble the
+        regularisers (reference utils.py:337-404).  Returns
+        (pred_rgb [B,3,H,W], pred_ws [B,1,H,W], loss)."""
+        rays_o, rays_d = data["rays_o"], data["rays_d"]
+        B, N = rays_o.shape[:2]
+        H, W = data["H"], data["W"]
+        if self.global_step < self.opt.albedo_iters:
+            shading, ambient_ratio = "albedo", 1.0
+        else:
+            r = random.random()
+            if r > 0.8:
+                shading, ambient_ratio = "albedo", 1.0
+            elif r > 0.4:
+                shading, ambient_ratio = "textureless", 0.1
+            else:
+                shading, ambient_ratio = "lambertian", 0.1
+        bg_color = torch.rand((B * N, 3), device=rays_o.device)
+        opt_kwargs = dict(vars(self.opt))
+        outputs = self.model.render(rays_o, rays_d, staged=False, perturb=True, bg_color=bg_color,
+                                    ambient_ratio=ambient_ratio, shading=shading,
+                                    force_all_rays=True, **opt_kwargs)
+        pred_rgb = outputs["image"].reshape(B, H, W, 3).permute(0, 3, 1, 2).contiguous()
+        text_z = self.text_z[data["dir"]] if self.opt.dir_text else self.text_z
+        if self.fused_backward and hasattr(self.guidance, "sds_grad"):
+            self._pending_sds = self.guidance.sds_grad(text_z, pred_rgb)
+            loss = 0
+        else:
+            loss = self.guidance.train_step(text_z, pred_rgb)
+        pred_ws = outputs["weights_sum"].reshape(B, 1, H, W)
+        if self.opt.lambda_opacity > 0:
+            loss = loss + self.opt.lambda_opacity * (pred_ws ** 2).mean()
+        if self.opt.lambda_entropy > 0:
+            a = pred_ws.clamp(1e-5, 1 - 1e-5)
+            ent = (-a * torch.log2(a) - (1 - a) * torch.log2(1 - a)).mean()
+            loss = loss + self.opt.lambda_entropy * ent
+        if self.opt.lambda_orient > 0 and "loss_orient" in outputs:
+            loss = loss + self.opt.lambda_orient * outputs["loss_orient"]
+        if self.opt.lambda_smooth > 0 and "loss_smooth" in outputs:
+            loss = loss + self.opt.lambda_smooth * outputs["loss_smooth"]
+        return pred_rgb, pred_ws, loss
+
+    def backward_and_step(self, loss):
+        """Back-propagate (fused or reference two-pass), exchange gradients across
+        ranks and take the (scaled) optimizer step."""
+        scaled = self.scaler.scale(loss) if torch.is_tensor(loss) else None
+        if self._pending_sds is not None:
+            latents, grad = self._pending_sds
+            self._pending_sds = None
+            roots, grads = [latents], [grad]
+            if scaled is not None:
+                roots.append(scaled)
+                grads.append(None)
+            torch.autograd.backward(roots, grads)
+        elif scaled is not None:
+            scaled.backward()
+        if self.world_size > 1:
+            flat_allreduce_(self.model.parameters(), self.world_size)
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+        if self.scheduler_update_every_step:
+            self.lr_scheduler.step()
+
+    def train_iteration(self, data):
+        """One optimisation step of the SDS loop (reference utils.py:693-715
+        minus the per-step loss.item())."""
+        if self.model.cuda_ray and self.global_step % self.opt.update_extra_interval == 0:
+            with torch.autocast("cuda", enabled=self.fp16):
+                self.model.update_extra_state()
+        self.local_step += 1
+        self.global_step += 1
+        self.optimizer.zero_grad()
+        with torch.autocast("cuda", enabled=self.fp16):
+            pred_rgbs, pred_ws, loss = self.train_step(data)
+        self.backward_and_step(loss)
+        return loss
+
+    def train_one_epoch(self, loader):
+        self.log(f"==> Start Training {self.workspace} Epoch {self.epoch}, "
+                 f"lr={self.optimizer.param_groups[0]['lr']:.6f} ...")
+        self.model.train()
+        self.local_step = 0
+        total = torch.zeros((), device=self.device)
+        for data in loader:
+            loss = self.train_iteration(data)
+            if torch.is_tensor(loss):
+                total += loss.detach().float()
+        if self.ema is not None:
+            self.ema.update()
+        average_loss = total.item() / max(1, self.local_step)
+        self.stats["loss"].append(average_loss)
+        if not self.scheduler_update_every_step:
+            self.lr_scheduler.step()
+        self.log(f"==> Finished Epoch {self.epoch}. loss={average_loss:.6f}")
+
+    def train(self, train_loader, valid_loader, max_epochs):
+        assert self.text_z is not None, "Training must provide a text prompt!"
+        start = time.time()
+        for epoch in range(self.epoch + 1, max_epochs + 1):
+            self.epoch = epoch
+            self.train_one_epoch(train_loader)
+            if self.workspace is not None and self.local_rank == 0:
+                self.save_checkpoint(full=True, best=False)
+        self.log(f"[INFO] training takes {(time.time() - start) / 60:.4f} minutes.")
+
+    # ------------------------------------------------------------ eval
+    @torch.no_grad()
+    def test_step(self, data, bg_color=None, perturb=False):
+        rays_o, rays_d = data["rays_o"], data["rays_d"]
+        B, N = rays_o.shape[:2]
+        H, W = data["H"], data["W"]
+        out = self.model.render(rays_o, rays_d, staged=True, perturb=perturb, light_d=None,
+                                ambient_ratio=1.0, shading="albedo", force_all_rays=True,
+                                bg_color=bg_color, **vars(self.opt))
+        return out["image"].reshape(B, H, W, 3), out["depth"].reshape(B, H, W)
+
+    # ------------------------------------------------------------ checkpoints
+    def save_checkpoint(self, name=None, full=False, best=False):
+        """Same checkpoint dict layout as the reference (utils.py:847-902)."""
+        if name is None:
+            name = f"{self.name}_ep{self.epoch:04d}"
+        state = {"epoch": self.epoch, "global_step": self.global_step, "stats": self.stats}
+        if self.model.cuda_ray:
+            state["mean_count"] = self.model.mean_count
+            state["mean_density"] = self.model.mean_density
+        if full:
+            state["optimizer"] = self.optimizer.state_dict()
+            state["lr_scheduler"] = self.lr_scheduler.state_dict()
+            state["scaler"] = self.scaler.state_dict()
+            if self.ema is not None:
+                state["ema"] = self.ema.state_dict()
+        state["model"] = self.model.state_dict()
+        if not best:
+            path = f"{name}.pth"
+            self.stats["checkpoints"].append(path)
+            if len(self.stats["checkpoints"]) > self.max_keep_ckpt:
+                old = os.path.join(self.ckpt_path, self.stats["checkpoints"].pop(0))
+                if os.path.exists(old):
+                    os.remove(old)
+            torch.save(state, os.path.join(self.ckpt_path, path))
+        else:
+            torch.save(state, self.best_path)
+
+    def load_checkpoint(self, checkpoint=None, model_only=False):
+        if checkpoint is None:
+            found = sorted(glob.glob(f"{self.ckpt_path}/{self.name}_ep*.pth"))
+            if not found:
+                self.log("[WARN] No checkpoint found, model randomly initialized.")
+                return
+            checkpoint = found[-1]
+        # our own checkpoints only: tensors + plain containers
+        ckpt = torch.load(checkpoint, map_location=self.device, weights_only=True)
+        if "model" not in ckpt:
+            self.model.load_state_dict(ckpt)
+            return
+        missing, unexpected = self.model.load_state_dict(ckpt["model"], strict=False)
+        if len(missing) > 0:
+            self.log(f"[WARN] missing keys: {missing}")
+        if len(unexpected) > 0:
+            self.log(f"[WARN] unexpected keys: {unexpected}")
+        if self.model.cuda_ray:
+            self.model.mean_count = ckpt.get("mean_count", self.model.mean_count)
+            self.model.mean_density = ckpt.get("mean_density", self.model.mean_density)
+        if model_only:
+            return
+        self.stats = ckpt.get("stats", self.stats)
+        self.epoch = ckpt.get("epoch", 0)
+        self.global_step = ckpt.get("global_step", 0)
+        for key, obj in (("optimizer", self.optimizer), ("lr_scheduler", self.lr_scheduler),
+                         ("scaler", self.scaler)):
+            if key in ckpt:
+                try:
+                    obj.load_state_dict(ckpt[key])
+                except Exception:  # noqa: BLE001 - mismatched groups: keep fresh state
+                    self.log(f"[WARN] failed to load {key}.")
+        if self.ema is not None and "ema" in ckpt:
+            self.ema.load_state_dict(ckpt["ema"])

@@ -1,0 +1,204 @@
+"""GPU parity of the grid / frequency / SH encoders against the CPU oracle.
+
+Bit-exact: grid forward in f32 and in f16 (the reference's per-corner half
+rounding is emulated by the oracle).  Tolerance: grid backward (atomic
+accumulation order is not deterministic; f16 accumulation additionally rounds
+every partial sum, exactly like the reference's half2 atomics), dy_dx / input
+gradients, frequency and SH encoders.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _grid_consts():
+    from gridencoder.grid import level_offsets
+    pls = np.exp2(np.log2(2048 / 16) / 15)
+    offs = level_offsets(16, 2, 3, 16, pls, 16, False)
+    return offs, float(np.log2(pls)), pls
+
+
+def _samples(n, seed, edge=True):
+    r = np.random.default_rng(seed)
+    x = r.random((n, 3), dtype=np.float32)
+    if edge:
+        x[:8] = [[0, 0, 0], [1, 1, 1], [1, 0, 1], [0.5, 1, 0], [1.0000001, 0.5, 0.5],
+                 [-1e-7, 0.2, 0.3], [0.999999, 0.999999, 1e-6], [0.25, 0.5, 0.75]]
+    return x
+
+
+@pytest.mark.parametrize("gridtype", [1, 0])
+@pytest.mark.parametrize("dtype", [np.float32, np.float16])
+def test_grid_forward_bitexact(gpu, gridtype, dtype):
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    emb = (np.random.default_rng(1).random((int(offs[-1]), 2)) * 2 - 1).astype(dtype)
+    x = _samples(20000, 2)
+    out = torch.empty(x.shape[0], 32, dtype=torch.float16 if dtype == np.float16 else torch.float32,
+                      device=gpu)
+    _gridencoder.grid_encode_forward_blc(T(x, gpu), T(emb, gpu), T(offs, gpu), out, x.shape[0], 3,
+                                         2, 16, S, 16, None, gridtype, False)
+    want, _ = oracle.grid_encode_forward(x, emb, offs, S, 16, gridtype=gridtype)
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
+    # reference [L, B, C] layout gives the same values
+    out_lbc = torch.empty(16, x.shape[0], 2, dtype=out.dtype, device=gpu)
+    _gridencoder.grid_encode_forward(T(x, gpu), T(emb, gpu), T(offs, gpu), out_lbc, x.shape[0], 3,
+                                     2, 16, S, 16, None, gridtype, False)
+    assert torch.equal(out_lbc.permute(1, 0, 2).reshape(-1, 32), out)
+
+
+@pytest.mark.parametrize("D,C", [(2, 4), (3, 8), (1, 1), (4, 2), (5, 2)])
+def test_grid_forward_other_shapes(gpu, D, C):
+    import _gridencoder
+    from gridencoder.grid import level_offsets
+    L, H = 6, 4
+    offs = level_offsets(L, C, D, H, 1.5, 12, True)
+    emb = np.random.default_rng(D * 10 + C).normal(size=(int(offs[-1]), C)).astype(np.float32)
+    x = np.random.default_rng(5).random((3000, D), dtype=np.float32)
+    S = float(np.log2(1.5))
+    for gt in (0, 1):
+        out = torch.empty(3000, L * C, device=gpu)
+        _gridencoder.grid_encode_forward_blc(T(x, gpu), T(emb, gpu), T(offs, gpu), out, 3000, D, C,
+                                             L, S, H, None, gt, True)
+        want, _ = oracle.grid_encode_forward(x, emb, offs, S, H, gridtype=gt, align_corners=True)
+        np.testing.assert_array_equal(out.cpu().numpy(), want)
+
+
+def test_grid_dy_dx_and_input_grad(gpu):
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    emb = np.random.default_rng(3).normal(size=(int(offs[-1]), 2)).astype(np.float32)
+    x = _samples(4000, 4)
+    B = x.shape[0]
+    out = torch.empty(B, 32, device=gpu)
+    dy = torch.empty(B, 16 * 3 * 2, device=gpu)
+    _gridencoder.grid_encode_forward_blc(T(x, gpu), T(emb, gpu), T(offs, gpu), out, B, 3, 2, 16, S,
+                                         16, dy, 1, False)
+    want, wdy = oracle.grid_encode_forward(x, emb, offs, S, 16, calc_dy_dx=True)
+    np.testing.assert_array_equal(dy.cpu().numpy(), wdy)
+    g = np.random.default_rng(5).normal(size=(B, 32)).astype(np.float32)
+    gemb = torch.zeros(int(offs[-1]), 2, device=gpu)
+    gin = torch.empty(B, 3, device=gpu)
+    _gridencoder.grid_encode_backward_blc(T(g, gpu), T(x, gpu), T(offs, gpu), gemb, B, 3, 2, 16, S,
+                                          16, dy, gin, 1, False)
+    np.testing.assert_allclose(gin.cpu().numpy(), oracle.grid_input_backward(g, wdy, 3, 2, 16),
+                               rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("acc", ["f32", "f16"])
+def test_grid_backward(gpu, acc):
+    """Embedding gradient vs the exact float64 oracle.  f32 atomics: only the
+    summation order differs.  f16 (reference half2 atomics): each partial sum
+    is rounded to half, so the tolerance scales with the half ulp of the
+    accumulated magnitude."""
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    x = _samples(30000, 6)
+    B = x.shape[0]
+    g = (np.random.default_rng(7).normal(size=(B, 32)) * 0.1).astype(np.float16)
+    want = oracle.grid_encode_backward(g, x, offs, 2, S, 16)
+    gemb = torch.zeros(rows, 2, dtype=torch.float32 if acc == "f32" else torch.float16, device=gpu)
+    _gridencoder.grid_encode_backward_blc(T(g, gpu), T(x, gpu), T(offs, gpu), gemb, B, 3, 2, 16, S,
+                                          16, None, None, 1, False)
+    got = gemb.double().cpu().numpy()
+    scale = np.abs(want).max()
+    if acc == "f32":
+        np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-6 * scale)
+    else:
+        # rows only touched a few times are near exact; the heavily shared
+        # coarse rows carry the half rounding of their running sums
+        err = np.abs(got - want)
+        assert err.max() <= 4e-3 * scale + 1e-3
+        fine = slice(int(offs[9]) * 1, rows)
+        np.testing.assert_allclose(got[fine], want[fine], rtol=2e-2, atol=2e-3 * scale)
+    # reference-form entry point: [L, B, C] grad in the table's dtype
+    gl = torch.zeros_like(gemb)
+    glbc = T(g, gpu).to(gemb.dtype).view(B, 16, 2).permute(1, 0, 2).contiguous()
+    _gridencoder.grid_encode_backward(glbc, T(x, gpu), gemb, T(offs, gpu), gl, B, 3, 2, 16, S, 16,
+                                      None, None, 1, False)
+    err = np.abs(gl.double().cpu().numpy() - want)
+    assert err.max() <= (1e-4 if acc == "f32" else 4e-3) * scale + (0 if acc == "f32" else 1e-3)
+
+
+def test_grid_backward_hash(gpu):
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    x = _samples(5000, 8)
+    g = np.random.default_rng(9).normal(size=(5000, 32)).astype(np.float32)
+    gemb = torch.zeros(int(offs[-1]), 2, device=gpu)
+    _gridencoder.grid_encode_backward_blc(T(g, gpu), T(x, gpu), T(offs, gpu), gemb, 5000, 3, 2, 16,
+                                          S, 16, None, None, 0, False)
+    want = oracle.grid_encode_backward(g, x, offs, 2, S, 16, gridtype=0)
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-4,
+                               atol=1e-5 * np.abs(want).max())
+
+
+def test_grid_encoder_module_autocast(gpu):
+    """GridEncoder under autocast: half table, [B, 32] half output, f32 grad."""
+    from gridencoder import GridEncoder
+    enc = GridEncoder(input_dim=3, num_levels=16, level_dim=2, base_resolution=16,
+                      log2_hashmap_size=16, desired_resolution=2048, gridtype="tiled").to(gpu)
+    with torch.no_grad():
+        enc.embeddings.uniform_(-0.5, 0.5)
+    xw = np.random.default_rng(10).random((8000, 3), dtype=np.float32) * 2 - 1
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = enc(T(xw, gpu), bound=1)
+    assert y.dtype == torch.float16 and y.shape == (8000, 32)
+    offs = enc.offsets.cpu().numpy()
+    S = float(np.log2(enc.per_level_scale))
+    emb16 = enc.embeddings.detach().half().cpu().numpy()
+    xin = ((T(xw, gpu) + 1) / 2).cpu().numpy()
+    want, _ = oracle.grid_encode_forward(xin, emb16, offs, S, 16)
+    np.testing.assert_array_equal(y.detach().cpu().numpy(), want)
+    y.float().pow(2).sum().backward()
+    assert enc.embeddings.grad.dtype == torch.float32
+    wg = oracle.grid_encode_backward((2 * y.detach().float()).half().cpu().numpy(), xin, offs, 2, S, 16)
+    got = enc.embeddings.grad.double().cpu().numpy()
+    assert np.abs(got - wg).max() <= 5e-3 * np.abs(wg).max() + 1e-3
+
+
+# ------------------------------------------------------------------ freq / sh
+
+def test_freq_encoder(gpu):
+    from freqencoder import FreqEncoder
+    enc = FreqEncoder(input_dim=3, degree=6)
+    x = (np.random.default_rng(11).random((20000, 3)) * 2 - 1).astype(np.float32)
+    xt = T(x, gpu).requires_grad_(True)
+    y = enc(xt)
+    want = oracle.freq_encode_forward(x, 6)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), want, rtol=0, atol=2e-6)
+    g = np.random.default_rng(12).normal(size=want.shape).astype(np.float32)
+    (y * T(g, gpu)).sum().backward()
+    gi = oracle.freq_encode_backward(g, y.detach().cpu().numpy(), 3, 6)
+    np.testing.assert_allclose(xt.grad.cpu().numpy(), gi, rtol=1e-5, atol=1e-5)
+
+
+def test_freq_encoder_empty(gpu):
+    from freqencoder import FreqEncoder
+    y = FreqEncoder(3, 6)(torch.zeros(0, 3, device=gpu))
+    assert y.shape == (0, 39)
+
+
+@pytest.mark.parametrize("degree", [1, 4, 8])
+def test_sh_encoder(gpu, degree):
+    from shencoder import SHEncoder
+    enc = SHEncoder(input_dim=3, degree=degree)
+    x = np.random.default_rng(13).normal(size=(5000, 3)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    xt = T(x, gpu).requires_grad_(True)
+    y = enc(xt)
+    want, jac = oracle.sh_encode(x.astype(np.float64), degree)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), want, rtol=1e-5, atol=2e-6)
+    g = np.random.default_rng(14).normal(size=want.shape)
+    (y * T(g.astype(np.float32), gpu)).sum().backward()
+    np.testing.assert_allclose(xt.grad.cpu().numpy(), np.einsum("bk,bdk->bd", g, jac), rtol=1e-4,
+                               atol=1e-4)

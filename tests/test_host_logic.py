@@ -1,0 +1,133 @@
+"""Host-side logic that needs no GPU: parameter layout, cameras, SDS math,
+the data-parallel gradient exchange (gloo, 2 ranks), the SH table."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def test_grid_layout_and_param_count():
+    import main
+    from nerf.network_grid import NeRFNetwork
+    opt = main.parse_opt(["--text", "x", "-O"])
+    torch.manual_seed(0)
+    net = NeRFNetwork(opt)
+    assert net.encoder.embeddings.shape == (903480, 2)
+    assert sum(p.numel() for p in net.parameters()) == 1816247
+    keys = set(net.state_dict())
+    for k in ["aabb_train", "aabb_infer", "density_grid", "density_bitfield", "step_counter",
+              "encoder.embeddings", "encoder.offsets", "sigma_net.net.0.weight",
+              "sigma_net.net.2.bias", "bg_net.net.1.weight"]:
+        assert k in keys, k
+    assert net.density_bitfield.numel() == 128 ** 3 // 8
+    groups = net.get_params(1e-3)
+    assert [g["lr"] for g in groups] == [1e-2, 1e-3, 1e-2, 1e-3]
+
+
+def test_rays_and_poses_shapes():
+    from nerf.provider import rand_poses, circle_poses, get_view_direction
+    from nerf.utils import get_rays
+    torch.manual_seed(0)
+    poses, dirs = rand_poses(1, "cpu", return_dirs=True)
+    assert poses.shape == (1, 4, 4) and dirs.shape == (1,)
+    r = get_rays(poses, np.array([100.0, 100.0, 64.0, 64.0]), 128, 128)
+    assert r["rays_o"].shape == (1, 16384, 3)
+    np.testing.assert_allclose(r["rays_d"].norm(dim=-1).numpy(), 1.0, atol=1e-6)
+    # rotation is orthonormal and the camera looks at the origin
+    R = poses[0, :3, :3]
+    np.testing.assert_allclose((R.T @ R).numpy(), np.eye(3), atol=1e-5)
+    c = poses[0, :3, 3]
+    np.testing.assert_allclose((R[:, 2] @ (-c / c.norm())).item(), 1.0, atol=1e-5)
+    p2, _ = circle_poses("cpu", radius=1.8, theta=60, phi=0)
+    np.testing.assert_allclose(p2[0, :3, 3].norm().item(), 1.8, atol=1e-6)
+    cls = get_view_direction(torch.tensor([0.1, 1.5, 1.5, 3.0]), torch.tensor([0.0, 0.5, 3.5, 0.0]),
+                             np.deg2rad(30), np.deg2rad(60))
+    assert cls.tolist() == [4, 0, 2, 5]
+
+
+def test_sds_math():
+    from nerf.sd import scaled_linear_alphas_cumprod, add_noise, cfg_combine, SyntheticSDS
+    a = scaled_linear_alphas_cumprod()
+    betas = np.linspace(0.00085 ** 0.5, 0.012 ** 0.5, 1000) ** 2
+    np.testing.assert_allclose(a.numpy(), np.cumprod(1 - betas), rtol=1e-5)
+    x, e = torch.randn(1, 4, 8, 8), torch.randn(1, 4, 8, 8)
+    t = torch.tensor([500])
+    np.testing.assert_allclose(add_noise(a, x, e, t).numpy(),
+                               (a[500].sqrt() * x + (1 - a[500]).sqrt() * e).numpy(), rtol=1e-6)
+    u, c = torch.randn(1, 4, 8, 8), torch.randn(1, 4, 8, 8)
+    np.testing.assert_allclose(cfg_combine(torch.cat([u, c]), 100).numpy(),
+                               (u + 100 * (c - u)).numpy(), rtol=1e-5, atol=1e-5)
+    g = SyntheticSDS("cpu")
+    tz = g.get_text_embeds(["a hamburger"], [""])
+    assert tz.shape == (2, 77, 768)
+    assert torch.equal(tz, g.get_text_embeds(["a hamburger"], [""]))  # deterministic
+    img = torch.rand(1, 3, 64, 64, requires_grad=True)
+    torch.manual_seed(3)
+    lat, grad = g.sds_grad(tz, img)
+    assert lat.shape == (1, 4, 64, 64) and grad.shape == lat.shape
+    # train_step == backward of sds_grad's pair
+    torch.manual_seed(3)
+    assert g.train_step(tz, img) == 0
+    g1 = img.grad.clone()
+    img.grad = None
+    torch.manual_seed(3)
+    lat, grad = g.sds_grad(tz, img)
+    lat.backward(grad)
+    assert torch.allclose(img.grad, g1)
+
+
+def _allreduce_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from nerf.utils import flat_allreduce_
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(4, 3)
+    emb = torch.nn.Parameter(torch.zeros(10, 2))
+    params = list(lin.parameters()) + [emb]
+    x = torch.full((2, 4), float(rank + 1))
+    lin(x).sum().backward()
+    emb.grad = torch.full_like(emb, float(rank))
+    flat_allreduce_(params, world)
+    out[rank] = torch.cat([p.grad.reshape(-1) for p in params]).clone()
+    dist.destroy_process_group()
+
+
+def test_flat_allreduce_gloo_two_ranks():
+    port = 29500 + (os.getpid() % 1000)
+    ctx = mp.get_context("spawn")
+    with ctx.Manager() as m:
+        out = m.dict()
+        procs = [ctx.Process(target=_allreduce_worker, args=(r, 2, port, out)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+            assert p.exitcode == 0
+        g0, g1 = out[0], out[1]
+    assert torch.equal(g0, g1)
+    # weight grad of sum(Wx+b) is the column sums of x: mean over ranks of 2*(r+1)
+    np.testing.assert_allclose(g0[:12].numpy(), np.full(12, 3.0))
+    np.testing.assert_allclose(g0[12:15].numpy(), np.full(3, 2.0))
+    np.testing.assert_allclose(g0[15:].numpy(), np.full(20, 0.5))
+
+
+def test_sh_table_matches_oracle():
+    """The generated kernel table (csrc/sh_table.h) equals the oracle's terms."""
+    import re
+    from pathlib import Path
+    import oracle
+    text = (Path(__file__).resolve().parents[1] / "single-stable-dreamfusion_amd" / "csrc" /
+            "sh_table.h").read_text()
+    rows = [list(map(lambda v: float(v.rstrip("f")), r.split(",")))
+            for r in re.findall(r"\{([^{}]*)\},", text)]
+    terms = {(idx, m): q for idx, m, q in oracle._sh_terms(8)}
+    k = 0
+    for l in range(8):
+        for m in range(l + 1):
+            q = terms[(l * l + l + m, m)]
+            np.testing.assert_allclose(rows[k][:len(q)], q, rtol=1e-7)
+            k += 1
