@@ -38,6 +38,14 @@ typedef _Float16 half_t;
 template <typename T> __device__ __forceinline__ float to_f(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f(float v) { return (T)v; }
 
+// Value barrier: stops the backend from fusing an f32 product with the f16
+// conversion that follows it (fptrunc(fmul) -> v_fma_mixlo_f16 rounds ONCE,
+// the reference's c10::Half arithmetic rounds twice: to f32, then to f16).
+__device__ __forceinline__ float f32_rounded(float x) {
+    asm("" : "+v"(x));
+    return x;
+}
+
 // Dispatch a templated launcher over the storage dtype (the reference's
 // AT_DISPATCH_FLOATING_TYPES_AND_HALF).
 #define DFHIP_DISPATCH(dtype, NAME, ...)                                        \

@@ -115,7 +115,7 @@ __device__ __forceinline__ void acc_corner(double &r, float w, double g) {
 }
 __device__ __forceinline__ void acc_corner(half_t &r, float w, half_t g) {
     // c10::Half: Half += float  ==>  Half(float(r) + float(Half(w * float(g))))
-    const half_t p = (half_t)(w * (float)g);
+    const half_t p = (half_t)f32_rounded(w * (float)g);
     r = (half_t)((float)r + (float)p);
 }
 
@@ -253,8 +253,8 @@ __device__ __forceinline__ void row_atomic_add(half_t *dst, const float v[C]) {
 #pragma unroll
     for (uint32_t ch = 0; ch < C; ch += 2) {
         half2_t p;
-        p.x = (half_t)v[ch];
-        p.y = (half_t)v[ch + 1];
+        p.x = (half_t)f32_rounded(v[ch]);
+        p.y = (half_t)f32_rounded(v[ch + 1]);
         typedef __attribute__((address_space(1))) half2_t global_half2_t;
         __builtin_amdgcn_global_atomic_fadd_v2f16((global_half2_t *)(dst + ch), p);
     }
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void k_grid_input_bwd(const scalar_t *__restri
                                    : grad[(size_t)l * B * C + (size_t)b * C + ch];
             const scalar_t m = j[l * D * C + d * C + ch];
             if constexpr (sizeof(scalar_t) == 2) {
-                const half_t p = (half_t)((float)a * (float)m);
+                const half_t p = (half_t)f32_rounded((float)a * (float)m);
                 r = (half_t)((float)r + (float)p);
             } else {
                 r = fma(a, m, r);

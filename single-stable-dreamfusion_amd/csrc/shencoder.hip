@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void k_sh_bwd(const scalar_t *__restrict__ gra
     scalar_t r = grad_inputs[t];
     for (uint32_t k = 0; k < C2; ++k) {
         if constexpr (sizeof(scalar_t) == 2) {
-            const half_t p = (half_t)((float)g[k] * (float)j[k]);
+            const half_t p = (half_t)f32_rounded((float)g[k] * (float)j[k]);
             r = (half_t)((float)r + (float)p);
         } else {
             r = fma(g[k], j[k], r);
