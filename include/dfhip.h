@@ -220,6 +220,25 @@ int dfhip_grid_encode_backward_blc(int grad_dtype, int acc_dtype, const void *gr
                                    uint32_t gridtype, int align_corners,
                                    dfhip_stream_t stream);
 
+/* Sliced embedding backward (native, no global atomics): the table's rows are
+ * cut into LDS-sized slices; workgroup (slice, part) accumulates the corner
+ * contributions of its part of the samples that land in its slice with LDS
+ * atomics, writes the slice to partial[part], and a second pass sums the
+ * parts in a fixed order.  grad: [L, B, C] (the reference's backward layout,
+ * gridencoder.cu:404) of grad_dtype (F32/F16).  grad_embeddings
+ * [total_rows, C] of out_dtype (F32/F16) is overwritten (accumulate == 0) or
+ * added into.  partial: dfhip_grid_backward_partial_floats(total_rows, C,
+ * parts) floats of caller scratch; parts >= 1 (default_parts() fills the CUs).
+ * Replaces gridencoder.cu:226-313 on the native path. */
+uint32_t dfhip_grid_backward_default_parts(uint32_t total_rows, uint32_t C);
+uint64_t dfhip_grid_backward_partial_floats(uint32_t total_rows, uint32_t C, uint32_t parts);
+int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, const void *grad,
+                                      const float *inputs, const int32_t *offsets,
+                                      void *grad_embeddings, uint32_t total_rows, uint32_t B,
+                                      uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                                      uint32_t gridtype, int align_corners, float *partial,
+                                      uint32_t parts, int accumulate, dfhip_stream_t stream);
+
 /* ---------------------------------------------------------------- freqencoder
  * Reference: freqencoder/src/freqencoder.h:6-9 (f32 only, freqencoder.cu:109). */
 int dfhip_freq_encode_forward(const float *inputs, uint32_t B, uint32_t D,

@@ -54,6 +54,8 @@ _SIGS = {
                                    _u32, _vp, _vp, _u32, _i32, _vp],
     "dfhip_grid_encode_backward_blc": [_i32, _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
                                        _f32, _u32, _vp, _vp, _u32, _i32, _vp],
+    "dfhip_grid_encode_backward_sliced": [_i32, _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
+                                          _u32, _f32, _u32, _u32, _i32, _vp, _u32, _i32, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],
@@ -77,6 +79,10 @@ def load() -> ctypes.CDLL:
     lib.dfhip_abi_version.restype = ctypes.c_int
     lib.dfhip_march_rays_train_scratch_ints.restype = _u32
     lib.dfhip_march_rays_train_scratch_ints.argtypes = [_u32]
+    lib.dfhip_grid_backward_default_parts.restype = _u32
+    lib.dfhip_grid_backward_default_parts.argtypes = [_u32, _u32]
+    lib.dfhip_grid_backward_partial_floats.restype = ctypes.c_uint64
+    lib.dfhip_grid_backward_partial_floats.argtypes = [_u32, _u32, _u32]
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -87,6 +93,7 @@ def load() -> ctypes.CDLL:
 
 def exported_symbols() -> list[str]:
     return ["dfhip_abi_version", "dfhip_last_error", "dfhip_march_rays_train_scratch_ints",
+            "dfhip_grid_backward_default_parts", "dfhip_grid_backward_partial_floats",
             *_SIGS.keys()]
 
 

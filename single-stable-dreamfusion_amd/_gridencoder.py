@@ -52,3 +52,26 @@ def grid_encode_backward_blc(grad, inputs, offsets, grad_embeddings, B, D, C, L,
          _d.dtype_code(grad_embeddings, "grad_embeddings"), ptr(grad), ptr(inputs), ptr(offsets),
          ptr(grad_embeddings), B, D, C, L, S, H, ptr(dy_dx), ptr(grad_inputs), gridtype,
          int(bool(align_corners)), stream())
+
+
+# ---- native sliced backward (LDS-privatised, no global atomics; see dfhip.h)
+
+def grid_backward_default_parts(total_rows, C):
+    return int(_d.load().dfhip_grid_backward_default_parts(total_rows, C))
+
+
+def grid_backward_partial_floats(total_rows, C, parts):
+    return int(_d.load().dfhip_grid_backward_partial_floats(total_rows, C, parts))
+
+
+def grid_encode_backward_sliced(grad_lbc, inputs, offsets, grad_embeddings, total_rows, B, D, C, L,
+                                S, H, gridtype, align_corners, partial, parts, accumulate=False):
+    checked(grad_lbc, "grad")
+    checked(inputs, "inputs")
+    checked(offsets, "offsets", "int")
+    checked(grad_embeddings, "grad_embeddings")
+    checked(partial, "partial")
+    call("dfhip_grid_encode_backward_sliced", _d.dtype_code(grad_lbc, "grad"),
+         _d.dtype_code(grad_embeddings, "grad_embeddings"), ptr(grad_lbc), ptr(inputs),
+         ptr(offsets), ptr(grad_embeddings), total_rows, B, D, C, L, S, H, gridtype,
+         int(bool(align_corners)), ptr(partial), parts, int(bool(accumulate)), stream())

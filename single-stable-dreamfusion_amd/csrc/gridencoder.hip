@@ -326,6 +326,268 @@ __global__ __launch_bounds__(256) void k_grid_bwd(const grad_t *__restrict__ gra
     }
 }
 
+// ------------------------------------------------------------ backward, sliced
+//
+// gridencoder.cu:226-313 restructured for gfx950.  The reference scatters
+// 2^D * L * C / 2 half2 atomics per sample straight to HBM: at the coarse
+// levels dozens of lanes of one wave hit the same row (serialised at the
+// memory-side atomic unit) and at the fine levels every lane hits its own
+// 64-B line, so the kernel runs at ~1 % of the chip's atomic rate.
+//
+// Owner-computes instead: the table's rows are cut into slices that fit in
+// one CU's 160 KiB LDS.  Workgroup (slice s, part p) walks the samples of
+// part p for every level overlapping slice s, and accumulates the corner
+// contributions that land in s with LDS float atomics (ds_add_f32).  The
+// slice is then written out with plain coalesced stores into partial[p]; a
+// second pass sums the P partials per row (fixed order) into the gradient.
+// No global atomics, HBM traffic = inputs + grads read once per slice of
+// their level + 2 * P * table bytes.
+// Flush the accumulated corner contributions of one cell into the LDS slice.
+template <uint32_t D, uint32_t C>
+__device__ __forceinline__ void flush_cell(float *acc, uint32_t r0, uint32_t r1,
+                                           const LevelCtx &c, uint32_t lead,
+                                           const uint32_t cell[D], const float (&cw)[1u << D][C]) {
+#pragma unroll
+    for (uint32_t k = 0; k < (1u << D); ++k) {
+        if (k >> lead) continue;
+        uint32_t p[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) p[d] = cell[d] + ((d < lead && (k & (1u << d))) ? 1u : 0u);
+        const uint32_t row = c.base + row_index<D>(c, p);
+        if (row >= r0 && row < r1) {
+            float *dst = acc + (row - r0) * C;
+#pragma unroll
+            for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch, cw[k][ch]);
+        }
+    }
+}
+
+constexpr uint32_t kRunLen = 8;  // samples walked sequentially per thread and level
+
+// Load n <= K consecutive items of W 32-bit words each into registers, as
+// 16-byte vectors when the run is full and aligned.
+template <uint32_t K, uint32_t W>
+__device__ __forceinline__ void load_run(const uint32_t *__restrict__ src, uint32_t n, bool vec,
+                                         uint32_t (&dst)[K * W]) {
+    if (vec && n == K) {
+        static_assert((K * W) % 4 == 0, "run must be a whole number of 16-B vectors");
+        const uint4 *v = reinterpret_cast<const uint4 *>(src);
+#pragma unroll
+        for (uint32_t i = 0; i < K * W / 4; ++i) {
+            const uint4 q = v[i];
+            dst[4 * i] = q.x; dst[4 * i + 1] = q.y; dst[4 * i + 2] = q.z; dst[4 * i + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < K * W; ++i) dst[i] = (i < n * W) ? src[i] : 0u;
+    }
+}
+
+// Generic shapes: one sample per lane, no run merging (lanes of a wave read
+// consecutive samples, coalesced).
+template <typename grad_t, uint32_t D, uint32_t C>
+__global__ __launch_bounds__(1024) void k_grid_bwd_sliced_simple(
+    const grad_t *__restrict__ grad, const float *__restrict__ inputs,
+    const int32_t *__restrict__ offsets, float *__restrict__ partial, uint32_t B, uint32_t L,
+    Levels lv, uint32_t gridtype, int align_corners, uint32_t rows_per_slice,
+    uint32_t total_rows, int vec_ok) {
+    (void)vec_ok;
+    extern __shared__ float acc[];
+    const uint32_t r0 = blockIdx.x * rows_per_slice;
+    const uint32_t r1 = min(r0 + rows_per_slice, total_rows);
+    const uint32_t n = (r1 - r0) * C;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0f;
+    __syncthreads();
+    const bool align = align_corners != 0;
+    const uint32_t chunk = ceil_div(B, gridDim.y);
+    const uint32_t b0 = blockIdx.y * chunk;
+    const uint32_t b1 = min(B, b0 + chunk);
+    for (uint32_t l = 0; l < L; ++l) {
+        const LevelCtx c = level_ctx<D>(offsets, lv, l, gridtype, align);
+        if (c.base >= r1 || c.base + c.hsize <= r0) continue;
+        const grad_t *gl = grad + (size_t)l * B * C;
+        const uint32_t lead = (!c.hashed) ? c.used : D;
+        for (uint32_t b = b0 + threadIdx.x; b < b1; b += blockDim.x) {
+            float x[D];
+            bool oob = false;
+#pragma unroll
+            for (uint32_t d = 0; d < D; ++d) {
+                x[d] = inputs[(size_t)b * D + d];
+                oob |= (x[d] < 0.0f) || (x[d] > 1.0f);
+            }
+            if (oob) continue;
+            float frac[D], cw[1u << D][C], g[C];
+            uint32_t cell[D];
+#pragma unroll
+            for (uint32_t d = 0; d < D; ++d) {
+                const float p = fmaf(x[d], c.scale, align ? 0.0f : 0.5f);
+                cell[d] = (uint32_t)floorf(p);
+                frac[d] = p - (float)cell[d];
+            }
+#pragma unroll
+            for (uint32_t ch = 0; ch < C; ++ch) g[ch] = (float)gl[(size_t)b * C + ch];
+            float tw = 1.0f;
+#pragma unroll
+            for (uint32_t d = 0; d < D; ++d)
+                if (d >= lead) tw *= (1.0f - frac[d]) + frac[d];
+#pragma unroll
+            for (uint32_t k = 0; k < (1u << D); ++k) {
+                float w = tw;
+#pragma unroll
+                for (uint32_t d = 0; d < D; ++d)
+                    if (d < lead) w *= (k & (1u << d)) ? frac[d] : 1.0f - frac[d];
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch) cw[k][ch] = w * g[ch];
+            }
+            flush_cell<D, C>(acc, r0, r1, c, lead, cell, cw);
+        }
+    }
+    __syncthreads();
+    float *out = partial + ((size_t)blockIdx.y * total_rows + r0) * C;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = acc[i];
+}
+
+// Runs of K consecutive samples per lane (the march emits each ray's samples
+// contiguously): a run is loaded with 16-B vector loads into registers and
+// walked in order; contributions to the same cell are summed in registers
+// and flushed to LDS once per cell change.
+template <typename grad_t, uint32_t D, uint32_t C, uint32_t K>
+__global__ __launch_bounds__(1024) void k_grid_bwd_sliced(
+    const grad_t *__restrict__ grad,  // [L, B, C] (reference layout)
+    const float *__restrict__ inputs, const int32_t *__restrict__ offsets,
+    float *__restrict__ partial,      // [P, total_rows, C]
+    uint32_t B, uint32_t L, Levels lv, uint32_t gridtype, int align_corners,
+    uint32_t rows_per_slice, uint32_t total_rows, int vec_ok) {
+    constexpr uint32_t GW = (C * sizeof(grad_t) + 3) / 4;  // 32-bit words of one sample's grad
+    constexpr bool GPACK = (C * sizeof(grad_t)) % 4 == 0;  // grads tile 32-bit words
+    extern __shared__ float acc[];
+    const uint32_t r0 = blockIdx.x * rows_per_slice;
+    const uint32_t r1 = min(r0 + rows_per_slice, total_rows);
+    const uint32_t n = (r1 - r0) * C;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0f;
+    __syncthreads();
+    const bool align = align_corners != 0;
+    // parts split the samples in whole runs, so every run starts 16-B aligned
+    const uint32_t chunk = ceil_div(ceil_div(B, gridDim.y), K) * K;
+    const uint32_t b0 = blockIdx.y * chunk;
+    const uint32_t b1 = min(B, b0 + chunk);
+    const uint32_t runs = b1 > b0 ? ceil_div(b1 - b0, K) : 0u;
+    // Interleave runs over lanes: neighbouring lanes walk runs blockDim/64
+    // apart, so one LDS atomic instruction rarely has two lanes on one row.
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t waves = blockDim.x >> 6;
+    const uint32_t my_run0 = lane * waves + wave;
+    for (uint32_t l = 0; l < L; ++l) {
+        const LevelCtx c = level_ctx<D>(offsets, lv, l, gridtype, align);
+        if (c.base >= r1 || c.base + c.hsize <= r0) continue;  // level not in this slice
+        const grad_t *gl = grad + (size_t)l * B * C;
+        const uint32_t lead = (!c.hashed) ? c.used : D;
+        for (uint32_t run = my_run0; run < runs; run += blockDim.x) {
+            const uint32_t s0 = b0 + run * K;
+            const uint32_t cnt = min(b1 - s0, K);
+            // the whole run's inputs and grads in registers, vector loads
+            uint32_t xw[K * D];
+            load_run<K, D>(reinterpret_cast<const uint32_t *>(inputs + (size_t)s0 * D), cnt,
+                           vec_ok != 0, xw);
+            grad_t gv[K * C];
+            if constexpr (GPACK) {
+                uint32_t gw[K * GW];
+                load_run<K, GW>(reinterpret_cast<const uint32_t *>(gl + (size_t)s0 * C), cnt,
+                                vec_ok != 0, gw);
+                __builtin_memcpy(gv, gw, sizeof(gv));
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < K * C; ++i)
+                    gv[i] = (i < cnt * C) ? gl[(size_t)s0 * C + i] : (grad_t)0.0f;
+            }
+            float cw[1u << D][C];
+            uint32_t cur[D];
+            bool have = false;
+#pragma unroll
+            for (uint32_t i = 0; i < K; ++i) {
+                // guard, not break: a break keeps the loop rolled and forces
+                // the run's register arrays into scratch
+                if (i < cnt) {
+                float x[D];
+                bool oob = false;
+#pragma unroll
+                for (uint32_t d = 0; d < D; ++d) {
+                    x[d] = __uint_as_float(xw[i * D + d]);
+                    oob |= (x[d] < 0.0f) || (x[d] > 1.0f);
+                }
+                if (!oob) {  // else grads stay zero (gridencoder.cu:253-258)
+                float frac[D];
+                uint32_t cell[D];
+#pragma unroll
+                for (uint32_t d = 0; d < D; ++d) {
+                    const float p = fmaf(x[d], c.scale, align ? 0.0f : 0.5f);
+                    cell[d] = (uint32_t)floorf(p);
+                    frac[d] = p - (float)cell[d];
+                }
+                // same rows as the run so far? (only the dims the index uses)
+                bool same = have;
+#pragma unroll
+                for (uint32_t d = 0; d < D; ++d)
+                    if (d < lead) same = same && (cell[d] == cur[d]);
+                if (!same) {
+                    if (have) flush_cell<D, C>(acc, r0, r1, c, lead, cur, cw);
+#pragma unroll
+                    for (uint32_t k = 0; k < (1u << D); ++k)
+#pragma unroll
+                        for (uint32_t ch = 0; ch < C; ++ch) cw[k][ch] = 0.0f;
+#pragma unroll
+                    for (uint32_t d = 0; d < D; ++d) cur[d] = cell[d];
+                    have = true;
+                }
+                float g[C];
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch) g[ch] = (float)gv[i * C + ch];
+                float tw = 1.0f;
+#pragma unroll
+                for (uint32_t d = 0; d < D; ++d)
+                    if (d >= lead) tw *= (1.0f - frac[d]) + frac[d];
+#pragma unroll
+                for (uint32_t k = 0; k < (1u << D); ++k) {
+                    if (k >> lead) continue;
+                    float w = tw;
+#pragma unroll
+                    for (uint32_t d = 0; d < D; ++d)
+                        if (d < lead) w *= (k & (1u << d)) ? frac[d] : 1.0f - frac[d];
+#pragma unroll
+                    for (uint32_t ch = 0; ch < C; ++ch) cw[k][ch] = fmaf(w, g[ch], cw[k][ch]);
+                }
+                }  // !oob
+                }  // i < cnt
+            }
+            if (have) flush_cell<D, C>(acc, r0, r1, c, lead, cur, cw);
+        }
+    }
+    __syncthreads();
+    float *out = partial + ((size_t)blockIdx.y * total_rows + r0) * C;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = acc[i];
+}
+
+// Sum the P partial tables (fixed order) into the gradient: overwrite, or add
+// into an existing buffer (accumulate != 0, the reference's zero-filled +=).
+template <typename out_t>
+__global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ partial,
+                                                      uint32_t P, uint64_t n,
+                                                      out_t *__restrict__ out, int accumulate) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        float s = accumulate ? (float)out[i] : 0.0f;
+        for (uint32_t p = 0; p < P; ++p) s += partial[(uint64_t)p * n + i];
+        out[i] = (out_t)s;
+    }
+}
+
+constexpr uint32_t kSliceLdsBytes = 160 * 1024;
+
+static uint32_t slice_rows(uint32_t C) {
+    // rows of C f32 accumulators that fit the CU's LDS, multiple of 256
+    return (kSliceLdsBytes / (4u * C)) & ~255u;
+}
+
 // gridencoder.cu:316-342.  BLC: grad in [B, L*C] (native) else [L, B, C].
 template <typename scalar_t, uint32_t D, uint32_t C, bool BLC>
 __global__ __launch_bounds__(256) void k_grid_input_bwd(const scalar_t *__restrict__ grad,
@@ -428,6 +690,73 @@ static void launch_input_bwd(uint32_t D, uint32_t C, hipStream_t s, const scalar
     case 5: DFHIP_IB(5) break;
     }
 #undef DFHIP_IB
+}
+
+template <typename grad_t, uint32_t D, uint32_t C>
+static void launch_sliced_dc(hipStream_t s, dim3 g, size_t lds, const grad_t *grad,
+                             const float *in, const int32_t *off, float *partial, uint32_t B,
+                             uint32_t L, const Levels &lv, uint32_t gt, int ac, uint32_t rows,
+                             uint32_t total_rows) {
+    // the run-merging kernel for the NeRF grid shape (D=3, C=2), the simple
+    // one otherwise
+    void (*kern)(const grad_t *, const float *, const int32_t *, float *, uint32_t, uint32_t,
+                 Levels, uint32_t, int, uint32_t, uint32_t, int);
+    if constexpr (D == 3 && C == 2)
+        kern = k_grid_bwd_sliced<grad_t, D, C, kRunLen>;
+    else
+        kern = k_grid_bwd_sliced_simple<grad_t, D, C>;
+    static bool attr_set = false;  // idempotent; racing first calls set the same value
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void *)kern,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kSliceLdsBytes);
+        attr_set = true;
+    }
+    // 16-B vector loads of whole runs: bases aligned and every level's grad
+    // plane a multiple of 16 B
+    const int vec_ok = (((uintptr_t)grad | (uintptr_t)in) & 15) == 0 &&
+                       ((uint64_t)B * C * sizeof(grad_t)) % 16 == 0;
+    kern<<<g, 1024, lds, s>>>(grad, in, off, partial, B, L, lv, gt, ac, rows, total_rows, vec_ok);
+}
+
+template <typename grad_t>
+static void launch_sliced(uint32_t D, uint32_t C, hipStream_t s, dim3 g, size_t lds,
+                          const grad_t *grad, const float *in, const int32_t *off,
+                          float *partial, uint32_t B, uint32_t L, const Levels &lv, uint32_t gt,
+                          int ac, uint32_t rows, uint32_t total_rows) {
+#define DFHIP_SL(DD, CC)                                                                    \
+    launch_sliced_dc<grad_t, DD, CC>(s, g, lds, grad, in, off, partial, B, L, lv, gt, ac, rows, \
+                                     total_rows)
+#define DFHIP_SL_C(DD)                       \
+    switch (C) {                             \
+    case 1: DFHIP_SL(DD, 1); break;          \
+    case 2: DFHIP_SL(DD, 2); break;          \
+    case 4: DFHIP_SL(DD, 4); break;          \
+    case 8: DFHIP_SL(DD, 8); break;          \
+    }
+    switch (D) {
+    case 1: DFHIP_SL_C(1) break;
+    case 2: DFHIP_SL_C(2) break;
+    case 3: DFHIP_SL_C(3) break;
+    case 4: DFHIP_SL_C(4) break;
+    case 5: DFHIP_SL_C(5) break;
+    }
+#undef DFHIP_SL_C
+#undef DFHIP_SL
+}
+
+static uint32_t device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            v > 0)
+            cus = v;
+        else
+            cus = 256;
+    }
+    return (uint32_t)cus;
 }
 
 static bool check_dc(const char *what, uint32_t D, uint32_t C, uint32_t L) {
@@ -563,4 +892,65 @@ extern "C" int dfhip_grid_encode_backward_blc(int grad_dtype, int acc_dtype, con
         (launch_input_bwd<scalar_t, true>)(D, C, as_stream(stream), (const scalar_t *)grad,
                                            (const scalar_t *)dy_dx, (scalar_t *)grad_inputs, B, L));
     return check_launch("grid_encode_backward_blc(inputs)");
+}
+
+extern "C" uint32_t dfhip_grid_backward_default_parts(uint32_t total_rows, uint32_t C) {
+    if (C == 0 || total_rows == 0) return 1;
+    const uint32_t slices = ceil_div(total_rows, slice_rows(C));
+    const uint32_t p = device_cus() / slices;
+    return p < 1 ? 1 : (p > 64 ? 64 : p);
+}
+
+extern "C" uint64_t dfhip_grid_backward_partial_floats(uint32_t total_rows, uint32_t C,
+                                                       uint32_t parts) {
+    return (uint64_t)total_rows * C * (parts ? parts : 1);
+}
+
+extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, const void *grad,
+                                                 const float *inputs, const int32_t *offsets,
+                                                 void *grad_embeddings, uint32_t total_rows,
+                                                 uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                                 float S, uint32_t H, uint32_t gridtype,
+                                                 int align_corners, float *partial,
+                                                 uint32_t parts, int accumulate,
+                                                 dfhip_stream_t stream) {
+    const char *name = "grid_encode_backward_sliced";
+    if (!check_dc(name, D, C, L)) return DFHIP_EINVAL;
+    if (parts == 0 || partial == nullptr) {
+        set_error("%s: needs parts >= 1 and a partial buffer", name);
+        return DFHIP_EINVAL;
+    }
+    if (out_dtype != DFHIP_F32 && out_dtype != DFHIP_F16) {
+        set_error("%s: output dtype must be f32 or f16", name);
+        return DFHIP_EDTYPE;
+    }
+    if (total_rows == 0) return DFHIP_OK;
+    hipStream_t s = as_stream(stream);
+    const uint64_t n = (uint64_t)total_rows * C;
+    if (B > 0 && L > 0) {
+        const Levels lv = make_levels(L, S, H);
+        const uint32_t rows = slice_rows(C);
+        const dim3 g(ceil_div(total_rows, rows), parts);
+        const size_t lds = (size_t)rows * C * sizeof(float);
+        switch (grad_dtype) {
+        case DFHIP_F32: launch_sliced<float>(D, C, s, g, lds, (const float *)grad, inputs, offsets,
+                                             partial, B, L, lv, gridtype, align_corners, rows,
+                                             total_rows); break;
+        case DFHIP_F16: launch_sliced<half_t>(D, C, s, g, lds, (const half_t *)grad, inputs,
+                                              offsets, partial, B, L, lv, gridtype, align_corners,
+                                              rows, total_rows); break;
+        default: set_error("%s: unsupported grad dtype %d", name, grad_dtype); return DFHIP_EDTYPE;
+        }
+    } else {
+        (void)hipMemsetAsync(partial, 0, n * parts * sizeof(float), s);
+    }
+    const uint64_t want_blocks = ceil_div<uint64_t>(n, 256);
+    const uint32_t blocks = (uint32_t)(want_blocks < 4096 ? want_blocks : 4096);
+    if (out_dtype == DFHIP_F32)
+        k_sum_partials<float><<<blocks, 256, 0, s>>>(partial, parts, n, (float *)grad_embeddings,
+                                                     accumulate);
+    else
+        k_sum_partials<half_t><<<blocks, 256, 0, s>>>(partial, parts, n, (half_t *)grad_embeddings,
+                                                      accumulate);
+    return check_launch(name);
 }

@@ -35,6 +35,20 @@ def _grad_acc_dtype(emb_dtype):
     return emb_dtype
 
 
+# Embedding backward: "sliced" (default; LDS-privatised owner slices, f32
+# sums, no global atomics) or "atomic" (the reference's scatter of half2 /
+# f32 atomics, kept for A/B and the reference-form ABI).
+_BWD_MODE = os.environ.get("DFHIP_GRID_BWD", "sliced").lower()
+_parts_cache = {}
+
+
+def _parts(total_rows, C):
+    key = (total_rows, C)
+    if key not in _parts_cache:
+        _parts_cache[key] = _backend.grid_backward_default_parts(total_rows, C)
+    return _parts_cache[key]
+
+
 class _grid_encode(Function):
     @staticmethod
     @custom_fwd(device_type="cuda")
@@ -71,7 +85,25 @@ class _grid_encode(Function):
         inputs, offsets, dy_dx = ctx.saved_tensors
         B, D, C, L, S, H, gridtype, align_corners = ctx.dims
         rows, table_dtype = ctx.table_meta
-        grad = grad.to(table_dtype).contiguous()  # [B, L*C], no permute
+        grad = grad.to(table_dtype)
+        if dy_dx is None and _BWD_MODE == "sliced" and grad.dtype in (torch.float16,
+                                                                       torch.float32):
+            # [B, L*C] -> the level-major [L, B, C] the slices stream through
+            grad_lbc = grad.view(B, L, C).transpose(0, 1).contiguous()
+            parts = _parts(rows, C)
+            partial = torch.empty(_backend.grid_backward_partial_floats(rows, C, parts),
+                                  dtype=torch.float32, device=grad.device)
+            # f32 sums returned as the f32 parameter's gradient directly
+            grad_embeddings = torch.empty(rows, C, device=grad.device, dtype=torch.float32)
+            # algorithmic bytes: inputs + grads once, the f32 table gradient written once
+            nbytes = B * (4 * D + L * C * grad.element_size()) + 4 * rows * C
+            with _dfhip.timed("grid_encode_backward", nbytes):
+                _backend.grid_encode_backward_sliced(grad_lbc, inputs, offsets, grad_embeddings,
+                                                     rows, B, D, C, L, S, H, gridtype,
+                                                     align_corners, partial, parts)
+            return None, grad_embeddings, None, None, None, None, None, None
+
+        grad = grad.contiguous()  # [B, L*C], no permute
         grad_embeddings = torch.zeros(rows, C, device=grad.device,
                                       dtype=_grad_acc_dtype(table_dtype))
         grad_inputs = None

@@ -15,6 +15,7 @@ import torch.nn.functional as F
 from activation import trunc_exp
 from encoding import get_encoder
 
+from .mlp import mlp_forward
 from .renderer import NeRFRenderer
 from .utils import safe_normalize
 
@@ -31,6 +32,9 @@ class MLP(nn.Module):
                                  for i in range(num_layers))
 
     def forward(self, x):
+        if x.is_cuda:
+            # same math as the Linear/ReLU stack, split-K weight gradients (mlp.py)
+            return mlp_forward(x, self.net)
         last = self.num_layers - 1
         for i, layer in enumerate(self.net):
             x = layer(x)

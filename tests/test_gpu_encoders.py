@@ -129,6 +129,68 @@ def test_grid_backward(gpu, acc):
     assert err.max() <= (1e-4 if acc == "f32" else 4e-3) * scale + (0 if acc == "f32" else 1e-3)
 
 
+@pytest.mark.parametrize("parts", [1, 3, 0])
+@pytest.mark.parametrize("out", ["f32", "f16"])
+def test_grid_backward_sliced(gpu, parts, out):
+    """LDS-sliced backward: f32 sums, so it matches the exact oracle to f32
+    rounding (f16 output: one final rounding)."""
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    x = _samples(40000, 16)
+    B = x.shape[0]
+    g = (np.random.default_rng(17).normal(size=(B, 32)) * 0.1).astype(np.float16)
+    want = oracle.grid_encode_backward(g, x, offs, 2, S, 16)
+    glbc = T(g, gpu).view(B, 16, 2).transpose(0, 1).contiguous()
+    parts = parts or _gridencoder.grid_backward_default_parts(rows, 2)
+    partial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, 2, parts), device=gpu)
+    dt = torch.float32 if out == "f32" else torch.float16
+    gemb = torch.full((rows, 2), float("nan"), dtype=dt, device=gpu)  # overwritten
+    _gridencoder.grid_encode_backward_sliced(glbc, T(x, gpu), T(offs, gpu), gemb, rows, B, 3, 2, 16,
+                                             S, 16, 1, False, partial, parts)
+    got = gemb.double().cpu().numpy()
+    scale = np.abs(want).max()
+    tol = 1e-6 * scale if out == "f32" else 0
+    np.testing.assert_allclose(got, want, rtol=1e-5 if out == "f32" else 1e-3, atol=tol + 1e-7)
+    # accumulate mode adds onto the existing buffer
+    _gridencoder.grid_encode_backward_sliced(glbc, T(x, gpu), T(offs, gpu), gemb, rows, B, 3, 2, 16,
+                                             S, 16, 1, False, partial, parts, accumulate=True)
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), 2 * want,
+                               rtol=1e-5 if out == "f32" else 2e-3, atol=2 * tol + 1e-7)
+
+
+@pytest.mark.parametrize("D,C,gt", [(2, 4, 1), (3, 8, 0), (1, 1, 1), (4, 2, 0), (3, 2, 0)])
+def test_grid_backward_sliced_shapes(gpu, D, C, gt):
+    import _gridencoder
+    from gridencoder.grid import level_offsets
+    L, H = 8, 4
+    offs = level_offsets(L, C, D, H, 2.0, 17, False)
+    rows = int(offs[-1])
+    x = np.random.default_rng(D + C).random((6000, D), dtype=np.float32)
+    g = np.random.default_rng(C).normal(size=(L, 6000, C)).astype(np.float32)
+    S = 1.0
+    want = oracle.grid_encode_backward(g, x, offs, C, S, H, gridtype=gt, blc=False)
+    parts = 2
+    partial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, C, parts), device=gpu)
+    gemb = torch.empty(rows, C, device=gpu)
+    _gridencoder.grid_encode_backward_sliced(T(g, gpu), T(x, gpu), T(offs, gpu), gemb, rows, 6000,
+                                             D, C, L, S, H, gt, False, partial, parts)
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
+                               atol=1e-6 * np.abs(want).max())
+
+
+def test_grid_backward_sliced_empty_batch(gpu):
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    partial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, 2, 2), device=gpu)
+    gemb = torch.full((rows, 2), 5.0, device=gpu)
+    e = torch.zeros(16, 0, 2, dtype=torch.float16, device=gpu)
+    _gridencoder.grid_encode_backward_sliced(e, torch.zeros(0, 3, device=gpu), T(offs, gpu), gemb,
+                                             rows, 0, 3, 2, 16, S, 16, 1, False, partial, 2)
+    assert torch.all(gemb == 0)
+
+
 def test_grid_backward_hash(gpu):
     import _gridencoder
     offs, S, _ = _grid_consts()
