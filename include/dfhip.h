@@ -230,6 +230,11 @@ int dfhip_grid_encode_backward_blc(int grad_dtype, int acc_dtype, const void *gr
  * added into.  partial: dfhip_grid_backward_partial_floats(total_rows, C,
  * parts) floats of caller scratch; parts >= 1 (default_parts() fills the CUs).
  * Replaces gridencoder.cu:226-313 on the native path. */
+/* [B, L*C] -> [L, B, C] copy of the native encoder gradient into the layout
+ * the sliced backward walks (the reference forms the same layout with a torch
+ * permute, grid.py:70).  dtype F16/F32/F64; C * sizeof(dtype) in {2,4,8,16}. */
+int dfhip_grid_grad_blc_to_lbc(int dtype, const void *src, void *dst, uint32_t B, uint32_t L,
+                               uint32_t C, dfhip_stream_t stream);
 uint32_t dfhip_grid_backward_default_parts(uint32_t total_rows, uint32_t C);
 uint64_t dfhip_grid_backward_partial_floats(uint32_t total_rows, uint32_t C, uint32_t parts);
 int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, const void *grad,

@@ -56,6 +56,7 @@ _SIGS = {
                                        _f32, _u32, _vp, _vp, _u32, _i32, _vp],
     "dfhip_grid_encode_backward_sliced": [_i32, _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
                                           _u32, _f32, _u32, _u32, _i32, _vp, _u32, _i32, _vp],
+    "dfhip_grid_grad_blc_to_lbc": [_i32, _vp, _vp, _u32, _u32, _u32, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],

@@ -56,6 +56,14 @@ def grid_encode_backward_blc(grad, inputs, offsets, grad_embeddings, B, D, C, L,
 
 # ---- native sliced backward (LDS-privatised, no global atomics; see dfhip.h)
 
+def grid_grad_blc_to_lbc(grad, out, B, L, C):
+    """[B, L*C] -> [L, B, C] (same dtype, contiguous out)."""
+    checked(grad, "grad")
+    checked(out, "out")
+    call("dfhip_grid_grad_blc_to_lbc", _d.dtype_code(grad, "grad"), ptr(grad), ptr(out), B, L, C,
+         stream())
+
+
 def grid_backward_default_parts(total_rows, C):
     return int(_d.load().dfhip_grid_backward_default_parts(total_rows, C))
 

@@ -337,14 +337,18 @@ __global__ __launch_bounds__(256) void k_grid_bwd(const grad_t *__restrict__ gra
 // Owner-computes instead: the table's rows are cut into slices that fit in
 // one CU's 160 KiB LDS.  Workgroup (slice s, part p) walks the samples of
 // part p for every level overlapping slice s, and accumulates the corner
-// contributions that land in s with LDS float atomics (ds_add_f32).  The
-// slice is then written out with plain coalesced stores into partial[p]; a
-// second pass sums the P partials per row (fixed order) into the gradient.
+// contributions that land in s with LDS atomics.  The accumulators are f64:
+// on gfx950 ds_add_f64 sustains ~2.5 lane-ops/CU/cycle against ~0.33 for
+// ds_add_f32 / ds_pk_add_f16 (tools/micro/lds_atomic.hip), so doubles halve
+// the rows per slice but make the accumulation ~8x faster (and the sums
+// exact to f32 output precision).  The slice is then written out as f32 with
+// plain coalesced stores into partial[p]; a second pass sums the P partials
+// per row (fixed order) into the gradient.
 // No global atomics, HBM traffic = inputs + grads read once per slice of
 // their level + 2 * P * table bytes.
 // Flush the accumulated corner contributions of one cell into the LDS slice.
 template <uint32_t D, uint32_t C>
-__device__ __forceinline__ void flush_cell(float *acc, uint32_t r0, uint32_t r1,
+__device__ __forceinline__ void flush_cell(double *acc, uint32_t r0, uint32_t r1,
                                            const LevelCtx &c, uint32_t lead,
                                            const uint32_t cell[D], const float (&cw)[1u << D][C]) {
 #pragma unroll
@@ -355,9 +359,9 @@ __device__ __forceinline__ void flush_cell(float *acc, uint32_t r0, uint32_t r1,
         for (uint32_t d = 0; d < D; ++d) p[d] = cell[d] + ((d < lead && (k & (1u << d))) ? 1u : 0u);
         const uint32_t row = c.base + row_index<D>(c, p);
         if (row >= r0 && row < r1) {
-            float *dst = acc + (row - r0) * C;
+            double *dst = acc + (row - r0) * C;
 #pragma unroll
-            for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch, cw[k][ch]);
+            for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch, (double)cw[k][ch]);
         }
     }
 }
@@ -392,11 +396,11 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced_simple(
     Levels lv, uint32_t gridtype, int align_corners, uint32_t rows_per_slice,
     uint32_t total_rows, int vec_ok) {
     (void)vec_ok;
-    extern __shared__ float acc[];
+    extern __shared__ double acc[];
     const uint32_t r0 = blockIdx.x * rows_per_slice;
     const uint32_t r1 = min(r0 + rows_per_slice, total_rows);
     const uint32_t n = (r1 - r0) * C;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0f;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
     const bool align = align_corners != 0;
     const uint32_t chunk = ceil_div(B, gridDim.y);
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced_simple(
     }
     __syncthreads();
     float *out = partial + ((size_t)blockIdx.y * total_rows + r0) * C;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = acc[i];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = (float)acc[i];
 }
 
 // Runs of K consecutive samples per lane (the march emits each ray's samples
@@ -460,11 +464,11 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced(
     uint32_t rows_per_slice, uint32_t total_rows, int vec_ok) {
     constexpr uint32_t GW = (C * sizeof(grad_t) + 3) / 4;  // 32-bit words of one sample's grad
     constexpr bool GPACK = (C * sizeof(grad_t)) % 4 == 0;  // grads tile 32-bit words
-    extern __shared__ float acc[];
+    extern __shared__ double acc[];
     const uint32_t r0 = blockIdx.x * rows_per_slice;
     const uint32_t r1 = min(r0 + rows_per_slice, total_rows);
     const uint32_t n = (r1 - r0) * C;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0f;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
     const bool align = align_corners != 0;
     // parts split the samples in whole runs, so every run starts 16-B aligned
@@ -564,7 +568,7 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced(
     }
     __syncthreads();
     float *out = partial + ((size_t)blockIdx.y * total_rows + r0) * C;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = acc[i];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = (float)acc[i];
 }
 
 // Sum the P partial tables (fixed order) into the gradient: overwrite, or add
@@ -583,9 +587,20 @@ __global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ 
 
 constexpr uint32_t kSliceLdsBytes = 160 * 1024;
 
-static uint32_t slice_rows(uint32_t C) {
-    // rows of C f32 accumulators that fit the CU's LDS, multiple of 256
-    return (kSliceLdsBytes / (4u * C)) & ~255u;
+static uint32_t slice_rows_cap(uint32_t C) {
+    // rows of C f64 accumulators that fit the CU's LDS, multiple of 256
+    return (kSliceLdsBytes / (8u * C)) & ~255u;
+}
+
+// Rows per slice for P parts: the smallest slices that still give one
+// workgroup per CU (slices * P <= CUs), capped by the LDS.  Larger slices
+// mean fewer redundant walks over the samples; more slices fill the chip.
+static uint32_t slice_rows(uint32_t total_rows, uint32_t C, uint32_t parts, uint32_t cus) {
+    const uint32_t cap = slice_rows_cap(C);
+    const uint32_t want_slices = cus / (parts ? parts : 1u);
+    if (want_slices == 0) return cap;
+    const uint32_t r = (ceil_div(total_rows, want_slices) + 255u) & ~255u;
+    return r < cap ? r : cap;
 }
 
 // gridencoder.cu:316-342.  BLC: grad in [B, L*C] (native) else [L, B, C].
@@ -614,6 +629,30 @@ __global__ __launch_bounds__(256) void k_grid_input_bwd(const scalar_t *__restri
         }
     }
     grad_inputs[t] = r;
+}
+
+// [B, L] -> [L, B] transposition of one (sample, level) cell of W bytes (the
+// native [B, L*C] encoder gradient into the [L, B, C] layout the sliced
+// backward walks): a tile of 256 samples is read contiguously into LDS and
+// written out level by level, both sides coalesced.
+template <typename word_t>
+__global__ __launch_bounds__(256) void k_blc_to_lbc(const word_t *__restrict__ src,
+                                                   word_t *__restrict__ dst, uint32_t B,
+                                                   uint32_t L) {
+    extern __shared__ unsigned char tile_raw[];
+    word_t *tile = reinterpret_cast<word_t *>(tile_raw);  // [blockDim][L + 1]
+    const uint32_t tb = blockDim.x;
+    const uint32_t b0 = blockIdx.x * tb;
+    const uint32_t nb = min(tb, B - b0);
+    const word_t *s = src + (size_t)b0 * L;
+    for (uint32_t i = threadIdx.x; i < nb * L; i += tb) {
+        const uint32_t b = i / L, l = i - b * L;
+        tile[b * (L + 1) + l] = s[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < nb)
+        for (uint32_t l = 0; l < L; ++l)
+            dst[(size_t)l * B + b0 + threadIdx.x] = tile[threadIdx.x * (L + 1) + l];
 }
 
 // ------------------------------------------------------------ dispatch
@@ -896,9 +935,13 @@ extern "C" int dfhip_grid_encode_backward_blc(int grad_dtype, int acc_dtype, con
 
 extern "C" uint32_t dfhip_grid_backward_default_parts(uint32_t total_rows, uint32_t C) {
     if (C == 0 || total_rows == 0) return 1;
-    const uint32_t slices = ceil_div(total_rows, slice_rows(C));
-    const uint32_t p = device_cus() / slices;
-    return p < 1 ? 1 : (p > 64 ? 64 : p);
+    // several workgroups per CU: one WG per CU (160 KiB LDS) cannot hide the
+    // walk's latency, so more, shorter parts win until the partial traffic
+    // (2 * parts * table bytes) shows (tools/bench_kernels.py: 1.1 M samples,
+    // 2 parts 2.6 ms, 8 parts 1.3 ms, 16 parts 1.16 ms, 24 parts 1.12 ms)
+    const uint32_t slices = ceil_div(total_rows, slice_rows_cap(C));
+    const uint32_t p = ceil_div(6u * device_cus(), slices);
+    return p < 1 ? 1 : (p > 16 ? 16 : p);
 }
 
 extern "C" uint64_t dfhip_grid_backward_partial_floats(uint32_t total_rows, uint32_t C,
@@ -929,9 +972,9 @@ extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, 
     const uint64_t n = (uint64_t)total_rows * C;
     if (B > 0 && L > 0) {
         const Levels lv = make_levels(L, S, H);
-        const uint32_t rows = slice_rows(C);
+        const uint32_t rows = slice_rows(total_rows, C, parts, device_cus());
         const dim3 g(ceil_div(total_rows, rows), parts);
-        const size_t lds = (size_t)rows * C * sizeof(float);
+        const size_t lds = (size_t)rows * C * sizeof(double);
         switch (grad_dtype) {
         case DFHIP_F32: launch_sliced<float>(D, C, s, g, lds, (const float *)grad, inputs, offsets,
                                              partial, B, L, lv, gridtype, align_corners, rows,
@@ -952,5 +995,41 @@ extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, 
     else
         k_sum_partials<half_t><<<blocks, 256, 0, s>>>(partial, parts, n, (half_t *)grad_embeddings,
                                                       accumulate);
+    return check_launch(name);
+}
+
+extern "C" int dfhip_grid_grad_blc_to_lbc(int dtype, const void *src, void *dst, uint32_t B,
+                                          uint32_t L, uint32_t C, dfhip_stream_t stream) {
+    const char *name = "grid_grad_blc_to_lbc";
+    size_t esz = dtype == DFHIP_F16 ? 2 : dtype == DFHIP_F32 ? 4 : dtype == DFHIP_F64 ? 8 : 0;
+    if (esz == 0) {
+        set_error("%s: unsupported dtype %d", name, dtype);
+        return DFHIP_EDTYPE;
+    }
+    if (L == 0 || L > kMaxLevels || C == 0) {
+        set_error("%s: bad L=%u C=%u", name, L, C);
+        return DFHIP_EINVAL;
+    }
+    if (B == 0) return DFHIP_OK;
+    const size_t w = esz * C;  // bytes of one (sample, level) cell
+    hipStream_t s = as_stream(stream);
+    // tile of tb samples x (L + 1) cells in LDS, within 64 KiB
+    uint32_t tb = 256;
+    while (tb > 64 && (size_t)tb * (L + 1) * w > 64 * 1024) tb /= 2;
+    const size_t lds = (size_t)tb * (L + 1) * w;
+    if (lds > 64 * 1024) {
+        set_error("%s: cell of %zu bytes x %u levels too large", name, w, L);
+        return DFHIP_EINVAL;
+    }
+    const uint32_t blocks = ceil_div(B, tb);
+    switch (w) {
+    case 2: k_blc_to_lbc<uint16_t><<<blocks, tb, lds, s>>>((const uint16_t *)src, (uint16_t *)dst, B, L); break;
+    case 4: k_blc_to_lbc<uint32_t><<<blocks, tb, lds, s>>>((const uint32_t *)src, (uint32_t *)dst, B, L); break;
+    case 8: k_blc_to_lbc<uint2><<<blocks, tb, lds, s>>>((const uint2 *)src, (uint2 *)dst, B, L); break;
+    case 16: k_blc_to_lbc<uint4><<<blocks, tb, lds, s>>>((const uint4 *)src, (uint4 *)dst, B, L); break;
+    default:
+        set_error("%s: cell of %zu bytes unsupported (C * dtype size must be 2, 4, 8 or 16)", name, w);
+        return DFHIP_EINVAL;
+    }
     return check_launch(name);
 }

@@ -89,7 +89,9 @@ class _grid_encode(Function):
         if dy_dx is None and _BWD_MODE == "sliced" and grad.dtype in (torch.float16,
                                                                        torch.float32):
             # [B, L*C] -> the level-major [L, B, C] the slices stream through
-            grad_lbc = grad.view(B, L, C).transpose(0, 1).contiguous()
+            grad = grad.contiguous()
+            grad_lbc = torch.empty(L, B, C, dtype=grad.dtype, device=grad.device)
+            _backend.grid_grad_blc_to_lbc(grad, grad_lbc, B, L, C)
             parts = _parts(rows, C)
             partial = torch.empty(_backend.grid_backward_partial_floats(rows, C, parts),
                                   dtype=torch.float32, device=grad.device)

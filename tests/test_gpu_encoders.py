@@ -191,6 +191,19 @@ def test_grid_backward_sliced_empty_batch(gpu):
     assert torch.all(gemb == 0)
 
 
+@pytest.mark.parametrize("dtype,C,B", [(torch.float16, 2, 70001), (torch.float32, 2, 300),
+                                       (torch.float32, 1, 257), (torch.float16, 8, 1000),
+                                       (torch.float64, 2, 513), (torch.float16, 1, 0)])
+def test_grid_grad_blc_to_lbc(gpu, dtype, C, B):
+    """Native [B, L*C] -> [L, B, C] copy equals the reference's permute (grid.py:70)."""
+    import _gridencoder
+    L = 16
+    g = torch.randn(B, L * C, device=gpu).to(dtype)
+    out = torch.empty(L, B, C, dtype=dtype, device=gpu)
+    _gridencoder.grid_grad_blc_to_lbc(g, out, B, L, C)
+    assert torch.equal(out, g.view(B, L, C).transpose(0, 1))
+
+
 def test_grid_backward_hash(gpu):
     import _gridencoder
     offs, S, _ = _grid_consts()

@@ -95,13 +95,15 @@ def main():
         out["grid_fwd_GBs"] = B * (12 + 64) / t / 1e3
     g = (torch.randn(B, 32, device=dev) * 0.01).half()
     if want("grid_bwd"):
-        glbc = g.view(B, 16, 2).transpose(0, 1).contiguous()
-        out["grid_bwd_transpose_us"] = timeit(
+        glbc = torch.empty(16, B, 2, dtype=g.dtype, device=dev)
+        out["grid_bwd_transpose_torch_us"] = timeit(
             lambda: g.view(B, 16, 2).transpose(0, 1).contiguous(), args.reps)
+        out["grid_bwd_transpose_us"] = timeit(
+            lambda: _gridencoder.grid_grad_blc_to_lbc(g, glbc, B, 16, 2), args.reps)
         gemb = torch.empty(rows, 2, device=dev)
         dflt = _gridencoder.grid_backward_default_parts(rows, 2)
         out["grid_bwd_default_parts"] = dflt
-        for parts in sorted({1, 2, 4, dflt, 8}):
+        for parts in sorted({2, 4, dflt, 6, 8, 12, 16, 24}):
             partial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, 2, parts),
                                   device=dev)
             t = timeit(lambda: _gridencoder.grid_encode_backward_sliced(
