@@ -117,9 +117,21 @@ def summarize_kernels(records):
     return out
 
 
+# timed region -> the kernel symbols launched inside it (for PMC traffic)
+REGION_KERNELS = {
+    "grid_encode_backward": ("k_grid_bwd_sliced", "k_sum_partials"),
+    "grid_encode_forward": ("k_grid_fwd",),
+    "march_rays_train_count": ("k_march_train_count",),
+    "march_rays_train_emit": ("k_march_train_emit",),
+    "composite_rays_train_forward": ("k_composite_train_fwd",),
+    "composite_rays_train_backward": ("k_composite_train_bwd",),
+}
+
+
 def load_pmc(name):
-    """Per-dispatch HBM bytes of `name` from the committed rocprofv3 PMC summary
-    (profiles/pmc_summary.json, made by tools/pmc_summary.py), or None."""
+    """Per-launch HBM bytes of timed region `name` (sum over its kernels) from
+    the committed rocprofv3 PMC summary (profiles/pmc_summary.json, made by
+    tools/gpu_pmc_bench.sh + tools/pmc_summary.py), or None."""
     path = ROOT / "profiles" / "pmc_summary.json"
     if not path.exists():
         return None
@@ -127,10 +139,14 @@ def load_pmc(name):
         data = json.loads(path.read_text())
     except ValueError:
         return None
-    for k, v in data.get("kernels", {}).items():
-        if name in k:
-            return v.get("hbm_bytes_per_dispatch")
-    return None
+    total, found = 0, False
+    for pat in REGION_KERNELS.get(name, (name,)):
+        for k, v in data.get("kernels", {}).items():
+            if pat in k:
+                total += v["hbm_bytes_per_dispatch"]
+                found = True
+                break
+    return total if found else None
 
 
 def main():
