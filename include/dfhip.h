@@ -263,6 +263,34 @@ int dfhip_sh_encode_backward(int dtype, const void *grad, const void *inputs,
                              uint32_t B, uint32_t D, uint32_t C, const void *dy_dx,
                              void *grad_inputs, dfhip_stream_t stream);
 
+/* ---------------------------------------------------------------- fused field head
+ * Replaces the torch ops of nerf/network_grid.py:13-32 (MLP: 3 nn.Linear +
+ * ReLU under fp16 autocast) and :76-87 (common_forward: sigma =
+ * trunc_exp(h0 + 5 exp(-|x|^2/0.08)), activation.py:5-18; albedo =
+ * sigmoid(h[1:4])).  Fixed shape: 32 -> 64 -> 64 -> 4 (the reference's
+ * sigma_net).  Parameters are the f32 nn.Linear tensors (w1 [64,32], b1 [64],
+ * w2 [64,64], b2 [64], w3 [4,64], b3 [4]), rounded to f16 inside as autocast
+ * does.  enc: [M, 32] f16 encoder features; xyz: [M, 3] f32 positions in
+ * [-bound, bound] (for the Gaussian blob). */
+uint32_t dfhip_field_mlp_params(void); /* 6532 */
+int dfhip_field_mlp_forward(const void *enc, const float *xyz, const float *w1, const float *b1,
+                            const float *w2, const float *b2, const float *w3, const float *b3,
+                            float *sigma, void *rgb, int rgb_dtype, uint32_t M,
+                            dfhip_stream_t stream);
+/* Backward from grad_sigma [M] f32 and grad_rgb [M, 3] (grad_rgb_dtype F16/F32):
+ * d_enc_lbc [16, M, 2] f16 receives the feature gradient in the level-major
+ * layout dfhip_grid_encode_backward_sliced consumes; gw1..gb3 (f32, shaped as
+ * the parameters) are overwritten (accumulate == 0) or added into.  partial:
+ * parts * dfhip_field_mlp_params() floats of scratch with
+ * parts = dfhip_field_mlp_backward_parts(M).  Deterministic. */
+uint32_t dfhip_field_mlp_backward_parts(uint32_t M);
+int dfhip_field_mlp_backward(const void *enc, const float *xyz, const float *w1, const float *b1,
+                             const float *w2, const float *b2, const float *w3, const float *b3,
+                             const float *grad_sigma, const void *grad_rgb, int grad_rgb_dtype,
+                             uint32_t M, void *d_enc_lbc, float *partial, uint32_t parts,
+                             float *gw1, float *gb1, float *gw2, float *gb2, float *gw3,
+                             float *gb3, int accumulate, dfhip_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,9 @@ _SIGS = {
     "dfhip_grid_encode_backward_sliced": [_i32, _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
                                           _u32, _f32, _u32, _u32, _i32, _vp, _u32, _i32, _vp],
     "dfhip_grid_grad_blc_to_lbc": [_i32, _vp, _vp, _u32, _u32, _u32, _vp],
+    "dfhip_field_mlp_forward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp],
+    "dfhip_field_mlp_backward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,
+                                 _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],
@@ -82,6 +85,10 @@ def load() -> ctypes.CDLL:
     lib.dfhip_march_rays_train_scratch_ints.argtypes = [_u32]
     lib.dfhip_grid_backward_default_parts.restype = _u32
     lib.dfhip_grid_backward_default_parts.argtypes = [_u32, _u32]
+    lib.dfhip_field_mlp_params.restype = _u32
+    lib.dfhip_field_mlp_params.argtypes = []
+    lib.dfhip_field_mlp_backward_parts.restype = _u32
+    lib.dfhip_field_mlp_backward_parts.argtypes = [_u32]
     lib.dfhip_grid_backward_partial_floats.restype = ctypes.c_uint64
     lib.dfhip_grid_backward_partial_floats.argtypes = [_u32, _u32, _u32]
     for name, args in _SIGS.items():
@@ -95,6 +102,7 @@ def load() -> ctypes.CDLL:
 def exported_symbols() -> list[str]:
     return ["dfhip_abi_version", "dfhip_last_error", "dfhip_march_rays_train_scratch_ints",
             "dfhip_grid_backward_default_parts", "dfhip_grid_backward_partial_floats",
+            "dfhip_field_mlp_params", "dfhip_field_mlp_backward_parts",
             *_SIGS.keys()]
 
 

@@ -1,0 +1,65 @@
+"""Native fused field head (csrc/fieldmlp.hip): the grid NeRF's sigma MLP
+32 -> 64 -> 64 -> 4 with trunc_exp density + Gaussian blob and sigmoid albedo
+(reference nerf/network_grid.py:13-32,72-87), forward and backward, on MFMA.
+No reference pybind counterpart: the reference runs this as torch ops."""
+import torch
+
+import _dfhip as _d
+from _dfhip import call, checked, ptr, stream
+
+IN, HIDDEN, OUT = 32, 64, 4
+
+
+def params_count():
+    return int(_d.load().dfhip_field_mlp_params())
+
+
+def backward_parts(M):
+    return int(_d.load().dfhip_field_mlp_backward_parts(M))
+
+
+def _f32(t, what):
+    checked(t, what)
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{what} must be a float32 tensor")
+
+
+def _weights(ws):
+    if len(ws) != 6:
+        raise RuntimeError("expected (w1, b1, w2, b2, w3, b3)")
+    shapes = [(HIDDEN, IN), (HIDDEN,), (HIDDEN, HIDDEN), (HIDDEN,), (OUT, HIDDEN), (OUT,)]
+    for i, (w, shp) in enumerate(zip(ws, shapes)):
+        _f32(w, f"param{i}")
+        if tuple(w.shape) != shp:
+            raise RuntimeError(f"param{i} must have shape {shp}, got {tuple(w.shape)}")
+    return [ptr(w) for w in ws]
+
+
+def field_mlp_forward(enc, xyz, weights, sigma, rgb):
+    """enc [M, 32] f16, xyz [M, 3] f32 -> sigma [M] f32, rgb [M, 3] (f16 or f32)."""
+    M = enc.shape[0]
+    checked(enc, "enc")
+    if enc.dtype != torch.float16 or enc.shape[1] != IN:
+        raise RuntimeError("enc must be a [M, 32] float16 tensor")
+    _f32(xyz, "xyz")
+    _f32(sigma, "sigma")
+    checked(rgb, "rgb")
+    call("dfhip_field_mlp_forward", ptr(enc), ptr(xyz), *_weights(weights), ptr(sigma), ptr(rgb),
+         _d.dtype_code(rgb, "rgb"), M, stream())
+
+
+def field_mlp_backward(enc, xyz, weights, grad_sigma, grad_rgb, d_enc_lbc, partial, grads,
+                       accumulate=False):
+    """grads: six f32 tensors shaped like the weights (overwritten, or added
+    into with accumulate).  d_enc_lbc: [16, M, 2] f16.  partial:
+    backward_parts(M) * params_count() f32 scratch."""
+    M = enc.shape[0]
+    for t, n in ((enc, "enc"), (grad_rgb, "grad_rgb"), (d_enc_lbc, "d_enc")):
+        checked(t, n)
+    _f32(xyz, "xyz")
+    _f32(grad_sigma, "grad_sigma")
+    _f32(partial, "partial")
+    gp = _weights(grads)
+    call("dfhip_field_mlp_backward", ptr(enc), ptr(xyz), *_weights(weights), ptr(grad_sigma),
+         ptr(grad_rgb), _d.dtype_code(grad_rgb, "grad_rgb"), M, ptr(d_enc_lbc), ptr(partial),
+         backward_parts(M) if M else 1, *gp, int(bool(accumulate)), stream())

@@ -1,0 +1,506 @@
+// Fused grid-NeRF field head on MFMA (gfx950): the sigma MLP
+// 32 -> 64 -> ReLU -> 64 -> ReLU -> 4, trunc_exp density with the Gaussian
+// blob, sigmoid albedo — forward, and backward with the weight gradients.
+//
+// Behavioural spec: nerf/network_grid.py:13-32 (MLP), :72-87 (common_forward:
+// sigma = trunc_exp(h0 + 5 exp(-|x|^2 / 0.08)), albedo = sigmoid(h[1:4])),
+// activation.py:5-18 (trunc_exp), run under torch.autocast(fp16)
+// (nerf/utils.py train_step), i.e. f16 GEMMs with f32 accumulation and f16
+// activations, f32 sigma.
+//
+// The reference runs this as 3 hipBLASLt GEMMs + ~15 elementwise kernels
+// forward and ~25 backward, every activation round-tripping HBM.  Here one
+// kernel holds a 16-sample tile in registers through all three layers:
+//
+//   v_mfma_f32_16x16x32_f16, operand maps (lane l, c = l & 15, h = l >> 4):
+//     A[i = c][k = 8h + j], B[k = 8h + j][col = c], D[row = 4h + r][col = c]
+//
+// Layers are computed transposed (H^T = W X^T): the sample sits on the lane
+// (column) and the neurons in the accumulator registers, so each layer's
+// accumulator tile is directly the next layer's B operand — summed over its
+// row index with the k order permuted (element j of lane group h is neuron
+// 32s + 16(j >> 2) + 4h + (j & 3) of k-step s); the A operand (weights) is
+// read from LDS in the same permuted order.  The backward recomputes the
+// forward from the saved encoder features (no activations are stored), runs
+// the three transposed-weight products, writes the encoder gradient directly
+// in the [L, B, C] layout the sliced grid backward walks, and forms the
+// weight gradients as MFMAs over 32-sample k-steps from a per-wave LDS image
+// of the activations.  Per-workgroup partial sums + a fixed-order reduction
+// make the weight gradients deterministic.
+#include "common.h"
+
+namespace dfhip {
+namespace fm {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kIn = 32, kHid = 64, kOut = 4;
+// packed parameter order (nn.Linear): W1 [64,32], b1 [64], W2 [64,64], b2 [64], W3 [4,64], b3 [4]
+constexpr int kOffW1 = 0, kOffB1 = kOffW1 + kHid * kIn, kOffW2 = kOffB1 + kHid,
+              kOffB2 = kOffW2 + kHid * kHid, kOffW3 = kOffB2 + kHid, kOffB3 = kOffW3 + kOut * kHid,
+              kParams = kOffB3 + kOut;  // 6532
+
+__device__ __forceinline__ f4 mfma(half8 a, half8 b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// Make this wave's LDS writes visible to its other lanes before they read.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Weights as f16 (autocast's cast of the f32 parameters), in LDS.
+struct Weights {
+    half_t w1[kHid * kIn];    // [n1][f]
+    half_t w2[kHid * kHid];   // [n2][n1]
+    half_t w3[16 * kHid];     // [o][n2], rows 4..15 zero
+    float b1[kHid], b2[kHid], b3[16];  // f32 of the f16-rounded biases; b3 rows 4.. zero
+};
+struct WeightsT {             // backward only
+    half_t w1t[kIn * kHid];   // [f][n1]
+    half_t w2t[kHid * kHid];  // [n1][n2]
+    half_t w3t[kHid * 32];    // [n2][o], o 4..31 zero
+};
+
+__device__ void load_weights(Weights &W, WeightsT *T, const float *w1, const float *b1,
+                             const float *w2, const float *b2, const float *w3, const float *b3) {
+    for (int i = threadIdx.x; i < kHid * kIn; i += blockDim.x) {
+        const half_t v = (half_t)w1[i];
+        W.w1[i] = v;
+        if (T) T->w1t[(i % kIn) * kHid + i / kIn] = v;
+    }
+    for (int i = threadIdx.x; i < kHid * kHid; i += blockDim.x) {
+        const half_t v = (half_t)w2[i];
+        W.w2[i] = v;
+        if (T) T->w2t[(i % kHid) * kHid + i / kHid] = v;
+    }
+    for (int i = threadIdx.x; i < 16 * kHid; i += blockDim.x)
+        W.w3[i] = i < kOut * kHid ? (half_t)w3[i] : (half_t)0.0f;
+    if (T)
+        for (int i = threadIdx.x; i < kHid * 32; i += blockDim.x) {
+            const int n2 = i / 32, o = i % 32;
+            T->w3t[i] = o < kOut ? (half_t)w3[o * kHid + n2] : (half_t)0.0f;
+        }
+    for (int i = threadIdx.x; i < kHid; i += blockDim.x) {
+        W.b1[i] = (float)(half_t)b1[i];
+        W.b2[i] = (float)(half_t)b2[i];
+    }
+    for (int i = threadIdx.x; i < 16; i += blockDim.x) W.b3[i] = i < kOut ? (float)(half_t)b3[i] : 0.0f;
+}
+
+// A operand, natural k order: row `row` of a row-major [*, ld] f16 matrix,
+// k = 8h .. 8h+7 (+ koff).
+__device__ __forceinline__ half8 a_nat(const half_t *m, int ld, int row, int koff, int h) {
+    return *reinterpret_cast<const half8 *>(m + row * ld + koff + 8 * h);
+}
+// A operand, permuted k order of k-step s (see header).
+__device__ __forceinline__ half8 a_perm(const half_t *m, int ld, int row, int s, int h) {
+    const half4 lo = *reinterpret_cast<const half4 *>(m + row * ld + 32 * s + 4 * h);
+    const half4 hi = *reinterpret_cast<const half4 *>(m + row * ld + 32 * s + 16 + 4 * h);
+    return half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// B operand of k-step s from four accumulator tiles' f16 values v[tile][reg].
+__device__ __forceinline__ half8 b_from_tiles(const half_t (&v)[4][4], int s) {
+    return half8{v[2 * s][0], v[2 * s][1], v[2 * s][2], v[2 * s][3],
+                 v[2 * s + 1][0], v[2 * s + 1][1], v[2 * s + 1][2], v[2 * s + 1][3]};
+}
+__device__ __forceinline__ f4 bias4(const float *b, int row0) {
+    return f4{b[row0], b[row0 + 1], b[row0 + 2], b[row0 + 3]};
+}
+
+// One 16-sample tile through the MLP.  xb: B operand of the encoder features
+// (lane: sample c, features 8h..8h+7).  Outputs the post-ReLU f16 activations
+// of both hidden layers and the f32 accumulators of the output layer.
+struct Fwd {
+    half_t a1[4][4], a2[4][4];  // [tile][reg]: neuron 16 t + 4 h + r of sample c
+    f4 o;                       // rows 4h + r (only h == 0 valid: outputs 0..3)
+};
+
+__device__ __forceinline__ void forward_tile(const Weights &W, half8 xb, int c, int h, Fwd &F) {
+    f4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        acc[t] = mfma(a_nat(W.w1, kIn, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const half_t v = (half_t)acc[t][r];
+            F.a1[t][r] = v > (half_t)0.0f ? v : (half_t)0.0f;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        f4 a = bias4(W.b2, 16 * u + 4 * h);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kHid, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const half_t v = (half_t)a[r];
+            F.a2[u][r] = v > (half_t)0.0f ? v : (half_t)0.0f;
+        }
+    }
+    f4 o = bias4(W.b3, 4 * h);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) o = mfma(a_perm(W.w3, kHid, c, s, h), b_from_tiles(F.a2, s), o);
+    F.o = o;
+}
+
+__device__ __forceinline__ float gaussian(const float *x) {
+    // network_grid.py gaussian: 5 * exp(-(x**2).sum(-1) / (2 * 0.2**2)), f32
+    const float s = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
+    return 5.0f * expf(-s / 0.08f);
+}
+
+__device__ __forceinline__ half8 load_x(const half_t *enc, uint32_t sample, uint32_t M, int h) {
+    if (sample >= M) return half8{};
+    return *reinterpret_cast<const half8 *>(enc + (size_t)sample * kIn + 8 * h);
+}
+
+// ------------------------------------------------------------------ forward
+template <typename rgb_t>
+__global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ enc,
+                                                   const float *__restrict__ xyz,
+                                                   const float *w1, const float *b1,
+                                                   const float *w2, const float *b2,
+                                                   const float *w3, const float *b3,
+                                                   float *__restrict__ sigma,
+                                                   rgb_t *__restrict__ rgb, uint32_t M) {
+    __shared__ Weights W;
+    load_weights(W, nullptr, w1, b1, w2, b2, w3, b3);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t tiles = ceil_div(M, 16u);
+    for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles;
+         tile += waves) {
+        const uint32_t sample = tile * 16 + c;
+        Fwd F;
+        forward_tile(W, load_x(enc, sample, M, h), c, h, F);
+        if (h == 0 && sample < M) {
+            const float *x = xyz + (size_t)sample * 3;
+            const float y = (float)(half_t)F.o[0] + gaussian(x);
+            sigma[sample] = expf(y);
+#pragma unroll
+            for (int r = 1; r < 4; ++r) {
+                const float v = (float)(half_t)F.o[r];
+                rgb[(size_t)sample * 3 + r - 1] = (rgb_t)(half_t)(1.0f / (1.0f + expf(-v)));
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ backward
+struct Stage {                      // per-wave LDS image of one 32-sample group, [row][sample]
+    half_t x[kIn * 32];
+    half_t a1[kHid * 32];
+    half_t a2[kHid * 32];
+    half_t d1[kHid * 32];
+    half_t d2[kHid * 32];
+    half_t dO[16 * 32];             // rows 4..15 stay zero
+};
+
+constexpr int kBwdWaves = 4;
+
+template <typename rgb_t>
+__global__ __launch_bounds__(256) void k_field_bwd(
+    const half_t *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
+    const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
+    const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t M,
+    half_t *__restrict__ d_enc,     // [16, M, 2] (level-major)
+    float *__restrict__ partial) {  // [gridDim.x, kParams]
+    __shared__ Weights W;
+    __shared__ WeightsT T;
+    __shared__ Stage stage[kBwdWaves];
+    load_weights(W, &T, w1, b1, w2, b2, w3, b3);
+    const int wave = threadIdx.x >> 6;
+    Stage &S = stage[wave];
+    for (int i = threadIdx.x & 63; i < 16 * 32; i += 64) S.dO[i] = (half_t)0.0f;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+
+    f4 gw1[4][2], gw2[4][4], gw3[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        gw3[i] = f4{0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) gw1[i][j] = f4{0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gw2[i][j] = f4{0, 0, 0, 0};
+    }
+    float gb1 = 0.0f, gb2 = 0.0f, gb3 = 0.0f;  // bias grads of neuron `lane`
+
+    const uint32_t groups = ceil_div(M, 32u);
+    for (uint32_t grp = blockIdx.x * kBwdWaves + wave; grp < groups;
+         grp += gridDim.x * kBwdWaves) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int col = 16 * q + c;  // column in the 32-sample stage
+            const uint32_t sample = grp * 32 + col;
+            const bool valid = sample < M;
+            const half8 xb = load_x(enc, sample, M, h);
+            Fwd F;
+            forward_tile(W, xb, c, h, F);
+            // dL/d(output layer), f16 as autocast's backward produces it
+            half8 dob = half8{};
+            if (h == 0) {
+                half_t dO[4] = {(half_t)0.0f, (half_t)0.0f, (half_t)0.0f, (half_t)0.0f};
+                if (valid) {
+                    const float y = (float)(half_t)F.o[0] + gaussian(xyz + (size_t)sample * 3);
+                    // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
+                    const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
+                    dO[0] = (half_t)(grad_sigma[sample] * expf(yc));
+#pragma unroll
+                    for (int r = 1; r < 4; ++r) {
+                        const float a = (float)(half_t)(1.0f / (1.0f + expf(-(float)(half_t)F.o[r])));
+                        const float g = (float)(half_t)grad_rgb[(size_t)sample * 3 + r - 1];
+                        dO[r] = (half_t)(g * (1.0f - a) * a);  // sigmoid_backward in f16 (opmath f32)
+                    }
+                }
+                dob = half8{dO[0], dO[1], dO[2], dO[3], (half_t)0.0f, (half_t)0.0f, (half_t)0.0f,
+                            (half_t)0.0f};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) S.dO[r * 32 + col] = dO[r];
+            }
+            // hidden layer 2: dA2^T = W3^T dO^T, ReLU mask
+            half_t dz2[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const f4 d = mfma(a_nat(T.w3t, 32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    dz2[u][r] = F.a2[u][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
+            }
+            // hidden layer 1: dA1^T = W2^T dZ2^T, ReLU mask
+            half_t dz1[4][4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                f4 d = f4{0, 0, 0, 0};
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    d = mfma(a_perm(T.w2t, kHid, 16 * t + c, s, h), b_from_tiles(dz2, s), d);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    dz1[t][r] = F.a1[t][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
+            }
+            // encoder features: dX^T = W1^T dZ1^T -> [L, B, C] directly
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                f4 d = f4{0, 0, 0, 0};
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    d = mfma(a_perm(T.w1t, kHid, 16 * f + c, s, h), b_from_tiles(dz1, s), d);
+                if (valid) {
+                    // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
+                    const uint32_t lv = 8 * f + 2 * h;
+                    typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+                    *reinterpret_cast<half2v *>(d_enc + ((size_t)lv * M + sample) * 2) =
+                        half2v{(half_t)d[0], (half_t)d[1]};
+                    *reinterpret_cast<half2v *>(d_enc + ((size_t)(lv + 1) * M + sample) * 2) =
+                        half2v{(half_t)d[2], (half_t)d[3]};
+                }
+            }
+            // stage [row][sample] images for the weight gradients
+#pragma unroll
+            for (int j = 0; j < 8; ++j) S.x[(8 * h + j) * 32 + col] = xb[j];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = (16 * t + 4 * h + r) * 32 + col;
+                    S.a1[row] = F.a1[t][r];
+                    S.a2[row] = F.a2[t][r];
+                    S.d1[row] = dz1[t][r];
+                    S.d2[row] = dz2[t][r];
+                }
+        }
+        wave_lds_sync();
+        // weight gradients over the group's 32 samples (k = sample)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+            const half8 a_d1 = a_nat(S.d1, 32, 16 * tn + c, 0, h);
+            const half8 a_d2 = a_nat(S.d2, 32, 16 * tn + c, 0, h);
+#pragma unroll
+            for (int tf = 0; tf < 2; ++tf)
+                gw1[tn][tf] = mfma(a_d1, a_nat(S.x, 32, 16 * tf + c, 0, h), gw1[tn][tf]);
+#pragma unroll
+            for (int tm = 0; tm < 4; ++tm)
+                gw2[tn][tm] = mfma(a_d2, a_nat(S.a1, 32, 16 * tm + c, 0, h), gw2[tn][tm]);
+            gw3[tn] = mfma(a_nat(S.dO, 32, c, 0, h), a_nat(S.a2, 32, 16 * tn + c, 0, h), gw3[tn]);
+        }
+        // bias gradients: lane n sums row n over the 32 samples
+        {
+            float s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                s1 += (float)S.d1[lane * 32 + k];
+                s2 += (float)S.d2[lane * 32 + k];
+                s3 += (float)S.dO[(lane & 15) * 32 + k];
+            }
+            gb1 += s1;
+            gb2 += s2;
+            gb3 += s3;
+        }
+        wave_lds_sync();  // the stage is rewritten by the next group
+    }
+
+    // ---- fixed-order workgroup reduction -> partial[blockIdx.x]
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(&stage[0]);  // kParams floats (26 KB) reuse the stage
+    for (int w = 0; w < kBwdWaves; ++w) {
+        if (wave == w) {
+            const bool first = (w == 0);
+#pragma unroll
+            for (int tn = 0; tn < 4; ++tn) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = 16 * tn + 4 * h + r;
+#pragma unroll
+                    for (int tf = 0; tf < 2; ++tf) {
+                        float &dst = red[kOffW1 + n * kIn + 16 * tf + c];
+                        dst = first ? gw1[tn][tf][r] : dst + gw1[tn][tf][r];
+                    }
+#pragma unroll
+                    for (int tm = 0; tm < 4; ++tm) {
+                        float &dst = red[kOffW2 + n * kHid + 16 * tm + c];
+                        dst = first ? gw2[tn][tm][r] : dst + gw2[tn][tm][r];
+                    }
+                }
+                if (h == 0)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float &dst = red[kOffW3 + r * kHid + 16 * tn + c];
+                        dst = first ? gw3[tn][r] : dst + gw3[tn][r];
+                    }
+            }
+            {
+                float &d1 = red[kOffB1 + lane];
+                d1 = first ? gb1 : d1 + gb1;
+                float &d2 = red[kOffB2 + lane];
+                d2 = first ? gb2 : d2 + gb2;
+                if (lane < kOut) {
+                    float &d3 = red[kOffB3 + lane];
+                    d3 = first ? gb3 : d3 + gb3;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    float *out = partial + (size_t)blockIdx.x * kParams;
+    for (int i = threadIdx.x; i < kParams; i += blockDim.x) out[i] = red[i];
+}
+
+// Sum the per-workgroup partials (fixed order) into the six f32 gradients.
+__global__ __launch_bounds__(256) void k_field_wgrad_sum(const float *__restrict__ partial,
+                                                         uint32_t parts, float *gw1, float *gb1,
+                                                         float *gw2, float *gb2, float *gw3,
+                                                         float *gb3, int accumulate) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kParams) return;
+    float s = 0.0f;
+    for (uint32_t p = 0; p < parts; ++p) s += partial[(size_t)p * kParams + i];
+    float *dst;
+    int k;
+    if (i < kOffB1) { dst = gw1; k = i - kOffW1; }
+    else if (i < kOffW2) { dst = gb1; k = i - kOffB1; }
+    else if (i < kOffB2) { dst = gw2; k = i - kOffW2; }
+    else if (i < kOffW3) { dst = gb2; k = i - kOffB2; }
+    else if (i < kOffB3) { dst = gw3; k = i - kOffW3; }
+    else { dst = gb3; k = i - kOffB3; }
+    dst[k] = accumulate ? dst[k] + s : s;
+}
+
+static uint32_t bwd_blocks(uint32_t M) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t want = ceil_div(ceil_div(M, 32u), (uint32_t)kBwdWaves);
+    const uint32_t cap = (uint32_t)cus;
+    return want < cap ? (want ? want : 1u) : cap;
+}
+
+}  // namespace fm
+}  // namespace dfhip
+
+using namespace dfhip;
+using namespace dfhip::fm;
+
+extern "C" uint32_t dfhip_field_mlp_params(void) { return (uint32_t)kParams; }
+
+extern "C" uint32_t dfhip_field_mlp_backward_parts(uint32_t M) { return bwd_blocks(M); }
+
+extern "C" int dfhip_field_mlp_forward(const void *enc, const float *xyz, const float *w1,
+                                       const float *b1, const float *w2, const float *b2,
+                                       const float *w3, const float *b3, float *sigma,
+                                       void *rgb, int rgb_dtype, uint32_t M,
+                                       dfhip_stream_t stream) {
+    const char *name = "field_mlp_forward";
+    if (M == 0) return DFHIP_OK;
+    if (!enc || !xyz || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !sigma || !rgb) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const uint32_t tiles = ceil_div(M, 16u);
+    const uint32_t blocks = ceil_div(tiles, 4u) < 2048u ? ceil_div(tiles, 4u) : 2048u;
+    if (rgb_dtype == DFHIP_F32)
+        k_field_fwd<float><<<blocks, 256, 0, s>>>((const half_t *)enc, xyz, w1, b1, w2, b2, w3,
+                                                  b3, sigma, (float *)rgb, M);
+    else if (rgb_dtype == DFHIP_F16)
+        k_field_fwd<half_t><<<blocks, 256, 0, s>>>((const half_t *)enc, xyz, w1, b1, w2, b2, w3,
+                                                   b3, sigma, (half_t *)rgb, M);
+    else {
+        set_error("%s: rgb dtype must be f32 or f16", name);
+        return DFHIP_EDTYPE;
+    }
+    return check_launch(name);
+}
+
+extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const float *w1,
+                                        const float *b1, const float *w2, const float *b2,
+                                        const float *w3, const float *b3, const float *grad_sigma,
+                                        const void *grad_rgb, int grad_rgb_dtype, uint32_t M,
+                                        void *d_enc_lbc, float *partial, uint32_t parts,
+                                        float *gw1, float *gb1, float *gw2, float *gb2,
+                                        float *gw3, float *gb3, int accumulate,
+                                        dfhip_stream_t stream) {
+    const char *name = "field_mlp_backward";
+    if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !gw1 || !gb1 || !gw2 || !gb2 || !gw3 || !gb3 ||
+        !partial) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    if (M > 0) {
+        if (!enc || !xyz || !grad_sigma || !grad_rgb || !d_enc_lbc) {
+            set_error("%s: null pointer", name);
+            return DFHIP_EINVAL;
+        }
+        if (parts != bwd_blocks(M)) {
+            set_error("%s: parts must be dfhip_field_mlp_backward_parts(M) = %u (got %u)", name,
+                      bwd_blocks(M), parts);
+            return DFHIP_EINVAL;
+        }
+        if (grad_rgb_dtype == DFHIP_F32)
+            k_field_bwd<float><<<parts, 256, 0, s>>>((const half_t *)enc, xyz, w1, b1, w2, b2, w3,
+                                                     b3, grad_sigma, (const float *)grad_rgb, M,
+                                                     (half_t *)d_enc_lbc, partial);
+        else if (grad_rgb_dtype == DFHIP_F16)
+            k_field_bwd<half_t><<<parts, 256, 0, s>>>((const half_t *)enc, xyz, w1, b1, w2, b2,
+                                                      w3, b3, grad_sigma,
+                                                      (const half_t *)grad_rgb, M,
+                                                      (half_t *)d_enc_lbc, partial);
+        else {
+            set_error("%s: grad_rgb dtype must be f32 or f16", name);
+            return DFHIP_EDTYPE;
+        }
+    } else {
+        parts = 1;
+        (void)hipMemsetAsync(partial, 0, kParams * sizeof(float), s);
+    }
+    k_field_wgrad_sum<<<ceil_div((uint32_t)kParams, 256u), 256, 0, s>>>(
+        partial, parts, gw1, gb1, gw2, gb2, gw3, gb3, accumulate);
+    return check_launch(name);
+}

@@ -8,6 +8,8 @@ order (hence seeded initialisation and state_dict keys) match the reference
 (network_grid.py:35-181), so the reference file itself also runs on this
 package unchanged.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -15,6 +17,7 @@ import torch.nn.functional as F
 from activation import trunc_exp
 from encoding import get_encoder
 
+from . import field as _field
 from .mlp import mlp_forward
 from .renderer import NeRFRenderer
 from .utils import safe_normalize
@@ -43,6 +46,9 @@ class MLP(nn.Module):
         return x
 
 
+# DFHIP_FUSED_FIELD=0 runs the encoder and the MLP as separate nodes
+_FUSED_FIELD = os.environ.get("DFHIP_FUSED_FIELD", "1") != "0"
+
 # unit offsets of the central-difference stencil (+x, -x, +y, -y, +z, -z)
 _STENCIL = ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1))
 
@@ -69,6 +75,9 @@ class NeRFNetwork(NeRFRenderer):
 
     def common_forward(self, x):
         """x [N, 3] in [-bound, bound] -> sigma [N] (f32), albedo [N, 3]."""
+        if _FUSED_FIELD and _field.eligible(self.encoder, self.sigma_net.net, x):
+            # encoder + MLP + heads as one native node (nerf/field.py)
+            return _field.grid_field(x, self.bound, self.encoder, self.sigma_net.net)
         h = self.sigma_net(self.encoder(x, bound=self.bound))
         sigma = trunc_exp(h[..., 0] + self.gaussian(x))
         albedo = torch.sigmoid(h[..., 1:])

@@ -1,0 +1,89 @@
+"""Fused field head (csrc/fieldmlp.hip + nerf/field.py) against the unfused
+reference composition (GridEncoder -> nn.Linear/ReLU stack under fp16
+autocast -> trunc_exp(h0 + gaussian) / sigmoid), network_grid.py:13-32,76-87.
+
+fp16 tolerance: the fused kernel accumulates each layer on MFMA in a different
+order than hipBLASLt and keeps f32 weight-gradient sums (the reference rounds
+the weight gradients to f16 before the f32 cast)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _field(gpu, seed=0, emb_scale=0.5):
+    from gridencoder import GridEncoder
+    torch.manual_seed(seed)
+    enc = GridEncoder(input_dim=3, num_levels=16, level_dim=2, base_resolution=16,
+                      log2_hashmap_size=16, desired_resolution=2048, gridtype="tiled").to(gpu)
+    with torch.no_grad():
+        enc.embeddings.uniform_(-emb_scale, emb_scale)
+    layers = nn.ModuleList([nn.Linear(32, 64), nn.Linear(64, 64), nn.Linear(64, 4)]).to(gpu)
+    return enc, layers
+
+
+def _reference(x, enc, layers):
+    h = enc(x, bound=1.0)
+    for i, lin in enumerate(layers):
+        h = lin(h)
+        if i < 2:
+            h = torch.relu(h)
+    g = 5 * torch.exp(-(x ** 2).sum(-1) / (2 * 0.2 ** 2))
+    from activation import trunc_exp
+    return trunc_exp(h[..., 0] + g), torch.sigmoid(h[..., 1:])
+
+
+@pytest.mark.parametrize("M", [1, 31, 50_003])
+def test_fused_field_matches_unfused(gpu, M):
+    from nerf.field import eligible, grid_field
+    enc, layers = _field(gpu)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = (torch.rand(M, 3, generator=g) * 2 - 1).mul_(0.9).to(gpu)
+    gs = torch.randn(M, generator=g).to(gpu)
+    ga = torch.randn(M, 3, generator=g).to(gpu)
+    with torch.autocast("cuda", dtype=torch.float16):
+        assert eligible(enc, layers, x)
+        s1, a1 = grid_field(x, 1.0, enc, layers)
+        s0, a0 = _reference(x, enc, layers)
+    assert s1.dtype == torch.float32 and a1.dtype == torch.float16 and a0.dtype == torch.float16
+    torch.testing.assert_close(s1, s0.float(), rtol=2e-2, atol=1e-3)
+    torch.testing.assert_close(a1.float(), a0.float(), rtol=0, atol=4e-3)
+    params = [enc.embeddings] + list(layers.parameters())
+    g1 = torch.autograd.grad((s1 * gs).sum() + (a1.float() * ga).sum(), params)
+    g0 = torch.autograd.grad((s0.float() * gs).sum() + (a0.float() * ga).sum(), params)
+    for i, (a, b) in enumerate(zip(g1, g0)):
+        assert a.dtype == torch.float32 and a.shape == b.shape
+        b = b.float()
+        err = (a - b).norm() / b.norm().clamp(min=1e-12)
+        assert err < 2e-2, f"param {i}: rel err {err:.3e}"
+
+
+def test_fused_field_deterministic(gpu):
+    from nerf.field import grid_field
+    enc, layers = _field(gpu, seed=2)
+    x = (torch.rand(70_001, 3, device=gpu) * 2 - 1)
+    gs = torch.randn(70_001, device=gpu)
+    outs = []
+    for _ in range(2):
+        with torch.autocast("cuda", dtype=torch.float16):
+            s, a = grid_field(x, 1.0, enc, layers)
+        gr = torch.autograd.grad((s * gs).sum() + a.float().sum(),
+                                 [enc.embeddings] + list(layers.parameters()))
+        outs.append([s, a] + list(gr))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
+def test_fused_field_empty(gpu):
+    from nerf.field import grid_field
+    enc, layers = _field(gpu)
+    x = torch.zeros(0, 3, device=gpu, requires_grad=False)
+    with torch.autocast("cuda", dtype=torch.float16):
+        s, a = grid_field(x, 1.0, enc, layers)
+    assert s.shape == (0,) and a.shape == (0, 3)
+    gr = torch.autograd.grad(s.sum() + a.float().sum(), list(layers.parameters()),
+                             allow_unused=True)
+    for t in gr:
+        assert t is None or torch.count_nonzero(t) == 0
