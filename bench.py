@@ -53,7 +53,7 @@ def make_trainer(res, seed, rank, world, fused):
     from nerf.network_grid import NeRFNetwork
     from nerf.provider import NeRFDataset
     from nerf.sd import SyntheticSDS
-    from nerf.utils import Trainer, seed_everything
+    from nerf.utils import Trainer, make_adam, seed_everything
 
     opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res),
                           "--guidance", "synthetic", "--seed", str(seed + rank)])
@@ -61,7 +61,7 @@ def make_trainer(res, seed, rank, world, fused):
     device = torch.device("cuda", torch.cuda.current_device())
     model = NeRFNetwork(opt)
     guidance = SyntheticSDS(device)
-    optimizer = lambda m: torch.optim.Adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)  # noqa
+    optimizer = lambda m: make_adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)  # noqa
     sched = lambda o: torch.optim.lr_scheduler.LambdaLR(o, lambda it: 0.1 ** min(it / opt.iters, 1))  # noqa
     trainer = Trainer("df", opt, model, guidance, device=device, workspace=None,
                       optimizer=optimizer, ema_decay=None, fp16=True, lr_scheduler=sched,

@@ -53,37 +53,44 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// LDS row strides (halves).  Operand reads put 16 lanes on 16 consecutive
+// rows; a row stride of 4 * odd dwords maps those rows to 16 distinct
+// 4-dword bank groups, so the 8-B / 16-B operand reads are conflict-free
+// (unpadded 64- and 128-B rows were 4- and 8-way conflicts).
+constexpr int kLd32 = 40;  // rows of 32 halves (+8)
+constexpr int kLd64 = 72;  // rows of 64 halves (+8)
+
 // Weights as f16 (autocast's cast of the f32 parameters), in LDS.
 struct Weights {
-    half_t w1[kHid * kIn];    // [n1][f]
-    half_t w2[kHid * kHid];   // [n2][n1]
-    half_t w3[16 * kHid];     // [o][n2], rows 4..15 zero
+    half_t w1[kHid * kLd32];  // [n1][f]
+    half_t w2[kHid * kLd64];  // [n2][n1]
+    half_t w3[16 * kLd64];    // [o][n2], rows 4..15 zero
     float b1[kHid], b2[kHid], b3[16];  // f32 of the f16-rounded biases; b3 rows 4.. zero
 };
 struct WeightsT {             // backward only
-    half_t w1t[kIn * kHid];   // [f][n1]
-    half_t w2t[kHid * kHid];  // [n1][n2]
-    half_t w3t[kHid * 32];    // [n2][o], o 4..31 zero
+    half_t w1t[kIn * kLd64];  // [f][n1]
+    half_t w2t[kHid * kLd64]; // [n1][n2]
+    half_t w3t[kHid * kLd32]; // [n2][o], o 4..31 zero
 };
 
 __device__ void load_weights(Weights &W, WeightsT *T, const float *w1, const float *b1,
                              const float *w2, const float *b2, const float *w3, const float *b3) {
     for (int i = threadIdx.x; i < kHid * kIn; i += blockDim.x) {
         const half_t v = (half_t)w1[i];
-        W.w1[i] = v;
-        if (T) T->w1t[(i % kIn) * kHid + i / kIn] = v;
+        W.w1[(i / kIn) * kLd32 + i % kIn] = v;
+        if (T) T->w1t[(i % kIn) * kLd64 + i / kIn] = v;
     }
     for (int i = threadIdx.x; i < kHid * kHid; i += blockDim.x) {
         const half_t v = (half_t)w2[i];
-        W.w2[i] = v;
-        if (T) T->w2t[(i % kHid) * kHid + i / kHid] = v;
+        W.w2[(i / kHid) * kLd64 + i % kHid] = v;
+        if (T) T->w2t[(i % kHid) * kLd64 + i / kHid] = v;
     }
     for (int i = threadIdx.x; i < 16 * kHid; i += blockDim.x)
-        W.w3[i] = i < kOut * kHid ? (half_t)w3[i] : (half_t)0.0f;
+        W.w3[(i / kHid) * kLd64 + i % kHid] = i < kOut * kHid ? (half_t)w3[i] : (half_t)0.0f;
     if (T)
         for (int i = threadIdx.x; i < kHid * 32; i += blockDim.x) {
             const int n2 = i / 32, o = i % 32;
-            T->w3t[i] = o < kOut ? (half_t)w3[o * kHid + n2] : (half_t)0.0f;
+            T->w3t[n2 * kLd32 + o] = o < kOut ? (half_t)w3[o * kHid + n2] : (half_t)0.0f;
         }
     for (int i = threadIdx.x; i < kHid; i += blockDim.x) {
         W.b1[i] = (float)(half_t)b1[i];
@@ -124,7 +131,7 @@ __device__ __forceinline__ void forward_tile(const Weights &W, half8 xb, int c, 
     f4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        acc[t] = mfma(a_nat(W.w1, kIn, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
+        acc[t] = mfma(a_nat(W.w1, kLd32, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const half_t v = (half_t)acc[t][r];
@@ -135,7 +142,7 @@ __device__ __forceinline__ void forward_tile(const Weights &W, half8 xb, int c, 
     for (int u = 0; u < 4; ++u) {
         f4 a = bias4(W.b2, 16 * u + 4 * h);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kHid, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
+        for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kLd64, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const half_t v = (half_t)a[r];
@@ -144,7 +151,7 @@ __device__ __forceinline__ void forward_tile(const Weights &W, half8 xb, int c, 
     }
     f4 o = bias4(W.b3, 4 * h);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) o = mfma(a_perm(W.w3, kHid, c, s, h), b_from_tiles(F.a2, s), o);
+    for (int s = 0; s < 2; ++s) o = mfma(a_perm(W.w3, kLd64, c, s, h), b_from_tiles(F.a2, s), o);
     F.o = o;
 }
 
@@ -174,13 +181,20 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     const uint32_t tiles = ceil_div(M, 16u);
-    for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles;
-         tile += waves) {
+    const uint32_t tile0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    half8 xb = tile0 < tiles ? load_x(enc, tile0 * 16 + c, M, h) : half8{};
+    for (uint32_t tile = tile0; tile < tiles; tile += waves) {
         const uint32_t sample = tile * 16 + c;
+        // prefetch the next tile's features while this one runs
+        const half8 xn = tile + waves < tiles ? load_x(enc, (tile + waves) * 16 + c, M, h) : half8{};
+        float x[3] = {0.0f, 0.0f, 0.0f};
+        if (h == 0 && sample < M)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) x[d] = xyz[(size_t)sample * 3 + d];
         Fwd F;
-        forward_tile(W, load_x(enc, sample, M, h), c, h, F);
+        forward_tile(W, xb, c, h, F);
+        xb = xn;
         if (h == 0 && sample < M) {
-            const float *x = xyz + (size_t)sample * 3;
             const float y = (float)(half_t)F.o[0] + gaussian(x);
             sigma[sample] = expf(y);
 #pragma unroll
@@ -194,15 +208,41 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
 
 // ------------------------------------------------------------------ backward
 struct Stage {                      // per-wave LDS image of one 32-sample group, [row][sample]
-    half_t x[kIn * 32];
-    half_t a1[kHid * 32];
-    half_t a2[kHid * 32];
-    half_t d1[kHid * 32];
-    half_t d2[kHid * 32];
-    half_t dO[16 * 32];             // rows 4..15 stay zero
+    half_t x[kIn * kLd32];
+    half_t a1[kHid * kLd32];
+    half_t a2[kHid * kLd32];
+    half_t d1[kHid * kLd32];
+    half_t d2[kHid * kLd32];
+    half_t dO[16 * kLd32];          // rows 4..15 stay zero
 };
 
 constexpr int kBwdWaves = 4;
+
+// One wave's inputs for a 32-sample group: encoder features (every lane), and
+// for the output-layer lanes (h == 0) positions and incoming gradients.
+template <typename rgb_t> struct GroupInT {
+    half8 xb[2];
+    float xyz[2][3], gs[2], grgb[2][3];
+};
+
+template <typename rgb_t>
+__device__ __forceinline__ void load_group_t(GroupInT<rgb_t> &g, uint32_t grp,
+                                             const half_t *enc, const float *xyz,
+                                             const float *grad_sigma, const rgb_t *grad_rgb,
+                                             uint32_t M, int c, int h) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t sample = grp * 32 + 16 * q + c;
+        g.xb[q] = load_x(enc, sample, M, h);
+        const bool v = (h == 0) && sample < M;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            g.xyz[q][d] = v ? xyz[(size_t)sample * 3 + d] : 0.0f;
+            g.grgb[q][d] = v ? (float)grad_rgb[(size_t)sample * 3 + d] : 0.0f;
+        }
+        g.gs[q] = v ? grad_sigma[sample] : 0.0f;
+    }
+}
 
 template <typename rgb_t>
 __global__ __launch_bounds__(256) void k_field_bwd(
@@ -211,13 +251,15 @@ __global__ __launch_bounds__(256) void k_field_bwd(
     const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t M,
     half_t *__restrict__ d_enc,     // [16, M, 2] (level-major)
     float *__restrict__ partial) {  // [gridDim.x, kParams]
+    typedef GroupInT<rgb_t> GroupIn;
+    auto load_group = load_group_t<rgb_t>;
     __shared__ Weights W;
     __shared__ WeightsT T;
     __shared__ Stage stage[kBwdWaves];
     load_weights(W, &T, w1, b1, w2, b2, w3, b3);
     const int wave = threadIdx.x >> 6;
     Stage &S = stage[wave];
-    for (int i = threadIdx.x & 63; i < 16 * 32; i += 64) S.dO[i] = (half_t)0.0f;
+    for (int i = threadIdx.x & 63; i < 16 * kLd32; i += 64) S.dO[i] = (half_t)0.0f;
     __syncthreads();
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
 
@@ -230,17 +272,27 @@ __global__ __launch_bounds__(256) void k_field_bwd(
 #pragma unroll
         for (int j = 0; j < 4; ++j) gw2[i][j] = f4{0, 0, 0, 0};
     }
-    float gb1 = 0.0f, gb2 = 0.0f, gb3 = 0.0f;  // bias grads of neuron `lane`
+    // bias gradients: per-lane sums of the lane's own D-layout values (neuron
+    // 16 t + 4 h + r of sample c), reduced over the 16 sample lanes at the end
+    float gb1[4][4] = {}, gb2[4][4] = {}, gb3[4] = {};
 
     const uint32_t groups = ceil_div(M, 32u);
-    for (uint32_t grp = blockIdx.x * kBwdWaves + wave; grp < groups;
-         grp += gridDim.x * kBwdWaves) {
+    const uint32_t gstride = gridDim.x * kBwdWaves;
+    // the next group's inputs are loaded while this one is processed (one
+    // wave per SIMD cannot hide HBM latency otherwise)
+    GroupIn cur;
+    const uint32_t grp0 = blockIdx.x * kBwdWaves + wave;
+    if (grp0 < groups) load_group(cur, grp0, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    for (uint32_t grp = grp0; grp < groups; grp += gstride) {
+        GroupIn nxt;
+        if (grp + gstride < groups)
+            load_group(nxt, grp + gstride, enc, xyz, grad_sigma, grad_rgb, M, c, h);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int col = 16 * q + c;  // column in the 32-sample stage
             const uint32_t sample = grp * 32 + col;
             const bool valid = sample < M;
-            const half8 xb = load_x(enc, sample, M, h);
+            const half8 xb = cur.xb[q];
             Fwd F;
             forward_tile(W, xb, c, h, F);
             // dL/d(output layer), f16 as autocast's backward produces it
@@ -248,27 +300,27 @@ __global__ __launch_bounds__(256) void k_field_bwd(
             if (h == 0) {
                 half_t dO[4] = {(half_t)0.0f, (half_t)0.0f, (half_t)0.0f, (half_t)0.0f};
                 if (valid) {
-                    const float y = (float)(half_t)F.o[0] + gaussian(xyz + (size_t)sample * 3);
+                    const float y = (float)(half_t)F.o[0] + gaussian(cur.xyz[q]);
                     // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
                     const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
-                    dO[0] = (half_t)(grad_sigma[sample] * expf(yc));
+                    dO[0] = (half_t)(cur.gs[q] * expf(yc));
 #pragma unroll
                     for (int r = 1; r < 4; ++r) {
                         const float a = (float)(half_t)(1.0f / (1.0f + expf(-(float)(half_t)F.o[r])));
-                        const float g = (float)(half_t)grad_rgb[(size_t)sample * 3 + r - 1];
+                        const float g = (float)(half_t)cur.grgb[q][r - 1];
                         dO[r] = (half_t)(g * (1.0f - a) * a);  // sigmoid_backward in f16 (opmath f32)
                     }
                 }
                 dob = half8{dO[0], dO[1], dO[2], dO[3], (half_t)0.0f, (half_t)0.0f, (half_t)0.0f,
                             (half_t)0.0f};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) S.dO[r * 32 + col] = dO[r];
+                for (int r = 0; r < 4; ++r) S.dO[r * kLd32 + col] = dO[r];
             }
             // hidden layer 2: dA2^T = W3^T dO^T, ReLU mask
             half_t dz2[4][4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const f4 d = mfma(a_nat(T.w3t, 32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
+                const f4 d = mfma(a_nat(T.w3t, kLd32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     dz2[u][r] = F.a2[u][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
@@ -280,7 +332,7 @@ __global__ __launch_bounds__(256) void k_field_bwd(
                 f4 d = f4{0, 0, 0, 0};
 #pragma unroll
                 for (int s = 0; s < 2; ++s)
-                    d = mfma(a_perm(T.w2t, kHid, 16 * t + c, s, h), b_from_tiles(dz2, s), d);
+                    d = mfma(a_perm(T.w2t, kLd64, 16 * t + c, s, h), b_from_tiles(dz2, s), d);
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     dz1[t][r] = F.a1[t][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
@@ -291,7 +343,7 @@ __global__ __launch_bounds__(256) void k_field_bwd(
                 f4 d = f4{0, 0, 0, 0};
 #pragma unroll
                 for (int s = 0; s < 2; ++s)
-                    d = mfma(a_perm(T.w1t, kHid, 16 * f + c, s, h), b_from_tiles(dz1, s), d);
+                    d = mfma(a_perm(T.w1t, kLd64, 16 * f + c, s, h), b_from_tiles(dz1, s), d);
                 if (valid) {
                     // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
                     const uint32_t lv = 8 * f + 2 * h;
@@ -304,46 +356,38 @@ __global__ __launch_bounds__(256) void k_field_bwd(
             }
             // stage [row][sample] images for the weight gradients
 #pragma unroll
-            for (int j = 0; j < 8; ++j) S.x[(8 * h + j) * 32 + col] = xb[j];
+            for (int j = 0; j < 8; ++j) S.x[(8 * h + j) * kLd32 + col] = xb[j];
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = (16 * t + 4 * h + r) * 32 + col;
+                    const int row = (16 * t + 4 * h + r) * kLd32 + col;
                     S.a1[row] = F.a1[t][r];
                     S.a2[row] = F.a2[t][r];
                     S.d1[row] = dz1[t][r];
                     S.d2[row] = dz2[t][r];
+                    gb1[t][r] += (float)dz1[t][r];
+                    gb2[t][r] += (float)dz2[t][r];
                 }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gb3[r] += (float)dob[r];
         }
         wave_lds_sync();
         // weight gradients over the group's 32 samples (k = sample)
 #pragma unroll
         for (int tn = 0; tn < 4; ++tn) {
-            const half8 a_d1 = a_nat(S.d1, 32, 16 * tn + c, 0, h);
-            const half8 a_d2 = a_nat(S.d2, 32, 16 * tn + c, 0, h);
+            const half8 a_d1 = a_nat(S.d1, kLd32, 16 * tn + c, 0, h);
+            const half8 a_d2 = a_nat(S.d2, kLd32, 16 * tn + c, 0, h);
 #pragma unroll
             for (int tf = 0; tf < 2; ++tf)
-                gw1[tn][tf] = mfma(a_d1, a_nat(S.x, 32, 16 * tf + c, 0, h), gw1[tn][tf]);
+                gw1[tn][tf] = mfma(a_d1, a_nat(S.x, kLd32, 16 * tf + c, 0, h), gw1[tn][tf]);
 #pragma unroll
             for (int tm = 0; tm < 4; ++tm)
-                gw2[tn][tm] = mfma(a_d2, a_nat(S.a1, 32, 16 * tm + c, 0, h), gw2[tn][tm]);
-            gw3[tn] = mfma(a_nat(S.dO, 32, c, 0, h), a_nat(S.a2, 32, 16 * tn + c, 0, h), gw3[tn]);
-        }
-        // bias gradients: lane n sums row n over the 32 samples
-        {
-            float s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 32; ++k) {
-                s1 += (float)S.d1[lane * 32 + k];
-                s2 += (float)S.d2[lane * 32 + k];
-                s3 += (float)S.dO[(lane & 15) * 32 + k];
-            }
-            gb1 += s1;
-            gb2 += s2;
-            gb3 += s3;
+                gw2[tn][tm] = mfma(a_d2, a_nat(S.a1, kLd32, 16 * tm + c, 0, h), gw2[tn][tm]);
+            gw3[tn] = mfma(a_nat(S.dO, kLd32, c, 0, h), a_nat(S.a2, kLd32, 16 * tn + c, 0, h), gw3[tn]);
         }
         wave_lds_sync();  // the stage is rewritten by the next group
+        cur = nxt;
     }
 
     // ---- fixed-order workgroup reduction -> partial[blockIdx.x]
@@ -375,14 +419,32 @@ __global__ __launch_bounds__(256) void k_field_bwd(
                         dst = first ? gw3[tn][r] : dst + gw3[tn][r];
                     }
             }
-            {
-                float &d1 = red[kOffB1 + lane];
-                d1 = first ? gb1 : d1 + gb1;
-                float &d2 = red[kOffB2 + lane];
-                d2 = first ? gb2 : d2 + gb2;
-                if (lane < kOut) {
-                    float &d3 = red[kOffB3 + lane];
-                    d3 = first ? gb3 : d3 + gb3;
+            // bias: sum over the 16 sample lanes (c) of each lane group
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v1 = gb1[t][r], v2 = gb2[t][r];
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) {
+                        v1 += __shfl_xor(v1, o, 64);
+                        v2 += __shfl_xor(v2, o, 64);
+                    }
+                    if (c == 0) {
+                        float &d1 = red[kOffB1 + 16 * t + 4 * h + r];
+                        d1 = first ? v1 : d1 + v1;
+                        float &d2 = red[kOffB2 + 16 * t + 4 * h + r];
+                        d2 = first ? v2 : d2 + v2;
+                    }
+                }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v3 = gb3[r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) v3 += __shfl_xor(v3, o, 64);
+                if (lane == 0) {
+                    float &d3 = red[kOffB3 + r];
+                    d3 = first ? v3 : d3 + v3;
                 }
             }
         }

@@ -77,7 +77,7 @@ def main(argv=None):
     from nerf.network_grid import NeRFNetwork
     from nerf.provider import NeRFDataset
     from nerf.sd import StableDiffusion, SyntheticSDS
-    from nerf.utils import Trainer, seed_everything
+    from nerf.utils import Trainer, make_adam, seed_everything
 
     opt = parse_opt(argv)
     if opt.backbone != "grid":
@@ -94,7 +94,7 @@ def main(argv=None):
         return
     train_loader = NeRFDataset(opt, device=device, type="train", H=opt.h, W=opt.w,
                                size=100).dataloader()
-    optimizer = lambda m: torch.optim.Adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)
+    optimizer = lambda m: make_adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)
     scheduler = lambda o: torch.optim.lr_scheduler.LambdaLR(o, lambda it: 0.1 ** min(it / opt.iters, 1))
     guidance = (SyntheticSDS(device) if opt.guidance == "synthetic" else StableDiffusion(device))
     trainer = Trainer("df", opt, model, guidance, device=device, workspace=opt.workspace,

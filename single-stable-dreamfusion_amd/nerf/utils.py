@@ -116,6 +116,21 @@ def flat_allreduce_(params, world_size, group=None):
     assert off == flat.numel() and flat.device == dev
 
 
+def make_adam(params, **kw):
+    """torch.optim.Adam as the reference builds it (main.py: betas (0.9, 0.99),
+    eps 1e-15), as the single-kernel fused implementation when every
+    parameter is on the GPU: it takes GradScaler's scale and inf flag on the
+    device, so scaler.step() needs no host synchronisation (the foreach
+    Adam + GradScaler path reads found_inf on the host every step)."""
+    groups = []
+    for g in params:  # materialise generators (e.g. module.parameters() in get_params groups)
+        groups.append(dict(g, params=list(g["params"])) if isinstance(g, dict) else g)
+    flat = [p for g in groups for p in (g["params"] if isinstance(g, dict) else [g])]
+    if flat and all(p.is_cuda for p in flat):
+        kw.setdefault("fused", True)
+    return torch.optim.Adam(groups, **kw)
+
+
 class _EMA:
     """Exponential moving average of parameters (stand-in for torch_ema)."""
 
@@ -181,7 +196,7 @@ class Trainer(object):
         self.criterion = criterion
 
         if optimizer is None:
-            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=0.001, weight_decay=5e-4)
+            self.optimizer = make_adam(self.model.parameters(), lr=0.001, weight_decay=5e-4)
         else:
             self.optimizer = optimizer(self.model)
         if lr_scheduler is None:

@@ -152,7 +152,7 @@ def test_gpu_encoders_golden(gpu):
     _raymarching.morton3D(c, c.shape[0], idx)
     _eq(idx.cpu(), G["morton_indices"])
     bits = torch.empty(G["pack_bits"].shape[0], dtype=torch.uint8, device=gpu)
-    _raymarching.packbits(_t(G["pack_grid"], gpu), G["pack_grid"].size, 1.0, bits)
+    _raymarching.packbits(_t(G["pack_grid"], gpu), bits.shape[0], 1.0, bits)  # N = bytes
     _eq(bits.cpu(), G["pack_bits"])
 
     x, offs = _t(G["grid_inputs"], gpu), _t(G["grid_offsets"], gpu)

@@ -81,6 +81,7 @@ def test_fused_backward_equals_two_pass(gpu):
 
 def test_train_iterations_run(gpu):
     trainer, data = _trainer(gpu, True, seed=1)
+    before = [p.detach().clone() for p in trainer.model.parameters() if p.requires_grad]
     losses = []
     for _ in range(20):
         loss = trainer.train_iteration(data.collate([0]))
@@ -91,6 +92,11 @@ def test_train_iterations_run(gpu):
     assert int(m.density_bitfield.count_nonzero()) > 0
     for p in m.parameters():
         assert torch.isfinite(p).all()
+    # every trainable tensor (encoder, sigma_net, bg_net) was updated by Adam
+    after = [p.detach() for p in m.parameters() if p.requires_grad]
+    assert len(after) == len(before) and len(after) >= 8
+    for a, b in zip(after, before):
+        assert not torch.equal(a, b)
 
 
 def test_inference_render(gpu):

@@ -131,3 +131,15 @@ def test_sh_table_matches_oracle():
             q = terms[(l * l + l + m, m)]
             np.testing.assert_allclose(rows[k][:len(q)], q, rtol=1e-7)
             k += 1
+
+
+def test_make_adam_keeps_generator_groups():
+    """get_params() hands Adam generator-valued groups; make_adam must not
+    consume them while deciding on the fused implementation."""
+    import torch.nn as nn
+    from nerf.utils import make_adam
+    a, b = nn.Linear(3, 4), nn.Linear(4, 2)
+    opt = make_adam([{"params": a.parameters(), "lr": 1e-2}, {"params": b.parameters(), "lr": 1e-3}],
+                    betas=(0.9, 0.99), eps=1e-15)
+    assert [len(g["params"]) for g in opt.param_groups] == [2, 2]
+    assert opt.param_groups[0]["lr"] == 1e-2

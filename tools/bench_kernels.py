@@ -114,6 +114,27 @@ def main():
         out["grid_bwd_atomic_f16_us"] = timeit(lambda: _gridencoder.grid_encode_backward_blc(
             g, x01, offs, gatom, B, 3, 2, 16, S, 16, None, None, 1, False), max(3, args.reps // 4))
 
+    # -------------------------------------------------------------- field MLP
+    if want("field"):
+        import _fieldmlp
+        enc16 = (torch.randn(B, 32, device=dev) * 0.5).half()
+        xw = (torch.rand(B, 3, device=dev) * 2 - 1)
+        torch.manual_seed(0)
+        ws = [torch.randn(64, 32, device=dev) * 0.2, torch.randn(64, device=dev) * 0.1,
+              torch.randn(64, 64, device=dev) * 0.15, torch.randn(64, device=dev) * 0.1,
+              torch.randn(4, 64, device=dev) * 0.15, torch.randn(4, device=dev) * 0.1]
+        sig = torch.empty(B, device=dev)
+        alb = torch.empty(B, 3, device=dev, dtype=torch.half)
+        out["field_fwd_us"] = timeit(lambda: _fieldmlp.field_mlp_forward(enc16, xw, ws, sig, alb),
+                                     args.reps)
+        gsig = torch.randn(B, device=dev)
+        galb = torch.randn(B, 3, device=dev).half()
+        denc = torch.empty(16, B, 2, device=dev, dtype=torch.half)
+        part = torch.empty(_fieldmlp.backward_parts(B) * _fieldmlp.params_count(), device=dev)
+        grads = [torch.empty_like(w) for w in ws]
+        out["field_bwd_us"] = timeit(lambda: _fieldmlp.field_mlp_backward(
+            enc16, xw, ws, gsig, galb, denc, part, grads), args.reps)
+
     # -------------------------------------------------------------- composite
     if want("composite"):
         sig = torch.rand(B, device=dev) * 30
