@@ -120,6 +120,8 @@ def summarize_kernels(records):
 # timed region -> the kernel symbols launched inside it (for PMC traffic)
 REGION_KERNELS = {
     "grid_encode_backward": ("k_grid_bwd_sliced", "k_sum_partials"),
+    "grid_field_forward": ("k_field_fwd_fused",),
+    "field_mlp_backward": ("k_field_bwd", "k_field_wgrad_sum"),
     "grid_encode_forward": ("k_grid_fwd",),
     "march_rays_train_count": ("k_march_train_count",),
     "march_rays_train_emit": ("k_march_train_emit",),

@@ -220,6 +220,18 @@ int dfhip_grid_encode_backward_blc(int grad_dtype, int acc_dtype, const void *gr
                                    uint32_t gridtype, int align_corners,
                                    dfhip_stream_t stream);
 
+/* As dfhip_grid_encode_backward_sliced, for capacity-sized buffers: grad is
+ * [L, B, C] with B the capacity (plane stride), only samples [0, *m_dev) are
+ * walked when m_dev is given, and with bound > 0 `inputs` are raw positions in
+ * [-bound, bound] mapped to [0, 1] as grid.py:142 (bound == 0: already [0,1]). */
+int dfhip_grid_encode_backward_sliced_dyn(int grad_dtype, int out_dtype, const void *grad,
+                                          const float *inputs, float bound,
+                                          const int32_t *offsets, void *grad_embeddings,
+                                          uint32_t total_rows, uint32_t B, const int32_t *m_dev,
+                                          uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                                          uint32_t gridtype, int align_corners, float *partial,
+                                          uint32_t parts, int accumulate, dfhip_stream_t stream);
+
 /* Sliced embedding backward (native, no global atomics): the table's rows are
  * cut into LDS-sized slices; workgroup (slice, part) accumulates the corner
  * contributions of its part of the samples that land in its slice with LDS
@@ -290,6 +302,36 @@ int dfhip_field_mlp_backward(const void *enc, const float *xyz, const float *w1,
                              uint32_t M, void *d_enc_lbc, float *partial, uint32_t parts,
                              float *gw1, float *gb1, float *gw2, float *gb2, float *gw3,
                              float *gb3, int accumulate, dfhip_stream_t stream);
+
+/* Fused grid field (native path of nerf/field.py): tiled-grid encoding
+ * (gridencoder.cu:75-178 arithmetic, f16 table) + the MLP/heads above in ONE
+ * kernel.  xyz: [cap, 3] f32 in [-bound, bound] (mapped to [0,1] as
+ * grid.py:142); table: [rows, 2] f16; L must be 16 (C = 2, D = 3).  Only
+ * samples [0, *m_dev) are processed when m_dev (device int32, e.g. the
+ * march's counter[0]) is given, else [0, cap): no host round trip is needed
+ * to size the batch.  enc (nullable): [cap, 32] f16 features in the kernel's
+ * permuted order, saved for dfhip_grid_field_backward. */
+int dfhip_grid_field_forward(const float *xyz, float bound, const void *table,
+                             const int32_t *offsets, uint32_t L, float S, uint32_t H,
+                             uint32_t gridtype, int align_corners, const float *w1,
+                             const float *b1, const float *w2, const float *b2, const float *w3,
+                             const float *b3, void *enc, float *sigma, void *rgb, int rgb_dtype,
+                             uint32_t cap, const int32_t *m_dev, dfhip_stream_t stream);
+/* Backward of dfhip_grid_field_forward: MLP backward (d_enc_lbc [16, cap, 2] f16
+ * scratch, mlp_partial: dfhip_field_mlp_backward_parts(cap) * params floats),
+ * f32 weight gradients (overwritten), then the sliced embedding backward into
+ * grad_embeddings [total_rows, 2] f32 (overwritten; nullable to skip) with
+ * grid_partial: dfhip_grid_backward_partial_floats(total_rows, 2, grid_parts). */
+int dfhip_grid_field_backward(const void *enc, const float *xyz, float bound, const float *w1,
+                              const float *b1, const float *w2, const float *b2,
+                              const float *w3, const float *b3, const float *grad_sigma,
+                              const void *grad_rgb, int grad_rgb_dtype, uint32_t cap,
+                              const int32_t *m_dev, void *d_enc_lbc, float *mlp_partial,
+                              uint32_t mlp_parts, float *gw1, float *gb1, float *gw2, float *gb2,
+                              float *gw3, float *gb3, const int32_t *offsets,
+                              uint32_t total_rows, uint32_t L, float S, uint32_t H,
+                              uint32_t gridtype, int align_corners, float *grad_embeddings,
+                              float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream);
 
 #ifdef __cplusplus
 }

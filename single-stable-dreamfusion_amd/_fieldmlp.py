@@ -63,3 +63,52 @@ def field_mlp_backward(enc, xyz, weights, grad_sigma, grad_rgb, d_enc_lbc, parti
     call("dfhip_field_mlp_backward", ptr(enc), ptr(xyz), *_weights(weights), ptr(grad_sigma),
          ptr(grad_rgb), _d.dtype_code(grad_rgb, "grad_rgb"), M, ptr(d_enc_lbc), ptr(partial),
          backward_parts(M) if M else 1, *gp, int(bool(accumulate)), stream())
+
+
+# ---- fused grid field (encoding + MLP in one kernel; device-side sample count)
+
+def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners, weights, enc,
+                       sigma, rgb, m_dev=None):
+    """xyz [cap, 3] f32 in [-bound, bound]; table [rows, 2] f16; offsets [17]
+    int32.  Writes sigma [cap] f32, rgb [cap, 3] (f16/f32) and, when given,
+    enc [cap, 32] f16 (permuted feature order, for grid_field_backward).  Only
+    rows [0, m_dev[0]) are computed when m_dev (int32 device tensor) is given."""
+    cap = xyz.shape[0]
+    _f32(xyz, "xyz")
+    checked(table, "table")
+    if table.dtype != torch.float16 or table.dim() != 2 or table.shape[1] != 2:
+        raise RuntimeError("table must be a [rows, 2] float16 tensor")
+    checked(offsets, "offsets", "int")
+    _f32(sigma, "sigma")
+    checked(rgb, "rgb")
+    if enc is not None:
+        checked(enc, "enc")
+    if m_dev is not None:
+        checked(m_dev, "m_dev", "int")
+    call("dfhip_grid_field_forward", ptr(xyz), float(bound), ptr(table), ptr(offsets),
+         offsets.shape[0] - 1, float(S), int(H), int(gridtype), int(bool(align_corners)),
+         *_weights(weights), ptr(enc), ptr(sigma), ptr(rgb), _d.dtype_code(rgb, "rgb"), cap,
+         ptr(m_dev), stream())
+
+
+def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lbc, mlp_partial,
+                        grads, offsets, total_rows, S, H, gridtype, align_corners,
+                        grad_embeddings, grid_partial, grid_parts, m_dev=None):
+    cap = xyz.shape[0]
+    for t, n in ((enc, "enc"), (grad_rgb, "grad_rgb"), (d_enc_lbc, "d_enc")):
+        checked(t, n)
+    _f32(xyz, "xyz")
+    _f32(grad_sigma, "grad_sigma")
+    _f32(mlp_partial, "mlp_partial")
+    if grad_embeddings is not None:
+        _f32(grad_embeddings, "grad_embeddings")
+        _f32(grid_partial, "grid_partial")
+    if m_dev is not None:
+        checked(m_dev, "m_dev", "int")
+    gp = _weights(grads)
+    call("dfhip_grid_field_backward", ptr(enc), ptr(xyz), float(bound), *_weights(weights),
+         ptr(grad_sigma), ptr(grad_rgb), _d.dtype_code(grad_rgb, "grad_rgb"), cap, ptr(m_dev),
+         ptr(d_enc_lbc), ptr(mlp_partial), backward_parts(cap) if cap else 1, *gp,
+         ptr(offsets), int(total_rows), offsets.shape[0] - 1, float(S), int(H), int(gridtype),
+         int(bool(align_corners)), ptr(grad_embeddings), ptr(grid_partial), int(grid_parts),
+         stream())

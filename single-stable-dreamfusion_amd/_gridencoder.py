@@ -83,3 +83,22 @@ def grid_encode_backward_sliced(grad_lbc, inputs, offsets, grad_embeddings, tota
          _d.dtype_code(grad_embeddings, "grad_embeddings"), ptr(grad_lbc), ptr(inputs),
          ptr(offsets), ptr(grad_embeddings), total_rows, B, D, C, L, S, H, gridtype,
          int(bool(align_corners)), ptr(partial), parts, int(bool(accumulate)), stream())
+
+
+def grid_encode_backward_sliced_dyn(grad_lbc, inputs, bound, offsets, grad_embeddings, total_rows,
+                                    B, m_dev, D, C, L, S, H, gridtype, align_corners, partial,
+                                    parts, accumulate=False):
+    """Capacity form: grad_lbc [L, B, C] with B the capacity; rows [0, m_dev[0])
+    walked; inputs raw positions in [-bound, bound] when bound > 0."""
+    checked(grad_lbc, "grad")
+    checked(inputs, "inputs")
+    checked(offsets, "offsets", "int")
+    checked(grad_embeddings, "grad_embeddings")
+    checked(partial, "partial")
+    if m_dev is not None:
+        checked(m_dev, "m_dev", "int")
+    call("dfhip_grid_encode_backward_sliced_dyn", _d.dtype_code(grad_lbc, "grad"),
+         _d.dtype_code(grad_embeddings, "grad_embeddings"), ptr(grad_lbc), ptr(inputs),
+         float(bound), ptr(offsets), ptr(grad_embeddings), total_rows, B, ptr(m_dev), D, C, L, S,
+         H, gridtype, int(bool(align_corners)), ptr(partial), parts, int(bool(accumulate)),
+         stream())

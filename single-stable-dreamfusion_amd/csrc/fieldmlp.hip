@@ -28,6 +28,7 @@
 // of the activations.  Per-workgroup partial sums + a fixed-order reduction
 // make the weight gradients deterministic.
 #include "common.h"
+#include "grid_common.h"
 
 namespace dfhip {
 namespace fm {
@@ -73,12 +74,22 @@ struct WeightsT {             // backward only
     half_t w3t[kHid * kLd32]; // [n2][o], o 4..31 zero
 };
 
+// Feature order of the fused path: position p = 8h + j of the layer-1 B
+// operand holds level 4 (j >> 1) + h, channel j & 1, so that for each j the
+// four lane groups work on four levels of the same kind (dense / tiled /
+// z-dropped): feature index 2 * level + channel.
+__host__ __device__ constexpr int perm_feature(int p) {
+    return 2 * (4 * ((p & 7) >> 1) + (p >> 3)) + (p & 1);
+}
+
+// PERM: layer-1 weights stored in the fused path's permuted feature order.
+template <bool PERM>
 __device__ void load_weights(Weights &W, WeightsT *T, const float *w1, const float *b1,
                              const float *w2, const float *b2, const float *w3, const float *b3) {
     for (int i = threadIdx.x; i < kHid * kIn; i += blockDim.x) {
-        const half_t v = (half_t)w1[i];
-        W.w1[(i / kIn) * kLd32 + i % kIn] = v;
-        if (T) T->w1t[(i % kIn) * kLd64 + i / kIn] = v;
+        const int n = i / kIn, p = i % kIn;
+        W.w1[n * kLd32 + p] = (half_t)w1[n * kIn + (PERM ? perm_feature(p) : p)];
+        if (T) T->w1t[(i % kIn) * kLd64 + i / kIn] = (half_t)w1[i];  // natural: rows = features
     }
     for (int i = threadIdx.x; i < kHid * kHid; i += blockDim.x) {
         const half_t v = (half_t)w2[i];
@@ -166,7 +177,111 @@ __device__ __forceinline__ half8 load_x(const half_t *enc, uint32_t sample, uint
     return *reinterpret_cast<const half8 *>(enc + (size_t)sample * kIn + 8 * h);
 }
 
+// Grid features of one sample at levels 4(j >> 1) + h (j = 0..7, channel
+// j & 1) in the permuted order above: exactly k_grid_fwd<half, 3, 2>'s
+// arithmetic (gridencoder.cu:75-178: half accumulators rounded per corner),
+// with the trailing-dim corners of z-dropped tiled levels gathered once.
+__device__ __forceinline__ half8 grid_features(const half_t *__restrict__ table,
+                                               const int32_t *__restrict__ offsets,
+                                               const ge::Levels &lv, uint32_t gridtype,
+                                               bool align, const float (&x)[3], int h) {
+    half8 out{};
+    if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
+        return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t l = 4 * q + h;
+        const ge::LevelCtx c = ge::level_ctx<3>(offsets, lv, l, gridtype, align);
+        const uint32_t *tab = reinterpret_cast<const uint32_t *>(table + (size_t)c.base * 2);
+        float frac[3];
+        uint32_t cell[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float p = fmaf(x[d], c.scale, align ? 0.0f : 0.5f);
+            cell[d] = (uint32_t)floorf(p);
+            frac[d] = p - (float)cell[d];
+        }
+        const uint32_t lead = (!c.hashed) ? c.used : 3u;
+        const uint32_t lead_mask = (1u << lead) - 1u;
+        uint32_t row_bits[8];
+        half_t a0 = (half_t)0.0f, a1 = (half_t)0.0f;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            float w = 1.0f;
+            uint32_t p[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                if (k & (1u << d)) { w *= frac[d]; p[d] = cell[d] + 1u; }
+                else { w *= 1.0f - frac[d]; p[d] = cell[d]; }
+            }
+            if ((k & ~lead_mask) == 0) row_bits[k] = tab[ge::row_index<3>(c, p)];
+            else row_bits[k] = row_bits[k & lead_mask];
+            half_t v[2];
+            __builtin_memcpy(v, &row_bits[k], 4);
+            ge::acc_corner(a0, w, v[0]);
+            ge::acc_corner(a1, w, v[1]);
+        }
+        out[2 * q] = a0;
+        out[2 * q + 1] = a1;
+    }
+    return out;
+}
+
+__device__ __forceinline__ uint32_t active_count(const int32_t *m_dev, uint32_t cap) {
+    if (!m_dev) return cap;
+    const int32_t m = *m_dev;
+    return m < 0 ? 0u : ((uint32_t)m < cap ? (uint32_t)m : cap);
+}
+
 // ------------------------------------------------------------------ forward
+// Grid encoding + MLP + heads in one pass: a wave takes 16 samples; lane
+// group h gathers levels {h, h+4, h+8, h+12} of its sample (32 independent
+// table loads in flight per lane), the features go straight into the MLP's
+// B operand, and are also written (permuted order, 16 B per lane) for the
+// backward.  xyz in [-bound, bound] is mapped to [0, 1] as grid.py:142 does.
+template <typename rgb_t>
+__global__ __launch_bounds__(256) void k_field_fwd_fused(
+    const float *__restrict__ xyz, float bound, const half_t *__restrict__ table,
+    const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
+    const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+    const float *b3, half_t *__restrict__ enc, float *__restrict__ sigma,
+    rgb_t *__restrict__ rgb, uint32_t cap, const int32_t *__restrict__ m_dev) {
+    __shared__ Weights W;
+    load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
+    __syncthreads();
+    const uint32_t M = active_count(m_dev, cap);
+    const bool align = align_corners != 0;
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t tiles = ceil_div(M, 16u);
+    for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles;
+         tile += waves) {
+        const uint32_t sample = tile * 16 + c;
+        const bool valid = sample < M;
+        float x[3] = {0.0f, 0.0f, 0.0f}, x01[3] = {-1.0f, -1.0f, -1.0f};
+        if (valid)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                x[d] = xyz[(size_t)sample * 3 + d];
+                x01[d] = (x[d] + bound) / (2.0f * bound);
+            }
+        const half8 xb = valid ? grid_features(table, offsets, lv, gridtype, align, x01, h)
+                               : half8{};
+        if (enc && valid) *reinterpret_cast<half8 *>(enc + (size_t)sample * kIn + 8 * h) = xb;
+        Fwd F;
+        forward_tile(W, xb, c, h, F);
+        if (h == 0 && valid) {
+            const float y = (float)(half_t)F.o[0] + gaussian(x);
+            sigma[sample] = expf(y);
+#pragma unroll
+            for (int r = 1; r < 4; ++r) {
+                const float v = (float)(half_t)F.o[r];
+                rgb[(size_t)sample * 3 + r - 1] = (rgb_t)(half_t)(1.0f / (1.0f + expf(-v)));
+            }
+        }
+    }
+}
+
 template <typename rgb_t>
 __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ enc,
                                                    const float *__restrict__ xyz,
@@ -176,7 +291,7 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
                                                    float *__restrict__ sigma,
                                                    rgb_t *__restrict__ rgb, uint32_t M) {
     __shared__ Weights W;
-    load_weights(W, nullptr, w1, b1, w2, b2, w3, b3);
+    load_weights<false>(W, nullptr, w1, b1, w2, b2, w3, b3);
     __syncthreads();
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
@@ -244,19 +359,24 @@ __device__ __forceinline__ void load_group_t(GroupInT<rgb_t> &g, uint32_t grp,
     }
 }
 
-template <typename rgb_t>
+// PERM: enc holds the fused forward's permuted feature order (k_field_fwd_fused);
+// otherwise the natural [M, 32] encoder output.  M = *m_dev (clamped to cap)
+// when m_dev is given; d_enc is [16, cap, 2].
+template <typename rgb_t, bool PERM>
 __global__ __launch_bounds__(256) void k_field_bwd(
     const half_t *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
     const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
-    const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t M,
-    half_t *__restrict__ d_enc,     // [16, M, 2] (level-major)
+    const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t cap,
+    const int32_t *__restrict__ m_dev,
+    half_t *__restrict__ d_enc,     // [16, cap, 2] (level-major)
     float *__restrict__ partial) {  // [gridDim.x, kParams]
     typedef GroupInT<rgb_t> GroupIn;
     auto load_group = load_group_t<rgb_t>;
     __shared__ Weights W;
     __shared__ WeightsT T;
     __shared__ Stage stage[kBwdWaves];
-    load_weights(W, &T, w1, b1, w2, b2, w3, b3);
+    load_weights<PERM>(W, &T, w1, b1, w2, b2, w3, b3);
+    const uint32_t M = active_count(m_dev, cap);
     const int wave = threadIdx.x >> 6;
     Stage &S = stage[wave];
     for (int i = threadIdx.x & 63; i < 16 * kLd32; i += 64) S.dO[i] = (half_t)0.0f;
@@ -348,9 +468,9 @@ __global__ __launch_bounds__(256) void k_field_bwd(
                     // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
                     const uint32_t lv = 8 * f + 2 * h;
                     typedef _Float16 half2v __attribute__((ext_vector_type(2)));
-                    *reinterpret_cast<half2v *>(d_enc + ((size_t)lv * M + sample) * 2) =
+                    *reinterpret_cast<half2v *>(d_enc + ((size_t)lv * cap + sample) * 2) =
                         half2v{(half_t)d[0], (half_t)d[1]};
-                    *reinterpret_cast<half2v *>(d_enc + ((size_t)(lv + 1) * M + sample) * 2) =
+                    *reinterpret_cast<half2v *>(d_enc + ((size_t)(lv + 1) * cap + sample) * 2) =
                         half2v{(half_t)d[2], (half_t)d[3]};
                 }
             }
@@ -403,7 +523,8 @@ __global__ __launch_bounds__(256) void k_field_bwd(
                     const int n = 16 * tn + 4 * h + r;
 #pragma unroll
                     for (int tf = 0; tf < 2; ++tf) {
-                        float &dst = red[kOffW1 + n * kIn + 16 * tf + c];
+                        const int p = 16 * tf + c;  // layer-1 input position
+                        float &dst = red[kOffW1 + n * kIn + (PERM ? perm_feature(p) : p)];
                         dst = first ? gw1[tn][tf][r] : dst + gw1[tn][tf][r];
                     }
 #pragma unroll
@@ -454,15 +575,25 @@ __global__ __launch_bounds__(256) void k_field_bwd(
     for (int i = threadIdx.x; i < kParams; i += blockDim.x) out[i] = red[i];
 }
 
-// Sum the per-workgroup partials (fixed order) into the six f32 gradients.
-__global__ __launch_bounds__(256) void k_field_wgrad_sum(const float *__restrict__ partial,
-                                                         uint32_t parts, float *gw1, float *gb1,
-                                                         float *gw2, float *gb2, float *gw3,
-                                                         float *gb3, int accumulate) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= kParams) return;
+// Sum the per-workgroup partials (fixed order) into the six f32 gradients:
+// a block takes 64 parameters; its 16 part-lanes sum the parts p = j, j+16,
+// ... of each, then lane j = 0 adds the 16 lane sums in order.
+__global__ __launch_bounds__(1024) void k_field_wgrad_sum(const float *__restrict__ partial,
+                                                          uint32_t parts, float *gw1, float *gb1,
+                                                          float *gw2, float *gb2, float *gw3,
+                                                          float *gb3, int accumulate) {
+    __shared__ float lane_sum[16][64];
+    const int col = threadIdx.x & 63, j = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + col;
     float s = 0.0f;
-    for (uint32_t p = 0; p < parts; ++p) s += partial[(size_t)p * kParams + i];
+    if (i < kParams)
+        for (uint32_t p = j; p < parts; p += 16) s += partial[(size_t)p * kParams + i];
+    lane_sum[j][col] = s;
+    __syncthreads();
+    if (j != 0 || i >= kParams) return;
+    s = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += lane_sum[q][col];
     float *dst;
     int k;
     if (i < kOffB1) { dst = gw1; k = i - kOffW1; }
@@ -546,14 +677,13 @@ extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const
             return DFHIP_EINVAL;
         }
         if (grad_rgb_dtype == DFHIP_F32)
-            k_field_bwd<float><<<parts, 256, 0, s>>>((const half_t *)enc, xyz, w1, b1, w2, b2, w3,
-                                                     b3, grad_sigma, (const float *)grad_rgb, M,
-                                                     (half_t *)d_enc_lbc, partial);
+            k_field_bwd<float, false><<<parts, 256, 0, s>>>(
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
+                (const float *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
         else if (grad_rgb_dtype == DFHIP_F16)
-            k_field_bwd<half_t><<<parts, 256, 0, s>>>((const half_t *)enc, xyz, w1, b1, w2, b2,
-                                                      w3, b3, grad_sigma,
-                                                      (const half_t *)grad_rgb, M,
-                                                      (half_t *)d_enc_lbc, partial);
+            k_field_bwd<half_t, false><<<parts, 256, 0, s>>>(
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
+                (const half_t *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
         else {
             set_error("%s: grad_rgb dtype must be f32 or f16", name);
             return DFHIP_EDTYPE;
@@ -562,7 +692,111 @@ extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const
         parts = 1;
         (void)hipMemsetAsync(partial, 0, kParams * sizeof(float), s);
     }
-    k_field_wgrad_sum<<<ceil_div((uint32_t)kParams, 256u), 256, 0, s>>>(
+    k_field_wgrad_sum<<<ceil_div((uint32_t)kParams, 64u), 1024, 0, s>>>(
         partial, parts, gw1, gb1, gw2, gb2, gw3, gb3, accumulate);
     return check_launch(name);
+}
+
+// ------------------------------------------------------------------ fused grid field
+static bool check_field_grid(const char *name, uint32_t L) {
+    if (L != 16) {
+        set_error("%s: the fused field supports the reference's 16-level x 2-channel 3-D grid "
+                  "(got L=%u)", name, L);
+        return false;
+    }
+    return true;
+}
+
+extern "C" int dfhip_grid_field_forward(const float *xyz, float bound, const void *table,
+                                        const int32_t *offsets, uint32_t L, float S, uint32_t H,
+                                        uint32_t gridtype, int align_corners, const float *w1,
+                                        const float *b1, const float *w2, const float *b2,
+                                        const float *w3, const float *b3, void *enc,
+                                        float *sigma, void *rgb, int rgb_dtype, uint32_t cap,
+                                        const int32_t *m_dev, dfhip_stream_t stream) {
+    const char *name = "grid_field_forward";
+    if (!check_field_grid(name, L)) return DFHIP_EINVAL;
+    if (!(bound > 0.0f)) {
+        set_error("%s: bound must be > 0", name);
+        return DFHIP_EINVAL;
+    }
+    if (cap == 0) return DFHIP_OK;
+    if (!xyz || !table || !offsets || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !sigma || !rgb) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const ge::Levels lv = ge::make_levels(L, S, H);
+    // persistent waves: enough to fill the chip, each walks 16-sample tiles
+    const uint32_t tiles = ceil_div(cap, 16u);
+    const uint32_t blocks = ceil_div(tiles, 4u) < 4096u ? ceil_div(tiles, 4u) : 4096u;
+    if (rgb_dtype == DFHIP_F32)
+        k_field_fwd_fused<float><<<blocks, 256, 0, s>>>(
+            xyz, bound, (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2,
+            b2, w3, b3, (half_t *)enc, sigma, (float *)rgb, cap, m_dev);
+    else if (rgb_dtype == DFHIP_F16)
+        k_field_fwd_fused<half_t><<<blocks, 256, 0, s>>>(
+            xyz, bound, (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2,
+            b2, w3, b3, (half_t *)enc, sigma, (half_t *)rgb, cap, m_dev);
+    else {
+        set_error("%s: rgb dtype must be f32 or f16", name);
+        return DFHIP_EDTYPE;
+    }
+    return check_launch(name);
+}
+
+extern "C" int dfhip_grid_field_backward(
+    const void *enc, const float *xyz, float bound, const float *w1, const float *b1,
+    const float *w2, const float *b2, const float *w3, const float *b3, const float *grad_sigma,
+    const void *grad_rgb, int grad_rgb_dtype, uint32_t cap, const int32_t *m_dev,
+    void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1, float *gb1, float *gw2,
+    float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
+    float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
+    float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream) {
+    const char *name = "grid_field_backward";
+    if (!check_field_grid(name, L)) return DFHIP_EINVAL;
+    if (!(bound > 0.0f)) {
+        set_error("%s: bound must be > 0", name);
+        return DFHIP_EINVAL;
+    }
+    if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !gw1 || !gb1 || !gw2 || !gb2 || !gw3 || !gb3 ||
+        !mlp_partial) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    if (cap > 0) {
+        if (!enc || !xyz || !grad_sigma || !grad_rgb || !d_enc_lbc) {
+            set_error("%s: null pointer", name);
+            return DFHIP_EINVAL;
+        }
+        if (mlp_parts != bwd_blocks(cap)) {
+            set_error("%s: mlp_parts must be dfhip_field_mlp_backward_parts(cap) = %u (got %u)",
+                      name, bwd_blocks(cap), mlp_parts);
+            return DFHIP_EINVAL;
+        }
+        if (grad_rgb_dtype == DFHIP_F32)
+            k_field_bwd<float, true><<<mlp_parts, 256, 0, s>>>(
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
+                (const float *)grad_rgb, cap, m_dev, (half_t *)d_enc_lbc, mlp_partial);
+        else if (grad_rgb_dtype == DFHIP_F16)
+            k_field_bwd<half_t, true><<<mlp_parts, 256, 0, s>>>(
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
+                (const half_t *)grad_rgb, cap, m_dev, (half_t *)d_enc_lbc, mlp_partial);
+        else {
+            set_error("%s: grad_rgb dtype must be f32 or f16", name);
+            return DFHIP_EDTYPE;
+        }
+    } else {
+        mlp_parts = 1;
+        (void)hipMemsetAsync(mlp_partial, 0, kParams * sizeof(float), s);
+    }
+    k_field_wgrad_sum<<<ceil_div((uint32_t)kParams, 64u), 1024, 0, s>>>(
+        mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, 0);
+    int rc = check_launch(name);
+    if (rc != DFHIP_OK || grad_embeddings == nullptr) return rc;
+    return ge::grid_backward_sliced(name, DFHIP_F16, DFHIP_F32, d_enc_lbc, xyz, offsets,
+                                    grad_embeddings, total_rows, cap, 3, 2, L, S, H, gridtype,
+                                    align_corners, grid_partial, grid_parts, 0,
+                                    ge::SliceDyn{m_dev, bound}, s);
 }

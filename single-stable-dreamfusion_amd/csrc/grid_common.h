@@ -1,0 +1,123 @@
+// Grid-encoder level geometry and corner arithmetic shared by the grid
+// kernels (gridencoder.hip) and the fused field kernels (fieldmlp.hip).
+// Behavioural spec: reference gridencoder/src/gridencoder.cu:35-72,125-165.
+#pragma once
+
+#include <math.h>
+
+#include "common.h"
+
+namespace dfhip {
+namespace ge {
+
+constexpr uint32_t kMaxLevels = 64;
+
+struct Levels {
+    float scale[kMaxLevels];
+    uint32_t res[kMaxLevels];
+};
+
+// gridencoder.cu:125-126, evaluated on the host.
+static Levels make_levels(uint32_t L, float S, uint32_t H) {
+    Levels lv;
+    for (uint32_t l = 0; l < L; ++l) {
+        const float ls = (float)l * S;
+        const float e = (float)exp2((double)ls);
+        const float scale = fmaf(e, (float)H, -1.0f);
+        lv.scale[l] = scale;
+        lv.res[l] = (uint32_t)ceilf(scale) + 1u;
+    }
+    return lv;
+}
+
+// gridencoder.cu:35-51 — instant-ngp spatial hash.
+template <uint32_t D>
+__device__ __forceinline__ uint32_t spatial_hash(const uint32_t p[D]) {
+    constexpr uint32_t kPrimes[7] = {1u, 2654435761u, 805459861u, 3674653429u,
+                                     2097192037u, 1434869437u, 2165219737u};
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) h ^= p[d] * kPrimes[d];
+    return h;
+}
+
+// Wave-uniform per-level context.
+struct LevelCtx {
+    uint32_t base;     // first table row of the level (offsets[l])
+    uint32_t hsize;    // rows in the level
+    uint32_t smul;     // stride multiplier: res (align_corners) or res + 1
+    uint32_t used;     // dims consumed by the tiled index before stride > hsize
+    bool hashed;       // gridtype == hash and stride overflowed -> spatial_hash
+    bool pow2;         // hsize is a power of two -> modulo is a mask
+    float scale;
+};
+
+template <uint32_t D>
+__device__ __forceinline__ LevelCtx level_ctx(const int32_t *__restrict__ offsets,
+                                              const Levels &lv, uint32_t l,
+                                              uint32_t gridtype, bool align) {
+    LevelCtx c;
+    c.base = (uint32_t)offsets[l];
+    c.hsize = (uint32_t)offsets[l + 1] - c.base;
+    c.scale = lv.scale[l];
+    c.smul = align ? lv.res[l] : lv.res[l] + 1u;
+    // gridencoder.cu:56-63: for (d < D && stride <= hashmap_size)
+    uint32_t stride = 1, used = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) {
+        if (stride <= c.hsize) { stride *= c.smul; ++used; }
+    }
+    c.used = used;
+    c.hashed = (gridtype == 0) && (stride > c.hsize);
+    c.pow2 = (c.hsize & (c.hsize - 1)) == 0;
+    return c;
+}
+
+// gridencoder.cu:54-72 (row index; the caller multiplies by C).
+template <uint32_t D>
+__device__ __forceinline__ uint32_t row_index(const LevelCtx &c, const uint32_t p[D]) {
+    uint32_t idx;
+    if (c.hashed) {
+        idx = spatial_hash<D>(p);
+    } else {
+        idx = 0;
+        uint32_t stride = 1;
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) {
+            if (d < c.used) { idx += p[d] * stride; stride *= c.smul; }
+        }
+    }
+    return c.pow2 ? (idx & (c.hsize - 1)) : (idx % c.hsize);
+}
+
+// ------------------------------------------------------------ storage helpers
+// Accumulate one corner contribution into a per-channel register, following
+// the reference's scalar_t arithmetic exactly (gridencoder.cu:142,165).
+__device__ __forceinline__ void acc_corner(float &r, float w, float g) { r = fmaf(w, g, r); }
+__device__ __forceinline__ void acc_corner(double &r, float w, double g) {
+    r = fma((double)w, g, r);
+}
+__device__ __forceinline__ void acc_corner(half_t &r, float w, half_t g) {
+    // c10::Half: Half += float  ==>  Half(float(r) + float(Half(w * float(g))))
+    const half_t p = (half_t)f32_rounded(w * (float)g);
+    r = (half_t)((float)r + (float)p);
+}
+
+// Dynamic sample count / coordinate mapping of the sliced embedding backward
+// (see gridencoder.hip k_grid_bwd_sliced).
+struct SliceDyn {
+    const int32_t *m_dev;
+    float bound;
+};
+
+// Host side of dfhip_grid_encode_backward_sliced, shared with the fused
+// field backward (fieldmlp.hip).
+int grid_backward_sliced(const char *name, int grad_dtype, int out_dtype, const void *grad,
+                         const float *inputs, const int32_t *offsets, void *grad_embeddings,
+                         uint32_t total_rows, uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                         float S, uint32_t H, uint32_t gridtype, int align_corners,
+                         float *partial, uint32_t parts, int accumulate, SliceDyn dyn,
+                         hipStream_t s);
+
+}  // namespace ge
+}  // namespace dfhip

@@ -21,103 +21,10 @@
 //    permute copies (grid.py:42,70).
 #include "common.h"
 
-#include <math.h>
+#include "grid_common.h"
 
 namespace dfhip {
 namespace ge {
-
-constexpr uint32_t kMaxLevels = 64;
-
-struct Levels {
-    float scale[kMaxLevels];
-    uint32_t res[kMaxLevels];
-};
-
-// gridencoder.cu:125-126, evaluated on the host.
-static Levels make_levels(uint32_t L, float S, uint32_t H) {
-    Levels lv;
-    for (uint32_t l = 0; l < L; ++l) {
-        const float ls = (float)l * S;
-        const float e = (float)exp2((double)ls);
-        const float scale = fmaf(e, (float)H, -1.0f);
-        lv.scale[l] = scale;
-        lv.res[l] = (uint32_t)ceilf(scale) + 1u;
-    }
-    return lv;
-}
-
-// gridencoder.cu:35-51 — instant-ngp spatial hash.
-template <uint32_t D>
-__device__ __forceinline__ uint32_t spatial_hash(const uint32_t p[D]) {
-    constexpr uint32_t kPrimes[7] = {1u, 2654435761u, 805459861u, 3674653429u,
-                                     2097192037u, 1434869437u, 2165219737u};
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) h ^= p[d] * kPrimes[d];
-    return h;
-}
-
-// Wave-uniform per-level context.
-struct LevelCtx {
-    uint32_t base;     // first table row of the level (offsets[l])
-    uint32_t hsize;    // rows in the level
-    uint32_t smul;     // stride multiplier: res (align_corners) or res + 1
-    uint32_t used;     // dims consumed by the tiled index before stride > hsize
-    bool hashed;       // gridtype == hash and stride overflowed -> spatial_hash
-    bool pow2;         // hsize is a power of two -> modulo is a mask
-    float scale;
-};
-
-template <uint32_t D>
-__device__ __forceinline__ LevelCtx level_ctx(const int32_t *__restrict__ offsets,
-                                              const Levels &lv, uint32_t l,
-                                              uint32_t gridtype, bool align) {
-    LevelCtx c;
-    c.base = (uint32_t)offsets[l];
-    c.hsize = (uint32_t)offsets[l + 1] - c.base;
-    c.scale = lv.scale[l];
-    c.smul = align ? lv.res[l] : lv.res[l] + 1u;
-    // gridencoder.cu:56-63: for (d < D && stride <= hashmap_size)
-    uint32_t stride = 1, used = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) {
-        if (stride <= c.hsize) { stride *= c.smul; ++used; }
-    }
-    c.used = used;
-    c.hashed = (gridtype == 0) && (stride > c.hsize);
-    c.pow2 = (c.hsize & (c.hsize - 1)) == 0;
-    return c;
-}
-
-// gridencoder.cu:54-72 (row index; the caller multiplies by C).
-template <uint32_t D>
-__device__ __forceinline__ uint32_t row_index(const LevelCtx &c, const uint32_t p[D]) {
-    uint32_t idx;
-    if (c.hashed) {
-        idx = spatial_hash<D>(p);
-    } else {
-        idx = 0;
-        uint32_t stride = 1;
-#pragma unroll
-        for (uint32_t d = 0; d < D; ++d) {
-            if (d < c.used) { idx += p[d] * stride; stride *= c.smul; }
-        }
-    }
-    return c.pow2 ? (idx & (c.hsize - 1)) : (idx % c.hsize);
-}
-
-// ------------------------------------------------------------ storage helpers
-// Accumulate one corner contribution into a per-channel register, following
-// the reference's scalar_t arithmetic exactly (gridencoder.cu:142,165).
-__device__ __forceinline__ void acc_corner(float &r, float w, float g) { r = fmaf(w, g, r); }
-__device__ __forceinline__ void acc_corner(double &r, float w, double g) {
-    r = fma((double)w, g, r);
-}
-__device__ __forceinline__ void acc_corner(half_t &r, float w, half_t g) {
-    // c10::Half: Half += float  ==>  Half(float(r) + float(Half(w * float(g))))
-    const half_t p = (half_t)f32_rounded(w * (float)g);
-    r = (half_t)((float)r + (float)p);
-}
 
 // ------------------------------------------------------------ forward
 
@@ -387,6 +294,20 @@ __device__ __forceinline__ void load_run(const uint32_t *__restrict__ src, uint3
     }
 }
 
+// Dynamic sample count / coordinate mapping of the fused field path: when
+// m_dev is set, only samples [0, *m_dev) of the B-row planes are walked (B is
+// then the plane stride, the capacity); when bound > 0 the inputs are raw
+// positions in [-bound, bound], mapped to [0, 1] as grid.py:142 does.
+__device__ __forceinline__ uint32_t dyn_count(const SliceDyn &dyn, uint32_t B) {
+    if (!dyn.m_dev) return B;
+    const int32_t m = *dyn.m_dev;
+    return m < 0 ? 0u : ((uint32_t)m < B ? (uint32_t)m : B);
+}
+
+__device__ __forceinline__ float dyn_map(const SliceDyn &dyn, float x) {
+    return dyn.bound > 0.0f ? (x + dyn.bound) / (2.0f * dyn.bound) : x;
+}
+
 // Generic shapes: one sample per lane, no run merging (lanes of a wave read
 // consecutive samples, coalesced).
 template <typename grad_t, uint32_t D, uint32_t C>
@@ -394,7 +315,7 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced_simple(
     const grad_t *__restrict__ grad, const float *__restrict__ inputs,
     const int32_t *__restrict__ offsets, float *__restrict__ partial, uint32_t B, uint32_t L,
     Levels lv, uint32_t gridtype, int align_corners, uint32_t rows_per_slice,
-    uint32_t total_rows, int vec_ok) {
+    uint32_t total_rows, int vec_ok, SliceDyn dyn) {
     (void)vec_ok;
     extern __shared__ double acc[];
     const uint32_t r0 = blockIdx.x * rows_per_slice;
@@ -403,9 +324,10 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced_simple(
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
     const bool align = align_corners != 0;
-    const uint32_t chunk = ceil_div(B, gridDim.y);
+    const uint32_t M = dyn_count(dyn, B);
+    const uint32_t chunk = ceil_div(M, gridDim.y);
     const uint32_t b0 = blockIdx.y * chunk;
-    const uint32_t b1 = min(B, b0 + chunk);
+    const uint32_t b1 = min(M, b0 + chunk);
     for (uint32_t l = 0; l < L; ++l) {
         const LevelCtx c = level_ctx<D>(offsets, lv, l, gridtype, align);
         if (c.base >= r1 || c.base + c.hsize <= r0) continue;
@@ -416,7 +338,7 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced_simple(
             bool oob = false;
 #pragma unroll
             for (uint32_t d = 0; d < D; ++d) {
-                x[d] = inputs[(size_t)b * D + d];
+                x[d] = dyn_map(dyn, inputs[(size_t)b * D + d]);
                 oob |= (x[d] < 0.0f) || (x[d] > 1.0f);
             }
             if (oob) continue;
@@ -461,7 +383,7 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced(
     const float *__restrict__ inputs, const int32_t *__restrict__ offsets,
     float *__restrict__ partial,      // [P, total_rows, C]
     uint32_t B, uint32_t L, Levels lv, uint32_t gridtype, int align_corners,
-    uint32_t rows_per_slice, uint32_t total_rows, int vec_ok) {
+    uint32_t rows_per_slice, uint32_t total_rows, int vec_ok, SliceDyn dyn) {
     constexpr uint32_t GW = (C * sizeof(grad_t) + 3) / 4;  // 32-bit words of one sample's grad
     constexpr bool GPACK = (C * sizeof(grad_t)) % 4 == 0;  // grads tile 32-bit words
     extern __shared__ double acc[];
@@ -472,9 +394,10 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced(
     __syncthreads();
     const bool align = align_corners != 0;
     // parts split the samples in whole runs, so every run starts 16-B aligned
-    const uint32_t chunk = ceil_div(ceil_div(B, gridDim.y), K) * K;
+    const uint32_t M = dyn_count(dyn, B);
+    const uint32_t chunk = ceil_div(ceil_div(M, gridDim.y), K) * K;
     const uint32_t b0 = blockIdx.y * chunk;
-    const uint32_t b1 = min(B, b0 + chunk);
+    const uint32_t b1 = min(M, b0 + chunk);
     const uint32_t runs = b1 > b0 ? ceil_div(b1 - b0, K) : 0u;
     // Interleave runs over lanes: neighbouring lanes walk runs blockDim/64
     // apart, so one LDS atomic instruction rarely has two lanes on one row.
@@ -516,7 +439,7 @@ __global__ __launch_bounds__(1024) void k_grid_bwd_sliced(
                 bool oob = false;
 #pragma unroll
                 for (uint32_t d = 0; d < D; ++d) {
-                    x[d] = __uint_as_float(xw[i * D + d]);
+                    x[d] = dyn_map(dyn, __uint_as_float(xw[i * D + d]));
                     oob |= (x[d] < 0.0f) || (x[d] > 1.0f);
                 }
                 if (!oob) {  // else grads stay zero (gridencoder.cu:253-258)
@@ -735,11 +658,11 @@ template <typename grad_t, uint32_t D, uint32_t C>
 static void launch_sliced_dc(hipStream_t s, dim3 g, size_t lds, const grad_t *grad,
                              const float *in, const int32_t *off, float *partial, uint32_t B,
                              uint32_t L, const Levels &lv, uint32_t gt, int ac, uint32_t rows,
-                             uint32_t total_rows) {
+                             uint32_t total_rows, SliceDyn dyn) {
     // the run-merging kernel for the NeRF grid shape (D=3, C=2), the simple
     // one otherwise
     void (*kern)(const grad_t *, const float *, const int32_t *, float *, uint32_t, uint32_t,
-                 Levels, uint32_t, int, uint32_t, uint32_t, int);
+                 Levels, uint32_t, int, uint32_t, uint32_t, int, SliceDyn);
     if constexpr (D == 3 && C == 2)
         kern = k_grid_bwd_sliced<grad_t, D, C, kRunLen>;
     else
@@ -755,17 +678,18 @@ static void launch_sliced_dc(hipStream_t s, dim3 g, size_t lds, const grad_t *gr
     // plane a multiple of 16 B
     const int vec_ok = (((uintptr_t)grad | (uintptr_t)in) & 15) == 0 &&
                        ((uint64_t)B * C * sizeof(grad_t)) % 16 == 0;
-    kern<<<g, 1024, lds, s>>>(grad, in, off, partial, B, L, lv, gt, ac, rows, total_rows, vec_ok);
+    kern<<<g, 1024, lds, s>>>(grad, in, off, partial, B, L, lv, gt, ac, rows, total_rows, vec_ok,
+                              dyn);
 }
 
 template <typename grad_t>
 static void launch_sliced(uint32_t D, uint32_t C, hipStream_t s, dim3 g, size_t lds,
                           const grad_t *grad, const float *in, const int32_t *off,
                           float *partial, uint32_t B, uint32_t L, const Levels &lv, uint32_t gt,
-                          int ac, uint32_t rows, uint32_t total_rows) {
+                          int ac, uint32_t rows, uint32_t total_rows, SliceDyn dyn) {
 #define DFHIP_SL(DD, CC)                                                                    \
     launch_sliced_dc<grad_t, DD, CC>(s, g, lds, grad, in, off, partial, B, L, lv, gt, ac, rows, \
-                                     total_rows)
+                                     total_rows, dyn)
 #define DFHIP_SL_C(DD)                       \
     switch (C) {                             \
     case 1: DFHIP_SL(DD, 1); break;          \
@@ -949,15 +873,14 @@ extern "C" uint64_t dfhip_grid_backward_partial_floats(uint32_t total_rows, uint
     return (uint64_t)total_rows * C * (parts ? parts : 1);
 }
 
-extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, const void *grad,
-                                                 const float *inputs, const int32_t *offsets,
-                                                 void *grad_embeddings, uint32_t total_rows,
-                                                 uint32_t B, uint32_t D, uint32_t C, uint32_t L,
-                                                 float S, uint32_t H, uint32_t gridtype,
-                                                 int align_corners, float *partial,
-                                                 uint32_t parts, int accumulate,
-                                                 dfhip_stream_t stream) {
-    const char *name = "grid_encode_backward_sliced";
+namespace dfhip {
+namespace ge {
+int grid_backward_sliced(const char *name, int grad_dtype, int out_dtype, const void *grad,
+                         const float *inputs, const int32_t *offsets, void *grad_embeddings,
+                         uint32_t total_rows, uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                         float S, uint32_t H, uint32_t gridtype, int align_corners,
+                         float *partial, uint32_t parts, int accumulate, SliceDyn dyn,
+                         hipStream_t s) {
     if (!check_dc(name, D, C, L)) return DFHIP_EINVAL;
     if (parts == 0 || partial == nullptr) {
         set_error("%s: needs parts >= 1 and a partial buffer", name);
@@ -968,7 +891,6 @@ extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, 
         return DFHIP_EDTYPE;
     }
     if (total_rows == 0) return DFHIP_OK;
-    hipStream_t s = as_stream(stream);
     const uint64_t n = (uint64_t)total_rows * C;
     if (B > 0 && L > 0) {
         const Levels lv = make_levels(L, S, H);
@@ -978,10 +900,10 @@ extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, 
         switch (grad_dtype) {
         case DFHIP_F32: launch_sliced<float>(D, C, s, g, lds, (const float *)grad, inputs, offsets,
                                              partial, B, L, lv, gridtype, align_corners, rows,
-                                             total_rows); break;
+                                             total_rows, dyn); break;
         case DFHIP_F16: launch_sliced<half_t>(D, C, s, g, lds, (const half_t *)grad, inputs,
                                               offsets, partial, B, L, lv, gridtype, align_corners,
-                                              rows, total_rows); break;
+                                              rows, total_rows, dyn); break;
         default: set_error("%s: unsupported grad dtype %d", name, grad_dtype); return DFHIP_EDTYPE;
         }
     } else {
@@ -996,6 +918,22 @@ extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, 
         k_sum_partials<half_t><<<blocks, 256, 0, s>>>(partial, parts, n, (half_t *)grad_embeddings,
                                                       accumulate);
     return check_launch(name);
+}
+}  // namespace ge
+}  // namespace dfhip
+
+extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, const void *grad,
+                                                 const float *inputs, const int32_t *offsets,
+                                                 void *grad_embeddings, uint32_t total_rows,
+                                                 uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                                 float S, uint32_t H, uint32_t gridtype,
+                                                 int align_corners, float *partial,
+                                                 uint32_t parts, int accumulate,
+                                                 dfhip_stream_t stream) {
+    return ge::grid_backward_sliced("grid_encode_backward_sliced", grad_dtype, out_dtype, grad,
+                                    inputs, offsets, grad_embeddings, total_rows, B, D, C, L, S,
+                                    H, gridtype, align_corners, partial, parts, accumulate,
+                                    ge::SliceDyn{nullptr, 0.0f}, as_stream(stream));
 }
 
 extern "C" int dfhip_grid_grad_blc_to_lbc(int dtype, const void *src, void *dst, uint32_t B,
@@ -1032,4 +970,20 @@ extern "C" int dfhip_grid_grad_blc_to_lbc(int dtype, const void *src, void *dst,
         return DFHIP_EINVAL;
     }
     return check_launch(name);
+}
+
+extern "C" int dfhip_grid_encode_backward_sliced_dyn(
+    int grad_dtype, int out_dtype, const void *grad, const float *inputs, float bound,
+    const int32_t *offsets, void *grad_embeddings, uint32_t total_rows, uint32_t B,
+    const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+    uint32_t gridtype, int align_corners, float *partial, uint32_t parts, int accumulate,
+    dfhip_stream_t stream) {
+    if (bound < 0.0f) {
+        set_error("grid_encode_backward_sliced_dyn: bound must be >= 0");
+        return DFHIP_EINVAL;
+    }
+    return ge::grid_backward_sliced("grid_encode_backward_sliced_dyn", grad_dtype, out_dtype, grad,
+                                    inputs, offsets, grad_embeddings, total_rows, B, D, C, L, S,
+                                    H, gridtype, align_corners, partial, parts, accumulate,
+                                    ge::SliceDyn{m_dev, bound}, as_stream(stream));
 }

@@ -3,10 +3,13 @@ ONE autograd node on the native kernels (the reference's
 network_grid.common_forward, nerf/network_grid.py:76-87, = GridEncoder ->
 MLP -> trunc_exp(h0 + gaussian) / sigmoid(h[1:])).
 
-Forward: grid_encode_forward_blc (f16 features) -> field_mlp_forward (MFMA).
-Backward: field_mlp_backward (recomputes the MLP from the saved features,
-writes the feature gradient straight into the [L, B, C] layout) ->
-grid_encode_backward_sliced.  Used under fp16 autocast for the reference's
+Forward: dfhip_grid_field_forward — grid gather and MLP in one kernel, the
+features kept (permuted order) for the backward.  Backward:
+dfhip_grid_field_backward — MLP backward (recomputed from the features, the
+feature gradient written straight into the [L, B, C] layout) then the sliced
+embedding backward.  With `m_dev` (the march's device-side sample count)
+only the live rows of capacity-sized buffers are processed, so the train
+step needs no host round trip.  Used under fp16 autocast for the reference's
 network shape (16 levels x 2 channels, 32 -> 64 -> 64 -> 4); anything else
 runs the unfused modules.
 """
@@ -35,67 +38,69 @@ def eligible(encoder, layers, x):
 
 class _GridField(Function):
     @staticmethod
-    def forward(ctx, x, bound, embeddings, offsets, meta, *weights):
-        """x [M, 3] in [-bound, bound] f32 -> sigma [M] f32, albedo [M, 3] f16."""
+    def forward(ctx, x, bound, embeddings, offsets, meta, m_dev, *weights):
+        """x [cap, 3] in [-bound, bound] f32 -> sigma [cap] f32, albedo [cap, 3]
+        f16 (rows >= m_dev[0] untouched when m_dev is given)."""
         S, H, gridtype, align = meta
         x = x.contiguous().float()
-        M = x.shape[0]
-        x01 = ((x + bound) / (2 * bound)).contiguous()
+        cap = x.shape[0]
         table = embeddings.to(torch.half).contiguous()
-        rows = table.shape[0]
         L, C = offsets.shape[0] - 1, table.shape[1]
-        enc = torch.empty(M, L * C, device=x.device, dtype=torch.half)
-        nbytes = M * (12 + L * C * 2) + table.numel() * 2
-        with _dfhip.timed("grid_encode_forward", nbytes):
-            _gridencoder.grid_encode_forward_blc(x01, table, offsets, enc, M, 3, C, L, S, H, None,
-                                                 gridtype, align)
-        sigma = torch.empty(M, device=x.device, dtype=torch.float32)
-        albedo = torch.empty(M, 3, device=x.device, dtype=torch.half)
+        enc = torch.empty(cap, L * C, device=x.device, dtype=torch.half)
+        sigma = torch.empty(cap, device=x.device, dtype=torch.float32)
+        albedo = torch.empty(cap, 3, device=x.device, dtype=torch.half)
         ws = [w.detach().float().contiguous() for w in weights]
-        with _dfhip.timed("field_mlp_forward", M * (64 + 12 + 4 + 6)):
-            _fieldmlp.field_mlp_forward(enc, x, ws, sigma, albedo)
-        ctx.save_for_backward(x, x01, enc, offsets, *ws)
-        ctx.meta = (S, H, gridtype, align, rows, L, C)
+        # algorithmic bytes per sample: xyz + features out + sigma/albedo out,
+        # plus the f16 table once (the gathers hit L2 / MALL)
+        with _dfhip.timed("grid_field_forward", cap * (12 + 64 + 4 + 6) + table.numel() * 2):
+            _fieldmlp.grid_field_forward(x, bound, table, offsets, S, H, gridtype, align, ws, enc,
+                                         sigma, albedo, m_dev)
+        ctx.save_for_backward(x, enc, offsets, m_dev, *ws)
+        ctx.meta = (S, H, gridtype, align, table.shape[0], L, C, float(bound))
         return sigma, albedo
 
     @staticmethod
     def backward(ctx, grad_sigma, grad_albedo):
-        x, x01, enc, offsets, *ws = ctx.saved_tensors
-        S, H, gridtype, align, rows, L, C = ctx.meta
-        M = x.shape[0]
+        x, enc, offsets, m_dev, *ws = ctx.saved_tensors
+        S, H, gridtype, align, rows, L, C, bound = ctx.meta
+        cap = x.shape[0]
         dev = x.device
         if grad_sigma is None:
-            grad_sigma = torch.zeros(M, device=dev)
+            grad_sigma = torch.zeros(cap, device=dev)
         if grad_albedo is None:
-            grad_albedo = torch.zeros(M, 3, device=dev, dtype=torch.half)
+            grad_albedo = torch.zeros(cap, 3, device=dev, dtype=torch.half)
         grad_sigma = grad_sigma.float().contiguous()
         grad_albedo = grad_albedo.contiguous()
-        d_enc = torch.empty(L, M, C, device=dev, dtype=torch.half)
-        parts = _fieldmlp.backward_parts(M) if M else 1
-        partial = torch.empty(parts * _fieldmlp.params_count(), device=dev)
+        d_enc = torch.empty(L, cap, C, device=dev, dtype=torch.half)
+        mlp_partial = torch.empty((_fieldmlp.backward_parts(cap) if cap else 1)
+                                  * _fieldmlp.params_count(), device=dev)
         grads = [torch.empty_like(w) for w in ws]
-        with _dfhip.timed("field_mlp_backward", M * (64 + 12 + 4 + 6 + 64)):
-            _fieldmlp.field_mlp_backward(enc, x, ws, grad_sigma, grad_albedo, d_enc, partial,
-                                         grads)
-        grad_emb = None
+        grad_emb = gpartial = None
+        gparts = _parts(rows, C)
         if ctx.needs_input_grad[2]:
-            gparts = _parts(rows, C)
+            grad_emb = torch.empty(rows, C, device=dev, dtype=torch.float32)
             gpartial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, C, gparts),
                                    device=dev)
-            grad_emb = torch.empty(rows, C, device=dev, dtype=torch.float32)
-            nbytes = M * (12 + L * C * 2) + 4 * rows * C
+        # MLP backward: features + positions + incoming grads in, feature grads out
+        with _dfhip.timed("field_mlp_backward", cap * (64 + 12 + 4 + 6 + 64)):
+            _fieldmlp.grid_field_backward(enc, x, bound, ws, grad_sigma, grad_albedo, d_enc,
+                                          mlp_partial, grads, offsets, rows, S, H, gridtype,
+                                          align, None, None, gparts, m_dev)
+        if grad_emb is not None:
+            nbytes = cap * (12 + L * C * 2) + 4 * rows * C
             with _dfhip.timed("grid_encode_backward", nbytes):
-                _gridencoder.grid_encode_backward_sliced(d_enc, x01, offsets, grad_emb, rows, M, 3,
-                                                         C, L, S, H, gridtype, align, gpartial,
-                                                         gparts)
-        return (None, None, grad_emb, None, None, *grads)
+                _gridencoder.grid_encode_backward_sliced_dyn(d_enc, x, bound, offsets, grad_emb,
+                                                             rows, cap, m_dev, 3, C, L, S, H,
+                                                             gridtype, align, gpartial, gparts)
+        return (None, None, grad_emb, None, None, None, *grads)
 
 
-def grid_field(x, bound, encoder, layers):
-    """sigma [M] (f32), albedo [M, 3] (f16) of the grid field at x [M, 3]."""
+def grid_field(x, bound, encoder, layers, m_dev=None):
+    """sigma [M] (f32), albedo [M, 3] (f16) of the grid field at x [M, 3].
+    m_dev: optional int32 device tensor holding the live row count."""
     meta = (float(np.log2(encoder.per_level_scale)), int(encoder.base_resolution),
             encoder.gridtype_id, bool(encoder.align_corners))
     weights = []
     for lin in layers:
         weights += [lin.weight, lin.bias]
-    return _GridField.apply(x, bound, encoder.embeddings, encoder.offsets, meta, *weights)
+    return _GridField.apply(x, bound, encoder.embeddings, encoder.offsets, meta, m_dev, *weights)

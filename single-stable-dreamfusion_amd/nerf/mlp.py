@@ -17,6 +17,7 @@ from torch.autograd import Function
 from torch.amp import custom_bwd, custom_fwd
 
 _CHUNK = 4096  # rows per split-K chunk
+_SPLIT_MIN = 2 * _CHUNK  # split only when K (rows) is larger than this
 
 
 _BMM_F32_OUT = [True]
@@ -35,7 +36,8 @@ def _bmm_f32(a, b):
 def _split_k_wgrad(dy, x):
     """sum over rows of dy^T x, i.e. [N, K] = dy[M, N]^T @ x[M, K], in f32."""
     m = dy.shape[0]
-    if m <= 2 * _CHUNK:
+    if m <= _SPLIT_MIN:
+        # small K (e.g. the per-ray background MLP): one GEMM is fine
         return (dy.t() @ x).float()
     s = m // _CHUNK
     head = s * _CHUNK

@@ -87,3 +87,26 @@ def test_fused_field_empty(gpu):
                              allow_unused=True)
     for t in gr:
         assert t is None or torch.count_nonzero(t) == 0
+
+
+def test_fused_field_device_count(gpu):
+    """m_dev mode: capacity-sized buffers, live row count read on the device —
+    same outputs on the live rows and the same gradients as an exact-size call."""
+    from nerf.field import grid_field
+    enc, layers = _field(gpu, seed=4)
+    M, cap = 40_001, 65_536
+    x = torch.rand(cap, 3, device=gpu) * 2 - 1
+    gs = torch.randn(cap, device=gpu)
+    ga = torch.randn(cap, 3, device=gpu)
+    params = [enc.embeddings] + list(layers.parameters())
+    m_dev = torch.tensor([M], dtype=torch.int32, device=gpu)
+    with torch.autocast("cuda", dtype=torch.float16):
+        s_cap, a_cap = grid_field(x, 1.0, enc, layers, m_dev)
+        s_m, a_m = grid_field(x[:M].contiguous(), 1.0, enc, layers)
+    assert torch.equal(s_cap[:M], s_m) and torch.equal(a_cap[:M], a_m)
+    # the dead rows carry garbage; their incoming gradient must not matter
+    g_cap = torch.autograd.grad((s_cap[:M] * gs[:M]).sum() + (a_cap[:M].float() * ga[:M]).sum(),
+                                params)
+    g_m = torch.autograd.grad((s_m * gs[:M]).sum() + (a_m.float() * ga[:M]).sum(), params)
+    for u, v in zip(g_cap, g_m):
+        torch.testing.assert_close(u, v, rtol=1e-6, atol=1e-7)
