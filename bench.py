@@ -42,13 +42,15 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--two-pass-backward", action="store_true",
                    help="reference double backward instead of the fused single pass")
+    p.add_argument("--eager", action="store_true",
+                   help="launch every kernel eagerly (no HIP-graph replay of the step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=1)
     return p.parse_args()
 
 
-def make_trainer(res, seed, rank, world, fused):
+def make_trainer(res, seed, rank, world, fused, graph=False):
     import main
     from nerf.network_grid import NeRFNetwork
     from nerf.provider import NeRFDataset
@@ -66,7 +68,8 @@ def make_trainer(res, seed, rank, world, fused):
     trainer = Trainer("df", opt, model, guidance, device=device, workspace=None,
                       optimizer=optimizer, ema_decay=None, fp16=True, lr_scheduler=sched,
                       use_checkpoint="scratch", scheduler_update_every_step=True,
-                      local_rank=rank, world_size=world, mute=True, fused_backward=fused)
+                      local_rank=rank, world_size=world, mute=True, fused_backward=fused,
+                      graph_step=graph)
     data = NeRFDataset(opt, device=device, type="train", H=res, W=res, size=100)
     trainer.model.train()
     return trainer, data
@@ -102,12 +105,13 @@ def cpu_baseline(res, steps):
 def summarize_kernels(records):
     torch.cuda.synchronize()
     per = {}
+    import _dfhip
     for name, e0, e1, nbytes in records:
         ms = e0.elapsed_time(e1)
         d = per.setdefault(name, [0.0, 0, 0])
         d[0] += ms
         d[1] += 1
-        d[2] += nbytes
+        d[2] += _dfhip.record_bytes(nbytes)
     out = {}
     for name, (ms, n, nbytes) in per.items():
         avg_ms = ms / n
@@ -163,7 +167,8 @@ def main():
 
     import _dfhip
     _dfhip.load()
-    trainer, data = make_trainer(args.res, args.seed, rank, world, not args.two_pass_backward)
+    trainer, data = make_trainer(args.res, args.seed, rank, world, not args.two_pass_backward,
+                                 graph=not (args.eager or args.two_pass_backward))
 
     def step():
         trainer.train_iteration(data.collate([0]))
@@ -213,6 +218,7 @@ def main():
                    "global_batch": world, "rays_per_step_per_gpu": rays_per_step,
                    "parallelism": f"dp{world}",
                    "backward": "two-pass (reference)" if args.two_pass_backward else "fused",
+                   "launch": "eager" if not trainer.graph_step else "hip-graph replay",
                    "mean_samples_per_step": round(samples, 1)},
         "steps_per_sec": round(steps_per_sec, 3),
     }

@@ -152,6 +152,29 @@ int dfhip_composite_rays_train_backward_dense(int dtype, const void *grad_weight
                                               void *grad_sigmas, void *grad_rgbs,
                                               dfhip_stream_t stream);
 
+/* Native mixed-precision form of the two calls above for the fp16 train step:
+ * sigmas, deltas, weights_sum, depth, image and their gradients are f32, the
+ * colours `rgbs` and `grad_rgbs` are `rgb_dtype` (DFHIP_F32 or DFHIP_F16).
+ * Same arithmetic as the reference, whose custom_fwd casts f16 colours to f32
+ * (exact) and whose autograd casts the f32 colour gradient back to f16 once.
+ * The backward is the dense form (needs ray-ordered contiguous rays);
+ * zero_tail = 0 leaves rows [total, M) untouched, for capacity-sized buffers
+ * whose consumers stop at the live sample count. */
+int dfhip_composite_rays_train_forward_mixed(int rgb_dtype, const float *sigmas,
+                                             const void *rgbs, const float *deltas,
+                                             const int32_t *rays, uint32_t M, uint32_t N,
+                                             float T_thresh, float *weights_sum,
+                                             float *depth, float *image,
+                                             dfhip_stream_t stream);
+int dfhip_composite_rays_train_backward_mixed(int rgb_dtype, const float *grad_weights_sum,
+                                              const float *grad_image, const float *sigmas,
+                                              const void *rgbs, const float *deltas,
+                                              const int32_t *rays, const float *weights_sum,
+                                              const float *image, uint32_t M, uint32_t N,
+                                              float T_thresh, float *grad_sigmas,
+                                              void *grad_rgbs, int zero_tail,
+                                              dfhip_stream_t stream);
+
 /* raymarching.cu:808 march_rays(n_alive, n_step, rays_alive, rays_t, rays_o,
  *   rays_d, bound, dt_gamma, max_steps, C, H, grid, near, far, xyzs, dirs,
  *   deltas, noises).  Every one of a ray's n_step slots is written (zeros past

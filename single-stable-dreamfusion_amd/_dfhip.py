@@ -43,6 +43,10 @@ _SIGS = {
                                             _u32, _f32, _vp, _vp, _vp],
     "dfhip_composite_rays_train_backward_dense": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                                   _u32, _u32, _f32, _vp, _vp, _vp],
+    "dfhip_composite_rays_train_forward_mixed": [_i32, _vp, _vp, _vp, _vp, _u32, _u32, _f32,
+                                                 _vp, _vp, _vp, _vp],
+    "dfhip_composite_rays_train_backward_mixed": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                  _u32, _u32, _f32, _vp, _vp, _i32, _vp],
     "dfhip_march_rays": [_i32, _u32, _u32, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _vp,
                          _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dfhip_composite_rays": [_i32, _u32, _u32, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -120,26 +124,38 @@ def exported_symbols() -> list[str]:
 
 class _KernelTimer:
     def __init__(self):
-        self.records = []  # (name, start_event, end_event, bytes)
+        self.records = []  # (name, start_event, end_event, bytes or callable -> bytes)
 
-    def region(self, name, nbytes):
-        return _Region(self, name, nbytes)
+    def region(self, name, nbytes, live=None, per_row=0):
+        return _Region(self, name, nbytes, live, per_row)
 
 
 class _Region:
-    __slots__ = ("timer", "name", "nbytes", "e0")
+    __slots__ = ("timer", "name", "nbytes", "e0", "live", "per_row")
 
-    def __init__(self, timer, name, nbytes):
+    def __init__(self, timer, name, nbytes, live, per_row):
         self.timer, self.name, self.nbytes = timer, name, nbytes
+        self.live, self.per_row = live, per_row
 
     def __enter__(self):
+        if self.live is not None:
+            # snapshot the device-side row count (read when the records are
+            # summarised, never inside the timed stretch)
+            snap, base, per_row = self.live.clone(), self.nbytes, self.per_row
+            self.nbytes = lambda: base + per_row * int(snap.item())
         self.e0 = torch.cuda.Event(enable_timing=True)
         self.e0.record()
+        return self
 
     def __exit__(self, *exc):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
         self.timer.records.append((self.name, self.e0, e1, self.nbytes))
+
+
+def record_bytes(nbytes):
+    """Bytes of a timing record (resolves deferred, device-count-based sizes)."""
+    return nbytes() if callable(nbytes) else nbytes
 
 
 class _NoRegion:
@@ -165,9 +181,16 @@ def new_kernel_timer():
     return _KernelTimer()
 
 
-def timed(name, nbytes):
-    """Context manager timing one launch region when a timer is installed."""
-    return _NO_REGION if _timer is None else _timer.region(name, nbytes)
+def timing():
+    """The installed _KernelTimer, or None."""
+    return _timer
+
+
+def timed(name, nbytes, live=None, per_row=0):
+    """Context manager timing one launch region when a timer is installed.
+    Algorithmic bytes = nbytes + per_row * live[0] when `live` (an int32
+    device tensor holding a row count) is given, else nbytes."""
+    return _NO_REGION if _timer is None else _timer.region(name, nbytes, live, per_row)
 
 
 def call(name: str, *args) -> None:

@@ -116,6 +116,42 @@ def composite_rays_train_backward_dense(*args):
     _composite_bwd("dfhip_composite_rays_train_backward_dense", *args)
 
 
+# ---- native mixed-precision train compositing (f32 sigmas, f16/f32 colours)
+
+def _f32_only(t, what):
+    checked(t, what)
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{what} must be a float32 tensor")
+
+
+def composite_rays_train_forward_mixed(sigmas, rgbs, deltas, rays, M, N, T_thresh, weights_sum,
+                                       depth, image):
+    for t, w in ((sigmas, "sigmas"), (deltas, "deltas"), (weights_sum, "weights_sum"),
+                 (depth, "depth"), (image, "image")):
+        _f32_only(t, w)
+    rd = _f(rgbs, "rgbs")
+    checked(rays, "rays", "int")
+    call("dfhip_composite_rays_train_forward_mixed", rd, ptr(sigmas), ptr(rgbs), ptr(deltas),
+         ptr(rays), M, N, T_thresh, ptr(weights_sum), ptr(depth), ptr(image), stream())
+
+
+def composite_rays_train_backward_mixed(grad_weights_sum, grad_image, sigmas, rgbs, deltas, rays,
+                                        weights_sum, image, M, N, T_thresh, grad_sigmas,
+                                        grad_rgbs, zero_tail=True):
+    for t, w in ((grad_weights_sum, "grad_weights_sum"), (grad_image, "grad_image"),
+                 (sigmas, "sigmas"), (deltas, "deltas"), (weights_sum, "weights_sum"),
+                 (image, "image"), (grad_sigmas, "grad_sigmas")):
+        _f32_only(t, w)
+    rd = _f(rgbs, "rgbs")
+    checked(grad_rgbs, "grad_rgbs")
+    if grad_rgbs.dtype != rgbs.dtype:
+        raise RuntimeError("grad_rgbs must have the dtype of rgbs")
+    checked(rays, "rays", "int")
+    call("dfhip_composite_rays_train_backward_mixed", rd, ptr(grad_weights_sum), ptr(grad_image),
+         ptr(sigmas), ptr(rgbs), ptr(deltas), ptr(rays), ptr(weights_sum), ptr(image), M, N,
+         T_thresh, ptr(grad_sigmas), ptr(grad_rgbs), int(bool(zero_tail)), stream())
+
+
 def march_rays(n_alive, n_step, rays_alive, rays_t, rays_o, rays_d, bound, dt_gamma, max_steps, C,
                H, grid, near, far, xyzs, dirs, deltas, noises):
     dt = _f(rays_o, "rays_o")

@@ -387,9 +387,9 @@ template <typename scalar_t> struct Acc { typedef float type; };
 template <> struct Acc<double> { typedef double type; };
 
 // raymarching.cu:500-577
-template <typename scalar_t>
+template <typename scalar_t, typename rgb_t = scalar_t>
 __global__ __launch_bounds__(64) void k_composite_train_fwd(
-    const scalar_t *__restrict__ sigmas, const scalar_t *__restrict__ rgbs,
+    const scalar_t *__restrict__ sigmas, const rgb_t *__restrict__ rgbs,
     const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays, uint32_t M,
     uint32_t N, float T_thresh, scalar_t *weights_sum, scalar_t *depth, scalar_t *image) {
     typedef typename Acc<scalar_t>::type acc_t;
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(64) void k_composite_train_fwd(
     acc_t T = 1, r = 0, g = 0, b = 0, ws = 0, t = 0, d = 0;
     if (num != 0 && offset + num <= M) {
         const scalar_t *s = sigmas + offset;
-        const scalar_t *c = rgbs + 3 * (size_t)offset;
+        const rgb_t *c = rgbs + 3 * (size_t)offset;
         const scalar_t *dl = deltas + 2 * (size_t)offset;
         for (uint32_t i = 0; i < num; ++i) {
             const acc_t alpha = (acc_t)1.0f - (acc_t)__expf(-to_f(s[i]) * to_f(dl[2 * i]));
@@ -423,14 +423,31 @@ __global__ __launch_bounds__(64) void k_composite_train_fwd(
     image[3 * index + 2] = (scalar_t)b;
 }
 
-// raymarching.cu:601-682.  DENSE: also zero rows the reference leaves untouched.
-template <typename scalar_t, bool DENSE>
+// Colour-gradient store.  f32 compositing of f16 colours: the f32 product is
+// rounded to f16 once, as the reference's autograd cast of its f32 gradient
+// does.  f32_rounded keeps the backend from fusing product and conversion into
+// one v_fma_mix, which rounds the exact product once and can differ in the
+// last f16 bit.
+template <typename scalar_t, typename rgb_t, typename acc_t>
+__device__ __forceinline__ rgb_t grad_cast(acc_t v) { return (rgb_t)v; }
+template <>
+__device__ __forceinline__ half_t grad_cast<float, half_t, float>(float v) {
+    return (half_t)f32_rounded(v);
+}
+
+// raymarching.cu:601-682.  DENSE: also zero rows the reference leaves untouched
+// (past each ray's break; with `tail`, also rows [total, M) after the last ray).
+// rgb_t = f16 reads the field's f16 colours and writes their f16 gradient
+// directly: the reference casts them to f32 on entry (custom_fwd) and its
+// autograd casts the f32 gradient back to f16 once, which is this rounding.
+template <typename scalar_t, bool DENSE, typename rgb_t = scalar_t>
 __global__ __launch_bounds__(64) void k_composite_train_bwd(
     const scalar_t *__restrict__ grad_ws, const scalar_t *__restrict__ grad_image,
-    const scalar_t *__restrict__ sigmas, const scalar_t *__restrict__ rgbs,
+    const scalar_t *__restrict__ sigmas, const rgb_t *__restrict__ rgbs,
     const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays,
     const scalar_t *__restrict__ weights_sum, const scalar_t *__restrict__ image,
-    uint32_t M, uint32_t N, float T_thresh, scalar_t *grad_sigmas, scalar_t *grad_rgbs) {
+    uint32_t M, uint32_t N, float T_thresh, scalar_t *grad_sigmas, rgb_t *grad_rgbs,
+    int tail = 1) {
     typedef typename Acc<scalar_t>::type acc_t;
     const uint32_t n = blockIdx.x * 64 + threadIdx.x;
     if (n >= N) return;
@@ -438,13 +455,14 @@ __global__ __launch_bounds__(64) void k_composite_train_bwd(
     const uint32_t offset = (uint32_t)rays[3 * n + 1];
     const uint32_t num = (uint32_t)rays[3 * n + 2];
     const scalar_t zero = (scalar_t)0.0f;
+    const rgb_t czero = (rgb_t)0.0f;
     uint32_t i = 0;
     if (num != 0 && offset + num <= M) {
         const scalar_t *s = sigmas + offset;
-        const scalar_t *c = rgbs + 3 * (size_t)offset;
+        const rgb_t *c = rgbs + 3 * (size_t)offset;
         const scalar_t *dl = deltas + 2 * (size_t)offset;
         scalar_t *gs = grad_sigmas + offset;
-        scalar_t *gc = grad_rgbs + 3 * (size_t)offset;
+        rgb_t *gc = grad_rgbs + 3 * (size_t)offset;
         const acc_t gr = to_f(grad_image[3 * index + 0]);
         const acc_t gg = to_f(grad_image[3 * index + 1]);
         const acc_t gb = to_f(grad_image[3 * index + 2]);
@@ -464,9 +482,9 @@ __global__ __launch_bounds__(64) void k_composite_train_bwd(
             b = fma(w, cb, b);
             ws += w;
             T *= (acc_t)1.0f - alpha;
-            gc[3 * i + 0] = (scalar_t)(gr * w);
-            gc[3 * i + 1] = (scalar_t)(gg * w);
-            gc[3 * i + 2] = (scalar_t)(gb * w);
+            gc[3 * i + 0] = grad_cast<scalar_t, rgb_t>(gr * w);
+            gc[3 * i + 1] = grad_cast<scalar_t, rgb_t>(gg * w);
+            gc[3 * i + 2] = grad_cast<scalar_t, rgb_t>(gb * w);
             // ((gr*A + gg*B) + gb*C) + gw*D, nvcc contraction: fuse the left product.
             acc_t acc = fma(gr, fma(T, cr, -(rf - r)), gg * fma(T, cg, -(gf - g)));
             acc = fma(gb, fma(T, cb, -(bf - b)), acc);
@@ -480,12 +498,12 @@ __global__ __launch_bounds__(64) void k_composite_train_bwd(
         const uint64_t end = min((uint64_t)offset + num, (uint64_t)M);
         for (uint64_t row = (uint64_t)offset + i; row < end; ++row) {
             grad_sigmas[row] = zero;
-            grad_rgbs[3 * row] = zero; grad_rgbs[3 * row + 1] = zero; grad_rgbs[3 * row + 2] = zero;
+            grad_rgbs[3 * row] = czero; grad_rgbs[3 * row + 1] = czero; grad_rgbs[3 * row + 2] = czero;
         }
-        if (n == N - 1) {
+        if (tail && n == N - 1) {
             for (uint64_t row = (uint64_t)offset + num; row < M; ++row) {
                 grad_sigmas[row] = zero;
-                grad_rgbs[3 * row] = zero; grad_rgbs[3 * row + 1] = zero; grad_rgbs[3 * row + 2] = zero;
+                grad_rgbs[3 * row] = czero; grad_rgbs[3 * row + 1] = czero; grad_rgbs[3 * row + 2] = czero;
             }
         }
     }
@@ -747,6 +765,54 @@ extern "C" int dfhip_composite_rays_train_backward_dense(
                                     grad_weights_sum, grad_image, sigmas, rgbs, deltas, rays,
                                     weights_sum, image, M, N, T_thresh, grad_sigmas, grad_rgbs,
                                     stream);
+}
+
+// Mixed-precision train compositing (native): sigmas / deltas / outputs f32,
+// colours (and their gradient) in `rgb_dtype` (f32 or f16).  The backward is
+// the dense form; `zero_tail` = 0 leaves rows past the last ray untouched (the
+// capacity-sized buffers of the device-count march, whose consumers stop at
+// the live count).
+extern "C" int dfhip_composite_rays_train_forward_mixed(
+    int rgb_dtype, const float *sigmas, const void *rgbs, const float *deltas,
+    const int32_t *rays, uint32_t M, uint32_t N, float T_thresh, float *weights_sum,
+    float *depth, float *image, dfhip_stream_t stream) {
+    const char *name = "composite_rays_train_forward_mixed";
+    if (N == 0) return DFHIP_OK;
+    hipStream_t s = as_stream(stream);
+    if (rgb_dtype == DFHIP_F32)
+        k_composite_train_fwd<float, float><<<ceil_div(N, 64u), 64, 0, s>>>(
+            sigmas, (const float *)rgbs, deltas, rays, M, N, T_thresh, weights_sum, depth, image);
+    else if (rgb_dtype == DFHIP_F16)
+        k_composite_train_fwd<float, half_t><<<ceil_div(N, 64u), 64, 0, s>>>(
+            sigmas, (const half_t *)rgbs, deltas, rays, M, N, T_thresh, weights_sum, depth, image);
+    else {
+        set_error("%s: rgb dtype must be f32 or f16 (got %d)", name, rgb_dtype);
+        return DFHIP_EDTYPE;
+    }
+    return check_launch(name);
+}
+
+extern "C" int dfhip_composite_rays_train_backward_mixed(
+    int rgb_dtype, const float *grad_weights_sum, const float *grad_image, const float *sigmas,
+    const void *rgbs, const float *deltas, const int32_t *rays, const float *weights_sum,
+    const float *image, uint32_t M, uint32_t N, float T_thresh, float *grad_sigmas,
+    void *grad_rgbs, int zero_tail, dfhip_stream_t stream) {
+    const char *name = "composite_rays_train_backward_mixed";
+    if (N == 0) return DFHIP_OK;
+    hipStream_t s = as_stream(stream);
+    if (rgb_dtype == DFHIP_F32)
+        k_composite_train_bwd<float, true, float><<<ceil_div(N, 64u), 64, 0, s>>>(
+            grad_weights_sum, grad_image, sigmas, (const float *)rgbs, deltas, rays, weights_sum,
+            image, M, N, T_thresh, grad_sigmas, (float *)grad_rgbs, zero_tail);
+    else if (rgb_dtype == DFHIP_F16)
+        k_composite_train_bwd<float, true, half_t><<<ceil_div(N, 64u), 64, 0, s>>>(
+            grad_weights_sum, grad_image, sigmas, (const half_t *)rgbs, deltas, rays, weights_sum,
+            image, M, N, T_thresh, grad_sigmas, (half_t *)grad_rgbs, zero_tail);
+    else {
+        set_error("%s: rgb dtype must be f32 or f16 (got %d)", name, rgb_dtype);
+        return DFHIP_EDTYPE;
+    }
+    return check_launch(name);
 }
 
 extern "C" int dfhip_march_rays(int dtype, uint32_t n_alive, uint32_t n_step,

@@ -23,6 +23,29 @@ import _gridencoder
 from gridencoder.grid import _parts
 
 
+# When a list, _GridField.backward appends (launch, grad_buffer) instead of
+# launching the embedding backward (see defer_embedding_backward).
+_deferred = None
+
+
+class defer_embedding_backward:
+    """Context: collect the fused field's embedding-gradient launches instead of
+    running them inside the backward.  Used while capturing the train step in
+    a HIP graph: the graph holds everything up to the feature gradients, and
+    the embedding scatter (the step's largest kernel) is launched after each
+    replay, timed on its stream like any eager launch."""
+
+    def __enter__(self):
+        global _deferred
+        self.prev, _deferred = _deferred, []
+        return _deferred
+
+    def __exit__(self, *exc):
+        global _deferred
+        _deferred = self.prev
+        return False
+
+
 def eligible(encoder, layers, x):
     if not (x.is_cuda and torch.is_autocast_enabled("cuda")):
         return False
@@ -52,7 +75,9 @@ class _GridField(Function):
         ws = [w.detach().float().contiguous() for w in weights]
         # algorithmic bytes per sample: xyz + features out + sigma/albedo out,
         # plus the f16 table once (the gathers hit L2 / MALL)
-        with _dfhip.timed("grid_field_forward", cap * (12 + 64 + 4 + 6) + table.numel() * 2):
+        per, base = 12 + 64 + 4 + 6, table.numel() * 2
+        with _dfhip.timed("grid_field_forward", base + (0 if m_dev is not None else cap * per),
+                          m_dev, per):
             _fieldmlp.grid_field_forward(x, bound, table, offsets, S, H, gridtype, align, ws, enc,
                                          sigma, albedo, m_dev)
         ctx.save_for_backward(x, enc, offsets, m_dev, *ws)
@@ -82,16 +107,33 @@ class _GridField(Function):
             gpartial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, C, gparts),
                                    device=dev)
         # MLP backward: features + positions + incoming grads in, feature grads out
-        with _dfhip.timed("field_mlp_backward", cap * (64 + 12 + 4 + 6 + 64)):
+        per = 64 + 12 + 4 + 6 + 64
+        with _dfhip.timed("field_mlp_backward", 0 if m_dev is not None else cap * per, m_dev,
+                          per):
             _fieldmlp.grid_field_backward(enc, x, bound, ws, grad_sigma, grad_albedo, d_enc,
                                           mlp_partial, grads, offsets, rows, S, H, gridtype,
                                           align, None, None, gparts, m_dev)
         if grad_emb is not None:
-            nbytes = cap * (12 + L * C * 2) + 4 * rows * C
-            with _dfhip.timed("grid_encode_backward", nbytes):
-                _gridencoder.grid_encode_backward_sliced_dyn(d_enc, x, bound, offsets, grad_emb,
-                                                             rows, cap, m_dev, 3, C, L, S, H,
-                                                             gridtype, align, gpartial, gparts)
+            def embedding_backward(grad_emb=grad_emb):
+                # algorithmic bytes: per live sample its position and feature
+                # grads, plus the table gradient once
+                per = 12 + L * C * 2
+                base, live = 4 * rows * C, m_dev
+                if live is None:
+                    base += cap * per
+                with _dfhip.timed("grid_encode_backward", base, live, per):
+                    _gridencoder.grid_encode_backward_sliced_dyn(
+                        d_enc, x, bound, offsets, grad_emb, rows, cap, m_dev, 3, C, L, S, H,
+                        gridtype, align, gpartial, gparts)
+                return grad_emb
+
+            if _deferred is not None:
+                # graph capture: the embedding scatter runs after the replay
+                # (Trainer), the gradient lands in grad_emb, not via autograd
+                _deferred.append((embedding_backward, grad_emb))
+                grad_emb = None
+            else:
+                embedding_backward()
         return (None, None, grad_emb, None, None, None, *grads)
 
 

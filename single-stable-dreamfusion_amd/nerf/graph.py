@@ -1,0 +1,117 @@
+"""HIP-graph capture of the SDS train step.
+
+The reference's train step (nerf/utils.py:693-715 -> train_step :337-404 ->
+NeRFRenderer.run_cuda, renderer.py:446-559) is ~300 small launches plus one
+host synchronisation (the march's `step_counter[0].item()`,
+raymarching.py:224).  On MI355X the kernels of one 128x128 step take ~2.7 ms
+while the eager step takes ~4.7 ms: the rest is launch latency and the drain
+after the sync.  Here the step is captured once per (shading, resolution) and
+replayed:
+
+* the march runs in its device-count form (raymarching.march_rays_train_dev):
+  capacity-sized sample buffers, the live count stays on the GPU, every
+  per-sample consumer (fused grid field, mixed compositing, their backwards)
+  stops at it;
+* the graph holds render -> SDS gradient -> regulariser -> backward down to
+  the feature gradients;
+* after each replay the embedding-gradient scatter (the step's largest
+  kernel) is launched eagerly (timed on its stream like any launch), then the
+  gradient all-reduce (multi-GPU), GradScaler + fused Adam and the LR
+  schedule run as in the eager step.
+
+Only the albedo shading is captured (the reference's first `albedo_iters`
+steps and 20 % of the later ones): the finite-difference normal paths run
+eagerly.  RNG draws inside the graph (march noise, background colour, light
+direction, timestep, SDS noise) use torch's graph-safe Philox offsets, so
+every replay draws fresh numbers.
+"""
+import torch
+
+import _dfhip
+from . import field as _field
+
+
+class GraphedTrainStep:
+    def __init__(self, trainer, data, shading, ambient_ratio, text_z, stream):
+        self.trainer = trainer
+        self.shading, self.ambient_ratio = shading, ambient_ratio
+        self.H, self.W = data["H"], data["W"]
+        self.rays_o = data["rays_o"].detach().clone()
+        self.rays_d = data["rays_d"].detach().clone()
+        self.text_z = text_z.detach().clone()
+        self.stream = stream
+        self.graph = torch.cuda.CUDAGraph()
+        self.deferred = []
+        self.grads = None
+        self.counter = None
+        self.loss = None
+
+    def _body(self, static):
+        t = self.trainer
+        with torch.autocast("cuda", enabled=t.fp16):
+            _, _, loss = t.train_step(static, shading=self.shading,
+                                      ambient_ratio=self.ambient_ratio, text_z=self.text_z)
+        t.backward_only(loss)
+        return loss
+
+    def capture(self):
+        """Record the step (nothing of it executes until replay()).
+
+        First one untimed dry run of the same code on the capture stream (its
+        gradients are dropped, no optimizer step): the BLAS / MIOpen libraries
+        set up per-stream state on first use, which must not happen inside the
+        capture (HIP then faults when the capture ends)."""
+        t = self.trainer
+        model = t.model
+        params = [p for p in model.parameters() if p.requires_grad]
+        static = {"H": self.H, "W": self.W, "rays_o": self.rays_o, "rays_d": self.rays_d,
+                  "dir": None}
+        model.device_count_march = True
+        timer = _dfhip.set_kernel_timer(None)  # no event records inside the graph
+        step0 = model.local_step
+        # the graph's march counts into a private row; every replay's count is
+        # copied into the row of its own step (Trainer)
+        step_counter = model.step_counter
+        model.step_counter = torch.zeros_like(step_counter)
+        try:
+            self.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                t.optimizer.zero_grad(set_to_none=True)
+                with _field.defer_embedding_backward():
+                    self._body(static)
+                t.optimizer.zero_grad(set_to_none=True)
+            model.local_step = step0
+            with _field.defer_embedding_backward() as deferred:
+                with torch.cuda.graph(self.graph, stream=self.stream):
+                    self.loss = self._body(static).detach()
+            torch.cuda.current_stream().wait_stream(self.stream)
+        finally:
+            model.device_count_march = False
+            model.step_counter = step_counter
+            _dfhip.set_kernel_timer(timer)
+        self.deferred = list(deferred)
+        self.counter = model.last_counter
+        # gradients written by the graph (the embedding's comes from the
+        # deferred launch), re-attached after every replay
+        emb = getattr(model, "encoder", None)
+        self.grads = []
+        for p in params:
+            g = p.grad
+            if g is None and emb is not None and p is emb.embeddings and self.deferred:
+                g = self.deferred[0][1]
+            self.grads.append((p, g))
+
+    def load(self, data, text_z):
+        """Copy this step's camera rays and prompt embedding into the graph's inputs."""
+        self.rays_o.copy_(data["rays_o"], non_blocking=True)
+        self.rays_d.copy_(data["rays_d"], non_blocking=True)
+        self.text_z.copy_(text_z, non_blocking=True)
+
+    def replay(self):
+        """Run the captured part, then the deferred embedding backward; leaves
+        every trainable parameter's .grad set for the optimizer step."""
+        self.graph.replay()
+        for launch, _ in self.deferred:
+            launch()
+        for p, g in self.grads:
+            p.grad = g

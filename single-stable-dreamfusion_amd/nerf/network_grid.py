@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import raymarching
 from activation import trunc_exp
 from encoding import get_encoder
 
@@ -77,7 +78,9 @@ class NeRFNetwork(NeRFRenderer):
         """x [N, 3] in [-bound, bound] -> sigma [N] (f32), albedo [N, 3]."""
         if _FUSED_FIELD and _field.eligible(self.encoder, self.sigma_net.net, x):
             # encoder + MLP + heads as one native node (nerf/field.py)
-            return _field.grid_field(x, self.bound, self.encoder, self.sigma_net.net)
+            # capacity-sized samples of the device-count march carry their live count
+            return _field.grid_field(x, self.bound, self.encoder, self.sigma_net.net,
+                                     m_dev=raymarching.live_rows(x))
         h = self.sigma_net(self.encoder(x, bound=self.bound))
         sigma = trunc_exp(h[..., 0] + self.gaussian(x))
         albedo = torch.sigmoid(h[..., 1:])

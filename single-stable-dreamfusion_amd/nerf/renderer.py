@@ -70,6 +70,10 @@ class NeRFRenderer(nn.Module):
             self.register_buffer("step_counter", torch.zeros(16, 2, dtype=torch.int32))
             self.mean_count = 0
             self.local_step = 0
+            self.last_counter = None
+        # march_rays_train_dev instead of march_rays_train on the albedo train
+        # path (set by the Trainer while it captures / replays the step graph)
+        self.device_count_march = False
 
     # field interface, implemented by the network subclass
     def forward(self, x, d):
@@ -204,10 +208,19 @@ class NeRFRenderer(nn.Module):
             counter = self.step_counter[self.local_step % 16]
             counter.zero_()
             self.local_step += 1
-            xyzs, dirs, deltas, rays = raymarching.march_rays_train(
-                rays_o, rays_d, self.bound, self.density_bitfield, self.cascade, self.grid_size,
-                nears, fars, counter, self.mean_count, perturb, 128, force_all_rays, dt_gamma,
-                max_steps)
+            self.last_counter = counter
+            if self.device_count_march and force_all_rays and shading == "albedo":
+                # no host sync: capacity-sized samples + device-side count (the
+                # graph-captured train step); only the albedo path, whose
+                # per-sample consumers all stop at the live count
+                xyzs, dirs, deltas, rays = raymarching.march_rays_train_dev(
+                    rays_o, rays_d, self.bound, self.density_bitfield, self.cascade,
+                    self.grid_size, nears, fars, counter, perturb, dt_gamma, max_steps)
+            else:
+                xyzs, dirs, deltas, rays = raymarching.march_rays_train(
+                    rays_o, rays_d, self.bound, self.density_bitfield, self.cascade,
+                    self.grid_size, nears, fars, counter, self.mean_count, perturb, 128,
+                    force_all_rays, dt_gamma, max_steps)
             sigmas, rgbs, normals = self(xyzs, dirs, light_d, ratio=ambient_ratio, shading=shading)
             weights_sum, depth, image = raymarching.composite_rays_train(sigmas, rgbs, deltas, rays,
                                                                          T_thresh)

@@ -159,7 +159,7 @@ class Trainer(object):
                  mute=False, fp16=False, eval_interval=1, max_keep_ckpt=2, workspace="workspace",
                  best_mode="min", use_loss_as_metric=True, report_metric_at_train=False,
                  use_checkpoint="latest", use_tensorboardX=True, scheduler_update_every_step=False,
-                 fused_backward=True):
+                 fused_backward=True, graph_step=False):
         self.name = name
         self.opt = opt
         self.mute = mute
@@ -179,6 +179,10 @@ class Trainer(object):
         self.time_stamp = time.strftime("%Y-%m-%d_%H-%M-%S")
         self.scheduler_update_every_step = scheduler_update_every_step
         self.fused_backward = fused_backward
+        # HIP-graph replay of albedo steps (nerf/graph.py)
+        self.graph_step = graph_step
+        self._graphs = {}
+        self._capture_stream = None
         self.device = device if device is not None else torch.device(
             f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu")
 
@@ -267,30 +271,36 @@ class Trainer(object):
             self.log_ptr.flush()
 
     # ------------------------------------------------------------ train step
-    def train_step(self, data):
+    def pick_shading(self):
+        """Shading of this step (utils.py:346-360): albedo during the first
+        albedo_iters steps, then albedo / textureless / lambertian at 20/40/40 %."""
+        if self.global_step < self.opt.albedo_iters:
+            return "albedo", 1.0
+        r = random.random()
+        if r > 0.8:
+            return "albedo", 1.0
+        if r > 0.4:
+            return "textureless", 0.1
+        return "lambertian", 0.1
+
+    def train_step(self, data, shading=None, ambient_ratio=None, text_z=None):
         """Render one random view, take the SDS step and assemble the
         regularisers (reference utils.py:337-404).  Returns
-        (pred_rgb [B,3,H,W], pred_ws [B,1,H,W], loss)."""
+        (pred_rgb [B,3,H,W], pred_ws [B,1,H,W], loss).  shading / text_z are
+        picked here (as the reference does) unless given."""
         rays_o, rays_d = data["rays_o"], data["rays_d"]
         B, N = rays_o.shape[:2]
         H, W = data["H"], data["W"]
-        if self.global_step < self.opt.albedo_iters:
-            shading, ambient_ratio = "albedo", 1.0
-        else:
-            r = random.random()
-            if r > 0.8:
-                shading, ambient_ratio = "albedo", 1.0
-            elif r > 0.4:
-                shading, ambient_ratio = "textureless", 0.1
-            else:
-                shading, ambient_ratio = "lambertian", 0.1
+        if shading is None:
+            shading, ambient_ratio = self.pick_shading()
         bg_color = torch.rand((B * N, 3), device=rays_o.device)
         opt_kwargs = dict(vars(self.opt))
         outputs = self.model.render(rays_o, rays_d, staged=False, perturb=True, bg_color=bg_color,
                                     ambient_ratio=ambient_ratio, shading=shading,
                                     force_all_rays=True, **opt_kwargs)
         pred_rgb = outputs["image"].reshape(B, H, W, 3).permute(0, 3, 1, 2).contiguous()
-        text_z = self.text_z[data["dir"]] if self.opt.dir_text else self.text_z
+        if text_z is None:
+            text_z = self.text_z[data["dir"]] if self.opt.dir_text else self.text_z
         if self.fused_backward and hasattr(self.guidance, "sds_grad"):
             self._pending_sds = self.guidance.sds_grad(text_z, pred_rgb)
             loss = 0
@@ -312,6 +322,11 @@ class Trainer(object):
     def backward_and_step(self, loss):
         """Back-propagate (fused or reference two-pass), exchange gradients across
         ranks and take the (scaled) optimizer step."""
+        self.backward_only(loss)
+        self.optimizer_step()
+
+    def backward_only(self, loss):
+        """The backward half of backward_and_step (captured in the step graph)."""
         scaled = self.scaler.scale(loss) if torch.is_tensor(loss) else None
         if self._pending_sds is not None:
             latents, grad = self._pending_sds
@@ -323,6 +338,9 @@ class Trainer(object):
             torch.autograd.backward(roots, grads)
         elif scaled is not None:
             scaled.backward()
+
+    def optimizer_step(self):
+        """Gradient exchange, GradScaler + optimizer step, LR schedule."""
         if self.world_size > 1:
             flat_allreduce_(self.model.parameters(), self.world_size)
         self.scaler.step(self.optimizer)
@@ -338,11 +356,46 @@ class Trainer(object):
                 self.model.update_extra_state()
         self.local_step += 1
         self.global_step += 1
+        shading, ambient_ratio = self.pick_shading()
+        if self._graph_eligible(shading):
+            return self._graph_iteration(data, shading, ambient_ratio)
         self.optimizer.zero_grad()
         with torch.autocast("cuda", enabled=self.fp16):
-            pred_rgbs, pred_ws, loss = self.train_step(data)
+            pred_rgbs, pred_ws, loss = self.train_step(data, shading, ambient_ratio)
         self.backward_and_step(loss)
-        return loss
+        # detached: a caller holding the loss must not keep this step's autograd
+        # graph (and its AccumulateGrad nodes, bound to this stream) alive into
+        # a later graph capture on another stream
+        return loss.detach() if torch.is_tensor(loss) else loss
+
+    # ------------------------------------------------------------ graph step
+    def _graph_eligible(self, shading):
+        return (self.graph_step and self.fp16 and self.model.cuda_ray and shading == "albedo"
+                and self.fused_backward and hasattr(self.guidance, "sds_grad")
+                and self.device.type == "cuda")
+
+    def _graph_iteration(self, data, shading, ambient_ratio):
+        """The step as a HIP-graph replay (nerf/graph.py): captured on the first
+        eligible step of each (shading, resolution), replayed afterwards."""
+        from .graph import GraphedTrainStep
+        model = self.model
+        text_z = self.text_z[data["dir"]] if self.opt.dir_text else self.text_z
+        if self._capture_stream is None:
+            self._capture_stream = torch.cuda.Stream(device=self.device)
+        key = (shading, ambient_ratio, data["H"], data["W"])
+        g = self._graphs.get(key)
+        row = model.local_step % 16
+        if g is None:
+            g = GraphedTrainStep(self, data, shading, ambient_ratio, text_z, self._capture_stream)
+            g.capture()  # run_cuda advanced model.local_step while recording
+            self._graphs[key] = g
+        else:
+            model.local_step += 1
+        g.load(data, text_z)
+        g.replay()
+        model.step_counter[row].copy_(g.counter)
+        self.optimizer_step()
+        return g.loss
 
     def train_one_epoch(self, loader):
         self.log(f"==> Start Training {self.workspace} Epoch {self.epoch}, "

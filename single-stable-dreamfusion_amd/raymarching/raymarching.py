@@ -199,29 +199,108 @@ class _march_rays_train(Function):
 
 march_rays_train = _march_rays_train.apply
 
+# Set on the capacity-sized tensors returned by march_rays_train_dev: an int32
+# device view of the live sample count (consumers that honour it, the fused
+# grid field and the mixed compositing, stop there; anything else reads the
+# whole capacity, which is correct but slower).
+LIVE_ROWS_ATTR = "_dfhip_live_rows"
+
+
+def live_rows(t):
+    """The int32 device view of the live row count attached to `t`, or None."""
+    return getattr(t, LIVE_ROWS_ATTR, None)
+
+
+@torch.no_grad()
+def march_rays_train_dev(rays_o, rays_d, bound, density_bitfield, C, H, nears, fars, step_counter,
+                         perturb=False, dt_gamma=0, max_steps=1024):
+    """Native form of march_rays_train(..., force_all_rays=True) with NO host
+    synchronisation (so a whole train step can be captured in a HIP graph).
+
+    Same samples, in the same ray order, as march_rays_train; the difference is
+    the shape: xyzs / dirs / deltas come back at their capacity N * max_steps
+    rows (only rows [0, step_counter[0]) are written) instead of being sliced
+    to the align-rounded count, which needs the count on the host
+    (reference raymarching.py:224).  Each returned tensor carries
+    `live_rows(t)` = step_counter[0:1]."""
+    rays_o = _flat3(rays_o)
+    rays_d = _flat3(rays_d)
+    n = rays_o.shape[0]
+    dev = rays_o.device
+    rays_o = rays_o.float()
+    rays_d = rays_d.float()
+    nears = nears.float().contiguous()
+    fars = fars.float().contiguous()
+    noises = (torch.rand(n, device=dev) if perturb else torch.zeros(n, device=dev))
+    rays = torch.empty(n, 3, dtype=torch.int32, device=dev)
+    block_sums = torch.empty(_backend.march_rays_train_scratch_ints(n), dtype=torch.int32,
+                             device=dev)
+    cap = n * max_steps
+    xyzs = torch.empty(cap, 3, device=dev)
+    dirs = torch.empty(cap, 3, device=dev)
+    deltas = torch.empty(cap, 2, device=dev)
+    density_bitfield = density_bitfield.contiguous()
+    ray_bytes = n * (4 * 9 + 12) + density_bitfield.numel()
+    with _dfhip.timed("march_rays_train_count", ray_bytes):
+        _backend.march_rays_train_count(rays_o, rays_d, density_bitfield, bound, dt_gamma,
+                                        max_steps, n, C, H, nears, fars, rays, step_counter,
+                                        noises, block_sums)
+    m_dev = step_counter[:1]
+    with _dfhip.timed("march_rays_train_emit", ray_bytes, m_dev, 32):
+        _backend.march_rays_train_emit(rays_o, rays_d, density_bitfield, bound, dt_gamma,
+                                       max_steps, n, C, H, cap, nears, fars, xyzs, dirs, deltas,
+                                       rays, noises, block_sums, 0)
+    for t in (xyzs, dirs, deltas, rays):
+        setattr(t, LIVE_ROWS_ATTR, m_dev)
+    setattr(rays, _ORDERED_ATTR, True)
+    return xyzs, dirs, deltas, rays
+
 
 class _composite_rays_train(Function):
     @staticmethod
-    @_fwd_f32
+    @custom_fwd(device_type="cuda")
     def forward(ctx, sigmas, rgbs, deltas, rays, T_thresh=1e-4):
         """Front-to-back alpha compositing of each ray's samples.
 
         sigmas [M], rgbs [M, 3], deltas [M, 2], rays [N, 3] -> weights_sum [N],
-        depth [N], image [N, 3] (colour already multiplied by alpha)."""
+        depth [N], image [N, 3] (colour already multiplied by alpha).
+
+        Under autocast every input is cast to float32 as the reference's
+        custom_fwd(cast_inputs=torch.float32) does, except that f16 colours of
+        ray-ordered samples are read (and their gradient written) as f16 by the
+        mixed kernels: the f16 -> f32 cast is exact and the reference's
+        autograd rounds the f32 colour gradient to f16 once, so the numbers are
+        the same without the two [M, 3] cast passes."""
+        ordered = bool(getattr(rays, _ORDERED_ATTR, False))
+        if torch.is_autocast_enabled("cuda"):
+            sigmas, deltas = sigmas.float(), deltas.float()
+            if not (ordered and rgbs.dtype == torch.float16):
+                rgbs = rgbs.float()
         sigmas = sigmas.contiguous()
         rgbs = rgbs.contiguous()
         deltas = deltas.contiguous()
         m, n = sigmas.shape[0], rays.shape[0]
+        # f32 sigmas with f16/f32 colours of ray-ordered samples: mixed kernels
+        mixed = (ordered and sigmas.dtype == torch.float32 and deltas.dtype == torch.float32
+                 and rgbs.dtype in (torch.float16, torch.float32))
         opts = dict(dtype=sigmas.dtype, device=sigmas.device)
         weights_sum = torch.empty(n, **opts)
         depth = torch.empty(n, **opts)
         image = torch.empty(n, 3, **opts)
-        with _dfhip.timed("composite_rays_train_forward", 24 * m + 32 * n):
-            _backend.composite_rays_train_forward(sigmas, rgbs, deltas, rays, m, n, T_thresh,
-                                                  weights_sum, depth, image)
+        live = live_rows(rays)
+        with _dfhip.timed("composite_rays_train_forward", 32 * n + (24 * m if live is None else 0),
+                          live, 24):
+            fn = (_backend.composite_rays_train_forward_mixed if mixed
+                  else _backend.composite_rays_train_forward)
+            fn(sigmas, rgbs, deltas, rays, m, n, T_thresh, weights_sum, depth, image)
         ctx.save_for_backward(sigmas, rgbs, deltas, rays, weights_sum, depth, image)
         ctx.dims = (m, n, T_thresh)
-        ctx.ordered = bool(getattr(rays, _ORDERED_ATTR, False))
+        ctx.ordered = ordered
+        ctx.mixed = mixed
+        # capacity-sized samples (march_rays_train_dev): rows past the live
+        # count are never read downstream, so the backward need not zero them
+        ctx.live = live
+        ctx.zero_tail = live is None
         return weights_sum, depth, image
 
     @staticmethod
@@ -232,6 +311,17 @@ class _composite_rays_train(Function):
         m, n, T_thresh = ctx.dims
         grad_weights_sum = grad_weights_sum.contiguous()
         grad_image = grad_image.contiguous()
+        nbytes = 40 * m + 44 * n
+        if ctx.mixed:
+            grad_sigmas = torch.empty_like(sigmas)
+            grad_rgbs = torch.empty_like(rgbs)
+            live = ctx.live
+            with _dfhip.timed("composite_rays_train_backward",
+                              nbytes if live is None else 44 * n, live, 40):
+                _backend.composite_rays_train_backward_mixed(
+                    grad_weights_sum.float(), grad_image.float(), sigmas, rgbs, deltas, rays,
+                    weights_sum, image, m, n, T_thresh, grad_sigmas, grad_rgbs, ctx.zero_tail)
+            return grad_sigmas, grad_rgbs, None, None, None
         if ctx.ordered:
             grad_sigmas = torch.empty_like(sigmas)
             grad_rgbs = torch.empty_like(rgbs)
@@ -240,7 +330,7 @@ class _composite_rays_train(Function):
             grad_sigmas = torch.zeros_like(sigmas)
             grad_rgbs = torch.zeros_like(rgbs)
             fn = _backend.composite_rays_train_backward
-        with _dfhip.timed("composite_rays_train_backward", 40 * m + 44 * n):
+        with _dfhip.timed("composite_rays_train_backward", nbytes):
             fn(grad_weights_sum, grad_image, sigmas, rgbs, deltas, rays, weights_sum, image, m, n,
                T_thresh, grad_sigmas, grad_rgbs)
         return grad_sigmas, grad_rgbs, None, None, None
