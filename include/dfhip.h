@@ -58,6 +58,16 @@ int dfhip_near_far_from_aabb(int dtype, const void *rays_o, const void *rays_d,
                              const void *aabb, uint32_t N, float min_near,
                              void *nears, void *fars, dfhip_stream_t stream);
 
+/* nerf/utils.py:42-106 get_rays(poses, intrinsics, H, W, N=-1) for one pose,
+ * as one launch (the reference runs ~10 torch ops per train step).  `pose` is a
+ * HOST pointer to the 3x4 cam2world matrix (row-major, 12 floats: rotation
+ * rows with the centre as 4th column); it is passed to the kernel by value.
+ * Writes rays_o, rays_d [H*W, 3] f32 for pixel centres (w + 0.5, h + 0.5),
+ * pixel n = h*W + w. */
+int dfhip_get_rays(const float *pose, float fx, float fy, float cx, float cy,
+                   uint32_t H, uint32_t W, float *rays_o, float *rays_d,
+                   dfhip_stream_t stream);
+
 /* raymarching.cu:201 sph_from_ray(rays_o, rays_d, radius, N, coords) */
 int dfhip_sph_from_ray(int dtype, const void *rays_o, const void *rays_d,
                        float radius, uint32_t N, void *coords,

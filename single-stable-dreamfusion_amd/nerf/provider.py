@@ -11,7 +11,7 @@ import torch
 import torch.nn.functional as F
 from torch.utils.data import DataLoader
 
-from .utils import get_rays, safe_normalize
+from .utils import get_rays, get_rays_host_pose, safe_normalize
 
 
 def get_view_direction(thetas, phis, overhead, front):
@@ -109,9 +109,15 @@ class NeRFDataset:
         self.cy = self.W / 2
 
     def collate(self, index):
+        """One full-image ray batch.  On the GPU the camera is drawn on the host
+        (a handful of scalar ops; the reference draws it with device ops whose
+        boolean-mask updates in get_view_direction synchronise every step) and
+        the rays are made by one native launch (get_rays_host_pose)."""
         B = len(index)
+        native = self.device is not None and torch.device(self.device).type == "cuda"
+        pose_dev = "cpu" if native else self.device
         if self.training:
-            poses, dirs = rand_poses(B, self.device, radius_range=self.radius_range,
+            poses, dirs = rand_poses(B, pose_dev, radius_range=self.radius_range,
                                      return_dirs=self.opt.dir_text,
                                      angle_overhead=self.opt.angle_overhead,
                                      angle_front=self.opt.angle_front, jitter=self.opt.jitter_pose,
@@ -119,14 +125,17 @@ class NeRFDataset:
             fov = random.random() * (self.fovy_range[1] - self.fovy_range[0]) + self.fovy_range[0]
         else:
             phi = (index[0] / self.size) * 360
-            poses, dirs = circle_poses(self.device, radius=self.radius_range[1] * 1.2, theta=60,
+            poses, dirs = circle_poses(pose_dev, radius=self.radius_range[1] * 1.2, theta=60,
                                        phi=phi, return_dirs=self.opt.dir_text,
                                        angle_overhead=self.opt.angle_overhead,
                                        angle_front=self.opt.angle_front)
             fov = (self.fovy_range[1] + self.fovy_range[0]) / 2
         focal = self.H / (2 * np.tan(np.deg2rad(fov) / 2))
         intrinsics = np.array([focal, focal, self.cx, self.cy])
-        rays = get_rays(poses, intrinsics, self.H, self.W, -1)
+        if native:
+            rays = get_rays_host_pose(poses, intrinsics, self.H, self.W, self.device)
+        else:
+            rays = get_rays(poses, intrinsics, self.H, self.W, -1)
         return {"H": self.H, "W": self.W, "rays_o": rays["rays_o"], "rays_d": rays["rays_d"],
                 "dir": dirs}
 

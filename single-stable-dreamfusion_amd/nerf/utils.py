@@ -80,6 +80,26 @@ def get_rays(poses, intrinsics, H, W, N=-1, error_map=None):
     return results
 
 
+def get_rays_host_pose(poses, intrinsics, H, W, device):
+    """get_rays(poses, intrinsics, H, W, N=-1) for host-side poses [B, 4, 4]:
+    one native launch per pose (csrc/camera.hip), the pose passed by value, so
+    the per-step camera needs neither a host->device copy nor a sync.
+    Returns {"rays_o", "rays_d"} [B, H*W, 3] f32 on `device`."""
+    import ctypes
+
+    import _dfhip
+    fx, fy, cx, cy = (float(v) for v in intrinsics)
+    B = poses.shape[0]
+    rays_o = torch.empty(B, H * W, 3, device=device)
+    rays_d = torch.empty(B, H * W, 3, device=device)
+    host = poses.detach().to("cpu", torch.float32).contiguous()
+    for b in range(B):
+        pose = (ctypes.c_float * 12)(*host[b, :3, :4].reshape(-1).tolist())
+        _dfhip.call("dfhip_get_rays", ctypes.cast(pose, ctypes.c_void_p), fx, fy, cx, cy, H, W,
+                    rays_o[b].data_ptr(), rays_d[b].data_ptr(), _dfhip.stream())
+    return {"rays_o": rays_o, "rays_d": rays_d}
+
+
 def seed_everything(seed):
     random.seed(seed)
     os.environ["PYTHONHASHSEED"] = str(seed)
