@@ -68,6 +68,22 @@ int dfhip_get_rays(const float *pose, float fx, float fy, float cx, float cy,
                    uint32_t H, uint32_t W, float *rays_o, float *rays_d,
                    dfhip_stream_t stream);
 
+/* nerf/renderer.py:562-615 update_extra_state, sync-free form (native).
+ * dfhip_density_grid_ema: for each queried point p, cell c = indices[p]
+ *   (int32, cascade offset included, c < cells): if grid[c] >= 0 then
+ *   grid[c] = max(grid[c] * decay, sigma[p]) (torch.maximum, NaN-propagating),
+ *   and that new value is added to acc[0], 1 to acc[1] (f64, device; the caller
+ *   zeroes acc before the first cascade).  Every cell must be queried once.
+ * dfhip_packbits_mean: thresh = min(acc[0] / acc[1], density_thresh) on the
+ *   device; bit i of byte n = grid[8n + i] > thresh (grid 16-B aligned f32);
+ *   mean_out[0] (optional) = acc[0] / acc[1] as f32. */
+int dfhip_density_grid_ema(const float *sigma, const int32_t *indices, uint32_t n,
+                           uint32_t cells, float decay, float *grid, double *acc,
+                           dfhip_stream_t stream);
+int dfhip_packbits_mean(const float *grid, uint32_t N, const double *acc,
+                        float density_thresh, uint8_t *bitfield, float *mean_out,
+                        dfhip_stream_t stream);
+
 /* raymarching.cu:201 sph_from_ray(rays_o, rays_d, radius, N, coords) */
 int dfhip_sph_from_ray(int dtype, const void *rays_o, const void *rays_d,
                        float radius, uint32_t N, void *coords,

@@ -28,6 +28,8 @@ _vp, _u32, _i32, _f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c
 _SIGS = {
     "dfhip_near_far_from_aabb": [_i32, _vp, _vp, _vp, _u32, _f32, _vp, _vp, _vp],
     "dfhip_get_rays": [_vp, _f32, _f32, _f32, _f32, _u32, _u32, _vp, _vp, _vp],
+    "dfhip_density_grid_ema": [_vp, _vp, _u32, _u32, _f32, _vp, _vp, _vp],
+    "dfhip_packbits_mean": [_vp, _u32, _vp, _f32, _vp, _vp, _vp],
     "dfhip_sph_from_ray": [_i32, _vp, _vp, _f32, _u32, _vp, _vp],
     "dfhip_morton3D": [_vp, _u32, _vp, _vp],
     "dfhip_morton3D_invert": [_vp, _u32, _vp, _vp],

@@ -74,6 +74,35 @@ class NeRFRenderer(nn.Module):
         # march_rays_train_dev instead of march_rays_train on the albedo train
         # path (set by the Trainer while it captures / replays the step graph)
         self.device_count_march = False
+        # sync-free occupancy refresh on the GPU (False: the reference's torch ops)
+        self.native_grid_update = True
+
+    # mean_density / mean_count: the sync-free grid refresh leaves them on the
+    # device; they are read to the host only when somebody asks (checkpoint,
+    # logging, the non-force_all_rays march), not every 16 steps.
+    @property
+    def mean_density(self):
+        v = self.__dict__.get("_mean_density", 0)
+        if torch.is_tensor(v):
+            v = float(v)
+            self.__dict__["_mean_density"] = v
+        return v
+
+    @mean_density.setter
+    def mean_density(self, v):
+        self.__dict__["_mean_density"] = v
+
+    @property
+    def mean_count(self):
+        v = self.__dict__.get("_mean_count", 0)
+        if torch.is_tensor(v):
+            v = int(v)
+            self.__dict__["_mean_count"] = v
+        return v
+
+    @mean_count.setter
+    def mean_count(self, v):
+        self.__dict__["_mean_count"] = v
 
     # field interface, implemented by the network subclass
     def forward(self, x, d):
@@ -219,8 +248,9 @@ class NeRFRenderer(nn.Module):
             else:
                 xyzs, dirs, deltas, rays = raymarching.march_rays_train(
                     rays_o, rays_d, self.bound, self.density_bitfield, self.cascade,
-                    self.grid_size, nears, fars, counter, self.mean_count, perturb, 128,
-                    force_all_rays, dt_gamma, max_steps)
+                    self.grid_size, nears, fars, counter,
+                    -1 if force_all_rays else self.mean_count,  # unused with force_all_rays
+                    perturb, 128, force_all_rays, dt_gamma, max_steps)
             sigmas, rgbs, normals = self(xyzs, dirs, light_d, ratio=ambient_ratio, shading=shading)
             weights_sum, depth, image = raymarching.composite_rays_train(sigmas, rgbs, deltas, rays,
                                                                          T_thresh)
@@ -276,6 +306,8 @@ class NeRFRenderer(nn.Module):
         re-pack the occupancy bitfield (reference renderer.py:562-615)."""
         if not self.cuda_ray:
             return
+        if self.density_grid.is_cuda and S >= self.grid_size and self.native_grid_update:
+            return self._update_extra_state_native(decay)
         tmp_grid = -torch.ones_like(self.density_grid)
         dev = self.density_bitfield.device
         axis = torch.arange(self.grid_size, dtype=torch.int32, device=dev).split(S)
@@ -304,6 +336,55 @@ class NeRFRenderer(nn.Module):
         total_step = min(16, self.local_step)
         if total_step > 0:
             self.mean_count = int(self.step_counter[:total_step, 0].sum().item() / total_step)
+        self.local_step = 0
+
+    def _grid_points(self):
+        """Cell-centre positions in [-1, 1] (x, y, z order of the reference's
+        meshgrid) and their morton cell indices: constant, built once."""
+        cached = self.__dict__.get("_grid_points_cache")
+        dev = self.density_grid.device
+        if cached is None or cached[0].device != dev:
+            axis = torch.arange(self.grid_size, dtype=torch.int32, device=dev)
+            xx, yy, zz = custom_meshgrid(axis, axis, axis)
+            coords = torch.stack([xx.reshape(-1), yy.reshape(-1), zz.reshape(-1)], -1)
+            indices = raymarching.morton3D(coords)
+            xyzs = 2 * coords.float() / (self.grid_size - 1) - 1
+            cached = (xyzs, indices)
+            self.__dict__["_grid_points_cache"] = cached
+        return cached
+
+    @torch.no_grad()
+    def _update_extra_state_native(self, decay):
+        """update_extra_state with no host round trip (csrc/occupancy.hip): the
+        same jittered queries (renderer.py:586-597), the EMA-max over valid
+        cells and the mean / threshold / packbits on the device.  mean_density
+        and mean_count stay device scalars until read."""
+        import _dfhip
+        xyzs, indices = self._grid_points()
+        cells = self.grid_size ** 3
+        acc = torch.zeros(2, dtype=torch.float64, device=xyzs.device)
+        for cas in range(self.cascade):
+            bound = min(2 ** cas, self.bound)
+            half = bound / self.grid_size
+            cas_xyzs = xyzs * (bound - half)
+            cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * half
+            sig = self.density(cas_xyzs)["sigma"].reshape(-1).detach().float().contiguous()
+            idx = indices if cas == 0 else indices + cas * cells
+            _dfhip.call("dfhip_density_grid_ema", sig.data_ptr(), idx.data_ptr(), sig.numel(),
+                        self.cascade * cells, float(decay), self.density_grid.data_ptr(),
+                        acc.data_ptr(), _dfhip.stream())
+        mean = torch.empty(1, dtype=torch.float32, device=xyzs.device)
+        n_bytes = self.density_grid.numel() // 8
+        _dfhip.call("dfhip_packbits_mean", self.density_grid.data_ptr(), n_bytes, acc.data_ptr(),
+                    float(self.density_thresh), self.density_bitfield.data_ptr(),
+                    mean.data_ptr(), _dfhip.stream())
+        self.mean_density = mean[0]
+        self.iter_density += 1
+        total_step = min(16, self.local_step)
+        if total_step > 0:
+            # reference: int(sum / total_step) (truncation toward zero)
+            self.mean_count = torch.div(self.step_counter[:total_step, 0].sum(), total_step,
+                                        rounding_mode="trunc")
         self.local_step = 0
 
     def render(self, rays_o, rays_d, staged=False, max_ray_batch=4096, **kwargs):

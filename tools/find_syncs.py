@@ -15,10 +15,10 @@ import torch  # noqa: E402
 
 def main():
     import bench
-    trainer, data = bench.make_trainer(128, 0, 0, 1, True)
-    b = data.collate([0])
+    graph = "--eager" not in sys.argv
+    trainer, data = bench.make_trainer(128, 0, 0, 1, True, graph=graph)
     for _ in range(3):
-        trainer.train_iteration(b)
+        trainer.train_iteration(data.collate([0]))
     torch.cuda.synchronize()
     sites = Counter()
 
@@ -30,7 +30,8 @@ def main():
     warnings.showwarning = hook
     warnings.simplefilter("always")
     torch.cuda.set_sync_debug_mode("warn")
-    trainer.train_iteration(b)
+    for _ in range(17):  # crosses one density-grid refresh
+        trainer.train_iteration(data.collate([0]))
     torch.cuda.set_sync_debug_mode(0)
     for k, v in sites.most_common():
         print(f"{v:4d}  {k}")
