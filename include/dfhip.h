@@ -382,6 +382,43 @@ int dfhip_grid_field_backward(const void *enc, const float *xyz, float bound, co
                               uint32_t gridtype, int align_corners, float *grad_embeddings,
                               float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream);
 
+/* Binned owner-computes form of grid_encode_backward (gridencoder.cu:226-313,
+ * csrc/gridbin.hip) for D = 3, C in {1, 2, 4}: (sample, level) pairs are binned
+ * by the 8192-row LDS slices their corners touch, each slice walks only its
+ * bin, partials are summed in a fixed order.  grad_lbc [L, B, C] (f16/f32, B =
+ * capacity; rows [0, *m_dev) walked when m_dev != NULL), inputs [B, 3] raw
+ * positions mapped (x + bound) / (2 bound) when bound > 0, else already in
+ * [0, 1].  offsets_host is a HOST copy of the L + 1 offsets (slice layout);
+ * offsets the device copy.  grad_embeddings [rows, C] f32 is overwritten, or
+ * added into when accumulate != 0.  [scratch] entries / counts (u32) and
+ * partial (f32) sized by dfhip_grid_backward_binned_scratch for capacity B. */
+int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host, uint32_t L,
+                                       uint32_t C, uint64_t *entries_u32, uint64_t *counts_u32,
+                                       uint64_t *partial_f32);
+int dfhip_grid_encode_backward_binned(int grad_dtype, const void *grad_lbc, const float *inputs,
+                                      float bound, const int32_t *offsets,
+                                      const int32_t *offsets_host, float *grad_embeddings,
+                                      uint32_t B, const int32_t *m_dev, uint32_t D, uint32_t C,
+                                      uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                      int align_corners, uint32_t *entries, uint32_t *counts,
+                                      float *partial, int accumulate, dfhip_stream_t stream);
+
+/* nerf/utils.py:708-713 scaler.step(optimizer); scaler.update() for
+ * torch.optim.Adam (csrc/optim.hip): non-finite check of every grad, then (if
+ * all finite) torch's fused Adam update with grad / *scale, then step += 1 per
+ * tensor and torch._amp_update_scale_ on (*scale, *growth_tracker);
+ * *found_inf (f32, zero on entry) is reset to 0 on exit.  Per tensor k (at
+ * most 24): f32 param / grad / exp_avg / exp_avg_sq [numel[k]], the device f32
+ * step counter, and the group's lr, betas, eps, weight_decay.  Pointer and
+ * hyper-parameter arrays are HOST arrays. */
+int dfhip_adam_amp_step(int count, float *const *params, const float *const *grads,
+                        float *const *exp_avg, float *const *exp_avg_sq, float *const *steps,
+                        const uint64_t *numel, const float *lr, const float *beta1,
+                        const float *beta2, const float *eps, const float *weight_decay,
+                        float *scale, int32_t *growth_tracker, float *found_inf,
+                        float growth_factor, float backoff_factor, int growth_interval,
+                        dfhip_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

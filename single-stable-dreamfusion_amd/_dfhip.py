@@ -66,6 +66,10 @@ _SIGS = {
     "dfhip_grid_encode_backward_sliced_dyn": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _u32, _u32,
                                               _vp, _u32, _u32, _u32, _f32, _u32, _u32, _i32, _vp,
                                               _u32, _i32, _vp],
+    "dfhip_grid_backward_binned_scratch": [_u32, _vp, _u32, _u32, _vp, _vp, _vp],
+    "dfhip_grid_encode_backward_binned": [_i32, _vp, _vp, _f32, _vp, _vp, _vp, _u32, _vp, _u32,
+                                          _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _vp,
+                                          _i32, _vp],
     "dfhip_grid_grad_blc_to_lbc": [_i32, _vp, _vp, _u32, _u32, _u32, _vp],
     "dfhip_field_mlp_forward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp],
     "dfhip_field_mlp_backward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,
@@ -75,6 +79,8 @@ _SIGS = {
     "dfhip_grid_field_backward": [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                   _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32, _vp],
+    "dfhip_adam_amp_step": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                            _vp, _vp, _f32, _f32, _i32, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],

@@ -102,3 +102,43 @@ def grid_encode_backward_sliced_dyn(grad_lbc, inputs, bound, offsets, grad_embed
          float(bound), ptr(offsets), ptr(grad_embeddings), total_rows, B, ptr(m_dev), D, C, L, S,
          H, gridtype, int(bool(align_corners)), ptr(partial), parts, int(bool(accumulate)),
          stream())
+
+
+# ---- binned owner-computes backward (csrc/gridbin.hip; see dfhip.h)
+
+def grid_backward_binned_scratch(cap, offsets_host, L, C):
+    """(entries u32, counts u32, partial f32) element counts for capacity cap."""
+    import ctypes
+    import numpy as np
+    off = np.ascontiguousarray(offsets_host, dtype=np.int32)
+    e, c, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    call("dfhip_grid_backward_binned_scratch", int(cap), off.ctypes.data, int(L), int(C),
+         ctypes.byref(e), ctypes.byref(c), ctypes.byref(p))
+    return int(e.value), int(c.value), int(p.value)
+
+
+def grid_encode_backward_binned(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddings,
+                                B, m_dev, D, C, L, S, H, gridtype, align_corners, entries, counts,
+                                partial, accumulate=False):
+    """grad_lbc [L, B, C] (B = capacity), inputs [B, D] raw positions in
+    [-bound, bound] (bound > 0) or [0, 1] (bound = 0); rows [0, m_dev[0]) walked
+    when m_dev is given.  grad_embeddings [rows, C] f32 is overwritten (or
+    added into with accumulate)."""
+    import numpy as np
+    checked(grad_lbc, "grad")
+    checked(inputs, "inputs")
+    checked(offsets, "offsets", "int")
+    checked(grad_embeddings, "grad_embeddings")
+    if grad_embeddings.dtype.itemsize != 4:
+        raise RuntimeError("grad_embeddings must be float32")
+    checked(entries, "entries", "int")
+    checked(counts, "counts", "int")
+    checked(partial, "partial")
+    if m_dev is not None:
+        checked(m_dev, "m_dev", "int")
+    off = np.ascontiguousarray(offsets_host, dtype=np.int32)
+    call("dfhip_grid_encode_backward_binned", _d.dtype_code(grad_lbc, "grad"), ptr(grad_lbc),
+         ptr(inputs), float(bound), ptr(offsets), off.ctypes.data, ptr(grad_embeddings), int(B),
+         ptr(m_dev), int(D), int(C), int(L), float(S), int(H), int(gridtype),
+         int(bool(align_corners)), ptr(entries), ptr(counts), ptr(partial),
+         int(bool(accumulate)), stream())

@@ -294,20 +294,6 @@ __device__ __forceinline__ void load_run(const uint32_t *__restrict__ src, uint3
     }
 }
 
-// Dynamic sample count / coordinate mapping of the fused field path: when
-// m_dev is set, only samples [0, *m_dev) of the B-row planes are walked (B is
-// then the plane stride, the capacity); when bound > 0 the inputs are raw
-// positions in [-bound, bound], mapped to [0, 1] as grid.py:142 does.
-__device__ __forceinline__ uint32_t dyn_count(const SliceDyn &dyn, uint32_t B) {
-    if (!dyn.m_dev) return B;
-    const int32_t m = *dyn.m_dev;
-    return m < 0 ? 0u : ((uint32_t)m < B ? (uint32_t)m : B);
-}
-
-__device__ __forceinline__ float dyn_map(const SliceDyn &dyn, float x) {
-    return dyn.bound > 0.0f ? (x + dyn.bound) / (2.0f * dyn.bound) : x;
-}
-
 // Generic shapes: one sample per lane, no run merging (lanes of a wave read
 // consecutive samples, coalesced).
 template <typename grad_t, uint32_t D, uint32_t C>

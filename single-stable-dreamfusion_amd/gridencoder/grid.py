@@ -165,6 +165,7 @@ class GridEncoder(nn.Module):
         offsets = level_offsets(num_levels, level_dim, input_dim, base_resolution,
                                 per_level_scale, log2_hashmap_size, align_corners)
         self.register_buffer("offsets", torch.from_numpy(offsets))
+        self.offsets_host = offsets  # host copy (the binned backward sizes its slices from it)
         self.n_params = self.offsets[-1] * level_dim
         self.embeddings = nn.Parameter(torch.empty(int(offsets[-1]), level_dim))
         self.reset_parameters()

@@ -13,6 +13,8 @@ step needs no host round trip.  Used under fp16 autocast for the reference's
 network shape (16 levels x 2 channels, 32 -> 64 -> 64 -> 4); anything else
 runs the unfused modules.
 """
+import os
+
 import numpy as np
 import torch
 from torch.autograd import Function
@@ -22,6 +24,10 @@ import _fieldmlp
 import _gridencoder
 from gridencoder.grid import _parts
 
+
+# Embedding backward: binned owner-computes (csrc/gridbin.hip, default) or the
+# LDS-sliced walk (DFHIP_GRID_BWD=sliced)
+_BINNED = os.environ.get("DFHIP_GRID_BWD", "binned") != "sliced"
 
 # When a list, _GridField.backward appends (launch, grad_buffer) instead of
 # launching the embedding backward (see defer_embedding_backward).
@@ -64,7 +70,7 @@ class _GridField(Function):
     def forward(ctx, x, bound, embeddings, offsets, meta, m_dev, *weights):
         """x [cap, 3] in [-bound, bound] f32 -> sigma [cap] f32, albedo [cap, 3]
         f16 (rows >= m_dev[0] untouched when m_dev is given)."""
-        S, H, gridtype, align = meta
+        S, H, gridtype, align, offsets_host = meta
         x = x.contiguous().float()
         cap = x.shape[0]
         table = embeddings.to(torch.half).contiguous()
@@ -81,13 +87,13 @@ class _GridField(Function):
             _fieldmlp.grid_field_forward(x, bound, table, offsets, S, H, gridtype, align, ws, enc,
                                          sigma, albedo, m_dev)
         ctx.save_for_backward(x, enc, offsets, m_dev, *ws)
-        ctx.meta = (S, H, gridtype, align, table.shape[0], L, C, float(bound))
+        ctx.meta = (S, H, gridtype, align, table.shape[0], L, C, float(bound), offsets_host)
         return sigma, albedo
 
     @staticmethod
     def backward(ctx, grad_sigma, grad_albedo):
         x, enc, offsets, m_dev, *ws = ctx.saved_tensors
-        S, H, gridtype, align, rows, L, C, bound = ctx.meta
+        S, H, gridtype, align, rows, L, C, bound, offsets_host = ctx.meta
         cap = x.shape[0]
         dev = x.device
         if grad_sigma is None:
@@ -102,10 +108,17 @@ class _GridField(Function):
         grads = [torch.empty_like(w) for w in ws]
         grad_emb = gpartial = None
         gparts = _parts(rows, C)
+        binned = _BINNED and offsets_host is not None
         if ctx.needs_input_grad[2]:
             grad_emb = torch.empty(rows, C, device=dev, dtype=torch.float32)
-            gpartial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, C, gparts),
-                                   device=dev)
+            if binned:
+                ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offsets_host, L, C)
+                scratch = (torch.empty(ne, device=dev, dtype=torch.int32),
+                           torch.empty(nc, device=dev, dtype=torch.int32),
+                           torch.empty(npf, device=dev))
+            else:
+                gpartial = torch.empty(_gridencoder.grid_backward_partial_floats(rows, C, gparts),
+                                       device=dev)
         # MLP backward: features + positions + incoming grads in, feature grads out
         per = 64 + 12 + 4 + 6 + 64
         with _dfhip.timed("field_mlp_backward", 0 if m_dev is not None else cap * per, m_dev,
@@ -122,9 +135,14 @@ class _GridField(Function):
                 if live is None:
                     base += cap * per
                 with _dfhip.timed("grid_encode_backward", base, live, per):
-                    _gridencoder.grid_encode_backward_sliced_dyn(
-                        d_enc, x, bound, offsets, grad_emb, rows, cap, m_dev, 3, C, L, S, H,
-                        gridtype, align, gpartial, gparts)
+                    if binned:
+                        _gridencoder.grid_encode_backward_binned(
+                            d_enc, x, bound, offsets, offsets_host, grad_emb, cap, m_dev, 3, C,
+                            L, S, H, gridtype, align, *scratch)
+                    else:
+                        _gridencoder.grid_encode_backward_sliced_dyn(
+                            d_enc, x, bound, offsets, grad_emb, rows, cap, m_dev, 3, C, L, S, H,
+                            gridtype, align, gpartial, gparts)
                 return grad_emb
 
             if _deferred is not None:
@@ -141,7 +159,8 @@ def grid_field(x, bound, encoder, layers, m_dev=None):
     """sigma [M] (f32), albedo [M, 3] (f16) of the grid field at x [M, 3].
     m_dev: optional int32 device tensor holding the live row count."""
     meta = (float(np.log2(encoder.per_level_scale)), int(encoder.base_resolution),
-            encoder.gridtype_id, bool(encoder.align_corners))
+            encoder.gridtype_id, bool(encoder.align_corners),
+            getattr(encoder, "offsets_host", None))
     weights = []
     for lin in layers:
         weights += [lin.weight, lin.bias]

@@ -1,0 +1,93 @@
+"""GradScaler + Adam step of the train loop as one native call (csrc/optim.hip).
+
+The reference steps `scaler.step(optimizer); scaler.update()` with
+torch.optim.Adam (nerf/utils.py:708-713).  With a fused torch Adam that is
+~15 launches and ~0.4 ms of host Python per step, which on a graph-replayed
+step is the host's largest cost.  `NativeAdamAmp.step()` does the same update
+with three launches: the non-finite check, the Adam update of every tensor
+(skipped on inf) and the scale / step-count update.  It reads and writes the
+torch objects' own state (Adam's `step` / `exp_avg` / `exp_avg_sq` per
+parameter, GradScaler's `_scale` / `_growth_tracker`), so state_dict /
+load_state_dict and checkpoints are unchanged.
+"""
+import ctypes
+
+import torch
+
+import _dfhip
+
+_MAX_TENSORS = 24
+
+
+def eligible(optimizer, scaler):
+    if not isinstance(optimizer, torch.optim.Adam) or type(optimizer) is not torch.optim.Adam:
+        return False
+    if scaler is None or not scaler.is_enabled():
+        return False
+    if (scaler._growth_factor, scaler._backoff_factor) != (2.0, 0.5):
+        return False
+    n = 0
+    for g in optimizer.param_groups:
+        if g.get("amsgrad") or g.get("maximize") or g.get("differentiable"):
+            return False
+        if torch.is_tensor(g["lr"]):
+            return False
+        for p in g["params"]:
+            if not (p.is_cuda and p.dtype == torch.float32):
+                return False
+            n += 1
+    return 0 < n <= _MAX_TENSORS
+
+
+class NativeAdamAmp:
+    def __init__(self, optimizer, scaler):
+        self.optimizer = optimizer
+        self.scaler = scaler
+        self.found_inf = None
+        self._ptr_key = None
+        self._arrays = None
+
+    def _state(self, p):
+        st = self.optimizer.state[p]
+        if not st:  # torch fused Adam's lazy init (adam.py _init_group)
+            st["step"] = torch.tensor(0.0, dtype=torch.float32, device=p.device)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        elif not st["step"].is_cuda:
+            st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+        return st
+
+    def step(self):
+        """One scaler.step(optimizer) + scaler.update() (parameters without a
+        gradient are skipped, as torch does)."""
+        sc = self.scaler
+        if sc._scale is None:
+            return  # scale() never called: nothing was back-propagated
+        dev = sc._scale.device
+        if self.found_inf is None:
+            self.found_inf = torch.zeros(1, dtype=torch.float32, device=dev)
+        ts = []
+        for g in self.optimizer.param_groups:
+            b1, b2 = g["betas"]
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                st = self._state(p)
+                ts.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], st["step"], g["lr"], b1,
+                           b2, g["eps"], g["weight_decay"]))
+        if not ts:
+            return
+        key = tuple(t[i].data_ptr() for t in ts for i in range(5))
+        if key != self._ptr_key:
+            n = len(ts)
+            vp = ctypes.c_void_p * n
+            self._arrays = (n, *(vp(*[t[i].data_ptr() for t in ts]) for i in range(5)),
+                            (ctypes.c_uint64 * n)(*[t[0].numel() for t in ts]))
+            self._ptr_key = key
+        n, P, G, M, V, S, N = self._arrays
+        f = ctypes.c_float * n
+        hyper = [f(*[float(t[i]) for t in ts]) for i in range(5, 10)]
+        _dfhip.call("dfhip_adam_amp_step", n, P, G, M, V, S, N, *hyper, sc._scale.data_ptr(),
+                    sc._growth_tracker.data_ptr(), self.found_inf.data_ptr(),
+                    float(sc._growth_factor), float(sc._backoff_factor),
+                    int(sc._growth_interval), _dfhip.stream())

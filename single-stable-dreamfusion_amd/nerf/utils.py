@@ -202,6 +202,9 @@ class Trainer(object):
         # HIP-graph replay of albedo steps (nerf/graph.py)
         self.graph_step = graph_step
         self._graphs = {}
+        # GradScaler + Adam as one native call (nerf/optim.py) when eligible
+        self.native_optimizer = os.environ.get("DFHIP_NATIVE_ADAM", "1") != "0"
+        self._native_opt = None
         self._capture_stream = None
         self.device = device if device is not None else torch.device(
             f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu")
@@ -363,8 +366,17 @@ class Trainer(object):
         """Gradient exchange, GradScaler + optimizer step, LR schedule."""
         if self.world_size > 1:
             flat_allreduce_(self.model.parameters(), self.world_size)
-        self.scaler.step(self.optimizer)
-        self.scaler.update()
+        if self._native_opt is None:
+            from . import optim as _optim
+            self._native_opt = (_optim.NativeAdamAmp(self.optimizer, self.scaler)
+                                if self.native_optimizer and _optim.eligible(self.optimizer,
+                                                                            self.scaler)
+                                else False)
+        if self._native_opt:
+            self._native_opt.step()
+        else:
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
         if self.scheduler_update_every_step:
             self.lr_scheduler.step()
 

@@ -277,3 +277,78 @@ def test_sh_encoder(gpu, degree):
     (y * T(g.astype(np.float32), gpu)).sum().backward()
     np.testing.assert_allclose(xt.grad.cpu().numpy(), np.einsum("bk,bdk->bd", g, jac), rtol=1e-4,
                                atol=1e-4)
+
+
+def _binned(glbc, x, bound, offs, rows, B, m_dev, D, C, L, S, H, gt, gpu, accumulate=False,
+            gemb=None):
+    import _gridencoder
+    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, C)
+    ent = torch.empty(ne, dtype=torch.int32, device=gpu)
+    cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
+    part = torch.full((npf,), float("nan"), device=gpu)
+    if gemb is None:
+        gemb = torch.full((rows, C), float("nan"), device=gpu)  # overwritten
+    _gridencoder.grid_encode_backward_binned(glbc, x, bound, T(offs, gpu), offs, gemb, B, m_dev,
+                                             D, C, L, S, H, gt, False, ent, cnt, part,
+                                             accumulate)
+    return gemb
+
+
+@pytest.mark.parametrize("gt", [1, 0])
+def test_grid_backward_binned(gpu, gt):
+    """Binned owner-computes backward (csrc/gridbin.hip) against the exact
+    f64 oracle: f64 sums rounded to f32 once."""
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    x = _samples(50000, 21)
+    B = x.shape[0]
+    g = (np.random.default_rng(22).normal(size=(B, 32)) * 0.1).astype(np.float16)
+    want = oracle.grid_encode_backward(g, x, offs, 2, S, 16, gridtype=gt)
+    glbc = T(g, gpu).view(B, 16, 2).transpose(0, 1).contiguous()
+    gemb = _binned(glbc, T(x, gpu), 0.0, offs, rows, B, None, 3, 2, 16, S, 16, gt, gpu)
+    scale = np.abs(want).max()
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-6, atol=1e-7 * scale)
+    _binned(glbc, T(x, gpu), 0.0, offs, rows, B, None, 3, 2, 16, S, 16, gt, gpu,
+            accumulate=True, gemb=gemb)
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), 2 * want, rtol=1e-6,
+                               atol=2e-7 * scale)
+
+
+def test_grid_backward_binned_device_count(gpu):
+    """Capacity-sized planes, live count on the device, raw [-bound, bound]
+    positions: only rows [0, m) contribute (the graph-captured train step)."""
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    cap, m, bound = 9000, 6123, 1.0
+    x01 = _samples(cap, 23, edge=False)
+    g = (np.random.default_rng(24).normal(size=(cap, 32)) * 0.1).astype(np.float16)
+    want = oracle.grid_encode_backward(g[:m], x01[:m], offs, 2, S, 16)
+    glbc = T(g, gpu).view(cap, 16, 2).transpose(0, 1).contiguous()
+    xr = T(x01 * 2 * bound - bound, gpu)
+    m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+    gemb = _binned(glbc, xr, bound, offs, rows, cap, m_dev, 3, 2, 16, S, 16, 1, gpu)
+    scale = np.abs(want).max()
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5, atol=1e-6 * scale)
+
+
+@pytest.mark.parametrize("C,L,H,log2T", [(1, 8, 4, 17), (4, 6, 8, 15), (2, 16, 16, 19)])
+def test_grid_backward_binned_shapes(gpu, C, L, H, log2T):
+    from gridencoder.grid import level_offsets
+    offs = level_offsets(L, C, 3, H, 2.0, log2T, False)
+    rows = int(offs[-1])
+    x = np.random.default_rng(C + L).random((7000, 3), dtype=np.float32)
+    g = np.random.default_rng(C).normal(size=(L, 7000, C)).astype(np.float32)
+    want = oracle.grid_encode_backward(g, x, offs, C, 1.0, H, gridtype=1, blc=False)
+    gemb = _binned(T(g, gpu), T(x, gpu), 0.0, offs, rows, 7000, None, 3, C, L, 1.0, H, 1, gpu)
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
+                               atol=1e-6 * np.abs(want).max())
+
+
+def test_grid_backward_binned_empty(gpu):
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    m_dev = torch.zeros(1, dtype=torch.int32, device=gpu)
+    e = torch.zeros(16, 100, 2, dtype=torch.float16, device=gpu)
+    gemb = _binned(e, torch.zeros(100, 3, device=gpu), 1.0, offs, rows, 100, m_dev, 3, 2, 16, S,
+                   16, 1, gpu)
+    assert torch.all(gemb == 0)

@@ -143,3 +143,31 @@ def test_make_adam_keeps_generator_groups():
                     betas=(0.9, 0.99), eps=1e-15)
     assert [len(g["params"]) for g in opt.param_groups] == [2, 2]
     assert opt.param_groups[0]["lr"] == 1e-2
+
+
+def test_rand_poses_host():
+    """Host (numpy) camera sampler: orthonormal look-at-origin poses, radius in
+    range, view classes consistent with the torch get_view_direction."""
+    import random
+
+    import numpy as np
+    import torch
+
+    from nerf.provider import get_view_direction, rand_poses_host
+    np.random.seed(0)
+    random.seed(0)
+    for _ in range(20):
+        poses, dirs = rand_poses_host(4, radius_range=[1.0, 1.5], return_dirs=True)
+        assert poses.shape == (4, 4, 4) and poses.dtype == np.float32
+        R, c = poses[:, :3, :3], poses[:, :3, 3]
+        np.testing.assert_allclose(R.transpose(0, 2, 1) @ R, np.tile(np.eye(3), (4, 1, 1)),
+                                   atol=1e-5)
+        r = np.linalg.norm(c, axis=1)
+        assert np.all(r >= 1.0 - 1e-5) and np.all(r <= 1.5 + 1e-5)
+        np.testing.assert_allclose(R[:, :, 2], -c / r[:, None], atol=1e-5)  # forward -> origin
+        assert dirs.dtype == torch.int64 and int(dirs.min()) >= 0 and int(dirs.max()) <= 5
+        thetas = torch.from_numpy(np.arccos(np.clip(c[:, 1] / r, -1, 1)).astype(np.float32))
+        phis = np.arctan2(c[:, 0], c[:, 2])
+        phis = torch.from_numpy(np.where(phis < 0, phis + 2 * np.pi, phis).astype(np.float32))
+        want = get_view_direction(thetas, phis, np.deg2rad(30), np.deg2rad(60))
+        assert (want == dirs).float().mean() >= 0.75  # boundary rounding may differ
