@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--two-pass-backward", action="store_true",
                    help="reference double backward instead of the fused single pass")
+    p.add_argument("--mock-sds", action="store_true",
+                   help="SyntheticSDS (SDS arithmetic around stand-in VAE/UNet) instead of the "
+                        "injected w(t) N(0,1) gradient")
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel eagerly (no HIP-graph replay of the step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,11 +53,11 @@ def parse():
     return p.parse_args()
 
 
-def make_trainer(res, seed, rank, world, fused, graph=False):
+def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False):
     import main
     from nerf.network_grid import NeRFNetwork
     from nerf.provider import NeRFDataset
-    from nerf.sd import SyntheticSDS
+    from nerf.sd import InjectedSDS, SyntheticSDS
     from nerf.utils import Trainer, make_adam, seed_everything
 
     opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res),
@@ -62,7 +65,7 @@ def make_trainer(res, seed, rank, world, fused, graph=False):
     seed_everything(seed + rank)
     device = torch.device("cuda", torch.cuda.current_device())
     model = NeRFNetwork(opt)
-    guidance = SyntheticSDS(device)
+    guidance = SyntheticSDS(device) if mock_sds else InjectedSDS(device)
     optimizer = lambda m: make_adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)  # noqa
     sched = lambda o: torch.optim.lr_scheduler.LambdaLR(o, lambda it: 0.1 ** min(it / opt.iters, 1))  # noqa
     trainer = Trainer("df", opt, model, guidance, device=device, workspace=None,
@@ -168,7 +171,8 @@ def main():
     import _dfhip
     _dfhip.load()
     trainer, data = make_trainer(args.res, args.seed, rank, world, not args.two_pass_backward,
-                                 graph=not (args.eager or args.two_pass_backward))
+                                 graph=not (args.eager or args.two_pass_backward),
+                                 mock_sds=args.mock_sds)
 
     def step():
         trainer.train_iteration(data.collate([0]))
@@ -211,8 +215,10 @@ def main():
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp16+f32",
-        "data": "synthetic: random orbit cameras, random-init grid network, synthetic SDS "
-                "gradient (no SD-1.5 weights offline)",
+        "data": "synthetic: random orbit cameras, random-init grid network, "
+                + ("SDS arithmetic around stand-in VAE/UNet" if args.mock_sds else
+                   "seeded w(t)*N(0,1) SDS gradient injected at pred_rgb")
+                + " (no SD-1.5 weights offline)",
         "config": {"workload": f"C2: -O (fp16, cuda_ray, dir_text) {args.res}x{args.res} render, "
                                f"batch 1, max_steps 512, density grid update every 16 steps",
                    "global_batch": world, "rays_per_step_per_gpu": rays_per_step,

@@ -419,6 +419,38 @@ int dfhip_adam_amp_step(int count, float *const *params, const float *const *gra
                         float growth_factor, float backoff_factor, int growth_interval,
                         dfhip_stream_t stream);
 
+/* Per-ray tail of run_cuda (nerf/renderer.py:536-551, csrc/head.hip).
+ * Forward: bg = sigmoid(W2 relu(W1 freq6(rays_d) + b1) + b2) with the
+ * reference's fp16 autocast rounding (w1 != NULL: W1 [64, 39], b1 [64], W2
+ * [3, 64], b2 [3] f32), else bg = bg_color [N, 3] (or 1 when NULL);
+ * out_image [3, N] (channel-major) = image + (1 - ws) * bg;
+ * out_depth = max(depth - near, 0) / (far - near); mask = near < far (0/1
+ * bytes).  Backward: grad_image [N, 3] = g_image^T, grad_ws = -sum_c g_c bg_c,
+ * grad_bg = g * (1 - ws) (bg_color mode, optional) or the MLP weight grads
+ * gw1..gb2 (f32, overwritten) via `partial` sized by
+ * dfhip_ray_head_partial_floats(N). */
+uint32_t dfhip_ray_head_partial_floats(uint32_t N);
+int dfhip_ray_head_forward(uint32_t N, const float *ws, const float *depth, const float *image,
+                           const float *rays_d, const float *nears, const float *fars,
+                           const float *w1, const float *b1, const float *w2, const float *b2,
+                           const float *bg_color, float *out_image, float *out_depth,
+                           uint8_t *mask, dfhip_stream_t stream);
+int dfhip_ray_head_backward(uint32_t N, const float *g_image, const float *ws,
+                            const float *rays_d, const float *w1, const float *b1,
+                            const float *w2, const float *b2, const float *bg_color,
+                            float *grad_image, float *grad_ws, float *grad_bg, float *partial,
+                            float *gw1, float *gb1, float *gw2, float *gb2,
+                            dfhip_stream_t stream);
+
+/* nerf/utils.py:386-391 entropy regulariser: loss[0] = lambda * mean(-a log2 a
+ * - (1 - a) log2(1 - a)), a = clamp(ws, 1e-5, 1 - 1e-5) (f64 sum); backward
+ * grad_ws = grad_loss[0] * lambda / N * log2((1 - a) / a) where the clamp
+ * passes, 0 elsewhere. */
+int dfhip_entropy_forward(uint32_t N, const float *ws, float lambda, float *loss,
+                          dfhip_stream_t stream);
+int dfhip_entropy_backward(uint32_t N, const float *ws, const float *grad_loss, float lambda,
+                           float *grad_ws, dfhip_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,12 @@ _SIGS = {
                                   _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32, _vp],
     "dfhip_adam_amp_step": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                             _vp, _vp, _f32, _f32, _i32, _vp],
+    "dfhip_ray_head_forward": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _vp],
+    "dfhip_ray_head_backward": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _vp, _vp, _vp, _vp],
+    "dfhip_entropy_forward": [_u32, _vp, _f32, _vp, _vp],
+    "dfhip_entropy_backward": [_u32, _vp, _vp, _f32, _vp, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],
@@ -110,6 +116,8 @@ def load() -> ctypes.CDLL:
     lib.dfhip_field_mlp_params.argtypes = []
     lib.dfhip_field_mlp_backward_parts.restype = _u32
     lib.dfhip_field_mlp_backward_parts.argtypes = [_u32]
+    lib.dfhip_ray_head_partial_floats.restype = _u32
+    lib.dfhip_ray_head_partial_floats.argtypes = [_u32]
     lib.dfhip_grid_backward_partial_floats.restype = ctypes.c_uint64
     lib.dfhip_grid_backward_partial_floats.argtypes = [_u32, _u32, _u32]
     for name, args in _SIGS.items():
@@ -124,6 +132,7 @@ def exported_symbols() -> list[str]:
     return ["dfhip_abi_version", "dfhip_last_error", "dfhip_march_rays_train_scratch_ints",
             "dfhip_grid_backward_default_parts", "dfhip_grid_backward_partial_floats",
             "dfhip_field_mlp_params", "dfhip_field_mlp_backward_parts",
+            "dfhip_ray_head_partial_floats",
             *_SIGS.keys()]
 
 

@@ -1,0 +1,374 @@
+// Per-ray tail of the render and its regulariser, fused (reference
+// nerf/renderer.py:536-551 and nerf/utils.py:386-391):
+//
+//   bg    = sigmoid(W2 relu(W1 freq(d) + b1) + b2)         (network_grid.py:158-167,
+//                                                           fp16 Linear layers under autocast)
+//   image = image + (1 - ws) * bg                          -> written channel-major [3, N]
+//   depth = clamp(depth - near, min=0) / (far - near);  mask = near < far
+//   loss  = lambda * mean(-a log2 a - (1 - a) log2 (1 - a)),  a = clamp(ws, 1e-5, 1 - 1e-5)
+//
+// The reference runs these as ~45 small torch launches forward and backward
+// (frequency encoding, casts, two GEMMs, activations, the mix, the depth
+// normalisation, the permute of pred_rgb, the entropy terms).  Here: one
+// forward kernel, a backward kernel that also forms per-block partials of the
+// background MLP's weight gradients, one partial-sum kernel; one kernel each
+// way for the entropy term.  Rounding follows the reference's autocast
+// dtypes: the MLP's inputs, weights, hidden and output activations are f16
+// values (f32 accumulation), the colour mix is f32.  The writes of pred_rgb
+// channel-major make the reference's reshape/permute/contiguous a no-op.
+#include "common.h"
+
+#include <math.h>
+
+namespace dfhip {
+namespace hd {
+
+constexpr int kDeg = 6;
+constexpr int kIn = 3 + 3 * 2 * kDeg;  // 39
+constexpr int kHid = 64;
+constexpr int kOut = 3;
+constexpr int kW1 = kHid * kIn, kB1 = kHid, kW2 = kOut * kHid, kB2 = kOut;
+constexpr int kParams = kW1 + kB1 + kW2 + kB2;  // 2755
+constexpr int kBlock = 64;  // one wave per block: 16k rays -> 256 blocks fill the chip
+constexpr float kHalfPi = 3.141592653589793f / 2.0f;
+
+__device__ __forceinline__ float r16(float x) { return (float)(half_t)f32_rounded(x); }
+
+struct W {
+    float w1[kW1], b1[kB1], w2[kW2], b2[kB2];
+};
+
+__device__ __forceinline__ void load_w(W &w, const float *w1, const float *b1, const float *w2,
+                                       const float *b2) {
+    for (int i = threadIdx.x; i < kW1; i += blockDim.x) w.w1[i] = r16(w1[i]);
+    for (int i = threadIdx.x; i < kB1; i += blockDim.x) w.b1[i] = r16(b1[i]);
+    for (int i = threadIdx.x; i < kW2; i += blockDim.x) w.w2[i] = r16(w2[i]);
+    for (int i = threadIdx.x; i < kB2; i += blockDim.x) w.b2[i] = r16(b2[i]);
+}
+
+// freqencoder.cu:30-58 for D = 3, degree 6 (same expression as k_freq_fwd),
+// then the autocast cast to f16.
+__device__ __forceinline__ void features(const float *d, float x[kIn]) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) x[c] = r16(d[c]);
+#pragma unroll
+    for (int col = 0; col < 2 * kDeg; ++col)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float phase = (float)(col & 1) * kHalfPi;
+            x[3 + 3 * col + c] = r16(sinf(scalbnf(d[c], col >> 1) + phase));
+        }
+}
+
+// Hidden layer (f16 values) and the f16 output pre-activation.
+__device__ __forceinline__ void mlp(const W &w, const float x[kIn], float h[kHid],
+                                   float o[kOut]) {
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) {
+        float a = 0.0f;
+#pragma unroll
+        for (int i = 0; i < kIn; ++i) a = fmaf(x[i], w.w1[j * kIn + i], a);
+        a = a + w.b1[j];
+        h[j] = r16(a > 0.0f ? a : 0.0f);
+    }
+#pragma unroll
+    for (int k = 0; k < kOut; ++k) {
+        float a = 0.0f;
+#pragma unroll
+        for (int j = 0; j < kHid; ++j) a = fmaf(h[j], w.w2[k * kHid + j], a);
+        o[k] = r16(a + w.b2[k]);
+    }
+}
+
+__device__ __forceinline__ float sigmoid16(float o) { return r16(1.0f / (1.0f + expf(-o))); }
+
+template <bool NET>
+__global__ __launch_bounds__(kBlock) void k_head_fwd(
+    uint32_t N, const float *__restrict__ ws, const float *__restrict__ depth,
+    const float *__restrict__ image, const float *__restrict__ rays_d,
+    const float *__restrict__ nears, const float *__restrict__ fars, const float *w1,
+    const float *b1, const float *w2, const float *b2, const float *__restrict__ bg_color,
+    float *__restrict__ out_image, float *__restrict__ out_depth, uint8_t *__restrict__ mask) {
+    __shared__ W w;
+    if (NET) {
+        load_w(w, w1, b1, w2, b2);
+        __syncthreads();
+    }
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    float bg[3];
+    if (NET) {
+        float x[kIn], h[kHid], o[kOut];
+        features(rays_d + 3 * (size_t)n, x);
+        mlp(w, x, h, o);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) bg[k] = bg_color ? bg_color[3 * (size_t)n + k] : 1.0f;
+    }
+    const float t = 1.0f - ws[n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out_image[(size_t)k * N + n] = image[3 * (size_t)n + k] + t * bg[k];
+    const float nr = nears[n], fr = fars[n];
+    const float dd = depth[n] - nr;
+    out_depth[n] = (dd < 0.0f ? 0.0f : dd) / (fr - nr);
+    mask[n] = nr < fr ? 1 : 0;
+}
+
+// Backward.  grad_image [N, 3] = g; grad_ws = -sum_c g_c bg_c; with the
+// network also the background MLP's weight-gradient partials of this block.
+template <bool NET>
+__global__ __launch_bounds__(kBlock) void k_head_bwd(
+    uint32_t N, const float *__restrict__ g_image /* [3, N] */, const float *__restrict__ ws,
+    const float *__restrict__ rays_d, const float *w1, const float *b1, const float *w2,
+    const float *b2, const float *__restrict__ bg_color, float *__restrict__ grad_image,
+    float *__restrict__ grad_ws, float *__restrict__ grad_bg, float *__restrict__ partial) {
+    __shared__ W w;
+    __shared__ half_t s_dh[kBlock][kHid];   // relu-masked hidden grads (f16 values)
+    __shared__ half_t s_x[kBlock][kIn + 1];  // features
+    __shared__ half_t s_h[kBlock][kHid];    // hidden activations
+    __shared__ half_t s_do[kBlock][4];      // output pre-activation grads
+    if (NET) {
+        load_w(w, w1, b1, w2, b2);
+        __syncthreads();
+    }
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = n < N;
+    float g[3] = {0.0f, 0.0f, 0.0f};
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            g[k] = g_image[(size_t)k * N + n];
+            grad_image[3 * (size_t)n + k] = g[k];
+        }
+    }
+    float bg[3];
+    float x[kIn], h[kHid], o[kOut];
+    if (NET) {
+        if (live) {
+            features(rays_d + 3 * (size_t)n, x);
+            mlp(w, x, h, o);
+        } else {
+#pragma unroll
+            for (int i = 0; i < kIn; ++i) x[i] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < kHid; ++j) h[j] = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kOut; ++k) o[k] = 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) bg[k] = (live && bg_color) ? bg_color[3 * (size_t)n + k] : 1.0f;
+    }
+    if (live) {
+        // ((1 - ws) * bg) backward: d ws = -(sum_c g_c * bg_c)
+        float sw = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sw = sw + g[k] * bg[k];
+        grad_ws[n] = -sw;
+        if (!NET && grad_bg) {
+            const float t = 1.0f - ws[n];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) grad_bg[3 * (size_t)n + k] = g[k] * t;
+        }
+    }
+    if (!NET) return;
+    // sigmoid (f16) and the two f16 Linear layers, backward
+    const float t = live ? 1.0f - ws[n] : 0.0f;
+    float dout[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float dbg = r16(g[k] * t);
+        dout[k] = r16(dbg * (1.0f - bg[k]) * bg[k]);
+    }
+    const int r = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kHid; ++j) {
+        float a = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kOut; ++k) a = fmaf(dout[k], w.w2[k * kHid + j], a);
+        s_dh[r][j] = (half_t)(h[j] > 0.0f ? r16(a) : 0.0f);
+        s_h[r][j] = (half_t)h[j];
+    }
+#pragma unroll
+    for (int i = 0; i < kIn; ++i) s_x[r][i] = (half_t)x[i];
+#pragma unroll
+    for (int k = 0; k < kOut; ++k) s_do[r][k] = (half_t)dout[k];
+    __syncthreads();
+    // per-block weight-gradient partials: f32 sums of f16 products over the rays
+    float *out = partial + (size_t)blockIdx.x * kParams;
+    for (int p = threadIdx.x; p < kParams; p += blockDim.x) {
+        float s = 0.0f;
+        if (p < kW1) {
+            const int j = p / kIn, i = p - j * kIn;
+            for (int q = 0; q < kBlock; ++q) s = fmaf((float)s_dh[q][j], (float)s_x[q][i], s);
+        } else if (p < kW1 + kB1) {
+            const int j = p - kW1;
+            for (int q = 0; q < kBlock; ++q) s += (float)s_dh[q][j];
+        } else if (p < kW1 + kB1 + kW2) {
+            const int k = (p - kW1 - kB1) / kHid, j = (p - kW1 - kB1) - k * kHid;
+            for (int q = 0; q < kBlock; ++q) s = fmaf((float)s_do[q][k], (float)s_h[q][j], s);
+        } else {
+            const int k = p - kW1 - kB1 - kW2;
+            for (int q = 0; q < kBlock; ++q) s += (float)s_do[q][k];
+        }
+        out[p] = s;
+    }
+}
+
+// Fixed-order sum of the per-block partials: block = 64 outputs, its four
+// waves take every fourth partial, then a fixed-order sum of the four.
+__global__ __launch_bounds__(256) void k_head_wsum(const float *__restrict__ partial,
+                                                   uint32_t blocks, float *gw1, float *gb1,
+                                                   float *gw2, float *gb2) {
+    __shared__ float red[4][64];
+    const int o = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int p = blockIdx.x * 64 + o;
+    float s = 0.0f;
+    if (p < kParams)
+        for (uint32_t b = grp; b < blocks; b += 4) s += partial[(size_t)b * kParams + p];
+    red[grp][o] = s;
+    __syncthreads();
+    if (grp != 0 || p >= kParams) return;
+    s = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+    if (p < kW1) gw1[p] = s;
+    else if (p < kW1 + kB1) gb1[p - kW1] = s;
+    else if (p < kW1 + kB1 + kW2) gw2[p - kW1 - kB1] = s;
+    else gb2[p - kW1 - kB1 - kW2] = s;
+}
+
+// ---------------------------------------------------------------- entropy
+constexpr float kLo = 1e-5f, kHi = 1.0f - 1e-5f;
+
+__global__ __launch_bounds__(1024) void k_entropy_fwd(uint32_t N, const float *__restrict__ ws,
+                                                      float lambda, float *__restrict__ loss) {
+    __shared__ double part[16];
+    double s = 0.0;
+    for (uint32_t n = threadIdx.x; n < N; n += blockDim.x) {
+        float a = ws[n];
+        a = a < kLo ? kLo : (a > kHi ? kHi : a);
+        const float e = -a * log2f(a) - (1.0f - a) * log2f(1.0f - a);
+        s += (double)e;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += part[i];
+        loss[0] = lambda * (float)(t / (double)N);
+    }
+}
+
+// d loss / d ws = g * lambda / N * log2((1 - a) / a), zero where the clamp is
+// active (torch.clamp's backward passes the gradient for lo <= ws <= hi).
+__global__ __launch_bounds__(256) void k_entropy_bwd(uint32_t N, const float *__restrict__ ws,
+                                                     const float *__restrict__ g, float lambda,
+                                                     float *__restrict__ grad_ws) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const float a = ws[n];
+    const float scale = g[0] * lambda / (float)N;
+    grad_ws[n] = (a >= kLo && a <= kHi) ? scale * (log2f(1.0f - a) - log2f(a)) : 0.0f;
+}
+
+}  // namespace hd
+}  // namespace dfhip
+
+using namespace dfhip;
+
+extern "C" uint32_t dfhip_ray_head_partial_floats(uint32_t N) {
+    return ceil_div(N, (uint32_t)hd::kBlock) * (uint32_t)hd::kParams;
+}
+
+extern "C" int dfhip_ray_head_forward(uint32_t N, const float *ws, const float *depth,
+                                      const float *image, const float *rays_d, const float *nears,
+                                      const float *fars, const float *w1, const float *b1,
+                                      const float *w2, const float *b2, const float *bg_color,
+                                      float *out_image, float *out_depth, uint8_t *mask,
+                                      dfhip_stream_t stream) {
+    const char *name = "ray_head_forward";
+    if (N == 0) return DFHIP_OK;
+    if (!ws || !depth || !image || !nears || !fars || !out_image || !out_depth || !mask) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    const bool net = w1 != nullptr;
+    if (net && (!b1 || !w2 || !b2 || !rays_d)) {
+        set_error("%s: the background network needs w1, b1, w2, b2 and rays_d", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const uint32_t blocks = ceil_div(N, (uint32_t)hd::kBlock);
+    if (net)
+        hd::k_head_fwd<true><<<blocks, hd::kBlock, 0, s>>>(N, ws, depth, image, rays_d, nears,
+                                                          fars, w1, b1, w2, b2, nullptr,
+                                                          out_image, out_depth, mask);
+    else
+        hd::k_head_fwd<false><<<blocks, hd::kBlock, 0, s>>>(N, ws, depth, image, rays_d, nears,
+                                                           fars, nullptr, nullptr, nullptr,
+                                                           nullptr, bg_color, out_image,
+                                                           out_depth, mask);
+    return check_launch(name);
+}
+
+extern "C" int dfhip_ray_head_backward(uint32_t N, const float *g_image, const float *ws,
+                                       const float *rays_d, const float *w1, const float *b1,
+                                       const float *w2, const float *b2, const float *bg_color,
+                                       float *grad_image, float *grad_ws, float *grad_bg,
+                                       float *partial, float *gw1, float *gb1, float *gw2,
+                                       float *gb2, dfhip_stream_t stream) {
+    const char *name = "ray_head_backward";
+    if (N == 0) return DFHIP_OK;
+    if (!g_image || !ws || !grad_image || !grad_ws) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    const bool net = w1 != nullptr;
+    if (net && (!b1 || !w2 || !b2 || !rays_d || !partial || !gw1 || !gb1 || !gw2 || !gb2)) {
+        set_error("%s: the background network needs its weights, rays_d, partial and grads",
+                  name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const uint32_t blocks = ceil_div(N, (uint32_t)hd::kBlock);
+    if (net) {
+        hd::k_head_bwd<true><<<blocks, hd::kBlock, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
+                                                          nullptr, grad_image, grad_ws, nullptr,
+                                                          partial);
+        hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u), 256, 0, s>>>(
+            partial, blocks, gw1, gb1, gw2, gb2);
+    } else {
+        hd::k_head_bwd<false><<<blocks, hd::kBlock, 0, s>>>(N, g_image, ws, nullptr, nullptr,
+                                                           nullptr, nullptr, nullptr, bg_color,
+                                                           grad_image, grad_ws, grad_bg,
+                                                           nullptr);
+    }
+    return check_launch(name);
+}
+
+extern "C" int dfhip_entropy_forward(uint32_t N, const float *ws, float lambda, float *loss,
+                                     dfhip_stream_t stream) {
+    if (!ws || !loss) {
+        set_error("entropy_forward: null pointer");
+        return DFHIP_EINVAL;
+    }
+    hd::k_entropy_fwd<<<1, 1024, 0, as_stream(stream)>>>(N, ws, lambda, loss);
+    return check_launch("entropy_forward");
+}
+
+extern "C" int dfhip_entropy_backward(uint32_t N, const float *ws, const float *grad_loss,
+                                      float lambda, float *grad_ws, dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    if (!ws || !grad_loss || !grad_ws) {
+        set_error("entropy_backward: null pointer");
+        return DFHIP_EINVAL;
+    }
+    hd::k_entropy_bwd<<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(N, ws, grad_loss, lambda,
+                                                                       grad_ws);
+    return check_launch("entropy_backward");
+}

@@ -76,7 +76,7 @@ def parse_opt(argv=None):
 def main(argv=None):
     from nerf.network_grid import NeRFNetwork
     from nerf.provider import NeRFDataset
-    from nerf.sd import StableDiffusion, SyntheticSDS
+    from nerf.sd import InjectedSDS, StableDiffusion, SyntheticSDS
     from nerf.utils import Trainer, make_adam, seed_everything
 
     opt = parse_opt(argv)
@@ -96,7 +96,12 @@ def main(argv=None):
                                size=100).dataloader()
     optimizer = lambda m: make_adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)
     scheduler = lambda o: torch.optim.lr_scheduler.LambdaLR(o, lambda it: 0.1 ** min(it / opt.iters, 1))
-    guidance = (SyntheticSDS(device) if opt.guidance == "synthetic" else StableDiffusion(device))
+    if opt.guidance == "synthetic":
+        guidance = InjectedSDS(device)
+    elif opt.guidance == "mock":
+        guidance = SyntheticSDS(device)
+    else:
+        guidance = StableDiffusion(device)
     trainer = Trainer("df", opt, model, guidance, device=device, workspace=opt.workspace,
                       optimizer=optimizer, ema_decay=None, fp16=opt.fp16, lr_scheduler=scheduler,
                       use_checkpoint=opt.ckpt, eval_interval=opt.eval_interval,

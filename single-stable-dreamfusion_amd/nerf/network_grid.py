@@ -122,6 +122,15 @@ class NeRFNetwork(NeRFRenderer):
         sigma, albedo = self.common_forward(x)
         return {"sigma": sigma, "albedo": albedo}
 
+    def native_background_layers(self):
+        from freqencoder import FreqEncoder
+        if self.bg_radius <= 0 or not isinstance(self.encoder_bg, FreqEncoder):
+            return None
+        if self.encoder_bg.input_dim != 3 or self.encoder_bg.degree != 6:
+            return None
+        layers = list(self.bg_net.net)
+        return layers if len(layers) == 2 else None
+
     def background(self, d):
         return torch.sigmoid(self.bg_net(self.encoder_bg(d)))
 

@@ -76,6 +76,8 @@ class NeRFRenderer(nn.Module):
         self.device_count_march = False
         # sync-free occupancy refresh on the GPU (False: the reference's torch ops)
         self.native_grid_update = True
+        # native background mix / depth / mask (nerf/head.py; False: torch ops)
+        self.native_head = True
 
     # mean_density / mean_count: the sync-free grid refresh leaves them on the
     # device; they are read to the host only when somebody asks (checkpoint,
@@ -264,13 +266,38 @@ class NeRFRenderer(nn.Module):
                                                          ambient_ratio, shading, perturb,
                                                          dt_gamma, max_steps, T_thresh)
 
-        image = image + (1 - weights_sum).unsqueeze(-1) * self._bg(rays_d, bg_color)
-        results["image"] = image.view(*prefix, 3)
-        # depth relative to the ray's near plane, normalised (renderer.py:547)
-        results["depth"] = (torch.clamp(depth - nears, min=0) / (fars - nears)).view(*prefix)
-        results["weights_sum"] = weights_sum.reshape(*prefix)
-        results["mask"] = (nears < fars).reshape(*prefix)
+        results.update(self._compose(rays_d, nears, fars, weights_sum, depth, image, bg_color,
+                                     prefix))
         return results
+
+    def _compose(self, rays_d, nears, fars, weights_sum, depth, image, bg_color, prefix):
+        """Background mix, depth normalisation, mask (renderer.py:536-551); on the
+        GPU as the native ray head (nerf/head.py) when the shapes allow."""
+        from . import head as _head
+        net = self.bg_radius > 0
+        layers = self.native_background_layers() if net else None
+        bgc = None if net else bg_color
+        ok = (self.native_head and len(prefix) == 2 and prefix[0] == 1
+              and (layers is not None if net else
+                   (bgc is None or (torch.is_tensor(bgc) and bgc.shape == image.shape)))
+              and _head.head_eligible(weights_sum, layers))
+        if ok:
+            out_image, out_depth, mask = _head.ray_head(weights_sum, depth, image, rays_d, nears,
+                                                        fars, bgc, layers)
+            # pred_rgb is stored channel-major: [1, N, 3] is a view of [3, N]
+            return {"image": out_image.t().unsqueeze(0), "depth": out_depth.view(*prefix),
+                    "weights_sum": weights_sum.reshape(*prefix), "mask": mask.view(*prefix)}
+        image = image + (1 - weights_sum).unsqueeze(-1) * self._bg(rays_d, bg_color)
+        # depth relative to the ray's near plane, normalised (renderer.py:547)
+        return {"image": image.view(*prefix, 3),
+                "depth": (torch.clamp(depth - nears, min=0) / (fars - nears)).view(*prefix),
+                "weights_sum": weights_sum.reshape(*prefix),
+                "mask": (nears < fars).reshape(*prefix)}
+
+    def native_background_layers(self):
+        """The background MLP's nn.Linear layers when the native ray head can
+        evaluate it (frequency-encoded 39 -> 64 -> 3), else None (subclass hook)."""
+        return None
 
     def _infer_loop(self, rays_o, rays_d, nears, fars, light_d, ambient_ratio, shading, perturb,
                     dt_gamma, max_steps, T_thresh):

@@ -6,7 +6,9 @@ train_step -> 0 after an injected latent backward, sd.py:54-118) and adds
 backward with the regulariser backward.  The real model needs `diffusers` and
 LOCAL weights (nothing is ever fetched by name).
 
-`SyntheticSDS` is the offline stand-in used when no weights exist: the same
+`InjectedSDS` is the benchmark's offline guidance (a seeded w(t)-weighted N(0,1)
+gradient injected at pred_rgb).  `SyntheticSDS` is the
+fuller offline stand-in: the same
 SDS arithmetic (timestep draw, scaled_linear alphas_cumprod, add_noise,
 classifier-free guidance with scale 100, w(t) = 1 - alphas_cumprod[t],
 gradient injection at the latents) around fixed random 1x1-conv "VAE" /
@@ -38,6 +40,16 @@ def add_noise(alphas_cumprod, latents, noise, t):
 def cfg_combine(noise_pred, guidance_scale):
     uncond, text = noise_pred.chunk(2)
     return uncond + guidance_scale * (text - uncond)
+
+
+def seeded_text_embeds(prompt, negative_prompt, dim, device):
+    """Offline stand-in for CLIP text embeddings: [negatives..., prompts...]
+    each a [77, dim] N(0, 1) tensor seeded by the text's CRC32."""
+    out = []
+    for text in list(negative_prompt) + list(prompt):
+        gen = torch.Generator().manual_seed(zlib.crc32(text.encode("utf-8")))
+        out.append(torch.randn(77, dim, generator=gen))
+    return torch.stack(out).to(device)
 
 
 class _SDSBase(nn.Module):
@@ -94,11 +106,7 @@ class SyntheticSDS(_SDSBase):
         self.to(device)
 
     def get_text_embeds(self, prompt, negative_prompt):
-        out = []
-        for text in list(negative_prompt) + list(prompt):
-            gen = torch.Generator().manual_seed(zlib.crc32(text.encode("utf-8")))
-            out.append(torch.randn(77, self.text_dim, generator=gen))
-        return torch.stack(out).to(self.device)
+        return seeded_text_embeds(prompt, negative_prompt, self.text_dim, self.device)
 
     def encode_imgs(self, imgs):
         x = F.avg_pool2d(2 * imgs - 1, 8)
@@ -108,6 +116,29 @@ class SyntheticSDS(_SDSBase):
         eps = F.conv2d(latent_model_input, self.eps_w.to(latent_model_input.dtype))
         bias = text_embeddings.mean(1).to(eps.dtype) @ self.txt_w.t().to(eps.dtype)  # [2, 4]
         return eps + bias[:, :, None, None]
+
+
+class InjectedSDS(_SDSBase):
+    """The benchmark's guidance (SURVEY.md §8(d) "synthetic SDS"): SD's VAE /
+    UNet are absent offline, so the SDS gradient w(t) (eps_hat - eps) is
+    replaced by a seeded N(0, 1) gradient of pred_rgb's shape, weighted by
+    w(t) = 1 - alphas_cumprod[t] of a drawn timestep, and injected at pred_rgb
+    (the backward topology of the render graph minus VAE / UNet).  The full
+    SDS arithmetic around stand-in networks is `SyntheticSDS`."""
+
+    def __init__(self, device, text_dim=768):
+        super().__init__(device)
+        self.text_dim = text_dim
+        self.to(device)
+
+    def get_text_embeds(self, prompt, negative_prompt):
+        return seeded_text_embeds(prompt, negative_prompt, self.text_dim, self.device)
+
+    def sds_grad(self, text_embeddings, pred_rgb, guidance_scale=100):
+        t = torch.randint(self.min_step, self.max_step + 1, [1], dtype=torch.long,
+                          device=pred_rgb.device)
+        w = 1 - self.alphas[t]
+        return pred_rgb, w * torch.randn_like(pred_rgb, dtype=torch.float32)
 
 
 class StableDiffusion(_SDSBase):

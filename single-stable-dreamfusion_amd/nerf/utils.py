@@ -204,6 +204,8 @@ class Trainer(object):
         self._graphs = {}
         # GradScaler + Adam as one native call (nerf/optim.py) when eligible
         self.native_optimizer = os.environ.get("DFHIP_NATIVE_ADAM", "1") != "0"
+        # entropy regulariser as one native kernel each way (nerf/head.py)
+        self.native_losses = True
         self._native_opt = None
         self._capture_stream = None
         self.device = device if device is not None else torch.device(
@@ -333,9 +335,13 @@ class Trainer(object):
         if self.opt.lambda_opacity > 0:
             loss = loss + self.opt.lambda_opacity * (pred_ws ** 2).mean()
         if self.opt.lambda_entropy > 0:
-            a = pred_ws.clamp(1e-5, 1 - 1e-5)
-            ent = (-a * torch.log2(a) - (1 - a) * torch.log2(1 - a)).mean()
-            loss = loss + self.opt.lambda_entropy * ent
+            if pred_ws.is_cuda and pred_ws.dtype == torch.float32 and self.native_losses:
+                from .head import ray_entropy  # native fwd / bwd (csrc/head.hip)
+                loss = loss + ray_entropy(pred_ws, self.opt.lambda_entropy)
+            else:
+                a = pred_ws.clamp(1e-5, 1 - 1e-5)
+                ent = (-a * torch.log2(a) - (1 - a) * torch.log2(1 - a)).mean()
+                loss = loss + self.opt.lambda_entropy * ent
         if self.opt.lambda_orient > 0 and "loss_orient" in outputs:
             loss = loss + self.opt.lambda_orient * outputs["loss_orient"]
         if self.opt.lambda_smooth > 0 and "loss_smooth" in outputs:

@@ -158,3 +158,42 @@ def test_native_grid_update_matches_torch(gpu):
     diff = int((b0 != b1).sum())
     # only cells within rounding of the threshold may flip
     assert diff == 0 or diff <= 2
+
+
+@pytest.mark.parametrize("bg_radius", [1.4, 0.0])
+def test_native_ray_head_matches_torch(gpu, bg_radius):
+    """Native background mix / depth / mask / entropy (csrc/head.hip) against
+    the reference's torch expressions on the same render: outputs and the
+    gradients of the background MLP, the colour and the weights."""
+    import random
+    outs = {}
+    for native in (False, True):
+        trainer, data = _trainer(gpu, True, seed=5)
+        m = trainer.model
+        m.native_head = native
+        trainer.native_losses = native
+        if bg_radius == 0:
+            m.bg_radius = 0.0
+        torch.manual_seed(7)
+        random.seed(7)
+        batch = data.collate([0])
+        m.update_extra_state()
+        trainer.optimizer.zero_grad()
+        torch.manual_seed(8)
+        with torch.autocast("cuda", dtype=torch.float16):
+            pred_rgb, pred_ws, loss = trainer.train_step(batch, "albedo", 1.0)
+        g = torch.randn(pred_rgb.shape, device=gpu, generator=torch.Generator(gpu).manual_seed(1))
+        trainer._pending_sds = None
+        torch.autograd.backward([pred_rgb, loss], [g, None])
+        grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()
+                 if p.grad is not None}
+        outs[native] = (pred_rgb.detach().clone(), pred_ws.detach().clone(),
+                        loss.detach().clone(), grads)
+    (r0, w0, l0, g0), (r1, w1, l1, g1) = outs[False], outs[True]
+    assert torch.equal(w0, w1)
+    torch.testing.assert_close(r1, r0, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-9)
+    assert g0.keys() == g1.keys()
+    for n in g0:
+        scale = g0[n].abs().max().clamp(min=1e-12)
+        torch.testing.assert_close(g1[n], g0[n], rtol=2e-2, atol=2e-2 * scale, msg=n)
