@@ -196,6 +196,7 @@ def main():
     for _ in range(args.steps):
         step()
         counts.append(trainer.model.step_counter[(trainer.model.local_step - 1) % 16, 0].clone())
+    host_issue = time.perf_counter() - t0  # host done issuing (no sync inside the loop)
     barrier()
     elapsed = time.perf_counter() - t0
     _dfhip.set_kernel_timer(None)
@@ -227,6 +228,7 @@ def main():
                    "launch": "eager" if not trainer.graph_step else "hip-graph replay",
                    "mean_samples_per_step": round(samples, 1)},
         "steps_per_sec": round(steps_per_sec, 3),
+        "host_issue_ms_per_step": round(host_issue / args.steps * 1e3, 3),
     }
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])

@@ -117,9 +117,14 @@ def grid_backward_binned_scratch(cap, offsets_host, L, C):
     return int(e.value), int(c.value), int(p.value)
 
 
-def grid_encode_backward_binned(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddings,
-                                B, m_dev, D, C, L, S, H, gridtype, align_corners, entries, counts,
-                                partial, accumulate=False):
+def grid_encode_backward_binned(*args, **kw):
+    """Validate and launch once (see binned_launcher)."""
+    binned_launcher(*args, **kw)()
+
+
+def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddings,
+                    B, m_dev, D, C, L, S, H, gridtype, align_corners, entries, counts,
+                    partial, accumulate=False):
     """grad_lbc [L, B, C] (B = capacity), inputs [B, D] raw positions in
     [-bound, bound] (bound > 0) or [0, 1] (bound = 0); rows [0, m_dev[0]) walked
     when m_dev is given.  grad_embeddings [rows, C] f32 is overwritten (or
@@ -137,8 +142,14 @@ def grid_encode_backward_binned(grad_lbc, inputs, bound, offsets, offsets_host, 
     if m_dev is not None:
         checked(m_dev, "m_dev", "int")
     off = np.ascontiguousarray(offsets_host, dtype=np.int32)
-    call("dfhip_grid_encode_backward_binned", _d.dtype_code(grad_lbc, "grad"), ptr(grad_lbc),
-         ptr(inputs), float(bound), ptr(offsets), off.ctypes.data, ptr(grad_embeddings), int(B),
-         ptr(m_dev), int(D), int(C), int(L), float(S), int(H), int(gridtype),
-         int(bool(align_corners)), ptr(entries), ptr(counts), ptr(partial),
-         int(bool(accumulate)), stream())
+    args = (_d.dtype_code(grad_lbc, "grad"), ptr(grad_lbc), ptr(inputs), float(bound),
+            ptr(offsets), off.ctypes.data, ptr(grad_embeddings), int(B), ptr(m_dev), int(D),
+            int(C), int(L), float(S), int(H), int(gridtype), int(bool(align_corners)),
+            ptr(entries), ptr(counts), ptr(partial), int(bool(accumulate)))
+    keep = (grad_lbc, inputs, offsets, off, grad_embeddings, m_dev, entries, counts, partial)
+
+    def launch(_keep=keep):
+        """Launch on the current stream with the validated, pre-marshalled
+        arguments (the graph-replayed step calls this every step)."""
+        call("dfhip_grid_encode_backward_binned", *args, stream())
+    return launch

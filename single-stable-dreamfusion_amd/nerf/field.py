@@ -127,6 +127,12 @@ class _GridField(Function):
                                           mlp_partial, grads, offsets, rows, S, H, gridtype,
                                           align, None, None, gparts, m_dev)
         if grad_emb is not None:
+            launch = None
+            if binned:
+                launch = _gridencoder.binned_launcher(d_enc, x, bound, offsets, offsets_host,
+                                                      grad_emb, cap, m_dev, 3, C, L, S, H,
+                                                      gridtype, align, *scratch)
+
             def embedding_backward(grad_emb=grad_emb):
                 # algorithmic bytes: per live sample its position and feature
                 # grads, plus the table gradient once
@@ -135,10 +141,8 @@ class _GridField(Function):
                 if live is None:
                     base += cap * per
                 with _dfhip.timed("grid_encode_backward", base, live, per):
-                    if binned:
-                        _gridencoder.grid_encode_backward_binned(
-                            d_enc, x, bound, offsets, offsets_host, grad_emb, cap, m_dev, 3, C,
-                            L, S, H, gridtype, align, *scratch)
+                    if launch is not None:
+                        launch()
                     else:
                         _gridencoder.grid_encode_backward_sliced_dyn(
                             d_enc, x, bound, offsets, grad_emb, rows, cap, m_dev, 3, C, L, S, H,

@@ -39,6 +39,7 @@ class GraphedTrainStep:
         self.rays_o = data["rays_o"].detach().clone()
         self.rays_d = data["rays_d"].detach().clone()
         self.text_z = text_z.detach().clone()
+        self._text_src = text_z.data_ptr()  # prompt tensor currently in self.text_z
         self.stream = stream
         self.graph = torch.cuda.CUDAGraph()
         self.deferred = []
@@ -102,10 +103,18 @@ class GraphedTrainStep:
             self.grads.append((p, g))
 
     def load(self, data, text_z):
-        """Copy this step's camera rays and prompt embedding into the graph's inputs."""
-        self.rays_o.copy_(data["rays_o"], non_blocking=True)
-        self.rays_d.copy_(data["rays_d"], non_blocking=True)
-        self.text_z.copy_(text_z, non_blocking=True)
+        """This step's camera rays (made straight into the graph's input buffers
+        from a host pose when the batch has one) and prompt embedding."""
+        if "pose" in data and "rays_o" not in data:
+            from .utils import get_rays_host_pose
+            get_rays_host_pose(data["pose"], data["intrinsics"], self.H, self.W, None,
+                               out=(self.rays_o, self.rays_d))
+        else:
+            self.rays_o.copy_(data["rays_o"], non_blocking=True)
+            self.rays_d.copy_(data["rays_d"], non_blocking=True)
+        if text_z.data_ptr() != self._text_src:
+            self.text_z.copy_(text_z, non_blocking=True)
+            self._text_src = text_z.data_ptr()
 
     def replay(self):
         """Run the captured part, then the deferred embedding backward; leaves

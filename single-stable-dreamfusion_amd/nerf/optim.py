@@ -63,31 +63,47 @@ class NativeAdamAmp:
         sc = self.scaler
         if sc._scale is None:
             return  # scale() never called: nothing was back-propagated
-        dev = sc._scale.device
         if self.found_inf is None:
-            self.found_inf = torch.zeros(1, dtype=torch.float32, device=dev)
+            self.found_inf = torch.zeros(1, dtype=torch.float32, device=sc._scale.device)
+        # fast path: same parameters / gradient buffers as last step (the graph-
+        # replayed step keeps its gradients in place) -> only the lrs are new
+        # (a reloaded optimizer state is a new dict: its identity is part of the key)
+        key = (id(self.optimizer.state), len(self.optimizer.state),
+               *(p.grad.data_ptr() if p.grad is not None else 0
+                 for g in self.optimizer.param_groups for p in g["params"]))
+        if key != self._ptr_key:
+            self._rebuild(key)
+        if self._arrays is None:
+            return
+        n, P, G, M, V, S, N, B1, B2, E, WD, groups = self._arrays
+        lr = (ctypes.c_float * n)(*[float(self.optimizer.param_groups[i]["lr"]) for i in groups])
+        rc = self._fn(n, P, G, M, V, S, N, lr, B1, B2, E, WD, sc._scale.data_ptr(),
+                      sc._growth_tracker.data_ptr(), self.found_inf.data_ptr(),
+                      float(sc._growth_factor), float(sc._backoff_factor),
+                      int(sc._growth_interval), _dfhip.stream())
+        if rc != 0:
+            raise RuntimeError(f"dfhip_adam_amp_step failed ({rc}): "
+                               f"{_dfhip.load().dfhip_last_error().decode()}")
+
+    def _rebuild(self, key):
         ts = []
-        for g in self.optimizer.param_groups:
+        for gi, g in enumerate(self.optimizer.param_groups):
             b1, b2 = g["betas"]
             for p in g["params"]:
                 if p.grad is None:
                     continue
                 st = self._state(p)
-                ts.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], st["step"], g["lr"], b1,
-                           b2, g["eps"], g["weight_decay"]))
+                ts.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], st["step"], gi, b1, b2,
+                           g["eps"], g["weight_decay"]))
+        self._ptr_key = key
         if not ts:
+            self._arrays = None
             return
-        key = tuple(t[i].data_ptr() for t in ts for i in range(5))
-        if key != self._ptr_key:
-            n = len(ts)
-            vp = ctypes.c_void_p * n
-            self._arrays = (n, *(vp(*[t[i].data_ptr() for t in ts]) for i in range(5)),
-                            (ctypes.c_uint64 * n)(*[t[0].numel() for t in ts]))
-            self._ptr_key = key
-        n, P, G, M, V, S, N = self._arrays
+        n = len(ts)
+        vp = ctypes.c_void_p * n
         f = ctypes.c_float * n
-        hyper = [f(*[float(t[i]) for t in ts]) for i in range(5, 10)]
-        _dfhip.call("dfhip_adam_amp_step", n, P, G, M, V, S, N, *hyper, sc._scale.data_ptr(),
-                    sc._growth_tracker.data_ptr(), self.found_inf.data_ptr(),
-                    float(sc._growth_factor), float(sc._backoff_factor),
-                    int(sc._growth_interval), _dfhip.stream())
+        ptrs = [vp(*[t[i].data_ptr() for t in ts]) for i in range(5)]
+        hyper = [f(*[float(t[i]) for t in ts]) for i in range(6, 10)]
+        self._arrays = (n, *ptrs, (ctypes.c_uint64 * n)(*[t[0].numel() for t in ts]), *hyper,
+                        [t[5] for t in ts])
+        self._fn = _dfhip.load().dfhip_adam_amp_step

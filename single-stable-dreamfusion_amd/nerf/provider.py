@@ -4,6 +4,7 @@
 reference's signatures, RNG call order (torch then Python `random`) and
 outputs: one full image of rays per batch (provider.py:202-236).
 """
+import math
 import random
 
 import numpy as np
@@ -76,61 +77,66 @@ def rand_poses(size, device, radius_range=[1, 1.5], theta_range=[0, 100], phi_ra
     return poses, dirs
 
 
-def _normalize_np(v):
-    n = np.sqrt(np.maximum(np.sum(v * v, -1, keepdims=True), np.float32(1e-20)))
-    return (v / n).astype(np.float32)
+def _unit(v):
+    n = math.sqrt(max(v[0] * v[0] + v[1] * v[1] + v[2] * v[2], 1e-20))
+    return (v[0] / n, v[1] / n, v[2] / n)
+
+
+def _cross(a, b):
+    return (a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0])
 
 
 def rand_poses_host(size, radius_range=(1, 1.5), theta_range=(0, 100), phi_range=(0, 360),
                     return_dirs=False, angle_overhead=30, angle_front=60, jitter=False,
                     uniform_sphere_rate=0.5):
-    """rand_poses on the host in numpy f32 (same distributions and formulas, a
-    few microseconds instead of ~30 torch CPU ops): poses [size, 4, 4] f32
+    """rand_poses on the host in scalar Python (same distributions and formulas
+    as provider.py:72-141, draws from Python's `random`; a few microseconds per
+    camera instead of ~30 device ops and their syncs): poses [size, 4, 4] f32
     numpy, direction classes as a CPU long tensor (or None)."""
-    theta_range = np.deg2rad(theta_range)
-    phi_range = np.deg2rad(phi_range)
-    angle_overhead = np.deg2rad(angle_overhead)
-    angle_front = np.deg2rad(angle_front)
-    rnd = np.random.random_sample
-    f32 = np.float32
-    radius = (rnd(size).astype(f32) * f32(radius_range[1] - radius_range[0])
-              + f32(radius_range[0]))
-    if random.random() < uniform_sphere_rate:
-        unit = _normalize_np(np.stack([(rnd(size).astype(f32) - f32(0.5)) * f32(2.0),
-                                       rnd(size).astype(f32),
-                                       (rnd(size).astype(f32) - f32(0.5)) * f32(2.0)], -1))
-        thetas = np.arccos(unit[:, 1])
-        phis = np.arctan2(unit[:, 0], unit[:, 2])
-        phis = np.where(phis < 0, phis + f32(2 * np.pi), phis).astype(f32)
-        centers = unit * radius[:, None]
-    else:
-        thetas = (rnd(size).astype(f32) * f32(theta_range[1] - theta_range[0])
-                  + f32(theta_range[0]))
-        phis = rnd(size).astype(f32) * f32(phi_range[1] - phi_range[0]) + f32(phi_range[0])
-        centers = np.stack([radius * np.sin(thetas) * np.sin(phis), radius * np.cos(thetas),
-                            radius * np.sin(thetas) * np.cos(phis)], -1).astype(f32)
-    targets = np.zeros_like(centers)
-    if jitter:
-        centers = centers + (rnd(centers.shape).astype(f32) * f32(0.2) - f32(0.1))
-        targets = targets + np.random.standard_normal(centers.shape).astype(f32) * f32(0.2)
-    forward = _normalize_np(targets - centers)
-    up = np.tile(np.array([[0, -1, 0]], f32), (size, 1))
-    right = _normalize_np(np.cross(forward, up))
-    noise = np.random.standard_normal(up.shape).astype(f32) * f32(0.02) if jitter else f32(0)
-    up = _normalize_np(np.cross(right, forward) + noise)
-    poses = np.tile(np.eye(4, dtype=f32)[None], (size, 1, 1))
-    poses[:, :3, :3] = np.stack((right, up, forward), -1)
-    poses[:, :3, 3] = centers
-    dirs = None
-    if return_dirs:  # get_view_direction in numpy (same class order)
-        res = np.zeros(size, dtype=np.int64)
-        res[phis < angle_front] = 0
-        res[(phis >= angle_front) & (phis < np.pi)] = 1
-        res[(phis >= np.pi) & (phis < (np.pi + angle_front))] = 2
-        res[phis >= (np.pi + angle_front)] = 3
-        res[thetas <= angle_overhead] = 4
-        res[thetas >= (np.pi - angle_overhead)] = 5
-        dirs = torch.from_numpy(res)
+    t0, t1 = math.radians(theta_range[0]), math.radians(theta_range[1])
+    p0, p1 = math.radians(phi_range[0]), math.radians(phi_range[1])
+    overhead, front = math.radians(angle_overhead), math.radians(angle_front)
+    rnd = random.random
+    poses = np.zeros((size, 4, 4), np.float32)
+    classes = []
+    for b in range(size):
+        radius = rnd() * (radius_range[1] - radius_range[0]) + radius_range[0]
+        if rnd() < uniform_sphere_rate:
+            u = _unit(((rnd() - 0.5) * 2.0, rnd(), (rnd() - 0.5) * 2.0))
+            theta = math.acos(max(-1.0, min(1.0, u[1])))
+            phi = math.atan2(u[0], u[2])
+            if phi < 0:
+                phi += 2 * math.pi
+            center = (u[0] * radius, u[1] * radius, u[2] * radius)
+        else:
+            theta = rnd() * (t1 - t0) + t0
+            phi = rnd() * (p1 - p0) + p0
+            st = math.sin(theta)
+            center = (radius * st * math.sin(phi), radius * math.cos(theta),
+                      radius * st * math.cos(phi))
+        target = (0.0, 0.0, 0.0)
+        if jitter:
+            center = tuple(c + (rnd() * 0.2 - 0.1) for c in center)
+            target = tuple(random.gauss(0.0, 1.0) * 0.2 for _ in range(3))
+        forward = _unit((target[0] - center[0], target[1] - center[1], target[2] - center[2]))
+        right = _unit(_cross(forward, (0.0, -1.0, 0.0)))
+        up = _cross(right, forward)
+        if jitter:
+            up = tuple(v + random.gauss(0.0, 1.0) * 0.02 for v in up)
+        up = _unit(up)
+        poses[b] = ((right[0], up[0], forward[0], center[0]),
+                    (right[1], up[1], forward[1], center[1]),
+                    (right[2], up[2], forward[2], center[2]),
+                    (0.0, 0.0, 0.0, 1.0))
+        if return_dirs:  # get_view_direction (same class order)
+            cls = 0 if phi < front else (1 if phi < math.pi else (2 if phi < math.pi + front
+                                                                    else 3))
+            if theta <= overhead:
+                cls = 4
+            if theta >= math.pi - overhead:
+                cls = 5
+            classes.append(cls)
+    dirs = torch.tensor(classes, dtype=torch.long) if return_dirs else None
     return poses, dirs
 
 
@@ -147,6 +153,21 @@ def circle_poses(device, radius=1.25, theta=60, phi=0, return_dirs=False, angle_
     dirs = (get_view_direction(thetas, phis, np.deg2rad(angle_overhead), np.deg2rad(angle_front))
             if return_dirs else None)
     return poses, dirs
+
+
+class RayBatch(dict):
+    """A collated camera batch whose full-image rays ("rays_o", "rays_d") are
+    made on first access from the host pose ("pose", "intrinsics"): the
+    graph-replayed train step writes them straight into its own input
+    buffers instead (nerf/graph.py), eager callers see the usual dict."""
+
+    def __missing__(self, key):
+        if key in ("rays_o", "rays_d"):
+            rays = get_rays_host_pose(self["pose"], self["intrinsics"], self["H"], self["W"],
+                                      self["device"])
+            self["rays_o"], self["rays_d"] = rays["rays_o"], rays["rays_d"]
+            return self[key]
+        raise KeyError(key)
 
 
 class NeRFDataset:
@@ -199,10 +220,11 @@ class NeRFDataset:
             fov = (self.fovy_range[1] + self.fovy_range[0]) / 2
         focal = self.H / (2 * np.tan(np.deg2rad(fov) / 2))
         intrinsics = np.array([focal, focal, self.cx, self.cy])
-        if native:
-            rays = get_rays_host_pose(poses, intrinsics, self.H, self.W, self.device)
-        else:
-            rays = get_rays(poses, intrinsics, self.H, self.W, -1)
+        if native:  # rays made lazily from the host pose (RayBatch)
+            return RayBatch(H=self.H, W=self.W, dir=dirs, device=self.device,
+                            pose=np.asarray(poses, dtype=np.float32),
+                            intrinsics=tuple(float(v) for v in intrinsics))
+        rays = get_rays(poses, intrinsics, self.H, self.W, -1)
         return {"H": self.H, "W": self.W, "rays_o": rays["rays_o"], "rays_d": rays["rays_d"],
                 "dir": dirs}
 

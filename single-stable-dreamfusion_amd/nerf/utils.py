@@ -80,23 +80,41 @@ def get_rays(poses, intrinsics, H, W, N=-1, error_map=None):
     return results
 
 
-def get_rays_host_pose(poses, intrinsics, H, W, device):
-    """get_rays(poses, intrinsics, H, W, N=-1) for host-side poses [B, 4, 4]:
-    one native launch per pose (csrc/camera.hip), the pose passed by value, so
-    the per-step camera needs neither a host->device copy nor a sync.
-    Returns {"rays_o", "rays_d"} [B, H*W, 3] f32 on `device`."""
+_RAYS_FN = None
+
+
+def get_rays_host_pose(poses, intrinsics, H, W, device, out=None):
+    """get_rays(poses, intrinsics, H, W, N=-1) for host-side poses [B, 4, 4]
+    (numpy or CPU tensor): one native launch per pose (csrc/camera.hip), the
+    pose passed by value, so the per-step camera needs neither a host->device
+    copy nor a sync.  Returns {"rays_o", "rays_d"} [B, H*W, 3] f32 on `device`
+    (written into `out` = (rays_o, rays_d) when given)."""
     import ctypes
 
     import _dfhip
+    global _RAYS_FN
+    if _RAYS_FN is None:
+        _RAYS_FN = _dfhip.load().dfhip_get_rays
     fx, fy, cx, cy = (float(v) for v in intrinsics)
-    B = poses.shape[0]
-    rays_o = torch.empty(B, H * W, 3, device=device)
-    rays_d = torch.empty(B, H * W, 3, device=device)
-    host = poses.detach().to("cpu", torch.float32).contiguous()
+    host = np.ascontiguousarray(poses.numpy() if torch.is_tensor(poses) else poses,
+                                dtype=np.float32)
+    B = host.shape[0]
+    if out is None:
+        rays_o = torch.empty(B, H * W, 3, device=device)
+        rays_d = torch.empty(B, H * W, 3, device=device)
+    else:
+        rays_o, rays_d = out
+        if rays_o.shape != (B, H * W, 3) or rays_d.shape != (B, H * W, 3):
+            raise RuntimeError("get_rays_host_pose: output buffers must be [B, H*W, 3]")
+    stream = _dfhip.stream()
+    step = H * W * 3 * 4
     for b in range(B):
         pose = (ctypes.c_float * 12)(*host[b, :3, :4].reshape(-1).tolist())
-        _dfhip.call("dfhip_get_rays", ctypes.cast(pose, ctypes.c_void_p), fx, fy, cx, cy, H, W,
-                    rays_o[b].data_ptr(), rays_d[b].data_ptr(), _dfhip.stream())
+        rc = _RAYS_FN(ctypes.cast(pose, ctypes.c_void_p), fx, fy, cx, cy, H, W,
+                      rays_o.data_ptr() + b * step, rays_d.data_ptr() + b * step, stream)
+        if rc != 0:
+            raise RuntimeError(f"dfhip_get_rays failed ({rc}): "
+                               f"{_dfhip.load().dfhip_last_error().decode()}")
     return {"rays_o": rays_o, "rays_d": rays_d}
 
 
