@@ -61,10 +61,13 @@ def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False):
     from nerf.utils import Trainer, make_adam, seed_everything
 
     opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res),
-                          "--guidance", "synthetic", "--seed", str(seed + rank)])
-    seed_everything(seed + rank)
+                          "--guidance", "synthetic", "--seed", str(seed)])
+    # identical model initialisation on every rank; per-rank RNG (cameras,
+    # march noise, background, SDS draws) from here on
+    seed_everything(seed)
     device = torch.device("cuda", torch.cuda.current_device())
     model = NeRFNetwork(opt)
+    seed_everything(seed + rank)
     guidance = SyntheticSDS(device) if mock_sds else InjectedSDS(device)
     optimizer = lambda m: make_adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)  # noqa
     sched = lambda o: torch.optim.lr_scheduler.LambdaLR(o, lambda it: 0.1 ** min(it / opt.iters, 1))  # noqa

@@ -84,6 +84,7 @@ class NativeAdamAmp:
         if rc != 0:
             raise RuntimeError(f"dfhip_adam_amp_step failed ({rc}): "
                                f"{_dfhip.load().dfhip_last_error().decode()}")
+        self.optimizer._opt_called = True  # what LRScheduler checks for "stepped"
 
     def _rebuild(self, key):
         ts = []

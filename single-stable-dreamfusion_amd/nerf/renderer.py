@@ -78,6 +78,8 @@ class NeRFRenderer(nn.Module):
         self.native_grid_update = True
         # native background mix / depth / mask (nerf/head.py; False: torch ops)
         self.native_head = True
+        # generator of the density-grid jitter (None: torch's default)
+        self.grid_generator = None
 
     # mean_density / mean_count: the sync-free grid refresh leaves them on the
     # device; they are read to the host only when somebody asks (checkpoint,
@@ -350,7 +352,7 @@ class NeRFRenderer(nn.Module):
                         bound = min(2 ** cas, self.bound)
                         half = bound / self.grid_size
                         cas_xyzs = xyzs * (bound - half)
-                        cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * half
+                        cas_xyzs += (self._grid_rand(cas_xyzs) * 2 - 1) * half
                         sig = self.density(cas_xyzs)["sigma"].reshape(-1).detach()
                         tmp_grid[cas, indices] = sig.to(tmp_grid.dtype)
         valid = self.density_grid >= 0
@@ -364,6 +366,16 @@ class NeRFRenderer(nn.Module):
         if total_step > 0:
             self.mean_count = int(self.step_counter[:total_step, 0].sum().item() / total_step)
         self.local_step = 0
+
+    def _grid_rand(self, like):
+        """Jitter draws of the grid refresh: from `grid_generator` when set (the
+        Trainer seeds one identically on every rank, so data-parallel ranks
+        keep identical occupancy grids without a collective),
+        else torch's default generator (rand_like, renderer.py:593)."""
+        gen = self.grid_generator
+        if gen is None:
+            return torch.rand_like(like)
+        return torch.rand(like.shape, dtype=like.dtype, device=like.device, generator=gen)
 
     def _grid_points(self):
         """Cell-centre positions in [-1, 1] (x, y, z order of the reference's
@@ -394,7 +406,7 @@ class NeRFRenderer(nn.Module):
             bound = min(2 ** cas, self.bound)
             half = bound / self.grid_size
             cas_xyzs = xyzs * (bound - half)
-            cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * half
+            cas_xyzs += (self._grid_rand(cas_xyzs) * 2 - 1) * half
             sig = self.density(cas_xyzs)["sigma"].reshape(-1).detach().float().contiguous()
             idx = indices if cas == 0 else indices + cas * cells
             _dfhip.call("dfhip_density_grid_ema", sig.data_ptr(), idx.data_ptr(), sig.numel(),

@@ -231,6 +231,16 @@ class Trainer(object):
 
         model.to(self.device)
         self.model = model
+        if world_size > 1 and dist.is_available() and dist.is_initialized():
+            # one replica: rank 0's parameters and buffers on every rank
+            with torch.no_grad():
+                for t in list(model.parameters()) + list(model.buffers()):
+                    dist.broadcast(t.data, src=0)
+        if getattr(model, "cuda_ray", False) and self.device.type == "cuda":
+            # the density-grid jitter draws the same numbers on every rank, so
+            # the occupancy grids stay identical without a collective
+            model.grid_generator = torch.Generator(device=self.device).manual_seed(
+                int(getattr(opt, "seed", 0) or 0))
         self.guidance = guidance
         if self.guidance is not None:
             for p in self.guidance.parameters():
