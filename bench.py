@@ -127,9 +127,11 @@ def summarize_kernels(records):
     return out
 
 
-# timed region -> the kernel symbols launched inside it (for PMC traffic)
+# timed region -> its kernels, each as alternative name fragments (rocprofv3
+# reports some names demangled, some mangled)
 REGION_KERNELS = {
-    "grid_encode_backward": ("k_grid_bwd_sliced", "k_sum_partials"),
+    "grid_encode_backward": (("gb::k_bin", "gb5k_bin"), ("gb::k_walk", "gb6k_walk"),
+                             ("gb::k_sum", "gb5k_sum")),
     "grid_field_forward": ("k_field_fwd_fused",),
     "field_mlp_backward": ("k_field_bwd", "k_field_wgrad_sum"),
     "grid_encode_forward": ("k_grid_fwd",),
@@ -151,14 +153,15 @@ def load_pmc(name):
         data = json.loads(path.read_text())
     except ValueError:
         return None
-    total, found = 0, False
-    for pat in REGION_KERNELS.get(name, (name,)):
-        for k, v in data.get("kernels", {}).items():
-            if pat in k:
-                total += v["hbm_bytes_per_dispatch"]
-                found = True
-                break
-    return total if found else None
+    kernels = data.get("kernels", {})
+    total = 0
+    for pats in REGION_KERNELS.get(name, (name,)):
+        pats = (pats,) if isinstance(pats, str) else pats
+        hit = next((v for k, v in kernels.items() if any(p in k for p in pats)), None)
+        if hit is None:
+            return None  # a kernel of the region was not profiled
+        total += hit["hbm_bytes_per_dispatch"]
+    return total
 
 
 def main():

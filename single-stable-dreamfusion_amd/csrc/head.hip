@@ -29,7 +29,6 @@ constexpr int kHid = 64;
 constexpr int kOut = 3;
 constexpr int kW1 = kHid * kIn, kB1 = kHid, kW2 = kOut * kHid, kB2 = kOut;
 constexpr int kParams = kW1 + kB1 + kW2 + kB2;  // 2755
-constexpr int kBlock = 64;  // one wave per block: 16k rays -> 256 blocks fill the chip
 constexpr float kHalfPi = 3.141592653589793f / 2.0f;
 
 __device__ __forceinline__ float r16(float x) { return (float)(half_t)f32_rounded(x); }
@@ -44,69 +43,61 @@ __device__ __forceinline__ void load_w(W &w, const float *w1, const float *b1, c
     for (int i = threadIdx.x; i < kB1; i += blockDim.x) w.b1[i] = r16(b1[i]);
     for (int i = threadIdx.x; i < kW2; i += blockDim.x) w.w2[i] = r16(w2[i]);
     for (int i = threadIdx.x; i < kB2; i += blockDim.x) w.b2[i] = r16(b2[i]);
-}
+}  // (callers __syncthreads before reading)
+
+// The network kernels give each ray kSub = 4 lanes (consecutive threads):
+// sub-lane q makes feature columns q, q + 4, q + 8 and hidden units
+// [16q, 16q + 16), the output layer's partial sums are combined with two
+// xor-shuffles (the same order in all four lanes).  A block is 64 rays.
+constexpr int kSub = 4;
+constexpr int kRays = 256 / kSub;  // rays per 256-thread block
 
 // freqencoder.cu:30-58 for D = 3, degree 6 (same expression as k_freq_fwd),
-// then the autocast cast to f16.
-__device__ __forceinline__ void features(const float *d, float x[kIn]) {
+// then the autocast cast to f16; this sub-lane's share into sx[ray][*].
+__device__ __forceinline__ void features_part(const float *d, int q, float *sx) {
+    if (q == 0)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) x[c] = r16(d[c]);
+        for (int c = 0; c < 3; ++c) sx[c] = r16(d[c]);
 #pragma unroll
-    for (int col = 0; col < 2 * kDeg; ++col)
+    for (int i = 0; i < 3; ++i) {
+        const int col = q + kSub * i;  // 0..11: frequency col >> 1, sin / cos col & 1
+        const float phase = (float)(col & 1) * kHalfPi;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float phase = (float)(col & 1) * kHalfPi;
-            x[3 + 3 * col + c] = r16(sinf(scalbnf(d[c], col >> 1) + phase));
-        }
+        for (int c = 0; c < 3; ++c) sx[3 + 3 * col + c] = r16(sinf(scalbnf(d[c], col >> 1) + phase));
+    }
 }
 
-// Hidden layer (f16 values) and the f16 output pre-activation.
-__device__ __forceinline__ void mlp(const W &w, const float x[kIn], float h[kHid],
-                                   float o[kOut]) {
+// This sub-lane's 16 hidden units (f16 values) and the full f16 output
+// pre-activation (partials combined across the ray's four lanes).
+__device__ __forceinline__ void mlp_part(const W &w, const float *x, int q, float h[16],
+                                        float o[kOut]) {
 #pragma unroll
-    for (int j = 0; j < kHid; ++j) {
+    for (int jj = 0; jj < 16; ++jj) {
+        const int j = 16 * q + jj;
         float a = 0.0f;
 #pragma unroll
         for (int i = 0; i < kIn; ++i) a = fmaf(x[i], w.w1[j * kIn + i], a);
         a = a + w.b1[j];
-        h[j] = r16(a > 0.0f ? a : 0.0f);
+        h[jj] = r16(a > 0.0f ? a : 0.0f);
     }
 #pragma unroll
     for (int k = 0; k < kOut; ++k) {
         float a = 0.0f;
 #pragma unroll
-        for (int j = 0; j < kHid; ++j) a = fmaf(h[j], w.w2[k * kHid + j], a);
+        for (int jj = 0; jj < 16; ++jj) a = fmaf(h[jj], w.w2[k * kHid + 16 * q + jj], a);
+        a = a + __shfl_xor(a, 1, 64);
+        a = a + __shfl_xor(a, 2, 64);
         o[k] = r16(a + w.b2[k]);
     }
 }
 
 __device__ __forceinline__ float sigmoid16(float o) { return r16(1.0f / (1.0f + expf(-o))); }
 
-template <bool NET>
-__global__ __launch_bounds__(kBlock) void k_head_fwd(
-    uint32_t N, const float *__restrict__ ws, const float *__restrict__ depth,
-    const float *__restrict__ image, const float *__restrict__ rays_d,
-    const float *__restrict__ nears, const float *__restrict__ fars, const float *w1,
-    const float *b1, const float *w2, const float *b2, const float *__restrict__ bg_color,
-    float *__restrict__ out_image, float *__restrict__ out_depth, uint8_t *__restrict__ mask) {
-    __shared__ W w;
-    if (NET) {
-        load_w(w, w1, b1, w2, b2);
-        __syncthreads();
-    }
-    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= N) return;
-    float bg[3];
-    if (NET) {
-        float x[kIn], h[kHid], o[kOut];
-        features(rays_d + 3 * (size_t)n, x);
-        mlp(w, x, h, o);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) bg[k] = bg_color ? bg_color[3 * (size_t)n + k] : 1.0f;
-    }
+__device__ __forceinline__ void write_outputs(uint32_t N, uint32_t n, const float bg[3],
+                                             const float *ws, const float *depth,
+                                             const float *image, const float *nears,
+                                             const float *fars, float *out_image,
+                                             float *out_depth, uint8_t *mask) {
     const float t = 1.0f - ws[n];
 #pragma unroll
     for (int k = 0; k < 3; ++k) out_image[(size_t)k * N + n] = image[3 * (size_t)n + k] + t * bg[k];
@@ -116,124 +107,164 @@ __global__ __launch_bounds__(kBlock) void k_head_fwd(
     mask[n] = nr < fr ? 1 : 0;
 }
 
-// Backward.  grad_image [N, 3] = g; grad_ws = -sum_c g_c bg_c; with the
-// network also the background MLP's weight-gradient partials of this block.
-template <bool NET>
-__global__ __launch_bounds__(kBlock) void k_head_bwd(
+__global__ __launch_bounds__(256) void k_head_fwd_plain(
+    uint32_t N, const float *__restrict__ ws, const float *__restrict__ depth,
+    const float *__restrict__ image, const float *__restrict__ nears,
+    const float *__restrict__ fars, const float *__restrict__ bg_color,
+    float *__restrict__ out_image, float *__restrict__ out_depth, uint8_t *__restrict__ mask) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    float bg[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bg[k] = bg_color ? bg_color[3 * (size_t)n + k] : 1.0f;
+    write_outputs(N, n, bg, ws, depth, image, nears, fars, out_image, out_depth, mask);
+}
+
+__global__ __launch_bounds__(256) void k_head_fwd_net(
+    uint32_t N, const float *__restrict__ ws, const float *__restrict__ depth,
+    const float *__restrict__ image, const float *__restrict__ rays_d,
+    const float *__restrict__ nears, const float *__restrict__ fars, const float *w1,
+    const float *b1, const float *w2, const float *b2, float *__restrict__ out_image,
+    float *__restrict__ out_depth, uint8_t *__restrict__ mask) {
+    __shared__ W w;
+    __shared__ float s_x[kRays][kIn + 1];
+    load_w(w, w1, b1, w2, b2);
+    const int q = threadIdx.x & (kSub - 1), r = threadIdx.x / kSub;
+    const uint32_t n = blockIdx.x * kRays + r;
+    const bool live = n < N;
+    if (live) features_part(rays_d + 3 * (size_t)n, q, s_x[r]);
+    __syncthreads();
+    float x[kIn], h[16], o[kOut];
+#pragma unroll
+    for (int i = 0; i < kIn; ++i) x[i] = live ? s_x[r][i] : 0.0f;
+    mlp_part(w, x, q, h, o);
+    if (!live || q != 0) return;
+    float bg[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
+    write_outputs(N, n, bg, ws, depth, image, nears, fars, out_image, out_depth, mask);
+}
+
+// Backward.  grad_image [N, 3] = g; grad_ws = -sum_c g_c bg_c; grad_bg =
+// g (1 - ws) when bg_color needs it.
+__global__ __launch_bounds__(256) void k_head_bwd_plain(
+    uint32_t N, const float *__restrict__ g_image /* [3, N] */, const float *__restrict__ ws,
+    const float *__restrict__ bg_color, float *__restrict__ grad_image,
+    float *__restrict__ grad_ws, float *__restrict__ grad_bg) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    float g[3], sw = 0.0f;
+    const float t = 1.0f - ws[n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        g[k] = g_image[(size_t)k * N + n];
+        grad_image[3 * (size_t)n + k] = g[k];
+        const float bg = bg_color ? bg_color[3 * (size_t)n + k] : 1.0f;
+        sw = sw + g[k] * bg;
+        if (grad_bg) grad_bg[3 * (size_t)n + k] = g[k] * t;
+    }
+    grad_ws[n] = -sw;
+}
+
+// Network backward: the forward is recomputed (four lanes per ray), then the
+// sigmoid and the two f16 Linear layers are run backward and this block's
+// weight-gradient partials (f32 sums over its 64 rays of f16 products) formed
+// from LDS images of the activations.
+__global__ __launch_bounds__(256) void k_head_bwd_net(
     uint32_t N, const float *__restrict__ g_image /* [3, N] */, const float *__restrict__ ws,
     const float *__restrict__ rays_d, const float *w1, const float *b1, const float *w2,
-    const float *b2, const float *__restrict__ bg_color, float *__restrict__ grad_image,
-    float *__restrict__ grad_ws, float *__restrict__ grad_bg, float *__restrict__ partial) {
+    const float *b2, float *__restrict__ grad_image, float *__restrict__ grad_ws,
+    float *__restrict__ partial) {
     __shared__ W w;
-    __shared__ half_t s_dh[kBlock][kHid];   // relu-masked hidden grads (f16 values)
-    __shared__ half_t s_x[kBlock][kIn + 1];  // features
-    __shared__ half_t s_h[kBlock][kHid];    // hidden activations
-    __shared__ half_t s_do[kBlock][4];      // output pre-activation grads
-    if (NET) {
-        load_w(w, w1, b1, w2, b2);
-        __syncthreads();
-    }
-    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ float s_x[kRays][kIn + 1];
+    __shared__ half_t s_dh[kRays][kHid];  // relu-masked hidden grads (f16 values)
+    __shared__ half_t s_h[kRays][kHid];   // hidden activations
+    __shared__ float s_do[kRays][4];      // output pre-activation grads (f16 values)
+    load_w(w, w1, b1, w2, b2);
+    const int q = threadIdx.x & (kSub - 1), r = threadIdx.x / kSub;
+    const uint32_t n = blockIdx.x * kRays + r;
     const bool live = n < N;
-    float g[3] = {0.0f, 0.0f, 0.0f};
-    if (live) {
+    if (live) features_part(rays_d + 3 * (size_t)n, q, s_x[r]);
+    else if (q == 0)
+        for (int i = 0; i < kIn; ++i) s_x[r][i] = 0.0f;
+    __syncthreads();
+    float x[kIn], h[16], o[kOut];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            g[k] = g_image[(size_t)k * N + n];
-            grad_image[3 * (size_t)n + k] = g[k];
-        }
-    }
-    float bg[3];
-    float x[kIn], h[kHid], o[kOut];
-    if (NET) {
-        if (live) {
-            features(rays_d + 3 * (size_t)n, x);
-            mlp(w, x, h, o);
-        } else {
+    for (int i = 0; i < kIn; ++i) x[i] = s_x[r][i];
+    mlp_part(w, x, q, h, o);
+    float g[3] = {0.0f, 0.0f, 0.0f}, bg[3];
+    if (live)
 #pragma unroll
-            for (int i = 0; i < kIn; ++i) x[i] = 0.0f;
+        for (int k = 0; k < 3; ++k) g[k] = g_image[(size_t)k * N + n];
 #pragma unroll
-            for (int j = 0; j < kHid; ++j) h[j] = 0.0f;
-#pragma unroll
-            for (int k = 0; k < kOut; ++k) o[k] = 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) bg[k] = (live && bg_color) ? bg_color[3 * (size_t)n + k] : 1.0f;
-    }
-    if (live) {
+    for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
+    if (live && q == 0) {
         // ((1 - ws) * bg) backward: d ws = -(sum_c g_c * bg_c)
         float sw = 0.0f;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) sw = sw + g[k] * bg[k];
-        grad_ws[n] = -sw;
-        if (!NET && grad_bg) {
-            const float t = 1.0f - ws[n];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) grad_bg[3 * (size_t)n + k] = g[k] * t;
+        for (int k = 0; k < 3; ++k) {
+            grad_image[3 * (size_t)n + k] = g[k];
+            sw = sw + g[k] * bg[k];
         }
+        grad_ws[n] = -sw;
     }
-    if (!NET) return;
-    // sigmoid (f16) and the two f16 Linear layers, backward
     const float t = live ? 1.0f - ws[n] : 0.0f;
     float dout[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const float dbg = r16(g[k] * t);
-        dout[k] = r16(dbg * (1.0f - bg[k]) * bg[k]);
+        const float dbg = r16(g[k] * t);             // grad of the f16 bg
+        dout[k] = r16(dbg * (1.0f - bg[k]) * bg[k]);  // sigmoid_backward, f16
     }
-    const int r = threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < kHid; ++j) {
+    for (int jj = 0; jj < 16; ++jj) {
+        const int j = 16 * q + jj;
         float a = 0.0f;
 #pragma unroll
         for (int k = 0; k < kOut; ++k) a = fmaf(dout[k], w.w2[k * kHid + j], a);
-        s_dh[r][j] = (half_t)(h[j] > 0.0f ? r16(a) : 0.0f);
-        s_h[r][j] = (half_t)h[j];
+        s_dh[r][j] = (half_t)(h[jj] > 0.0f ? r16(a) : 0.0f);
+        s_h[r][j] = (half_t)h[jj];
     }
+    if (q == 0)
 #pragma unroll
-    for (int i = 0; i < kIn; ++i) s_x[r][i] = (half_t)x[i];
-#pragma unroll
-    for (int k = 0; k < kOut; ++k) s_do[r][k] = (half_t)dout[k];
+        for (int k = 0; k < kOut; ++k) s_do[r][k] = dout[k];
     __syncthreads();
-    // per-block weight-gradient partials: f32 sums of f16 products over the rays
     float *out = partial + (size_t)blockIdx.x * kParams;
     for (int p = threadIdx.x; p < kParams; p += blockDim.x) {
         float s = 0.0f;
         if (p < kW1) {
             const int j = p / kIn, i = p - j * kIn;
-            for (int q = 0; q < kBlock; ++q) s = fmaf((float)s_dh[q][j], (float)s_x[q][i], s);
+            for (int y = 0; y < kRays; ++y) s = fmaf((float)s_dh[y][j], s_x[y][i], s);
         } else if (p < kW1 + kB1) {
             const int j = p - kW1;
-            for (int q = 0; q < kBlock; ++q) s += (float)s_dh[q][j];
+            for (int y = 0; y < kRays; ++y) s += (float)s_dh[y][j];
         } else if (p < kW1 + kB1 + kW2) {
             const int k = (p - kW1 - kB1) / kHid, j = (p - kW1 - kB1) - k * kHid;
-            for (int q = 0; q < kBlock; ++q) s = fmaf((float)s_do[q][k], (float)s_h[q][j], s);
+            for (int y = 0; y < kRays; ++y) s = fmaf(s_do[y][k], (float)s_h[y][j], s);
         } else {
             const int k = p - kW1 - kB1 - kW2;
-            for (int q = 0; q < kBlock; ++q) s += (float)s_do[q][k];
+            for (int y = 0; y < kRays; ++y) s += s_do[y][k];
         }
         out[p] = s;
     }
 }
 
-// Fixed-order sum of the per-block partials: block = 64 outputs, its four
-// waves take every fourth partial, then a fixed-order sum of the four.
-__global__ __launch_bounds__(256) void k_head_wsum(const float *__restrict__ partial,
-                                                   uint32_t blocks, float *gw1, float *gb1,
-                                                   float *gw2, float *gb2) {
-    __shared__ float red[4][64];
+// Fixed-order sum of the per-block partials: block = 64 outputs, its 16
+// waves take every 16th partial, then a fixed-order sum of the 16.
+__global__ __launch_bounds__(1024) void k_head_wsum(const float *__restrict__ partial,
+                                                    uint32_t blocks, float *gw1, float *gb1,
+                                                    float *gw2, float *gb2) {
+    __shared__ float red[16][64];
     const int o = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int p = blockIdx.x * 64 + o;
     float s = 0.0f;
     if (p < kParams)
-        for (uint32_t b = grp; b < blocks; b += 4) s += partial[(size_t)b * kParams + p];
+        for (uint32_t b = grp; b < blocks; b += 16) s += partial[(size_t)b * kParams + p];
     red[grp][o] = s;
     __syncthreads();
     if (grp != 0 || p >= kParams) return;
-    s = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+    s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][o];
     if (p < kW1) gw1[p] = s;
     else if (p < kW1 + kB1) gb1[p - kW1] = s;
     else if (p < kW1 + kB1 + kW2) gw2[p - kW1 - kB1] = s;
@@ -282,7 +313,7 @@ __global__ __launch_bounds__(256) void k_entropy_bwd(uint32_t N, const float *__
 using namespace dfhip;
 
 extern "C" uint32_t dfhip_ray_head_partial_floats(uint32_t N) {
-    return ceil_div(N, (uint32_t)hd::kBlock) * (uint32_t)hd::kParams;
+    return ceil_div(N, (uint32_t)hd::kRays) * (uint32_t)hd::kParams;
 }
 
 extern "C" int dfhip_ray_head_forward(uint32_t N, const float *ws, const float *depth,
@@ -303,16 +334,13 @@ extern "C" int dfhip_ray_head_forward(uint32_t N, const float *ws, const float *
         return DFHIP_EINVAL;
     }
     hipStream_t s = as_stream(stream);
-    const uint32_t blocks = ceil_div(N, (uint32_t)hd::kBlock);
     if (net)
-        hd::k_head_fwd<true><<<blocks, hd::kBlock, 0, s>>>(N, ws, depth, image, rays_d, nears,
-                                                          fars, w1, b1, w2, b2, nullptr,
-                                                          out_image, out_depth, mask);
+        hd::k_head_fwd_net<<<ceil_div(N, (uint32_t)hd::kRays), 256, 0, s>>>(
+            N, ws, depth, image, rays_d, nears, fars, w1, b1, w2, b2, out_image, out_depth, mask);
     else
-        hd::k_head_fwd<false><<<blocks, hd::kBlock, 0, s>>>(N, ws, depth, image, rays_d, nears,
-                                                           fars, nullptr, nullptr, nullptr,
-                                                           nullptr, bg_color, out_image,
-                                                           out_depth, mask);
+        hd::k_head_fwd_plain<<<ceil_div(N, 256u), 256, 0, s>>>(N, ws, depth, image, nears, fars,
+                                                               bg_color, out_image, out_depth,
+                                                               mask);
     return check_launch(name);
 }
 
@@ -335,18 +363,15 @@ extern "C" int dfhip_ray_head_backward(uint32_t N, const float *g_image, const f
         return DFHIP_EINVAL;
     }
     hipStream_t s = as_stream(stream);
-    const uint32_t blocks = ceil_div(N, (uint32_t)hd::kBlock);
     if (net) {
-        hd::k_head_bwd<true><<<blocks, hd::kBlock, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
-                                                          nullptr, grad_image, grad_ws, nullptr,
-                                                          partial);
-        hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u), 256, 0, s>>>(
+        const uint32_t blocks = ceil_div(N, (uint32_t)hd::kRays);
+        hd::k_head_bwd_net<<<blocks, 256, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
+                                                  grad_image, grad_ws, partial);
+        hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u), 1024, 0, s>>>(
             partial, blocks, gw1, gb1, gw2, gb2);
     } else {
-        hd::k_head_bwd<false><<<blocks, hd::kBlock, 0, s>>>(N, g_image, ws, nullptr, nullptr,
-                                                           nullptr, nullptr, nullptr, bg_color,
-                                                           grad_image, grad_ws, grad_bg,
-                                                           nullptr);
+        hd::k_head_bwd_plain<<<ceil_div(N, 256u), 256, 0, s>>>(N, g_image, ws, bg_color,
+                                                               grad_image, grad_ws, grad_bg);
     }
     return check_launch(name);
 }
