@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=1)
+    p.add_argument("--no-infer", action="store_true",
+                   help="skip the C4 inference-render measurement")
+    p.add_argument("--infer-res", type=int, default=800)
     return p.parse_args()
 
 
@@ -106,6 +109,82 @@ def cpu_baseline(res, steps):
             "cores": torch.get_num_threads(), "kind": "port", "cpu_model": model,
             "sample": f"{steps} timed + 1 warm-up --cuda_ray-off train steps at {res}x{res} "
                       f"(64 coarse + 64 importance samples/ray, fp32, synthetic SDS, Adam)"}
+
+
+def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1):
+    """C4 (BASELINE configs[3]): res x res inference render of run_cuda's eval
+    branch (albedo, fp16 autocast, max_steps 512, T_thresh 1e-4) from the
+    reference's test-view camera, on a grid whose occupancy comes from
+    update_extra_state of a seeded network with U(-0.5, 0.5) embeddings
+    (SURVEY §8d preset R0; no trained checkpoint exists offline).  Times the
+    fused persistent renderer (the product path) and, for comparison, the
+    reference-structured host loop (march_rays -> field -> composite_rays with
+    one sync per iteration, renderer.py:496-532) on the same kernels."""
+    import main
+    import _dfhip
+    from nerf.network_grid import NeRFNetwork
+    from nerf.provider import NeRFDataset
+    opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res)])
+    torch.manual_seed(seed)
+    model = NeRFNetwork(opt).to(device)
+    with torch.no_grad():
+        model.encoder.embeddings.uniform_(-0.5, 0.5)
+    with torch.autocast("cuda", dtype=torch.float16):
+        for _ in range(3):
+            model.update_extra_state()
+    model.eval()
+    data = NeRFDataset(opt, device=device, type="test", H=res, W=res, size=8).collate([1])
+    rays_o, rays_d = data["rays_o"], data["rays_d"]
+    n = rays_o.shape[0] * rays_o.shape[1]
+
+    def frame():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            return model.render(rays_o, rays_d, staged=True, perturb=False, light_d=None,
+                                ambient_ratio=1.0, shading="albedo", force_all_rays=True,
+                                bg_color=None, **vars(opt))
+
+    def timed_frames(k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            frame()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k
+
+    model.native_infer = True
+    for _ in range(warmup):
+        frame()
+    timer = _dfhip.new_kernel_timer()
+    _dfhip.set_kernel_timer(timer)
+    fused_s = timed_frames(frames)
+    _dfhip.set_kernel_timer(None)
+    kern = summarize_kernels(timer.records).get("render_rays_infer", {})
+    work = model.last_infer_work.cpu().numpy().view(np.uint32)
+    samples = int(work[1]) + (int(work[2]) << 32)
+    out = {"workload": f"C4: {res}x{res} run_cuda eval render (albedo, fp16, max_steps 512, "
+                       "T_thresh 1e-4), test-view camera, occupancy from update_extra_state "
+                       "of a seeded U(-0.5,0.5) grid network",
+           "rays_per_frame": n, "ms_per_frame": round(fused_s * 1e3, 3),
+           "rays_per_sec": round(n / fused_s, 1), "samples_per_frame": samples,
+           "launch": "one persistent kernel (render_rays_infer)"}
+    if kern:
+        t = kern["avg_us"] * 1e-6
+        flops = 12800.0 * samples  # sigma MLP forward, SURVEY §8d
+        out["kernel_avg_us"] = kern["avg_us"]
+        out["samples_per_sec"] = round(samples / t, 1)
+        out["mfma"] = {"achieved": round(flops / t / 1e12, 2), "peak": 2500.0,
+                       "unit": "TFLOP/s", "frac": round(flops / t / 2.5e15, 5)}
+        # what the reference's loop moves through HBM for the same work
+        # (SURVEY §8d C4 line: 212 B per sample + 96 B per ray)
+        out["unfused_equivalent_GBs"] = round((212.0 * samples + 96.0 * n) / t / 1e9, 1)
+    if loop_frames > 0:
+        model.native_infer = False
+        frame()
+        loop_s = timed_frames(loop_frames)
+        model.native_infer = True
+        out["loop_ms_per_frame"] = round(loop_s * 1e3, 3)
+        out["speedup_vs_loop"] = round(loop_s / fused_s, 2)
+    return out
 
 
 def summarize_kernels(records):
@@ -249,6 +328,8 @@ def main():
         step_ms = result["ms_per_step"]
         result["kernel_share_of_step"] = {k: round(v["total_ms"] / args.steps / step_ms, 4)
                                           for k, v in kernels.items()}
+    if rank == 0 and world == 1 and not args.no_infer:
+        result["inference"] = bench_inference(device, args.infer_res)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.res, args.cpu_steps)
         result["gpu_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)

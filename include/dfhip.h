@@ -451,6 +451,34 @@ int dfhip_entropy_forward(uint32_t N, const float *ws, float lambda, float *loss
 int dfhip_entropy_backward(uint32_t N, const float *ws, const float *grad_loss, float lambda,
                            float *grad_ws, dfhip_stream_t stream);
 
+/* nerf/renderer.py:496-532 — the inference branch of run_cuda (the host loop
+ * of march_rays raymarching.cu:700-804 -> network_grid.common_forward
+ * network_grid.py:76-87 under fp16 autocast -> composite_rays
+ * raymarching.cu:818-905 -> rays_alive compaction), fused into ONE persistent
+ * launch for the albedo shading of the reference's grid field (16 levels x 2
+ * channels, sigma MLP 32 -> 64 -> 64 -> 4).
+ * In:  rays_o, rays_d [N,3] f32; nears, fars [N] f32 (near_far_from_aabb);
+ *      noises [N] f32 or NULL (perturbation of the first march step);
+ *      bound, dt_gamma, max_steps, C (cascade), H (density grid size), grid =
+ *      density bitfield [C*H^3/8] u8; T_thresh; table [rows,2] f16 (the
+ *      autocast copy of the embeddings), offsets [L+1] i32, L, S = log2
+ *      per-level scale, base_res, gridtype, align_corners (as
+ *      dfhip_grid_encode_forward); w1..b3 the f32 nn.Linear parameters.
+ * Out: weights_sum [N], depth [N] (sum of w * t with t measured from the
+ *      near plane's rays_t, as composite_rays leaves it), image [N,3] f32 —
+ *      every ray written once (no zero-fill needed).
+ * work: [4] u32 caller scratch, zeroed here; after the launch work[1] +
+ *      2^32 work[2] = number of samples evaluated. */
+int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d,
+                            const float *nears, const float *fars, const float *noises,
+                            float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
+                            uint32_t H, const uint8_t *grid, float T_thresh, const void *table,
+                            const int32_t *offsets, uint32_t L, float S, uint32_t base_res,
+                            uint32_t gridtype, int align_corners, const float *w1,
+                            const float *b1, const float *w2, const float *b2, const float *w3,
+                            const float *b3, float *weights_sum, float *depth, float *image,
+                            uint32_t *work, dfhip_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -112,3 +112,45 @@ def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lb
          ptr(offsets), int(total_rows), offsets.shape[0] - 1, float(S), int(H), int(gridtype),
          int(bool(align_corners)), ptr(grad_embeddings), ptr(grid_partial), int(grid_parts),
          stream())
+
+
+# ---- fused inference render (march + field + composite, persistent queue)
+
+def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
+                      bitfield, T_thresh, table, offsets, S, base_res, gridtype, align_corners,
+                      weights, weights_sum, depth, image, work):
+    """Inference render of N rays in one launch (csrc/render.hip; reference
+    nerf/renderer.py:496-532).  rays_o/rays_d [N, 3] f32, nears/fars [N] f32,
+    noises [N] f32 or None, bitfield u8, table [rows, 2] f16, offsets int32.
+    Writes weights_sum [N], depth [N], image [N, 3] f32; work: [4] int32
+    scratch whose words 1, 2 hold the evaluated sample count afterwards."""
+    n = rays_o.shape[0]
+    for t, what in ((rays_o, "rays_o"), (rays_d, "rays_d"), (nears, "nears"), (fars, "fars"),
+                    (weights_sum, "weights_sum"), (depth, "depth"), (image, "image")):
+        _f32(t, what)
+    if tuple(rays_d.shape) != (n, 3) or tuple(rays_o.shape) != (n, 3):
+        raise RuntimeError("rays_o and rays_d must be [N, 3]")
+    for t, what, shp in ((nears, "nears", (n,)), (fars, "fars", (n,)),
+                         (weights_sum, "weights_sum", (n,)), (depth, "depth", (n,)),
+                         (image, "image", (n, 3))):
+        if tuple(t.shape) != shp:
+            raise RuntimeError(f"{what} must have shape {shp}, got {tuple(t.shape)}")
+    if noises is not None:
+        _f32(noises, "noises")
+        if tuple(noises.shape) != (n,):
+            raise RuntimeError("noises must be [N]")
+    checked(bitfield, "bitfield", "u8")
+    if bitfield.numel() * 8 < C * H ** 3:
+        raise RuntimeError("bitfield is smaller than C * H^3 / 8 bytes")
+    checked(table, "table")
+    if table.dtype != torch.float16 or table.dim() != 2 or table.shape[1] != 2:
+        raise RuntimeError("table must be a [rows, 2] float16 tensor")
+    checked(offsets, "offsets", "int")
+    checked(work, "work", "int")
+    if work.numel() < 4:
+        raise RuntimeError("work must hold 4 int32")
+    call("dfhip_render_rays_infer", n, ptr(rays_o), ptr(rays_d), ptr(nears), ptr(fars),
+         ptr(noises), float(bound), float(dt_gamma), int(max_steps), int(C), int(H), ptr(bitfield),
+         float(T_thresh), ptr(table), ptr(offsets), offsets.shape[0] - 1, float(S),
+         int(base_res), int(gridtype), int(bool(align_corners)), *_weights(weights),
+         ptr(weights_sum), ptr(depth), ptr(image), ptr(work), stream())

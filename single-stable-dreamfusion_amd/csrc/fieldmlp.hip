@@ -27,211 +27,10 @@
 // weight gradients as MFMAs over 32-sample k-steps from a per-wave LDS image
 // of the activations.  Per-workgroup partial sums + a fixed-order reduction
 // make the weight gradients deterministic.
-#include "common.h"
-#include "grid_common.h"
+#include "field_common.h"
 
 namespace dfhip {
 namespace fm {
-
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-constexpr int kIn = 32, kHid = 64, kOut = 4;
-// packed parameter order (nn.Linear): W1 [64,32], b1 [64], W2 [64,64], b2 [64], W3 [4,64], b3 [4]
-constexpr int kOffW1 = 0, kOffB1 = kOffW1 + kHid * kIn, kOffW2 = kOffB1 + kHid,
-              kOffB2 = kOffW2 + kHid * kHid, kOffW3 = kOffB2 + kHid, kOffB3 = kOffW3 + kOut * kHid,
-              kParams = kOffB3 + kOut;  // 6532
-
-__device__ __forceinline__ f4 mfma(half8 a, half8 b, f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-
-// Make this wave's LDS writes visible to its other lanes before they read.
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// LDS row strides (halves).  Operand reads put 16 lanes on 16 consecutive
-// rows; a row stride of 4 * odd dwords maps those rows to 16 distinct
-// 4-dword bank groups, so the 8-B / 16-B operand reads are conflict-free
-// (unpadded 64- and 128-B rows were 4- and 8-way conflicts).
-constexpr int kLd32 = 40;  // rows of 32 halves (+8)
-constexpr int kLd64 = 72;  // rows of 64 halves (+8)
-
-// Weights as f16 (autocast's cast of the f32 parameters), in LDS.
-struct Weights {
-    half_t w1[kHid * kLd32];  // [n1][f]
-    half_t w2[kHid * kLd64];  // [n2][n1]
-    half_t w3[16 * kLd64];    // [o][n2], rows 4..15 zero
-    float b1[kHid], b2[kHid], b3[16];  // f32 of the f16-rounded biases; b3 rows 4.. zero
-};
-struct WeightsT {             // backward only
-    half_t w1t[kIn * kLd64];  // [f][n1]
-    half_t w2t[kHid * kLd64]; // [n1][n2]
-    half_t w3t[kHid * kLd32]; // [n2][o], o 4..31 zero
-};
-
-// Feature order of the fused path: position p = 8h + j of the layer-1 B
-// operand holds level 4 (j >> 1) + h, channel j & 1, so that for each j the
-// four lane groups work on four levels of the same kind (dense / tiled /
-// z-dropped): feature index 2 * level + channel.
-__host__ __device__ constexpr int perm_feature(int p) {
-    return 2 * (4 * ((p & 7) >> 1) + (p >> 3)) + (p & 1);
-}
-
-// PERM: layer-1 weights stored in the fused path's permuted feature order.
-template <bool PERM>
-__device__ void load_weights(Weights &W, WeightsT *T, const float *w1, const float *b1,
-                             const float *w2, const float *b2, const float *w3, const float *b3) {
-    for (int i = threadIdx.x; i < kHid * kIn; i += blockDim.x) {
-        const int n = i / kIn, p = i % kIn;
-        W.w1[n * kLd32 + p] = (half_t)w1[n * kIn + (PERM ? perm_feature(p) : p)];
-        if (T) T->w1t[(i % kIn) * kLd64 + i / kIn] = (half_t)w1[i];  // natural: rows = features
-    }
-    for (int i = threadIdx.x; i < kHid * kHid; i += blockDim.x) {
-        const half_t v = (half_t)w2[i];
-        W.w2[(i / kHid) * kLd64 + i % kHid] = v;
-        if (T) T->w2t[(i % kHid) * kLd64 + i / kHid] = v;
-    }
-    for (int i = threadIdx.x; i < 16 * kHid; i += blockDim.x)
-        W.w3[(i / kHid) * kLd64 + i % kHid] = i < kOut * kHid ? (half_t)w3[i] : (half_t)0.0f;
-    if (T)
-        for (int i = threadIdx.x; i < kHid * 32; i += blockDim.x) {
-            const int n2 = i / 32, o = i % 32;
-            T->w3t[n2 * kLd32 + o] = o < kOut ? (half_t)w3[o * kHid + n2] : (half_t)0.0f;
-        }
-    for (int i = threadIdx.x; i < kHid; i += blockDim.x) {
-        W.b1[i] = (float)(half_t)b1[i];
-        W.b2[i] = (float)(half_t)b2[i];
-    }
-    for (int i = threadIdx.x; i < 16; i += blockDim.x) W.b3[i] = i < kOut ? (float)(half_t)b3[i] : 0.0f;
-}
-
-// A operand, natural k order: row `row` of a row-major [*, ld] f16 matrix,
-// k = 8h .. 8h+7 (+ koff).
-__device__ __forceinline__ half8 a_nat(const half_t *m, int ld, int row, int koff, int h) {
-    return *reinterpret_cast<const half8 *>(m + row * ld + koff + 8 * h);
-}
-// A operand, permuted k order of k-step s (see header).
-__device__ __forceinline__ half8 a_perm(const half_t *m, int ld, int row, int s, int h) {
-    const half4 lo = *reinterpret_cast<const half4 *>(m + row * ld + 32 * s + 4 * h);
-    const half4 hi = *reinterpret_cast<const half4 *>(m + row * ld + 32 * s + 16 + 4 * h);
-    return half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-// B operand of k-step s from four accumulator tiles' f16 values v[tile][reg].
-__device__ __forceinline__ half8 b_from_tiles(const half_t (&v)[4][4], int s) {
-    return half8{v[2 * s][0], v[2 * s][1], v[2 * s][2], v[2 * s][3],
-                 v[2 * s + 1][0], v[2 * s + 1][1], v[2 * s + 1][2], v[2 * s + 1][3]};
-}
-__device__ __forceinline__ f4 bias4(const float *b, int row0) {
-    return f4{b[row0], b[row0 + 1], b[row0 + 2], b[row0 + 3]};
-}
-
-// One 16-sample tile through the MLP.  xb: B operand of the encoder features
-// (lane: sample c, features 8h..8h+7).  Outputs the post-ReLU f16 activations
-// of both hidden layers and the f32 accumulators of the output layer.
-struct Fwd {
-    half_t a1[4][4], a2[4][4];  // [tile][reg]: neuron 16 t + 4 h + r of sample c
-    f4 o;                       // rows 4h + r (only h == 0 valid: outputs 0..3)
-};
-
-__device__ __forceinline__ void forward_tile(const Weights &W, half8 xb, int c, int h, Fwd &F) {
-    f4 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        acc[t] = mfma(a_nat(W.w1, kLd32, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const half_t v = (half_t)acc[t][r];
-            F.a1[t][r] = v > (half_t)0.0f ? v : (half_t)0.0f;
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        f4 a = bias4(W.b2, 16 * u + 4 * h);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kLd64, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const half_t v = (half_t)a[r];
-            F.a2[u][r] = v > (half_t)0.0f ? v : (half_t)0.0f;
-        }
-    }
-    f4 o = bias4(W.b3, 4 * h);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) o = mfma(a_perm(W.w3, kLd64, c, s, h), b_from_tiles(F.a2, s), o);
-    F.o = o;
-}
-
-__device__ __forceinline__ float gaussian(const float *x) {
-    // network_grid.py gaussian: 5 * exp(-(x**2).sum(-1) / (2 * 0.2**2)), f32
-    const float s = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
-    return 5.0f * expf(-s / 0.08f);
-}
-
-__device__ __forceinline__ half8 load_x(const half_t *enc, uint32_t sample, uint32_t M, int h) {
-    if (sample >= M) return half8{};
-    return *reinterpret_cast<const half8 *>(enc + (size_t)sample * kIn + 8 * h);
-}
-
-// Grid features of one sample at levels 4(j >> 1) + h (j = 0..7, channel
-// j & 1) in the permuted order above: exactly k_grid_fwd<half, 3, 2>'s
-// arithmetic (gridencoder.cu:75-178: half accumulators rounded per corner),
-// with the trailing-dim corners of z-dropped tiled levels gathered once.
-__device__ __forceinline__ half8 grid_features(const half_t *__restrict__ table,
-                                               const int32_t *__restrict__ offsets,
-                                               const ge::Levels &lv, uint32_t gridtype,
-                                               bool align, const float (&x)[3], int h) {
-    half8 out{};
-    if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
-        return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t l = 4 * q + h;
-        const ge::LevelCtx c = ge::level_ctx<3>(offsets, lv, l, gridtype, align);
-        const uint32_t *tab = reinterpret_cast<const uint32_t *>(table + (size_t)c.base * 2);
-        float frac[3];
-        uint32_t cell[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const float p = fmaf(x[d], c.scale, align ? 0.0f : 0.5f);
-            cell[d] = (uint32_t)floorf(p);
-            frac[d] = p - (float)cell[d];
-        }
-        const uint32_t lead = (!c.hashed) ? c.used : 3u;
-        const uint32_t lead_mask = (1u << lead) - 1u;
-        uint32_t row_bits[8];
-        half_t a0 = (half_t)0.0f, a1 = (half_t)0.0f;
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            float w = 1.0f;
-            uint32_t p[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                if (k & (1u << d)) { w *= frac[d]; p[d] = cell[d] + 1u; }
-                else { w *= 1.0f - frac[d]; p[d] = cell[d]; }
-            }
-            if ((k & ~lead_mask) == 0) row_bits[k] = tab[ge::row_index<3>(c, p)];
-            else row_bits[k] = row_bits[k & lead_mask];
-            half_t v[2];
-            __builtin_memcpy(v, &row_bits[k], 4);
-            ge::acc_corner(a0, w, v[0]);
-            ge::acc_corner(a1, w, v[1]);
-        }
-        out[2 * q] = a0;
-        out[2 * q + 1] = a1;
-    }
-    return out;
-}
-
-__device__ __forceinline__ uint32_t active_count(const int32_t *m_dev, uint32_t cap) {
-    if (!m_dev) return cap;
-    const int32_t m = *m_dev;
-    return m < 0 ? 0u : ((uint32_t)m < cap ? (uint32_t)m : cap);
-}
 
 // ------------------------------------------------------------------ forward
 // Grid encoding + MLP + heads in one pass: a wave takes 16 samples; lane

@@ -1,0 +1,236 @@
+// Fused persistent inference renderer for gfx950: occupancy-grid march +
+// tiled-grid gather + sigma MLP (MFMA) + front-to-back compositing of the
+// albedo field in ONE launch with a device work queue of rays.
+//
+// Behavioural spec: the reference's inference branch of run_cuda
+// (nerf/renderer.py:496-532): a host loop of
+//   march_rays (raymarching.cu:700-804) -> network_grid.common_forward
+//   (network_grid.py:76-87, under fp16 autocast) -> composite_rays
+//   (raymarching.cu:818-905) -> rays_alive compaction (one host sync)
+// for up to max_steps / n_step iterations.  The per-ray arithmetic is the
+// same sequence of operations, instruction for instruction:
+//   * the march is rm::march_next, the reference loop in register form;
+//   * the field is fm::grid_features + fm::forward_tile, the kernels the
+//     train path and the eval loop run (f16 per-corner accumulation, f16
+//     activations, f32 MFMA accumulators, expf density, f16 albedo);
+//   * compositing is k_composite_infer's: T = 1 - sum(w), alpha =
+//     1 - __expf(-sigma dt), t (relative to the near plane's rays_t) summed
+//     from deltas[1], the T < T_thresh break.
+// The loop restarts each ray's march from the composited t (rays_t = near +
+// the f32 sum of deltas[1]) at iteration boundaries, and the boundaries come
+// from a global schedule (n_step = clamp(N / n_alive, 1, 8)).  This kernel
+// restarts after every sample, i.e. it is the loop with n_step = 1, which is
+// the reference's own schedule while more than half the rays are alive, and
+// is bit-identical to it (same samples, same compositing, and the loop's
+// max_steps iterations become at most max_steps samples per ray).  Under a
+// larger n_step the loop continues from the march's own t inside an
+// iteration; the two agree except where near + sum(t_i - last_t) != t in
+// f32 (a rounding of the difference after an empty-space jump), a 1-ulp
+// shift of the following samples (tests: bit-exact vs n_step = 1, 1e-4 vs
+// the default schedule).
+//
+// MI355X design:
+//  * one lane owns one ray; a wave runs 64 rays.  Each iteration every lane
+//    marches to its next occupied sample, then the wave evaluates the 64
+//    samples as four 16-sample MFMA tiles (lane group h gathers levels
+//    h, h+4, h+8, h+12 of the tile's sample, 32 table loads in flight per
+//    lane), the outputs are shuffled back to the ray's lane and composited.
+//  * persistent waves + one global atomic per refill: a lane whose ray
+//    terminated takes the next ray id (ballot / mbcnt), so there is no host
+//    loop, no compaction, no per-iteration sync, and the xyzs / dirs /
+//    deltas / sigma / rgb intermediates never touch HBM.  Every ray id
+//    taken is finished before its wave exits, so each output is written
+//    exactly once (no zero-fill).
+#include "march_common.h"
+#include "field_common.h"
+
+namespace dfhip {
+namespace rd {
+
+constexpr int kWaves = 4;
+
+__global__ __launch_bounds__(256) void k_render_infer(
+    uint32_t N, const float *__restrict__ rays_o, const float *__restrict__ rays_d,
+    const float *__restrict__ nears, const float *__restrict__ fars,
+    const float *__restrict__ noises, rm::MarchConsts k, const uint8_t *__restrict__ grid,
+    uint32_t max_samples, float T_thresh, const half_t *__restrict__ table,
+    const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
+    const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+    const float *b3, float *__restrict__ weights_sum, float *__restrict__ depth,
+    float *__restrict__ image, uint32_t *__restrict__ work) {
+    __shared__ fm::Weights W;
+    fm::load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    const bool align = align_corners != 0;
+    const float inv_extent = 1.0f / (2.0f * k.bound);
+
+    int ray = -1;
+    bool exhausted = false;
+    rm::Ray r{};
+    float t = 0.0f, far = 0.0f, last_t = 0.0f, tc = 0.0f;
+    float ws = 0.0f, dp = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    uint32_t taken = 0;
+    uint32_t samples = 0;  // per-lane count of evaluated samples (stats)
+
+    while (true) {
+        // ---- refill lanes whose ray finished from the global queue
+        const bool need = ray < 0 && !exhausted;
+        const uint64_t needm = __ballot(need);
+        if (needm) {
+            const int leader = __ffsll((unsigned long long)needm) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&work[0], (uint32_t)__popcll(needm));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+                const uint32_t id = base + rank;
+                if (id < N) {
+                    ray = (int)id;
+                    r = rm::load_ray(rays_o + 3 * (size_t)id, rays_d + 3 * (size_t)id);
+                    // rays_t starts at the near plane (renderer.py:509); the
+                    // perturbation applies to the first march only (:522)
+                    tc = nears[id];
+                    far = fars[id];
+                    t = tc;
+                    if (noises)
+                        t = fmaf(rm::clampf(t * k.dt_gamma, k.dt_min, k.dt_max), noises[id], t);
+                    last_t = t;
+                    ws = dp = cr = cg = cb = 0.0f;
+                    taken = 0;
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (__ballot(ray >= 0) == 0) break;
+
+        // ---- march: each live lane to its next occupied sample
+        float xyz[3] = {0.0f, 0.0f, 0.0f}, sdt = 0.0f, sdl = 0.0f;
+        bool valid = false;
+        if (ray >= 0) valid = rm::march_next(k, r, grid, t, last_t, far, xyz, sdt, sdl);
+
+        if (__ballot(valid)) {
+            // ---- field: four 16-sample tiles; tile j holds lanes 16 j .. 16 j + 15
+            float x01[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) x01[d] = valid ? (xyz[d] + k.bound) * inv_extent : -1.0f;
+            float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int src = 16 * j + c;
+                float xs[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) xs[d] = __shfl(x01[d], src);
+                const fm::half8 xb = fm::grid_features(table, offsets, lv, gridtype, align, xs, h);
+                fm::Fwd F;
+                fm::forward_tile(W, xb, c, h, F);
+                // outputs of sample c sit on lane c (rows 0..3 of lane group 0)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float v = __shfl(F.o[q], lane & 15);
+                    if ((lane >> 4) == j) o[q] = v;
+                }
+            }
+            if (valid) {
+                // k_field_fwd_fused's heads: f16-rounded MLP outputs, f32 density
+                const float sigma = expf((float)(half_t)o[0] + fm::gaussian(xyz));
+                float rgb[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const float v = (float)(half_t)o[q + 1];
+                    rgb[q] = (float)(half_t)(1.0f / (1.0f + expf(-v)));
+                }
+                // k_composite_infer (raymarching.cu:848-873)
+                const float alpha = 1.0f - __expf(-sigma * sdt);
+                const float T = 1.0f - ws;
+                const float w = alpha * T;
+                ws += w;
+                tc += sdl;
+                dp = fmaf(w, tc, dp);
+                cr = fmaf(w, rgb[0], cr);
+                cg = fmaf(w, rgb[1], cg);
+                cb = fmaf(w, rgb[2], cb);
+                ++taken;
+                ++samples;
+                if (T < T_thresh || taken >= max_samples) valid = false;  // terminated
+                // the next march restarts from rays_t (raymarching.cu:739-748)
+                t = tc;
+                last_t = tc;
+            }
+        }
+        // ---- retire: rays that left the grid (no sample) or terminated
+        if (ray >= 0 && !valid) {
+            weights_sum[ray] = ws;
+            depth[ray] = dp;
+            image[3 * (size_t)ray] = cr;
+            image[3 * (size_t)ray + 1] = cg;
+            image[3 * (size_t)ray + 2] = cb;
+            ray = -1;
+        }
+    }
+    // stats: evaluated samples (64-bit, low / high words)
+    uint32_t tot = (uint32_t)samples;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
+    if (lane == 0 && tot) {
+        const uint32_t old = atomicAdd(&work[1], tot);
+        if (old + tot < old) atomicAdd(&work[2], 1u);
+    }
+}
+
+}  // namespace rd
+}  // namespace dfhip
+
+using namespace dfhip;
+
+extern "C" int dfhip_render_rays_infer(
+    uint32_t N, const float *rays_o, const float *rays_d, const float *nears, const float *fars,
+    const float *noises, float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
+    uint32_t H, const uint8_t *grid, float T_thresh, const void *table, const int32_t *offsets,
+    uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
+    const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+    const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
+    dfhip_stream_t stream) {
+    const char *name = "render_rays_infer";
+    if (L != 16) {
+        set_error("%s: the fused renderer supports the reference's 16-level x 2-channel 3-D "
+                  "grid (got L=%u)", name, L);
+        return DFHIP_EINVAL;
+    }
+    if (C < 1 || C > 16 || H < 2 || H > 1024 || max_steps == 0 || !(bound > 0.0f)) {
+        set_error("%s: invalid C=%u H=%u max_steps=%u bound=%g", name, C, H, max_steps,
+                  (double)bound);
+        return DFHIP_EINVAL;
+    }
+    if (!rays_o || !rays_d || !nears || !fars || !grid || !table || !offsets || !w1 || !b1 ||
+        !w2 || !b2 || !w3 || !b3 || !weights_sum || !depth || !image || !work) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(work, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return check_launch(name);
+    if (N == 0) return DFHIP_OK;
+    const rm::MarchConsts k = rm::make_consts(bound, dt_gamma, max_steps, C, H);
+    const ge::Levels lv = ge::make_levels(L, S, base_res);
+    // persistent waves: as many workgroups as are co-resident on the chip
+    // (occupancy query, once); the queue balances the rays among them
+    static uint32_t resident = 0;
+    if (resident == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rd::k_render_infer,
+                                                         64 * rd::kWaves, 0) != hipSuccess)
+            per_cu = cus = 0;
+        resident = (uint32_t)((per_cu > 0 ? per_cu : 2) * (cus > 0 ? cus : 256));
+    }
+    const uint32_t want = ceil_div(N, 64u * rd::kWaves);
+    const uint32_t blocks = want < resident ? want : resident;
+    rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
+        N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
+        (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
+        weights_sum, depth, image, work);
+    return check_launch(name);
+}

@@ -122,6 +122,13 @@ class NeRFNetwork(NeRFRenderer):
         sigma, albedo = self.common_forward(x)
         return {"sigma": sigma, "albedo": albedo}
 
+    def native_infer_field(self, shading, x):
+        if shading != "albedo" or not _FUSED_FIELD:
+            return None
+        if not _field.eligible(self.encoder, self.sigma_net.net, x):
+            return None
+        return self.encoder, list(self.sigma_net.net)
+
     def native_background_layers(self):
         from freqencoder import FreqEncoder
         if self.bg_radius <= 0 or not isinstance(self.encoder_bg, FreqEncoder):

@@ -78,6 +78,9 @@ class NeRFRenderer(nn.Module):
         self.native_grid_update = True
         # native background mix / depth / mask (nerf/head.py; False: torch ops)
         self.native_head = True
+        # fused persistent inference render when the field allows it (False: the
+        # reference's march / field / composite host loop)
+        self.native_infer = True
         # generator of the density-grid jitter (None: torch's default)
         self.grid_generator = None
 
@@ -264,9 +267,15 @@ class NeRFRenderer(nn.Module):
                 jitter = self.normal(xyzs + torch.randn_like(xyzs) * 1e-2)
                 results["loss_smooth"] = (normals - jitter).abs().mean()
         else:
-            weights_sum, depth, image = self._infer_loop(rays_o, rays_d, nears, fars, light_d,
-                                                         ambient_ratio, shading, perturb,
-                                                         dt_gamma, max_steps, T_thresh)
+            field = self.native_infer_field(shading, rays_o) if self.native_infer else None
+            if field is not None:
+                weights_sum, depth, image = self._infer_fused(rays_o, rays_d, nears, fars, field,
+                                                              perturb, dt_gamma, max_steps,
+                                                              T_thresh)
+            else:
+                weights_sum, depth, image = self._infer_loop(rays_o, rays_d, nears, fars, light_d,
+                                                             ambient_ratio, shading, perturb,
+                                                             dt_gamma, max_steps, T_thresh)
 
         results.update(self._compose(rays_d, nears, fars, weights_sum, depth, image, bg_color,
                                      prefix))
@@ -301,9 +310,50 @@ class NeRFRenderer(nn.Module):
         evaluate it (frequency-encoded 39 -> 64 -> 3), else None (subclass hook)."""
         return None
 
+    def native_infer_field(self, shading, x):
+        """(encoder, [Linear] * 3) when the fused inference renderer can evaluate
+        this field for `shading`, else None (subclass hook)."""
+        return None
+
+    def _infer_fused(self, rays_o, rays_d, nears, fars, field, perturb, dt_gamma, max_steps,
+                     T_thresh):
+        """The inference loop below as ONE persistent launch (csrc/render.hip):
+        march, grid field and compositing per ray with a device work queue, no
+        host sync and no per-sample intermediates in HBM."""
+        import _fieldmlp
+        import numpy as np
+        encoder, layers = field
+        N = rays_o.shape[0]
+        dev = rays_o.device
+        weights_sum = torch.empty(N, dtype=torch.float32, device=dev)
+        depth = torch.empty(N, dtype=torch.float32, device=dev)
+        image = torch.empty(N, 3, dtype=torch.float32, device=dev)
+        work = torch.empty(4, dtype=torch.int32, device=dev)
+        noises = torch.rand(N, device=dev) if perturb else None
+        weights = []
+        for lin in layers:
+            weights += [lin.weight.detach().float().contiguous(),
+                        lin.bias.detach().float().contiguous()]
+        table = encoder.embeddings.detach().to(torch.half).contiguous()
+        import _dfhip
+        # algorithmic bytes of the launch: rays in (o, d, near, far), outputs,
+        # the f16 table and the bitfield once
+        nbytes = N * (32 + 20) + table.numel() * 2 + self.density_bitfield.numel()
+        with _dfhip.timed("render_rays_infer", nbytes):
+            _fieldmlp.render_rays_infer(
+                rays_o.float().contiguous(), rays_d.float().contiguous(),
+                nears.float().contiguous(), fars.float().contiguous(), noises, self.bound,
+                dt_gamma, max_steps, self.cascade, self.grid_size, self.density_bitfield,
+                T_thresh, table, encoder.offsets, float(np.log2(encoder.per_level_scale)),
+                int(encoder.base_resolution), encoder.gridtype_id, bool(encoder.align_corners),
+                weights, weights_sum, depth, image, work)
+        self.last_infer_work = work  # work[1] (+ 2^32 work[2]) = samples evaluated
+        return weights_sum, depth, image
+
     def _infer_loop(self, rays_o, rays_d, nears, fars, light_d, ambient_ratio, shading, perturb,
-                    dt_gamma, max_steps, T_thresh):
-        """Alive-ray compaction loop of the inference render (renderer.py:496-532)."""
+                    dt_gamma, max_steps, T_thresh, n_step_max=8):
+        """Alive-ray compaction loop of the inference render (renderer.py:496-532).
+        n_step_max: the schedule's cap (8 in the reference; tests use 1)."""
         N = rays_o.shape[0]
         device = rays_o.device
         weights_sum = torch.zeros(N, dtype=torch.float32, device=device)
@@ -316,7 +366,7 @@ class NeRFRenderer(nn.Module):
             n_alive = rays_alive.shape[0]
             if n_alive <= 0:
                 break
-            n_step = max(min(N // n_alive, 8), 1)
+            n_step = max(min(N // n_alive, n_step_max), 1)
             xyzs, dirs, deltas = raymarching.march_rays(
                 n_alive, n_step, rays_alive, rays_t, rays_o, rays_d, self.bound,
                 self.density_bitfield, self.cascade, self.grid_size, nears, fars, 128,

@@ -1,0 +1,122 @@
+"""Fused persistent inference renderer (csrc/render.hip)
+against the reference-structured inference loop of run_cuda
+(renderer.py:496-532: march_rays -> grid field -> composite_rays, whose
+kernels test_gpu_raymarching pins to the CPU oracle).
+
+The fused kernel restarts each ray's march from the composited t after every
+sample, i.e. it is the loop with n_step = 1: against that schedule it must be
+bit-identical; against the reference's default schedule (n_step up to 8) it
+agrees to 1e-4 (see csrc/render.hip for why the two schedules differ)."""
+import numpy as np
+import pytest
+import torch
+
+from scenes import camera_rays, sphere_bitfield
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(gpu, seed=0, scale=0.5, occupancy="sphere"):
+    import main
+    from nerf.network_grid import NeRFNetwork
+    torch.manual_seed(seed)
+    opt = main.parse_opt(["--text", "render", "-O"])
+    m = NeRFNetwork(opt).to(gpu)
+    with torch.no_grad():
+        m.encoder.embeddings.uniform_(-scale, scale)
+    if occupancy == "sphere":
+        m.density_bitfield.copy_(torch.from_numpy(sphere_bitfield(0.6, 0.003, seed)).to(gpu))
+    else:
+        with torch.autocast("cuda", dtype=torch.float16):
+            m.update_extra_state()
+    m.eval()
+    return m
+
+
+def _rays(gpu, h, w, seed, radius=1.6):
+    o, d = camera_rays(h, w, seed, radius=radius)
+    return torch.from_numpy(o).to(gpu), torch.from_numpy(d).to(gpu)
+
+
+def _both(m, rays_o, rays_d, n_step_max, perturb=False, T_thresh=1e-4, max_steps=512):
+    import raymarching
+    nears, fars = raymarching.near_far_from_aabb(rays_o, rays_d, m.aabb_infer)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        field = m.native_infer_field("albedo", rays_o)
+        assert field is not None
+        torch.manual_seed(7)
+        fused = m._infer_fused(rays_o, rays_d, nears, fars, field, perturb, 0.0, max_steps,
+                               T_thresh)
+        torch.manual_seed(7)
+        loop = m._infer_loop(rays_o, rays_d, nears, fars, None, 1.0, "albedo", perturb, 0.0,
+                             max_steps, T_thresh, n_step_max=n_step_max)
+    torch.cuda.synchronize()
+    return [t.cpu().numpy() for t in fused], [t.cpu().numpy() for t in loop]
+
+
+@pytest.mark.parametrize("occupancy,scale,seed", [("sphere", 0.5, 0), ("sphere", 2.0, 1),
+                                                  ("grid", 1.0, 2)])
+def test_fused_infer_bit_exact_vs_nstep1_loop(gpu, occupancy, scale, seed):
+    m = _model(gpu, seed, scale, occupancy)
+    rays_o, rays_d = _rays(gpu, 48, 40, seed)
+    (fw, fd, fi), (lw, ld, li) = _both(m, rays_o, rays_d, n_step_max=1)
+    assert (lw > 0).sum() > 100  # the scene is not empty
+    np.testing.assert_array_equal(fw, lw)
+    np.testing.assert_array_equal(fd, ld)
+    np.testing.assert_array_equal(fi, li)
+
+
+def test_fused_infer_perturbed_bit_exact(gpu):
+    """perturb=True: the first march step of each ray moves by noise * dt_min
+    with the same torch.rand draw the loop makes (renderer.py:522)."""
+    m = _model(gpu, 3, 1.0, "sphere")
+    rays_o, rays_d = _rays(gpu, 32, 32, 3)
+    (fw, fd, fi), (lw, ld, li) = _both(m, rays_o, rays_d, n_step_max=1, perturb=True)
+    np.testing.assert_array_equal(fw, lw)
+    np.testing.assert_array_equal(fi, li)
+    np.testing.assert_array_equal(fd, ld)
+
+
+def test_fused_infer_vs_default_schedule(gpu):
+    m = _model(gpu, 4, 1.0, "sphere")
+    rays_o, rays_d = _rays(gpu, 64, 64, 4)
+    (fw, fd, fi), (lw, ld, li) = _both(m, rays_o, rays_d, n_step_max=8)
+    # the default schedule continues from the march's own t inside an iteration
+    # (1-ulp shifts where the f32 delta sum rounds): 1e-4 per ray
+    np.testing.assert_allclose(fw, lw, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(fi, li, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(fd, ld, rtol=1e-4, atol=1e-3)
+
+
+def test_fused_infer_edge_cases(gpu):
+    """Missing rays (near = far = FLT_MAX), an empty bitfield, an early
+    T_thresh and a tiny max_steps: every ray is written exactly once."""
+    m = _model(gpu, 5, 2.0, "sphere")
+    rays_o, rays_d = _rays(gpu, 16, 16, 5, radius=3.0)  # most rays miss the cube
+    for T_thresh, max_steps in ((1e-4, 512), (0.5, 512), (1e-4, 3)):
+        (fw, fd, fi), (lw, ld, li) = _both(m, rays_o, rays_d, 1, T_thresh=T_thresh,
+                                           max_steps=max_steps)
+        np.testing.assert_array_equal(fw, lw)
+        np.testing.assert_array_equal(fi, li)
+    m.density_bitfield.zero_()
+    (fw, fd, fi), _ = _both(m, rays_o, rays_d, 1)
+    assert not fw.any() and not fi.any() and not fd.any()
+
+
+def test_fused_infer_sample_count_and_render_api(gpu):
+    """run_cuda's eval branch uses the fused kernel (renderer.render, the
+    reference API) and reports the number of samples it evaluated."""
+    import raymarching
+    m = _model(gpu, 6, 1.0, "sphere")
+    rays_o, rays_d = _rays(gpu, 24, 24, 6)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        out = m.render(rays_o[None], rays_d[None], staged=True, perturb=False, max_steps=512)
+        work = m.last_infer_work.cpu().numpy().view(np.uint32)
+        m.native_infer = False
+        ref = m.render(rays_o[None], rays_d[None], staged=True, perturb=False, max_steps=512)
+    for k in ("image", "depth", "weights_sum"):
+        np.testing.assert_allclose(out[k].float().cpu().numpy(), ref[k].float().cpu().numpy(),
+                                   rtol=1e-4, atol=1e-4)
+    # sample count = the loop's n_step = 1 march counts (each sample evaluated once)
+    nears, fars = raymarching.near_far_from_aabb(rays_o, rays_d, m.aabb_infer)
+    assert work[1] > 0 and work[2] == 0
