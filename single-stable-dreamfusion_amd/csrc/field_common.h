@@ -155,47 +155,111 @@ __device__ __forceinline__ half8 load_x(const half_t *enc, uint32_t sample, uint
     return *reinterpret_cast<const half8 *>(enc + (size_t)sample * kIn + 8 * h);
 }
 
+// Per-level constants of the 16-level 3-D grid, staged once per workgroup
+// in LDS (the level a lane reads depends on its lane group, so they cannot
+// live in scalar registers; reading them from offsets[] / the kernarg Levels
+// per tile put dependent global loads in front of every gather).
+// Row of corner (p0, p1, p2) = base + wrap(p0 + p1 m1 + p2 m2) with m1 =
+// stride of y (0 when the tiled index stops before y), m2 = stride of z (0
+// for the z-dropped levels 9-15, gridencoder.cu:56-63); u32 arithmetic as the
+// reference's.  wrap: & wmask (power-of-two level, or all-ones for a dense
+// level whose index never reaches hsize), or % hsize (flag 1), or the
+// spatial hash (flag 2).
+struct LevelK {
+    uint32_t base, hsize, wmask, m1, m2, flags;
+    float scale;
+};
+constexpr int kLevels = 16;
+
+__device__ __forceinline__ void stage_levels(LevelK *lk, const int32_t *__restrict__ offsets,
+                                             const ge::Levels &lv, uint32_t gridtype, bool align) {
+    for (int l = threadIdx.x; l < kLevels; l += blockDim.x) {
+        const ge::LevelCtx c = ge::level_ctx<3>(offsets, lv, l, gridtype, align);
+        LevelK k;
+        k.base = c.base;
+        k.hsize = c.hsize;
+        k.scale = c.scale;
+        const uint32_t lead = c.hashed ? 3u : c.used;
+        k.m1 = lead > 1 ? c.smul : 0u;
+        k.m2 = lead > 2 ? c.smul * c.smul : 0u;
+        uint64_t span = 1;  // largest tiled index + 1
+        for (uint32_t d = 0; d < c.used; ++d) span *= c.smul;
+        k.flags = 0;
+        if (c.hashed) {
+            k.flags = 2u;
+            k.wmask = c.pow2 ? c.hsize - 1u : 0xFFFFFFFFu;
+            if (!c.pow2) k.flags |= 1u;
+        } else if (c.pow2) {
+            k.wmask = c.hsize - 1u;
+        } else if (span <= c.hsize) {
+            k.wmask = 0xFFFFFFFFu;
+        } else {
+            k.wmask = 0xFFFFFFFFu;
+            k.flags = 1u;
+        }
+        lk[l] = k;
+    }
+}
+
 // Grid features of one sample at levels 4(j >> 1) + h (j = 0..7, channel
 // j & 1) in the permuted order above: exactly k_grid_fwd<half, 3, 2>'s
-// arithmetic (gridencoder.cu:75-178: half accumulators rounded per corner),
-// with the trailing-dim corners of z-dropped tiled levels gathered once.
+// arithmetic (gridencoder.cu:75-178: half accumulators rounded per corner, in
+// corner order).  All 32 row loads of the four levels are issued before the
+// first accumulation (the corners of z-dropped tiled levels load the row of
+// their z = 0 twin, an L1 hit), so a lane has 32 gathers in flight.
 __device__ __forceinline__ half8 grid_features(const half_t *__restrict__ table,
-                                               const int32_t *__restrict__ offsets,
-                                               const ge::Levels &lv, uint32_t gridtype,
-                                               bool align, const float (&x)[3], int h) {
+                                               const LevelK *lk, bool align,
+                                               const float (&x)[3], int h) {
     half8 out{};
     if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
         return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
+    const uint32_t *tab = reinterpret_cast<const uint32_t *>(table);
+    float frac[4][3];
+    uint32_t row[4][8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t l = 4 * q + h;
-        const ge::LevelCtx c = ge::level_ctx<3>(offsets, lv, l, gridtype, align);
-        const uint32_t *tab = reinterpret_cast<const uint32_t *>(table + (size_t)c.base * 2);
-        float frac[3];
+        const LevelK k = lk[4 * q + h];
         uint32_t cell[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            const float p = fmaf(x[d], c.scale, align ? 0.0f : 0.5f);
+            const float p = fmaf(x[d], k.scale, align ? 0.0f : 0.5f);
             cell[d] = (uint32_t)floorf(p);
-            frac[d] = p - (float)cell[d];
+            frac[q][d] = p - (float)cell[d];
         }
-        const uint32_t lead = (!c.hashed) ? c.used : 3u;
-        const uint32_t lead_mask = (1u << lead) - 1u;
-        uint32_t row_bits[8];
+        if (k.flags == 0u) {
+            // tiled / dense: corner offsets {0, 1, m1, m1 + 1, m2, ...}
+            const uint32_t i0 = cell[0] + cell[1] * k.m1 + cell[2] * k.m2;
+            const uint32_t o[8] = {0u, 1u, k.m1, k.m1 + 1u, k.m2, k.m2 + 1u, k.m2 + k.m1,
+                                   k.m2 + k.m1 + 1u};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) row[q][c] = k.base + ((i0 + o[c]) & k.wmask);
+        } else {
+#pragma unroll
+            for (uint32_t c = 0; c < 8; ++c) {
+                const uint32_t px = cell[0] + (c & 1u), py = cell[1] + ((c >> 1) & 1u),
+                               pz = cell[2] + ((c >> 2) & 1u);
+                uint32_t idx = (k.flags & 2u) ? (px ^ (py * 2654435761u) ^ (pz * 805459861u))
+                                              : px + py * k.m1 + pz * k.m2;
+                idx = (k.flags & 1u) ? idx % k.hsize : (idx & k.wmask);
+                row[q][c] = k.base + idx;
+            }
+        }
+    }
+    uint32_t bits[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) bits[q][c] = tab[row[q][c]];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
         half_t a0 = (half_t)0.0f, a1 = (half_t)0.0f;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
+        for (uint32_t c = 0; c < 8; ++c) {
             float w = 1.0f;
-            uint32_t p[3];
 #pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                if (k & (1u << d)) { w *= frac[d]; p[d] = cell[d] + 1u; }
-                else { w *= 1.0f - frac[d]; p[d] = cell[d]; }
-            }
-            if ((k & ~lead_mask) == 0) row_bits[k] = tab[ge::row_index<3>(c, p)];
-            else row_bits[k] = row_bits[k & lead_mask];
+            for (int d = 0; d < 3; ++d) w *= (c & (1u << d)) ? frac[q][d] : 1.0f - frac[q][d];
             half_t v[2];
-            __builtin_memcpy(v, &row_bits[k], 4);
+            __builtin_memcpy(v, &bits[q][c], 4);
             ge::acc_corner(a0, w, v[0]);
             ge::acc_corner(a1, w, v[1]);
         }

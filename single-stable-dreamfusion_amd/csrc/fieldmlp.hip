@@ -46,10 +46,12 @@ __global__ __launch_bounds__(256) void k_field_fwd_fused(
     const float *b3, half_t *__restrict__ enc, float *__restrict__ sigma,
     rgb_t *__restrict__ rgb, uint32_t cap, const int32_t *__restrict__ m_dev) {
     __shared__ Weights W;
+    __shared__ LevelK LK[kLevels];
+    const bool align = align_corners != 0;
     load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
+    stage_levels(LK, offsets, lv, gridtype, align);
     __syncthreads();
     const uint32_t M = active_count(m_dev, cap);
-    const bool align = align_corners != 0;
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     const uint32_t tiles = ceil_div(M, 16u);
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256) void k_field_fwd_fused(
                 x[d] = xyz[(size_t)sample * 3 + d];
                 x01[d] = (x[d] + bound) / (2.0f * bound);
             }
-        const half8 xb = valid ? grid_features(table, offsets, lv, gridtype, align, x01, h)
+        const half8 xb = valid ? grid_features(table, LK, align, x01, h)
                                : half8{};
         if (enc && valid) *reinterpret_cast<half8 *>(enc + (size_t)sample * kIn + 8 * h) = xb;
         Fwd F;

@@ -48,6 +48,36 @@ namespace dfhip {
 namespace rd {
 
 constexpr int kWaves = 4;
+constexpr int kK = 4;              // samples marched ahead per ray per round
+constexpr int kSlots = 64 * kK;    // per-wave staged samples
+
+// Per-wave LDS staging of one round's samples, compacted across the wave's
+// rays (slot = exclusive scan of the per-ray counts + k).  pos holds the
+// sample position until the field has read it, then (sigma, rgb as f16).
+struct Stage {
+    float pos[kSlots * 3];
+    float dt[kSlots];
+    float tc[kSlots];  // rays_t after the sample (the depth weight's t)
+};
+
+__device__ __forceinline__ uint32_t pack_h2(half_t a, half_t b) {
+    uint16_t ua, ub;
+    __builtin_memcpy(&ua, &a, 2);
+    __builtin_memcpy(&ub, &b, 2);
+    return (uint32_t)ua | ((uint32_t)ub << 16);
+}
+__device__ __forceinline__ float lo_h(uint32_t v) {
+    const uint16_t u = (uint16_t)(v & 0xFFFFu);
+    half_t h;
+    __builtin_memcpy(&h, &u, 2);
+    return (float)h;
+}
+__device__ __forceinline__ float hi_h(uint32_t v) {
+    const uint16_t u = (uint16_t)(v >> 16);
+    half_t h;
+    __builtin_memcpy(&h, &u, 2);
+    return (float)h;
+}
 
 __global__ __launch_bounds__(256) void k_render_infer(
     uint32_t N, const float *__restrict__ rays_o, const float *__restrict__ rays_d,
@@ -59,10 +89,14 @@ __global__ __launch_bounds__(256) void k_render_infer(
     const float *b3, float *__restrict__ weights_sum, float *__restrict__ depth,
     float *__restrict__ image, uint32_t *__restrict__ work) {
     __shared__ fm::Weights W;
-    fm::load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
-    __syncthreads();
-    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    __shared__ fm::LevelK LK[fm::kLevels];
+    __shared__ Stage stages[kWaves];
     const bool align = align_corners != 0;
+    fm::load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
+    fm::stage_levels(LK, offsets, lv, gridtype, align);
+    __syncthreads();
+    Stage &S = stages[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const float inv_extent = 1.0f / (2.0f * k.bound);
 
     int ray = -1;
@@ -106,72 +140,114 @@ __global__ __launch_bounds__(256) void k_render_infer(
         }
         if (__ballot(ray >= 0) == 0) break;
 
-        // ---- march: each live lane to its next occupied sample
-        float xyz[3] = {0.0f, 0.0f, 0.0f}, sdt = 0.0f, sdl = 0.0f;
-        bool valid = false;
-        if (ray >= 0) valid = rm::march_next(k, r, grid, t, last_t, far, xyz, sdt, sdl);
-
-        if (__ballot(valid)) {
-            // ---- field: four 16-sample tiles; tile j holds lanes 16 j .. 16 j + 15
-            float x01[3];
+        // ---- march: up to kK samples per ray.  After each sample the march
+        // restarts from the composited t (rays_t, raymarching.cu:739-748):
+        // tc only depends on the deltas, so it is known before compositing.
+        uint32_t n = 0;
+        bool at_far = false;
+        float px[kK][3], pdt[kK], ptc[kK];
+        if (ray >= 0) {
+            const uint32_t budget = max_samples - taken;
 #pragma unroll
-            for (int d = 0; d < 3; ++d) x01[d] = valid ? (xyz[d] + k.bound) * inv_extent : -1.0f;
-            float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int src = 16 * j + c;
-                float xs[3];
-#pragma unroll
-                for (int d = 0; d < 3; ++d) xs[d] = __shfl(x01[d], src);
-                const fm::half8 xb = fm::grid_features(table, offsets, lv, gridtype, align, xs, h);
-                fm::Fwd F;
-                fm::forward_tile(W, xb, c, h, F);
-                // outputs of sample c sit on lane c (rows 0..3 of lane group 0)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float v = __shfl(F.o[q], lane & 15);
-                    if ((lane >> 4) == j) o[q] = v;
+            for (int q = 0; q < kK; ++q) {
+                if (n == (uint32_t)q && !at_far && (uint32_t)q < budget) {
+                    float dl;
+                    if (rm::march_next(k, r, grid, t, last_t, far, px[q], pdt[q], dl)) {
+                        tc += dl;
+                        t = tc;
+                        last_t = tc;
+                        ptc[q] = tc;
+                        n = q + 1;
+                    } else {
+                        at_far = true;
+                    }
                 }
             }
-            if (valid) {
-                // k_field_fwd_fused's heads: f16-rounded MLP outputs, f32 density
-                const float sigma = expf((float)(half_t)o[0] + fm::gaussian(xyz));
-                float rgb[3];
+        }
+        const uint32_t incl = (uint32_t)wave_inclusive_scan((int)n);
+        const uint32_t excl = incl - n;
+        const uint32_t total = __shfl(incl, 63);
+#pragma unroll
+        for (int q = 0; q < kK; ++q)
+            if ((uint32_t)q < n) {
+                const uint32_t slot = excl + q;
+                S.pos[3 * slot] = px[q][0];
+                S.pos[3 * slot + 1] = px[q][1];
+                S.pos[3 * slot + 2] = px[q][2];
+                S.dt[slot] = pdt[q];
+                S.tc[slot] = ptc[q];
+            }
+        fm::wave_lds_sync();
+
+        // ---- field over the compacted samples, 16 per MFMA tile
+        const uint32_t tiles = ceil_div(total, 16u);
+        for (uint32_t tile = 0; tile < tiles; ++tile) {
+            const uint32_t s = tile * 16 + c;
+            const bool valid = s < total;
+            float x[3] = {0.0f, 0.0f, 0.0f}, x01[3] = {-1.0f, -1.0f, -1.0f};
+            if (valid)
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    x[d] = S.pos[3 * s + d];
+                    x01[d] = (x[d] + k.bound) * inv_extent;
+                }
+            const fm::half8 xb = fm::grid_features(table, LK, align, x01, h);
+            fm::Fwd F;
+            fm::forward_tile(W, xb, c, h, F);
+            if (h == 0 && valid) {
+                // k_field_fwd_fused's heads: f16-rounded outputs, f32 density
+                const float sigma = expf((float)(half_t)F.o[0] + fm::gaussian(x));
+                half_t rgb[3];
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
-                    const float v = (float)(half_t)o[q + 1];
-                    rgb[q] = (float)(half_t)(1.0f / (1.0f + expf(-v)));
+                    const float v = (float)(half_t)F.o[q + 1];
+                    rgb[q] = (half_t)(1.0f / (1.0f + expf(-v)));
                 }
-                // k_composite_infer (raymarching.cu:848-873)
-                const float alpha = 1.0f - __expf(-sigma * sdt);
+                S.pos[3 * s] = sigma;
+                S.pos[3 * s + 1] = __uint_as_float(pack_h2(rgb[0], rgb[1]));
+                S.pos[3 * s + 2] = __uint_as_float(pack_h2(rgb[2], (half_t)0.0f));
+            }
+        }
+        fm::wave_lds_sync();
+
+        // ---- composite each ray's samples in order (k_composite_infer,
+        // raymarching.cu:848-873); retire on T < T_thresh, max_samples, or
+        // when the march left the grid
+        if (ray >= 0) {
+            bool done = at_far;
+            for (uint32_t q = 0; q < n; ++q) {
+                const uint32_t slot = excl + q;
+                const float sigma = S.pos[3 * slot];
+                const uint32_t rg = __float_as_uint(S.pos[3 * slot + 1]);
+                const uint32_t bz = __float_as_uint(S.pos[3 * slot + 2]);
+                const float alpha = 1.0f - __expf(-sigma * S.dt[slot]);
                 const float T = 1.0f - ws;
                 const float w = alpha * T;
                 ws += w;
-                tc += sdl;
-                dp = fmaf(w, tc, dp);
-                cr = fmaf(w, rgb[0], cr);
-                cg = fmaf(w, rgb[1], cg);
-                cb = fmaf(w, rgb[2], cb);
+                dp = fmaf(w, S.tc[slot], dp);
+                cr = fmaf(w, lo_h(rg), cr);
+                cg = fmaf(w, hi_h(rg), cg);
+                cb = fmaf(w, lo_h(bz), cb);
                 ++taken;
                 ++samples;
-                if (T < T_thresh || taken >= max_samples) valid = false;  // terminated
-                // the next march restarts from rays_t (raymarching.cu:739-748)
-                t = tc;
-                last_t = tc;
+                if (T < T_thresh || taken >= max_samples) {
+                    done = true;
+                    break;
+                }
+            }
+            if (done) {
+                weights_sum[ray] = ws;
+                depth[ray] = dp;
+                image[3 * (size_t)ray] = cr;
+                image[3 * (size_t)ray + 1] = cg;
+                image[3 * (size_t)ray + 2] = cb;
+                ray = -1;
             }
         }
-        // ---- retire: rays that left the grid (no sample) or terminated
-        if (ray >= 0 && !valid) {
-            weights_sum[ray] = ws;
-            depth[ray] = dp;
-            image[3 * (size_t)ray] = cr;
-            image[3 * (size_t)ray + 1] = cg;
-            image[3 * (size_t)ray + 2] = cb;
-            ray = -1;
-        }
+        fm::wave_lds_sync();
     }
-    // stats: evaluated samples (64-bit, low / high words)
-    uint32_t tot = (uint32_t)samples;
+    // stats: composited samples (64-bit, low / high words)
+    uint32_t tot = samples;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
     if (lane == 0 && tot) {
