@@ -45,7 +45,9 @@ __host__ __device__ __forceinline__ uint32_t compact3(uint32_t v) {
 // Per-launch constants of the marcher (raymarching.cu:337-346).
 struct MarchConsts {
     float bound, dt_gamma, dt_min, dt_max, rH, H3, Hf, Cf, Hm1;
+    float half_H;   // 0.5f * H (exact product when H is a power of two)
     uint32_t H;
+    uint32_t H_pow2;
 };
 
 inline MarchConsts make_consts(float bound, float dt_gamma, uint32_t max_steps,
@@ -60,13 +62,16 @@ inline MarchConsts make_consts(float bound, float dt_gamma, uint32_t max_steps,
     k.Hf = (float)H;
     k.Cf = (float)C;
     k.Hm1 = (float)(H - 1);
+    k.half_H = 0.5f * (float)H;
     k.H = H;
+    k.H_pow2 = (H >= 2 && (H & (H - 1)) == 0) ? 1u : 0u;
     return k;
 }
 
 // Cascade level of a point (raymarching.cu:42-54, max over position and dt).
 __device__ __forceinline__ int mip_level(const MarchConsts &k, float x, float y, float z,
                                          float dt) {
+    if (k.Cf == 1.0f) return 0;   // one cascade (bound <= 1): both terms clamp to 0
     int ep, ed;
     const float mx = fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z)));
     frexpf(mx, &ep);
@@ -79,9 +84,11 @@ __device__ __forceinline__ int mip_level(const MarchConsts &k, float x, float y,
 
 // Grid cell of a clamped coordinate (raymarching.cu:374-376: the product is
 // formed in double, then narrowed to float by the float clamp()).
+// For a power-of-two H the double product is u scaled by a power of two, so the
+// f32 product u * (H/2) has the same bits (no overflow at |u| <= 2).
 __device__ __forceinline__ int cell_of(const MarchConsts &k, float c, float rbound) {
     const float u = fmaf(c, rbound, 1.0f);
-    const float v = (float)(0.5 * (double)u * (double)k.H);
+    const float v = k.H_pow2 ? u * k.half_H : (float)(0.5 * (double)u * (double)k.H);
     return (int)clampf(v, 0.0f, k.Hm1);
 }
 
@@ -209,5 +216,198 @@ __device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
     return false;
 }
 
+// ---------------------------------------------------------------- wave march
+// One ray per wave64 (the train marcher, raymarching.hip).  Both branches of
+// the reference loop advance t by dt(t) = clamp(t*dt_gamma, dt_min, dt_max)
+// per step (raymarching.cu:380-398), so the t values a ray can visit form a
+// fixed sequence t_{j+1} = fl(t_j + dt(t_j)).  A window of 64 consecutive
+// candidates is evaluated at once, one per lane (position, cell, occupancy
+// bit, far-face distance), and the reference's visit order is then replayed
+// on the wave's ballots: a run of occupied candidates is taken as a block and
+// each skip jumps to the first candidate with t >= tt.  Visited samples,
+// counts and deltas are the serial loop's, bit for bit.
+
+// Lane j's candidate t_j, j steps after t_base; returns the window length L
+// (lanes >= L hold no candidate) and, when the window is arithmetic, the
+// bit pattern step `inc` (else 0).  dt_gamma == 0 (the train default) inside
+// one binade: t_base + j*dt rounds to t_base + j*inc ulps exactly, with
+// inc = rint(dt/ulp) unless dt/ulp is a tie; the window stops before the
+// binade ends.  Otherwise lane j repeats the reference's f32 additions.
+__device__ __forceinline__ int wave_window_t(const MarchConsts &k, float t_base, int lane,
+                                             float &tj, uint32_t &inc) {
+    if (k.dt_gamma == 0.0f) {
+        const uint32_t b0 = __float_as_uint(t_base);
+        const uint32_t ex = b0 >> 23;
+        if (b0 >= 0x00800000u && b0 < 0x7F800000u) {   // positive, normal, finite
+            const float dt = clampf(0.0f, k.dt_min, k.dt_max);
+            const float D = ldexpf(dt, 150 - (int)ex);   // dt in ulps of t_base
+            const float Dr = rintf(D);
+            if (D >= 0.5f && D < 8388608.0f && fabsf(D - Dr) != 0.5f) {
+                inc = (uint32_t)Dr;
+                const uint32_t room = (0x7FFFFFu - (b0 & 0x7FFFFFu)) / inc + 1u;
+                tj = __uint_as_float(b0 + (uint32_t)lane * inc);
+                return room < 64u ? (int)room : 64;
+            }
+        }
+    }
+    inc = 0;
+    float t = t_base;
+    for (int i = 0; i < lane; ++i) t += clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
+    tj = t;
+    return 64;
+}
+
+__device__ __forceinline__ float lane_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ uint64_t lanes_below(int j) {
+    return j >= 64 ? ~0ull : ((1ull << j) - 1ull);
+}
+__device__ __forceinline__ int top_lane(uint64_t m) { return 63 - __clzll((long long)m); }
+
+// March one ray with the whole wave (every lane passes the same ray; call from
+// wave-uniform control flow).  Calls emit(i, x, y, z, dt, dl) on each lane
+// holding the ray's i-th occupied sample (i < limit) and returns the sample
+// count: the serial march()'s samples and return value, bit for bit.
+//
+// Per window each lane j gets its successor in the reference's visit order:
+// j+1 if occupied, else the first lane with t >= tt_j (64: beyond the
+// window).  The lanes actually visited are the successor chain from the start
+// lane, found with binary lifting (lane m computes the m-th chain node in six
+// shuffle rounds) instead of a serial walk over the skips.
+template <typename Emit>
+__device__ __forceinline__ uint32_t march_wave(const MarchConsts &k, const Ray &r,
+                                               const uint8_t *__restrict__ grid, float t0,
+                                               float far, uint32_t limit, Emit emit) {
+    __shared__ uint8_t s_vis[1024];   // one 64-lane flag row per wave (<= 16 waves)
+    const int lane = (int)(threadIdx.x & 63);
+    uint8_t *vis = s_vis + (threadIdx.x & ~63u);
+    uint32_t count = 0;
+    float last_t = t0;          // t after the previous sample (deltas[1])
+    float t_base = t0;          // candidate 0 of the window
+    float pend = -INFINITY;     // a skip in flight: resume at the first t >= pend
+    if (limit == 0 || !(t0 < far)) return 0;
+    for (;;) {
+        float tj;
+        uint32_t inc;
+        const int L = wave_window_t(k, t_base, lane, tj, inc);
+        const bool valid = lane < L && tj < far;
+        const uint64_t vmask = __ballot(valid);
+        const int Lf = __popcll(vmask);   // t is increasing: a lane prefix
+
+        const float dt = clampf(tj * k.dt_gamma, k.dt_min, k.dt_max);
+        const float x = clampf(fmaf(tj, r.dx, r.ox), -k.bound, k.bound);
+        const float y = clampf(fmaf(tj, r.dy, r.oy), -k.bound, k.bound);
+        const float z = clampf(fmaf(tj, r.dz, r.oz), -k.bound, k.bound);
+        const int level = mip_level(k, x, y, z, dt);
+        const float mip_bound = fminf(scalbnf(1.0f, level), k.bound);
+        const float rbound = 1.0f / mip_bound;
+        const int nx = cell_of(k, x, rbound);
+        const int ny = cell_of(k, y, rbound);
+        const int nz = cell_of(k, z, rbound);
+        bool occ = false;
+        if (valid) {
+            const uint32_t idx =
+                (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
+            occ = (grid[idx >> 3] >> (idx & 7)) & 1;
+        }
+        const uint64_t omask = __ballot(occ);
+        const float tx = face_dist(k, nx, r.dx, r.rdx, x, mip_bound);
+        const float ty = face_dist(k, ny, r.dy, r.rdy, y, mip_bound);
+        const float tz = face_dist(k, nz, r.dz, r.rdz, z, mip_bound);
+        const float tt = tj + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+
+        // successor of each lane (64 = beyond the valid lanes)
+        int nxt;
+        if (occ) {
+            nxt = lane + 1;
+        } else if (inc != 0) {
+            // t_i >= tt  <=>  bits(t_i) >= bits(tt) for positive floats
+            const uint32_t b0 = __float_as_uint(t_base), bt = __float_as_uint(tt);
+            const uint32_t need = bt > b0 ? (bt - b0 + inc - 1u) / inc : 0u;
+            nxt = (int)min(max(need, (uint32_t)lane + 1u), 64u);
+        } else {
+            int lo = lane + 1, hi = 64;   // first lane in [lo, hi) with t >= tt
+#pragma unroll
+            for (int it = 0; it < 7; ++it) {
+                const int mid = (lo + hi) >> 1;
+                const float tm = __shfl(tj, mid & 63, 64);
+                const bool ge = tm >= tt;
+                if (lo < hi) {
+                    if (ge) hi = mid;
+                    else lo = mid + 1;
+                }
+            }
+            nxt = lo;
+        }
+        if (nxt >= Lf) nxt = 64;
+
+        // start lane of the chain
+        int s0;
+        if (pend == -INFINITY) {
+            s0 = Lf > 0 ? 0 : 64;
+        } else {
+            const uint64_t m = __ballot(valid && tj >= pend);
+            s0 = m ? __ffsll((long long)m) - 1 : 64;
+        }
+
+        uint64_t V = 0;   // visited lanes
+        if (s0 < 64) {
+            // P[b] = successor^(2^b); lane m follows the chain m steps from s0
+            int P[6];
+            P[0] = nxt;
+#pragma unroll
+            for (int b = 1; b < 6; ++b) {
+                const int q = __shfl(P[b - 1], P[b - 1] & 63, 64);
+                P[b] = P[b - 1] >= 64 ? 64 : q;
+            }
+            int node = s0;
+#pragma unroll
+            for (int b = 0; b < 6; ++b) {
+                const int q = __shfl(P[b], node & 63, 64);
+                if ((lane >> b) & 1) node = node >= 64 ? 64 : q;
+            }
+            vis[lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            if (node < 64) vis[node] = 1;
+            __builtin_amdgcn_wave_barrier();
+            V = __ballot(vis[lane] != 0);
+        }
+
+        bool done;
+        if (V) {
+            const int u = top_lane(V);
+            const float tt_u = lane_f(tt, u);
+            done = Lf < L;
+            if (!done) pend = ((omask >> u) & 1ull) ? -INFINITY : tt_u;
+        } else {
+            done = Lf < L;   // pend (if any) carries to the next window
+        }
+
+        uint64_t E = V & omask;   // emitted, in visit (= lane) order
+        const uint32_t room = limit - count;
+        if ((uint32_t)__popcll(E) >= room) {
+            for (uint32_t i = (uint32_t)__popcll(E); i > room; --i) E &= ~(1ull << top_lane(E));
+            done = true;
+        }
+        if (E) {
+            const float tn = tj + dt;   // t after taking this sample
+            const uint64_t below = E & lanes_below(lane);
+            const int prev = below ? top_lane(below) : lane;
+            const float tprev = __shfl(tn, prev, 64);
+            if ((E >> lane) & 1ull) {
+                emit(count + (uint32_t)__popcll(below), x, y, z, dt,
+                     tn - (below ? tprev : last_t));
+            }
+            last_t = lane_f(tn, top_lane(E));
+            count += (uint32_t)__popcll(E);
+        }
+        if (done) break;
+        // candidate L = candidate L-1 plus one reference step
+        const float tl = lane_f(tj, L - 1);
+        t_base = tl + clampf(tl * k.dt_gamma, k.dt_min, k.dt_max);
+    }
+    return count;
+}
 }  // namespace rm
 }  // namespace dfhip

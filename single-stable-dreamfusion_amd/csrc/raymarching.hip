@@ -8,14 +8,17 @@
 // sample contents bit-exact between the two.
 //
 // MI355X design notes:
-//  * march_rays_train is deterministic: a count pass (one wave per 64 rays,
-//    wave-reduced block totals, integer atomics only for the API counter), then
-//    an emit pass that derives each ray's offset from the block totals plus a
-//    wave64 inclusive scan.  Samples land in ray order, contiguous per ray, so
-//    compositing and the encoders read each ray's samples as one run.
+//  * march_rays_train marches one ray per wave64: 64 consecutive candidate
+//    steps are tested at once and the reference's visit order is replayed on
+//    the wave's ballots (march_wave, march_common.h), so a ray costs a few
+//    bitfield round trips instead of one per step.  It is deterministic: a
+//    count pass (block totals, integer atomics only for the API counter), then
+//    an emit pass that derives each ray's offset from the block totals.
+//    Samples land in ray order, contiguous per ray, so compositing and the
+//    encoders read each ray's samples as one run.
 //  * No N*max_steps zero-fill: the emit pass zeroes only the align tail.
-//  * One wave per workgroup for the per-ray kernels: 16k rays = 256 workgroups
-//    = one per CU, instead of 64 CUs with 256-thread blocks.
+//  * One wave per workgroup for the per-ray compositing kernels: 16k rays =
+//    256 workgroups = one per CU, instead of 64 CUs with 256-thread blocks.
 #include "march_common.h"
 
 namespace dfhip {
@@ -138,31 +141,44 @@ __global__ __launch_bounds__(256) void k_packbits_f32v(const float *__restrict__
 
 // ------------------------------------------------------------------ training march
 
+// Rays per workgroup of the train marcher: one wave per ray, 8 waves.  The
+// count pass leaves one total per workgroup in block_sums; the emit pass
+// derives a ray's offset from the preceding totals plus the block's counts.
+constexpr uint32_t kMarchRaysPerBlock = 8;
+
 // Pass 1 (raymarching.cu:341-400): count occupied samples per ray.
 template <typename scalar_t>
-__global__ __launch_bounds__(64) void k_march_train_count(
+__global__ __launch_bounds__(64 * kMarchRaysPerBlock) void k_march_train_count(
     const scalar_t *__restrict__ rays_o, const scalar_t *__restrict__ rays_d,
     const uint8_t *__restrict__ grid, MarchConsts k, uint32_t max_steps, uint32_t N,
     const scalar_t *__restrict__ nears, const scalar_t *__restrict__ fars,
     int32_t *rays, int32_t *counter, const scalar_t *__restrict__ noises,
     int32_t *block_sums) {
-    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    __shared__ int s_cnt[kMarchRaysPerBlock];
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t n = blockIdx.x * kMarchRaysPerBlock + w;
     int cnt = 0;
     if (n < N) {
         const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
         const float near = to_f(nears[n]), far = to_f(fars[n]);
         const float t0 = fmaf(clampf(near * k.dt_gamma, k.dt_min, k.dt_max),
                               to_f(noises[n]), near);
-        cnt = (int)march<false, scalar_t>(k, r, grid, t0, far, max_steps, nullptr,
-                                          nullptr, nullptr, nullptr);
-        rays[3 * n + 0] = (int32_t)n;
-        rays[3 * n + 2] = cnt;
+        cnt = (int)march_wave(k, r, grid, t0, far, max_steps,
+                              [](uint32_t, float, float, float, float, float) {});
+        if ((threadIdx.x & 63) == 0) {
+            rays[3 * n + 0] = (int32_t)n;
+            rays[3 * n + 2] = cnt;
+        }
     }
-    const int tot = wave_reduce_add(cnt);
+    if ((threadIdx.x & 63) == 0) s_cnt[w] = cnt;
+    __syncthreads();
     if (threadIdx.x == 0) {
+        int tot = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kMarchRaysPerBlock; ++i) tot += s_cnt[i];
         block_sums[blockIdx.x] = tot;
         atomicAdd(counter, tot);
-        atomicAdd(counter + 1, (int)min(64u, N - blockIdx.x * 64));
+        atomicAdd(counter + 1, (int)min(kMarchRaysPerBlock, N - blockIdx.x * kMarchRaysPerBlock));
     }
 }
 
@@ -178,33 +194,60 @@ __device__ __forceinline__ void zero_rows(scalar_t *xyzs, scalar_t *dirs, scalar
     }
 }
 
-// Pass 2 (raymarching.cu:405-479): offsets = block prefix + wave scan, then
-// re-march and write.  Rays whose range would cross M are not written
-// (raymarching.cu:416).
+// Pass 2 (raymarching.cu:405-479): offset = preceding block totals + the
+// counts of the block's earlier rays; then the wave re-marches its ray and
+// each lane writes the samples it holds (consecutive rows across the wave).
+// Rays whose range would cross M are not written (raymarching.cu:416).
 template <typename scalar_t>
-__global__ __launch_bounds__(64) void k_march_train_emit(
+__global__ __launch_bounds__(64 * kMarchRaysPerBlock) void k_march_train_emit(
     const scalar_t *__restrict__ rays_o, const scalar_t *__restrict__ rays_d,
     const uint8_t *__restrict__ grid, MarchConsts k, uint32_t N, uint32_t M,
     const scalar_t *__restrict__ nears, const scalar_t *__restrict__ fars,
     scalar_t *xyzs, scalar_t *dirs, scalar_t *deltas, int32_t *rays,
     const scalar_t *__restrict__ noises, const int32_t *__restrict__ block_sums,
     int zero_tail) {
-    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    __shared__ int s_part[kMarchRaysPerBlock];
+    __shared__ int s_cnt[kMarchRaysPerBlock];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t n = blockIdx.x * kMarchRaysPerBlock + w;
     int part = 0;
-    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 64) part += block_sums[i];
-    const int prefix = wave_reduce_add(part);
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += blockDim.x) part += block_sums[i];
+    part = wave_reduce_add(part);
     const int cnt = (n < N) ? rays[3 * n + 2] : 0;
-    const int incl = wave_inclusive_scan(cnt);
-    const uint32_t off = (uint32_t)(prefix + incl - cnt);
+    if (lane == 0) {
+        s_part[w] = part;
+        s_cnt[w] = cnt;
+    }
+    __syncthreads();
+    int prefix = 0, before = 0, block_tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kMarchRaysPerBlock; ++i) {
+        prefix += s_part[i];
+        before += i < w ? s_cnt[i] : 0;
+        block_tot += s_cnt[i];
+    }
+    const uint32_t off = (uint32_t)(prefix + before);
     if (n < N) {
-        rays[3 * n + 1] = (int32_t)off;
+        if (lane == 0) rays[3 * n + 1] = (int32_t)off;
         if (cnt > 0 && off + (uint32_t)cnt <= M) {
             const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
             const float near = to_f(nears[n]), far = to_f(fars[n]);
             const float t0 = fmaf(clampf(near * k.dt_gamma, k.dt_min, k.dt_max),
                                   to_f(noises[n]), near);
-            march<true, scalar_t>(k, r, grid, t0, far, (uint32_t)cnt, xyzs + 3 * (size_t)off,
-                                  dirs + 3 * (size_t)off, deltas + 2 * (size_t)off, nullptr);
+            scalar_t *px = xyzs + 3 * (size_t)off;
+            scalar_t *pd = dirs + 3 * (size_t)off;
+            scalar_t *pl = deltas + 2 * (size_t)off;
+            march_wave(k, r, grid, t0, far, (uint32_t)cnt,
+                       [&](uint32_t i, float x, float y, float z, float dt, float dl) {
+                           px[3 * i + 0] = from_f<scalar_t>(x);
+                           px[3 * i + 1] = from_f<scalar_t>(y);
+                           px[3 * i + 2] = from_f<scalar_t>(z);
+                           pd[3 * i + 0] = from_f<scalar_t>(r.dx);
+                           pd[3 * i + 1] = from_f<scalar_t>(r.dy);
+                           pd[3 * i + 2] = from_f<scalar_t>(r.dz);
+                           pl[2 * i + 0] = from_f<scalar_t>(dt);
+                           pl[2 * i + 1] = from_f<scalar_t>(dl);
+                       });
         } else if (zero_tail != 0 && cnt > 0 && off < M) {
             // first ray that does not fit: rows [off, M) stay unwritten -> zero
             // (end clipped by the align limit, like the tail below)
@@ -214,14 +257,14 @@ __global__ __launch_bounds__(64) void k_march_train_emit(
                 for (uint32_t i = blockIdx.x; i < gridDim.x; ++i) total += (uint32_t)block_sums[i];
                 end = min(end, total + (uint64_t)zero_tail - total % (uint64_t)zero_tail);
             }
-            zero_rows(xyzs, dirs, deltas, off, end, 0, 1);
+            zero_rows(xyzs, dirs, deltas, off, end, lane, 64);
         }
     }
     if (zero_tail != 0 && blockIdx.x == gridDim.x - 1) {
-        const uint64_t total = (uint64_t)prefix + (uint32_t)__shfl(incl, 63, 64);
+        const uint64_t total = (uint64_t)prefix + (uint32_t)block_tot;
         uint64_t end = M;
         if (zero_tail > 0) end = min(end, total + (uint64_t)zero_tail - total % (uint64_t)zero_tail);
-        zero_rows(xyzs, dirs, deltas, total, end, threadIdx.x, 64);
+        zero_rows(xyzs, dirs, deltas, total, end, threadIdx.x, blockDim.x);
     }
 }
 
@@ -492,7 +535,7 @@ extern "C" int dfhip_packbits(int dtype, const void *grid, uint32_t N, float den
 }
 
 extern "C" uint32_t dfhip_march_rays_train_scratch_ints(uint32_t N) {
-    return ceil_div(N, 64u) > 0 ? ceil_div(N, 64u) : 1u;
+    return ceil_div(N, kMarchRaysPerBlock) > 0 ? ceil_div(N, kMarchRaysPerBlock) : 1u;
 }
 
 extern "C" int dfhip_march_rays_train_count(int dtype, const void *rays_o, const void *rays_d,
@@ -506,7 +549,8 @@ extern "C" int dfhip_march_rays_train_count(int dtype, const void *rays_o, const
     if (N == 0) return DFHIP_OK;
     const MarchConsts k = make_consts(bound, dt_gamma, max_steps, C, H);
     DFHIP_DISPATCH(dtype, "march_rays_train_count",
-        k_march_train_count<scalar_t><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+        k_march_train_count<scalar_t><<<ceil_div(N, kMarchRaysPerBlock), 64 * kMarchRaysPerBlock,
+                                        0, as_stream(stream)>>>(
             (const scalar_t *)rays_o, (const scalar_t *)rays_d, grid, k, max_steps, N,
             (const scalar_t *)nears, (const scalar_t *)fars, rays, counter,
             (const scalar_t *)noises, block_sums));
@@ -525,7 +569,8 @@ extern "C" int dfhip_march_rays_train_emit(int dtype, const void *rays_o, const 
     if (N == 0) return DFHIP_OK;
     const MarchConsts k = make_consts(bound, dt_gamma, max_steps, C, H);
     DFHIP_DISPATCH(dtype, "march_rays_train_emit",
-        k_march_train_emit<scalar_t><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+        k_march_train_emit<scalar_t><<<ceil_div(N, kMarchRaysPerBlock), 64 * kMarchRaysPerBlock,
+                                       0, as_stream(stream)>>>(
             (const scalar_t *)rays_o, (const scalar_t *)rays_d, grid, k, N, M,
             (const scalar_t *)nears, (const scalar_t *)fars, (scalar_t *)xyzs,
             (scalar_t *)dirs, (scalar_t *)deltas, rays, (const scalar_t *)noises,
