@@ -211,6 +211,24 @@ __device__ __forceinline__ void flush(double *acc, uint32_t r0, uint32_t r1, con
 
 constexpr uint32_t kRun = 8;  // entries gathered per lane before they are walked
 
+// One sample's C gradient channels as one load where the row is 4 or 8 bytes.
+template <typename grad_t, uint32_t C>
+__device__ __forceinline__ void load_grad(const grad_t *__restrict__ p, float (&g)[C]) {
+    if constexpr (sizeof(grad_t) * C == 4 && sizeof(grad_t) == 2) {
+        typedef grad_t v2 __attribute__((ext_vector_type(2)));
+        const v2 v = *reinterpret_cast<const v2 *>(p);
+        g[0] = (float)v.x;
+        g[C - 1] = (float)v.y;
+    } else if constexpr (sizeof(grad_t) * C == 8 && sizeof(grad_t) == 4) {
+        const float2 v = *reinterpret_cast<const float2 *>(p);
+        g[0] = v.x;
+        g[C - 1] = v.y;
+    } else {
+#pragma unroll
+        for (uint32_t ch = 0; ch < C; ++ch) g[ch] = (float)p[ch];
+    }
+}
+
 // A segment's entries are (in chunks) in sample order, i.e. consecutive
 // samples of one ray.  Lane i walks the contiguous run [i*Q, (i+1)*Q) of the
 // segment (Q = ceil(cnt / 64)): neighbouring lanes sit Q samples apart, so one
@@ -264,20 +282,19 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         bool have = false;
         for (uint32_t e = e0; e < e1; e += kRun) {
             const uint32_t m = min(e1 - e, kRun);
+            // every load of the batch is issued before the first use: clamped
+            // indices instead of guarded loads (a guarded load is a branch
+            // with its own wait)
             uint32_t sid[kRun];
             float xs[kRun][D];
             float gs[kRun][C];
 #pragma unroll
-            for (uint32_t i = 0; i < kRun; ++i) sid[i] = (i < m) ? seg[e + i] : 0u;
+            for (uint32_t i = 0; i < kRun; ++i) sid[i] = seg[min(e + i, e1 - 1)];
 #pragma unroll
             for (uint32_t i = 0; i < kRun; ++i) {
-                if (i < m) {
 #pragma unroll
-                    for (uint32_t d = 0; d < D; ++d) xs[i][d] = inputs[(size_t)sid[i] * D + d];
-#pragma unroll
-                    for (uint32_t ch = 0; ch < C; ++ch)
-                        gs[i][ch] = (float)gl[(size_t)sid[i] * C + ch];
-                }
+                for (uint32_t d = 0; d < D; ++d) xs[i][d] = inputs[(size_t)sid[i] * D + d];
+                load_grad<grad_t, C>(gl + (size_t)sid[i] * C, gs[i]);
             }
 #pragma unroll
             for (uint32_t i = 0; i < kRun; ++i) {
