@@ -83,6 +83,11 @@ int dfhip_density_grid_ema(const float *sigma, const int32_t *indices, uint32_t 
 int dfhip_packbits_mean(const float *grid, uint32_t N, const double *acc,
                         float density_thresh, uint8_t *bitfield, float *mean_out,
                         dfhip_stream_t stream);
+/* renderer.py:611-613 mean_count = int(step_counter[:total_step, 0].sum() /
+ * total_step) on the device (step_counter int32 [>= total_step, 2] contiguous,
+ * 1 <= total_step <= 64; mean_count one int64). total_step 0 is a no-op. */
+int dfhip_mean_count(const int32_t *step_counter, uint32_t total_step,
+                     int64_t *mean_count, dfhip_stream_t stream);
 
 /* raymarching.cu:201 sph_from_ray(rays_o, rays_d, radius, N, coords) */
 int dfhip_sph_from_ray(int dtype, const void *rays_o, const void *rays_d,
@@ -450,6 +455,30 @@ int dfhip_entropy_forward(uint32_t N, const float *ws, float lambda, float *loss
                           dfhip_stream_t stream);
 int dfhip_entropy_backward(uint32_t N, const float *ws, const float *grad_loss, float lambda,
                            float *grad_ws, dfhip_stream_t stream);
+/* The same gradient added into grad_ws (grad_ws += ...): the autograd sum of
+ * the entropy term and the ray head's gradient of the weights sum, one
+ * launch (the native train step, nerf/native_step.py). */
+int dfhip_entropy_backward_accumulate(uint32_t N, const float *ws, const float *grad_loss,
+                                      float lambda, float *grad_ws, dfhip_stream_t stream);
+
+/* Prologue of the native albedo train step (nerf/native_step.py), one launch:
+ * camera rays of an H x W pinhole image from a host 3x4 cam2world `pose`
+ * (as dfhip_get_rays; nerf/utils.py:42-106), their box intersection with
+ * aabb[6] and min_near (as dfhip_near_far_from_aabb; raymarching.py:19-49),
+ * the march noise (raymarching.py:200, 0 unless perturb), the background
+ * colour draw bg_color [N,3] (utils.py:349; NULL to skip), the synthetic SDS
+ * gradient g_image [3,N] = (1 - alphas[t]) * eps, t ~ U{min_step..max_step},
+ * eps ~ N(0,1) (nerf/sd.py InjectedSDS; NULL to skip) and counter[0..1] = 0
+ * (renderer.py:470; NULL to skip).  Random numbers: Philox4x32-10 keyed by
+ * `seed`, counter (ray, step, stream) — fresh per step index, independent of
+ * the launch shape. */
+int dfhip_train_step_prologue(const float *pose, float fx, float fy, float cx, float cy,
+                              uint32_t H, uint32_t W, const float *aabb, float min_near,
+                              uint64_t seed, uint64_t step, int perturb, const float *alphas,
+                              uint32_t min_step, uint32_t max_step, float *rays_o,
+                              float *rays_d, float *nears, float *fars, float *noises,
+                              float *bg_color, float *g_image, int32_t *counter,
+                              dfhip_stream_t stream);
 
 /* nerf/renderer.py:496-532 — the inference branch of run_cuda (the host loop
  * of march_rays raymarching.cu:700-804 -> network_grid.common_forward

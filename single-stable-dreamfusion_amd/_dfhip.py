@@ -30,6 +30,7 @@ _SIGS = {
     "dfhip_get_rays": [_vp, _f32, _f32, _f32, _f32, _u32, _u32, _vp, _vp, _vp],
     "dfhip_density_grid_ema": [_vp, _vp, _u32, _u32, _f32, _vp, _vp, _vp],
     "dfhip_packbits_mean": [_vp, _u32, _vp, _f32, _vp, _vp, _vp],
+    "dfhip_mean_count": [_vp, _u32, _vp, _vp],
     "dfhip_sph_from_ray": [_i32, _vp, _vp, _f32, _u32, _vp, _vp],
     "dfhip_morton3D": [_vp, _u32, _vp, _vp],
     "dfhip_morton3D_invert": [_vp, _u32, _vp, _vp],
@@ -87,6 +88,10 @@ _SIGS = {
                                 _vp, _vp, _vp, _vp, _vp],
     "dfhip_entropy_forward": [_u32, _vp, _f32, _vp, _vp],
     "dfhip_entropy_backward": [_u32, _vp, _vp, _f32, _vp, _vp],
+    "dfhip_entropy_backward_accumulate": [_u32, _vp, _vp, _f32, _vp, _vp],
+    "dfhip_train_step_prologue": [_vp, _f32, _f32, _f32, _f32, _u32, _u32, _vp, _f32,
+                                  ctypes.c_uint64, ctypes.c_uint64, _i32, _vp, _u32, _u32, _vp,
+                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dfhip_render_rays_infer": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _vp,
                                 _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp, _vp, _vp, _vp],

@@ -12,15 +12,10 @@
 //   rays_d = R d  (row k: d0 R[k][0] + d1 R[k][1] + d2 R[k][2])
 // The GEMM's summation order is the library's, so rays_d can differ from the
 // torch version by an ulp (tests/test_gpu_camera.py bounds it).
-#include "common.h"
+#include "camera_common.h"
 
 namespace dfhip {
 namespace cam {
-
-struct Pose {
-    float r[9];  // rotation, row-major (cam2world[:3, :3])
-    float t[3];  // centre (cam2world[:3, 3])
-};
 
 __global__ __launch_bounds__(256) void k_get_rays(Pose p, float fx, float fy, float cx,
                                                   float cy, uint32_t H, uint32_t W,
@@ -28,17 +23,12 @@ __global__ __launch_bounds__(256) void k_get_rays(Pose p, float fx, float fy, fl
                                                   float *__restrict__ rays_d) {
     const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= H * W) return;
-    const uint32_t h = n / W, w = n - h * W;
-    // torch divides a tensor by a scalar as a multiply by its f32 reciprocal
-    const float x = ((float)w + 0.5f - cx) * (1.0f / fx);
-    const float y = ((float)h + 0.5f - cy) * (1.0f / fy);
-    const float s = (x * x + y * y) + 1.0f;
-    const float inv = sqrtf(fmaxf(s, 1e-20f));
-    const float d0 = x / inv, d1 = y / inv, d2 = 1.0f / inv;
+    float o[3], d[3];
+    pixel_ray(p, fx, fy, cx, cy, W, n, o, d);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        rays_d[3 * (size_t)n + k] = fmaf(d2, p.r[3 * k + 2], fmaf(d1, p.r[3 * k + 1], d0 * p.r[3 * k]));
-        rays_o[3 * (size_t)n + k] = p.t[k];
+        rays_d[3 * (size_t)n + k] = d[k];
+        rays_o[3 * (size_t)n + k] = o[k];
     }
 }
 
@@ -65,11 +55,7 @@ extern "C" int dfhip_get_rays(const float *pose, float fx, float fy, float cx, f
         set_error("%s: H*W too large", name);
         return DFHIP_EINVAL;
     }
-    cam::Pose p;
-    for (int k = 0; k < 3; ++k) {
-        for (int c = 0; c < 3; ++c) p.r[3 * k + c] = pose[4 * k + c];
-        p.t[k] = pose[4 * k + 3];
-    }
+    const cam::Pose p = cam::pose_from_3x4(pose);
     cam::k_get_rays<<<ceil_div((uint32_t)n, 256u), 256, 0, as_stream(stream)>>>(
         p, fx, fy, cx, cy, H, W, rays_o, rays_d);
     return check_launch(name);

@@ -297,6 +297,7 @@ __global__ __launch_bounds__(1024) void k_entropy_fwd(uint32_t N, const float *_
 
 // d loss / d ws = g * lambda / N * log2((1 - a) / a), zero where the clamp is
 // active (torch.clamp's backward passes the gradient for lo <= ws <= hi).
+template <bool ACC>
 __global__ __launch_bounds__(256) void k_entropy_bwd(uint32_t N, const float *__restrict__ ws,
                                                      const float *__restrict__ g, float lambda,
                                                      float *__restrict__ grad_ws) {
@@ -304,7 +305,8 @@ __global__ __launch_bounds__(256) void k_entropy_bwd(uint32_t N, const float *__
     if (n >= N) return;
     const float a = ws[n];
     const float scale = g[0] * lambda / (float)N;
-    grad_ws[n] = (a >= kLo && a <= kHi) ? scale * (log2f(1.0f - a) - log2f(a)) : 0.0f;
+    const float v = (a >= kLo && a <= kHi) ? scale * (log2f(1.0f - a) - log2f(a)) : 0.0f;
+    grad_ws[n] = ACC ? grad_ws[n] + v : v;
 }
 
 }  // namespace hd
@@ -393,7 +395,20 @@ extern "C" int dfhip_entropy_backward(uint32_t N, const float *ws, const float *
         set_error("entropy_backward: null pointer");
         return DFHIP_EINVAL;
     }
-    hd::k_entropy_bwd<<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(N, ws, grad_loss, lambda,
-                                                                       grad_ws);
+    hd::k_entropy_bwd<false><<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(
+        N, ws, grad_loss, lambda, grad_ws);
     return check_launch("entropy_backward");
+}
+
+extern "C" int dfhip_entropy_backward_accumulate(uint32_t N, const float *ws,
+                                                 const float *grad_loss, float lambda,
+                                                 float *grad_ws, dfhip_stream_t stream) {
+    if (N == 0) return DFHIP_OK;
+    if (!ws || !grad_loss || !grad_ws) {
+        set_error("entropy_backward_accumulate: null pointer");
+        return DFHIP_EINVAL;
+    }
+    hd::k_entropy_bwd<true><<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(
+        N, ws, grad_loss, lambda, grad_ws);
+    return check_launch("entropy_backward_accumulate");
 }

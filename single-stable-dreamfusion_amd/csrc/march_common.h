@@ -114,6 +114,29 @@ __device__ __forceinline__ Ray load_ray(const scalar_t *o, const scalar_t *d) {
     return r;
 }
 
+// Slab intersection of a ray with the box b = (x0, y0, z0, x1, y1, z1)
+// (raymarching.cu:104-145): false on a miss, else the entry / exit t with the
+// entry raised to min_near.
+__device__ __forceinline__ bool ray_aabb(const Ray &r, const float b[6], float min_near,
+                                         float &near, float &far) {
+    float lo = (b[0] - r.ox) * r.rdx, hi = (b[3] - r.ox) * r.rdx;
+    if (lo > hi) { float s = lo; lo = hi; hi = s; }
+    float lo_y = (b[1] - r.oy) * r.rdy, hi_y = (b[4] - r.oy) * r.rdy;
+    if (lo_y > hi_y) { float s = lo_y; lo_y = hi_y; hi_y = s; }
+    if (lo > hi_y || lo_y > hi) return false;
+    if (lo_y > lo) lo = lo_y;
+    if (hi_y < hi) hi = hi_y;
+    float lo_z = (b[2] - r.oz) * r.rdz, hi_z = (b[5] - r.oz) * r.rdz;
+    if (lo_z > hi_z) { float s = lo_z; lo_z = hi_z; hi_z = s; }
+    if (lo > hi_z || lo_z > hi) return false;
+    if (lo_z > lo) lo = lo_z;
+    if (hi_z < hi) hi = hi_z;
+    if (lo < min_near) lo = min_near;
+    near = lo;
+    far = hi;
+    return true;
+}
+
 // The march loop shared by the count pass, the emit pass and the inference
 // marcher (raymarching.cu:359-400, 427-479, 750-804).  Visits the same
 // t-sequence in every mode.  WRITE: store each occupied sample at out[step].

@@ -132,6 +132,19 @@ __global__ __launch_bounds__(256) void k_packbits_mean(const float *__restrict__
     bitfield[n] = (uint8_t)bits;
 }
 
+// mean_count = int(step_counter[:total_step, 0].sum() / total_step)
+// (renderer.py:611-613; the sum is exact in int64, the quotient truncated
+// toward zero as Python's int() of the float quotient does for a sum < 2^53).
+__global__ __launch_bounds__(64) void k_mean_count(const int32_t *__restrict__ step_counter,
+                                                   uint32_t total_step,
+                                                   int64_t *__restrict__ mean_count) {
+    const uint32_t lane = threadIdx.x;
+    int64_t s = lane < total_step ? (int64_t)step_counter[2 * lane] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) mean_count[0] = (int64_t)((double)s / (double)total_step);
+}
+
 }  // namespace occ
 }  // namespace dfhip
 
@@ -175,5 +188,21 @@ extern "C" int dfhip_packbits_mean(const float *grid, uint32_t N, const double *
     }
     occ::k_packbits_mean<<<ceil_div(N, 256u), 256, 0, as_stream(stream)>>>(
         grid, N, acc, density_thresh, bitfield, mean_out);
+    return check_launch(name);
+}
+
+extern "C" int dfhip_mean_count(const int32_t *step_counter, uint32_t total_step,
+                                int64_t *mean_count, dfhip_stream_t stream) {
+    const char *name = "mean_count";
+    if (total_step == 0) return DFHIP_OK;
+    if (!step_counter || !mean_count) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    if (total_step > 64) {
+        set_error("%s: total_step must be <= 64 (got %u)", name, total_step);
+        return DFHIP_EINVAL;
+    }
+    occ::k_mean_count<<<1, 64, 0, as_stream(stream)>>>(step_counter, total_step, mean_count);
     return check_launch(name);
 }

@@ -21,6 +21,8 @@
 //    256 workgroups = one per CU, instead of 64 CUs with 256-thread blocks.
 #include "march_common.h"
 
+#include <type_traits>
+
 namespace dfhip {
 namespace rm {
 
@@ -42,29 +44,14 @@ __global__ __launch_bounds__(256) void k_near_far(const scalar_t *__restrict__ r
     const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
     const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
-    const float b0 = to_f(aabb[0]), b1 = to_f(aabb[1]), b2 = to_f(aabb[2]);
-    const float b3 = to_f(aabb[3]), b4 = to_f(aabb[4]), b5 = to_f(aabb[5]);
-
-    float lo = (b0 - r.ox) * r.rdx, hi = (b3 - r.ox) * r.rdx;
-    if (lo > hi) { float s = lo; lo = hi; hi = s; }
-    float lo_y = (b1 - r.oy) * r.rdy, hi_y = (b4 - r.oy) * r.rdy;
-    if (lo_y > hi_y) { float s = lo_y; lo_y = hi_y; hi_y = s; }
-    const scalar_t miss = max_value<scalar_t>();
-    if (lo > hi_y || lo_y > hi) {
-        nears[n] = fars[n] = miss;
+    float b[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) b[i] = to_f(aabb[i]);
+    float lo, hi;
+    if (!ray_aabb(r, b, min_near, lo, hi)) {
+        nears[n] = fars[n] = max_value<scalar_t>();
         return;
     }
-    if (lo_y > lo) lo = lo_y;
-    if (hi_y < hi) hi = hi_y;
-    float lo_z = (b2 - r.oz) * r.rdz, hi_z = (b5 - r.oz) * r.rdz;
-    if (lo_z > hi_z) { float s = lo_z; lo_z = hi_z; hi_z = s; }
-    if (lo > hi_z || lo_z > hi) {
-        nears[n] = fars[n] = miss;
-        return;
-    }
-    if (lo_z > lo) lo = lo_z;
-    if (hi_z < hi) hi = hi_z;
-    if (lo < min_near) lo = min_near;
     nears[n] = from_f<scalar_t>(lo);
     fars[n] = from_f<scalar_t>(hi);
 }
@@ -396,6 +383,189 @@ __global__ __launch_bounds__(64) void k_composite_train_bwd(
     }
 }
 
+// ------------------------------------------------------------------ compositing, wave per ray
+// The same arithmetic as k_composite_train_fwd / _bwd in the same order, with a
+// ray's samples spread over the 64 lanes of one wave: each lane loads one
+// sample of the window (coalesced) and computes its alpha, then the wave runs
+// the reference's serial chain (T, the colour / weight / depth sums) over the
+// window with the per-sample values read from their lanes.  Bit-identical to
+// the one-thread-per-ray loop (same f32 operations, same order, same break);
+// 16k rays give 16k waves instead of 256.
+constexpr uint32_t kCompRaysPerBlock = 4;
+
+template <typename rgb_t>
+__device__ __forceinline__ void load_rgb3(const rgb_t *c, float &r, float &g, float &b) {
+    r = to_f(c[0]);
+    g = to_f(c[1]);
+    b = to_f(c[2]);
+}
+
+// raymarching.cu:500-577
+template <typename scalar_t, typename rgb_t>
+__global__ __launch_bounds__(64 * kCompRaysPerBlock) void k_composite_train_fwd_w(
+    const scalar_t *__restrict__ sigmas, const rgb_t *__restrict__ rgbs,
+    const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays, uint32_t M,
+    uint32_t N, float T_thresh, scalar_t *weights_sum, scalar_t *depth, scalar_t *image) {
+    const uint32_t n = blockIdx.x * kCompRaysPerBlock + (threadIdx.x >> 6);
+    if (n >= N) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t index = (uint32_t)rays[3 * n];
+    const uint32_t offset = (uint32_t)rays[3 * n + 1];
+    const uint32_t num = (uint32_t)rays[3 * n + 2];
+    float T = 1, r = 0, g = 0, b = 0, ws = 0, t = 0, d = 0;
+    if (num != 0 && offset + num <= M) {
+        bool stop = false;
+        for (uint32_t base = 0; base < num && !stop; base += 64) {
+            const uint32_t cnt = min(64u, num - base);
+            float a = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, dl = 0.0f;
+            if ((uint32_t)lane < cnt) {
+                const size_t i = (size_t)offset + base + lane;
+                a = 1.0f - __expf(-to_f(sigmas[i]) * to_f(deltas[2 * i]));
+                dl = to_f(deltas[2 * i + 1]);
+                load_rgb3(rgbs + 3 * i, cr, cg, cb);
+            }
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const float aj = rm::lane_f(a, (int)j);
+                const float w = aj * T;
+                r = fmaf(w, rm::lane_f(cr, (int)j), r);
+                g = fmaf(w, rm::lane_f(cg, (int)j), g);
+                b = fmaf(w, rm::lane_f(cb, (int)j), b);
+                t += rm::lane_f(dl, (int)j);
+                d = fmaf(w, t, d);
+                ws += w;
+                T *= 1.0f - aj;
+                if (T < T_thresh) {
+                    stop = true;
+                    break;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        weights_sum[index] = (scalar_t)ws;
+        depth[index] = (scalar_t)d;
+        image[3 * index + 0] = (scalar_t)r;
+        image[3 * index + 1] = (scalar_t)g;
+        image[3 * index + 2] = (scalar_t)b;
+    }
+}
+
+// raymarching.cu:601-682, DENSE as k_composite_train_bwd.
+template <typename scalar_t, bool DENSE, typename rgb_t>
+__global__ __launch_bounds__(64 * kCompRaysPerBlock) void k_composite_train_bwd_w(
+    const scalar_t *__restrict__ grad_ws, const scalar_t *__restrict__ grad_image,
+    const scalar_t *__restrict__ sigmas, const rgb_t *__restrict__ rgbs,
+    const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays,
+    const scalar_t *__restrict__ weights_sum, const scalar_t *__restrict__ image,
+    uint32_t M, uint32_t N, float T_thresh, scalar_t *grad_sigmas, rgb_t *grad_rgbs,
+    int tail) {
+    const uint32_t n = blockIdx.x * kCompRaysPerBlock + (threadIdx.x >> 6);
+    if (n >= N) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t index = (uint32_t)rays[3 * n];
+    const uint32_t offset = (uint32_t)rays[3 * n + 1];
+    const uint32_t num = (uint32_t)rays[3 * n + 2];
+    const scalar_t zero = (scalar_t)0.0f;
+    const rgb_t czero = (rgb_t)0.0f;
+    uint32_t done = 0;   // samples taken (the reference loop's final i)
+    if (num != 0 && offset + num <= M) {
+        const float gr = to_f(grad_image[3 * index + 0]);
+        const float gg = to_f(grad_image[3 * index + 1]);
+        const float gb = to_f(grad_image[3 * index + 2]);
+        const float gw = to_f(grad_ws[index]);
+        const float rf = to_f(image[3 * index + 0]);
+        const float gf = to_f(image[3 * index + 1]);
+        const float bf = to_f(image[3 * index + 2]);
+        const float wsf = to_f(weights_sum[index]);
+        float T = 1, r = 0, g = 0, b = 0;
+        bool stop = false;
+        for (uint32_t base = 0; base < num && !stop; base += 64) {
+            const uint32_t cnt = min(64u, num - base);
+            const size_t i = (size_t)offset + base + lane;
+            float a = 0.0f, dt = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+            if ((uint32_t)lane < cnt) {
+                dt = to_f(deltas[2 * i]);
+                a = 1.0f - __expf(-to_f(sigmas[i]) * dt);
+                load_rgb3(rgbs + 3 * i, cr, cg, cb);
+            }
+            // this lane's sample: weight, T after it, colour sums including it
+            float wl = 0.0f, Tl = 0.0f, rl = 0.0f, gl = 0.0f, bl = 0.0f;
+            uint32_t end = cnt;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const float aj = rm::lane_f(a, (int)j);
+                const float w = aj * T;
+                r = fmaf(w, rm::lane_f(cr, (int)j), r);
+                g = fmaf(w, rm::lane_f(cg, (int)j), g);
+                b = fmaf(w, rm::lane_f(cb, (int)j), b);
+                T *= 1.0f - aj;
+                const bool mine = (uint32_t)lane == j;
+                wl = mine ? w : wl;
+                Tl = mine ? T : Tl;
+                rl = mine ? r : rl;
+                gl = mine ? g : gl;
+                bl = mine ? b : bl;
+                if (T < T_thresh) {
+                    stop = true;
+                    end = j + 1;
+                    break;
+                }
+            }
+            if ((uint32_t)lane < end) {
+                grad_rgbs[3 * i + 0] = grad_cast<scalar_t, rgb_t>(gr * wl);
+                grad_rgbs[3 * i + 1] = grad_cast<scalar_t, rgb_t>(gg * wl);
+                grad_rgbs[3 * i + 2] = grad_cast<scalar_t, rgb_t>(gb * wl);
+                float acc = fmaf(gr, fmaf(Tl, cr, -(rf - rl)), gg * fmaf(Tl, cg, -(gf - gl)));
+                acc = fmaf(gb, fmaf(Tl, cb, -(bf - bl)), acc);
+                acc = fmaf(gw, 1.0f - wsf, acc);
+                grad_sigmas[i] = (scalar_t)(dt * acc);
+            }
+            done = base + end;
+        }
+    }
+    if (DENSE) {
+        // rows [offset + done, offset + num) of this ray, clipped to M
+        const uint64_t end = min((uint64_t)offset + num, (uint64_t)M);
+        for (uint64_t row = (uint64_t)offset + done + lane; row < end; row += 64) {
+            grad_sigmas[row] = zero;
+            grad_rgbs[3 * row] = czero; grad_rgbs[3 * row + 1] = czero; grad_rgbs[3 * row + 2] = czero;
+        }
+        if (tail && n == N - 1) {
+            for (uint64_t row = (uint64_t)offset + num + lane; row < M; row += 64) {
+                grad_sigmas[row] = zero;
+                grad_rgbs[3 * row] = czero; grad_rgbs[3 * row + 1] = czero; grad_rgbs[3 * row + 2] = czero;
+            }
+        }
+    }
+}
+
+template <typename scalar_t, typename rgb_t>
+static void launch_comp_fwd(hipStream_t s, const scalar_t *sig, const rgb_t *rgb,
+                            const scalar_t *dl, const int32_t *rays, uint32_t M, uint32_t N,
+                            float T_thresh, scalar_t *ws, scalar_t *depth, scalar_t *image) {
+    if constexpr (std::is_same<scalar_t, double>::value)
+        k_composite_train_fwd<scalar_t, rgb_t><<<ceil_div(N, 64u), 64, 0, s>>>(
+            sig, rgb, dl, rays, M, N, T_thresh, ws, depth, image);
+    else
+        k_composite_train_fwd_w<scalar_t, rgb_t>
+            <<<ceil_div(N, kCompRaysPerBlock), 64 * kCompRaysPerBlock, 0, s>>>(
+                sig, rgb, dl, rays, M, N, T_thresh, ws, depth, image);
+}
+
+template <typename scalar_t, bool DENSE, typename rgb_t>
+static void launch_comp_bwd(hipStream_t s, const scalar_t *gws, const scalar_t *gimg,
+                            const scalar_t *sig, const rgb_t *rgb, const scalar_t *dl,
+                            const int32_t *rays, const scalar_t *ws, const scalar_t *img,
+                            uint32_t M, uint32_t N, float T_thresh, scalar_t *gsig,
+                            rgb_t *grgb, int tail) {
+    if constexpr (std::is_same<scalar_t, double>::value)
+        k_composite_train_bwd<scalar_t, DENSE, rgb_t><<<ceil_div(N, 64u), 64, 0, s>>>(
+            gws, gimg, sig, rgb, dl, rays, ws, img, M, N, T_thresh, gsig, grgb, tail);
+    else
+        k_composite_train_bwd_w<scalar_t, DENSE, rgb_t>
+            <<<ceil_div(N, kCompRaysPerBlock), 64 * kCompRaysPerBlock, 0, s>>>(
+                gws, gimg, sig, rgb, dl, rays, ws, img, M, N, T_thresh, gsig, grgb, tail);
+}
+
 // ------------------------------------------------------------------ inference
 
 // raymarching.cu:700-804; also writes zeros into the slots it does not fill.
@@ -612,9 +782,9 @@ extern "C" int dfhip_composite_rays_train_forward(int dtype, const void *sigmas,
                                                   dfhip_stream_t stream) {
     if (N == 0) return DFHIP_OK;
     DFHIP_DISPATCH(dtype, "composite_rays_train_forward",
-        k_composite_train_fwd<scalar_t><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+        (launch_comp_fwd<scalar_t, scalar_t>(as_stream(stream),
             (const scalar_t *)sigmas, (const scalar_t *)rgbs, (const scalar_t *)deltas, rays,
-            M, N, T_thresh, (scalar_t *)weights_sum, (scalar_t *)depth, (scalar_t *)image));
+            M, N, T_thresh, (scalar_t *)weights_sum, (scalar_t *)depth, (scalar_t *)image)));
     return check_launch("composite_rays_train_forward");
 }
 
@@ -627,11 +797,11 @@ static int composite_bwd_impl(const char *name, int dtype, const void *grad_weig
                               void *grad_rgbs, dfhip_stream_t stream) {
     if (N == 0) return DFHIP_OK;
     DFHIP_DISPATCH(dtype, name,
-        (k_composite_train_bwd<scalar_t, DENSE><<<ceil_div(N, 64u), 64, 0, as_stream(stream)>>>(
+        (launch_comp_bwd<scalar_t, DENSE, scalar_t>(as_stream(stream),
             (const scalar_t *)grad_weights_sum, (const scalar_t *)grad_image,
             (const scalar_t *)sigmas, (const scalar_t *)rgbs, (const scalar_t *)deltas, rays,
             (const scalar_t *)weights_sum, (const scalar_t *)image, M, N, T_thresh,
-            (scalar_t *)grad_sigmas, (scalar_t *)grad_rgbs)));
+            (scalar_t *)grad_sigmas, (scalar_t *)grad_rgbs, 1)));
     return check_launch(name);
 }
 
@@ -669,11 +839,11 @@ extern "C" int dfhip_composite_rays_train_forward_mixed(
     if (N == 0) return DFHIP_OK;
     hipStream_t s = as_stream(stream);
     if (rgb_dtype == DFHIP_F32)
-        k_composite_train_fwd<float, float><<<ceil_div(N, 64u), 64, 0, s>>>(
-            sigmas, (const float *)rgbs, deltas, rays, M, N, T_thresh, weights_sum, depth, image);
+        launch_comp_fwd<float, float>(s, sigmas, (const float *)rgbs, deltas, rays, M, N,
+                                      T_thresh, weights_sum, depth, image);
     else if (rgb_dtype == DFHIP_F16)
-        k_composite_train_fwd<float, half_t><<<ceil_div(N, 64u), 64, 0, s>>>(
-            sigmas, (const half_t *)rgbs, deltas, rays, M, N, T_thresh, weights_sum, depth, image);
+        launch_comp_fwd<float, half_t>(s, sigmas, (const half_t *)rgbs, deltas, rays, M, N,
+                                       T_thresh, weights_sum, depth, image);
     else {
         set_error("%s: rgb dtype must be f32 or f16 (got %d)", name, rgb_dtype);
         return DFHIP_EDTYPE;
@@ -690,13 +860,15 @@ extern "C" int dfhip_composite_rays_train_backward_mixed(
     if (N == 0) return DFHIP_OK;
     hipStream_t s = as_stream(stream);
     if (rgb_dtype == DFHIP_F32)
-        k_composite_train_bwd<float, true, float><<<ceil_div(N, 64u), 64, 0, s>>>(
-            grad_weights_sum, grad_image, sigmas, (const float *)rgbs, deltas, rays, weights_sum,
-            image, M, N, T_thresh, grad_sigmas, (float *)grad_rgbs, zero_tail);
+        launch_comp_bwd<float, true, float>(s, grad_weights_sum, grad_image, sigmas,
+                                            (const float *)rgbs, deltas, rays, weights_sum,
+                                            image, M, N, T_thresh, grad_sigmas,
+                                            (float *)grad_rgbs, zero_tail);
     else if (rgb_dtype == DFHIP_F16)
-        k_composite_train_bwd<float, true, half_t><<<ceil_div(N, 64u), 64, 0, s>>>(
-            grad_weights_sum, grad_image, sigmas, (const half_t *)rgbs, deltas, rays, weights_sum,
-            image, M, N, T_thresh, grad_sigmas, (half_t *)grad_rgbs, zero_tail);
+        launch_comp_bwd<float, true, half_t>(s, grad_weights_sum, grad_image, sigmas,
+                                             (const half_t *)rgbs, deltas, rays, weights_sum,
+                                             image, M, N, T_thresh, grad_sigmas,
+                                             (half_t *)grad_rgbs, zero_tail);
     else {
         set_error("%s: rgb dtype must be f32 or f16 (got %d)", name, rgb_dtype);
         return DFHIP_EDTYPE;

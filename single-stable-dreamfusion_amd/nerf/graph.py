@@ -25,19 +25,33 @@ eagerly.  RNG draws inside the graph (march noise, background colour, light
 direction, timestep, SDS noise) use torch's graph-safe Philox offsets, so
 every replay draws fresh numbers.
 """
+import os
+
 import torch
 
 import _dfhip
 from . import field as _field
+from . import native_step as _native
+
+# DFHIP_NATIVE_STEP=0 keeps the autograd body even where the native step applies
+_NATIVE = os.environ.get("DFHIP_NATIVE_STEP", "1") != "0"
 
 
 class GraphedTrainStep:
-    def __init__(self, trainer, data, shading, ambient_ratio, text_z, stream):
+    def __init__(self, trainer, data, shading, ambient_ratio, text_z, stream, allow_native=True):
         self.trainer = trainer
         self.shading, self.ambient_ratio = shading, ambient_ratio
         self.H, self.W = data["H"], data["W"]
-        self.rays_o = data["rays_o"].detach().clone()
-        self.rays_d = data["rays_d"].detach().clone()
+        # the albedo step as native launches without autograd (nerf/native_step.py)
+        self.native = None
+        if (_NATIVE and allow_native and "pose" in data and "intrinsics" in data
+                and _native.eligible(trainer, shading)):
+            self.native = _native.NativeAlbedoStep(trainer, self.H, self.W)
+            self.rays_o = self.native.rays_o.view(1, -1, 3)
+            self.rays_d = self.native.rays_d.view(1, -1, 3)
+        else:
+            self.rays_o = data["rays_o"].detach().clone()
+            self.rays_d = data["rays_d"].detach().clone()
         self.text_z = text_z.detach().clone()
         self._text_src = text_z.data_ptr()  # prompt tensor currently in self.text_z
         self.stream = stream
@@ -55,13 +69,35 @@ class GraphedTrainStep:
         t.backward_only(loss)
         return loss
 
-    def capture(self):
+    def _capture_native(self, data):
+        nat = self.native
+        model = self.trainer.model
+        timer = _dfhip.set_kernel_timer(None)  # no event records inside the graph
+        try:
+            self.load(data, self.text_z)
+            self.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                nat.body()  # dry run (first-use setup outside the capture)
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                self.loss = nat.body()
+            torch.cuda.current_stream().wait_stream(self.stream)
+        finally:
+            _dfhip.set_kernel_timer(timer)
+        model.local_step += 1  # as run_cuda's step in the autograd capture
+        model.last_counter = nat.counter
+        self.counter = nat.counter
+        self.deferred = []
+        self.grads = list(nat.grads)
+
+    def capture(self, data=None):
         """Record the step (nothing of it executes until replay()).
 
         First one untimed dry run of the same code on the capture stream (its
         gradients are dropped, no optimizer step): the BLAS / MIOpen libraries
         set up per-stream state on first use, which must not happen inside the
         capture (HIP then faults when the capture ends)."""
+        if self.native is not None:
+            return self._capture_native(data)
         t = self.trainer
         model = t.model
         params = [p for p in model.parameters() if p.requires_grad]
@@ -105,6 +141,11 @@ class GraphedTrainStep:
     def load(self, data, text_z):
         """This step's camera rays (made straight into the graph's input buffers
         from a host pose when the batch has one) and prompt embedding."""
+        if self.native is not None:
+            t = self.trainer
+            self.native.prologue(data["pose"], data["intrinsics"],
+                                 int(t.opt.seed) * 1000003 + int(t.local_rank), t.global_step)
+            return
         if "pose" in data and "rays_o" not in data:
             from .utils import get_rays_host_pose
             get_rays_host_pose(data["pose"], data["intrinsics"], self.H, self.W, None,
@@ -120,6 +161,8 @@ class GraphedTrainStep:
         """Run the captured part, then the deferred embedding backward; leaves
         every trainable parameter's .grad set for the optimizer step."""
         self.graph.replay()
+        if self.native is not None:
+            self.native.embedding_backward()
         for launch, _ in self.deferred:
             launch()
         for p, g in self.grads:

@@ -1,0 +1,245 @@
+"""The albedo SDS train step as a fixed sequence of native launches, without
+autograd (captured once in a HIP graph by nerf/graph.py).
+
+The reference step (nerf/utils.py:337-404 train_step + 693-715 backward /
+optimizer, with NeRFRenderer.run_cuda renderer.py:446-559 and
+network_grid.common_forward :76-87) is, in the autograd form of this
+package, ~50 launches per 128x128 step: the native kernels plus ~30 small
+torch kernels (RNG draws, the light direction, SDS glue, loss assembly,
+gradient fills and adds).  On MI355X every launch costs ~5 us of GPU time
+even inside a graph, so the glue alone was ~140 us of a ~1.2 ms step.  Here
+the step is, with the same kernels and the same arithmetic:
+
+  prologue (eager, one launch; csrc/step.hip): camera rays from the host
+      pose, near/far, march noise, the synthetic SDS gradient w(t) * eps at
+      pred_rgb, step counter = 0
+  graph: march count / emit -> f16 table copy -> fused grid field ->
+      compositing -> ray head (background MLP, mix, depth, mask) -> entropy
+      loss -> ray head backward -> entropy backward (accumulated into the
+      weights-sum gradient) -> compositing backward -> field MLP backward
+  eager (timed): binned embedding backward -> GradScaler + Adam
+
+Gradients are bit-identical to the autograd step given the same draws
+(tests/test_gpu_native_step.py): the loss scale enters exactly where
+autograd puts it (the entropy term's upstream gradient is the scale; the SDS
+gradient is not scaled, the reference quirk kept by Trainer.backward_only).
+
+Applies to the albedo shading with the InjectedSDS guidance, the
+reference's grid network (16 x 2 tiled grid, 32 -> 64 -> 64 -> 4 MLP), a
+background MLP (bg_radius > 0) or a random background colour, and
+lambda_opacity == 0 (the -O defaults); anything else keeps the autograd step.
+"""
+import numpy as np
+import torch
+
+import _dfhip
+import _fieldmlp
+import _gridencoder
+import _raymarching
+from _dfhip import call, ptr, stream
+
+
+def eligible(trainer, shading):
+    """True when NativeAlbedoStep reproduces trainer.train_step for `shading`."""
+    from .sd import InjectedSDS
+    m, opt = trainer.model, trainer.opt
+    if shading != "albedo" or not isinstance(trainer.guidance, InjectedSDS):
+        return False
+    if not (trainer.fp16 and m.cuda_ray and trainer.fused_backward):
+        return False
+    if opt.lambda_opacity > 0:
+        return False
+    enc = getattr(m, "encoder", None)
+    if enc is None or getattr(enc, "offsets_host", None) is None:
+        return False
+    if (enc.num_levels, enc.level_dim, enc.input_dim) != (16, 2, 3):
+        return False
+    layers = list(m.sigma_net.net)
+    if len(layers) != 3 or layers[0].bias is None:
+        return False
+    if [tuple(l.weight.shape) for l in layers] != [(64, 32), (64, 64), (4, 64)]:
+        return False
+    if m.bg_radius > 0 and m.native_background_layers() is None:
+        return False
+    return all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters())
+
+
+class NativeAlbedoStep:
+    """Buffers and launches of one albedo train step at resolution H x W."""
+
+    def __init__(self, trainer, H, W):
+        self.trainer = trainer
+        m, opt = trainer.model, trainer.opt
+        dev = trainer.device
+        self.H, self.W = int(H), int(W)
+        N = self.N = self.H * self.W
+        self.max_steps = int(opt.max_steps)
+        cap = self.cap = N * self.max_steps
+        self.dt_gamma = float(opt.dt_gamma)
+        self.lam = float(opt.lambda_entropy)
+        f32 = dict(device=dev, dtype=torch.float32)
+        f16 = dict(device=dev, dtype=torch.float16)
+        i32 = dict(device=dev, dtype=torch.int32)
+        # prologue outputs (graph inputs)
+        self.rays_o = torch.empty(N, 3, **f32)
+        self.rays_d = torch.empty(N, 3, **f32)
+        self.nears = torch.empty(N, **f32)
+        self.fars = torch.empty(N, **f32)
+        self.noises = torch.empty(N, **f32)
+        self.g_image = torch.empty(3, N, **f32)  # d loss / d pred_rgb (channel-major)
+        self.bg_layers = m.native_background_layers() if m.bg_radius > 0 else None
+        self.bg_color = None if self.bg_layers is not None else torch.empty(N, 3, **f32)
+        self.counter = torch.zeros(2, **i32)
+        self.aabb = np.ascontiguousarray(m.aabb_train.detach().float().cpu().numpy())
+        g = trainer.guidance
+        self.alphas = g.alphas.detach().float().contiguous()
+        self.t_range = (int(g.min_step), int(g.max_step))
+        # march
+        self.rays = torch.empty(N, 3, **i32)
+        self.block_sums = torch.empty(_raymarching.march_rays_train_scratch_ints(N), **i32)
+        self.xyzs = torch.empty(cap, 3, **f32)
+        self.dirs = torch.empty(cap, 3, **f32)
+        self.deltas = torch.empty(cap, 2, **f32)
+        self.m_dev = self.counter[:1]
+        # field
+        enc = m.encoder
+        self.encoder = enc
+        self.L, self.C = enc.offsets.shape[0] - 1, enc.level_dim
+        self.rows = enc.embeddings.shape[0]
+        self.meta = (float(np.log2(enc.per_level_scale)), int(enc.base_resolution),
+                     enc.gridtype_id, bool(enc.align_corners), enc.offsets_host)
+        self.table = torch.empty(self.rows, self.C, **f16)
+        self.mlp = []
+        for lin in m.sigma_net.net:
+            self.mlp += [lin.weight, lin.bias]
+        self.enc = torch.empty(cap, self.L * self.C, **f16)
+        self.sigma = torch.empty(cap, **f32)
+        self.albedo = torch.empty(cap, 3, **f16)
+        # compositing + head
+        self.ws = torch.empty(N, **f32)
+        self.depth = torch.empty(N, **f32)
+        self.image = torch.empty(N, 3, **f32)
+        self.out_image = torch.empty(3, N, **f32)
+        self.out_depth = torch.empty(N, **f32)
+        self.mask = torch.empty(N, dtype=torch.uint8, device=dev)
+        self.loss = torch.zeros((), **f32)
+        # backward
+        self.grad_image = torch.empty(N, 3, **f32)
+        self.grad_ws = torch.empty(N, **f32)
+        self.head_partial = (torch.empty(int(_dfhip.load().dfhip_ray_head_partial_floats(N)),
+                                         **f32) if self.bg_layers is not None else None)
+        self.grad_sigma = torch.empty(cap, **f32)
+        self.grad_albedo = torch.empty(cap, 3, **f16)
+        self.d_enc = torch.empty(self.L, cap, self.C, **f16)
+        self.mlp_partial = torch.empty(_fieldmlp.backward_parts(cap) * _fieldmlp.params_count(),
+                                       **f32)
+        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, enc.offsets_host, self.L,
+                                                                self.C)
+        self.bin_scratch = (torch.empty(ne, **i32), torch.empty(nc, **i32),
+                            torch.empty(npf, **f32))
+        sc = trainer.scaler
+        if sc.is_enabled() and sc._scale is None:
+            sc._lazy_init_scale_growth_tracker(dev)  # what scaler.scale() does on first use
+        self._ones = torch.ones(1, **f32)  # upstream gradient of the loss without a scaler
+        # gradients live in persistent buffers, written in place every step
+        for p in m.parameters():
+            if p.requires_grad and p.grad is None:
+                p.grad = torch.zeros_like(p)
+        self.params = [p for p in m.parameters() if p.requires_grad]
+        self.grads = [(p, p.grad) for p in self.params]
+        self._emb_launch = None
+
+    # ------------------------------------------------------------ per step
+    def prologue(self, pose, intrinsics, seed, step):
+        """Rays, near/far, noise, the SDS gradient and counter reset from the
+        host pose [4, 4] (or [1, 4, 4]) of this step (one eager launch)."""
+        host = np.ascontiguousarray(np.asarray(pose, dtype=np.float32).reshape(-1, 4, 4)[0, :3, :4])
+        fx, fy, cx, cy = (float(v) for v in intrinsics)
+        lo, hi = self.t_range
+        call("dfhip_train_step_prologue", host.ctypes.data, fx, fy, cx, cy, self.H, self.W,
+             self.aabb.ctypes.data, 0.2, int(seed) & 0xFFFFFFFFFFFFFFFF,
+             int(step) & 0xFFFFFFFFFFFFFFFF, 1, ptr(self.alphas), lo, hi, ptr(self.rays_o),
+             ptr(self.rays_d), ptr(self.nears), ptr(self.fars), ptr(self.noises),
+             ptr(self.bg_color), ptr(self.g_image), ptr(self.counter), stream())
+
+    def body(self):
+        """Forward and backward down to the feature / network gradients (the
+        graph-captured part).  Returns the loss tensor."""
+        m = self.trainer.model
+        N, cap = self.N, self.cap
+        sc = self.trainer.scaler
+        scale = sc._scale if sc.is_enabled() else self._ones
+        # march (raymarching.py:161-235, device count)
+        _raymarching.march_rays_train_count(
+            self.rays_o, self.rays_d, m.density_bitfield, m.bound, self.dt_gamma, self.max_steps,
+            N, m.cascade, m.grid_size, self.nears, self.fars, self.rays, self.counter,
+            self.noises, self.block_sums)
+        _raymarching.march_rays_train_emit(
+            self.rays_o, self.rays_d, m.density_bitfield, m.bound, self.dt_gamma, self.max_steps,
+            N, m.cascade, m.grid_size, cap, self.nears, self.fars, self.xyzs, self.dirs,
+            self.deltas, self.rays, self.noises, self.block_sums, 0)
+        # field (grid.py:38-39 autocast table, network_grid.py:76-87)
+        self.table.copy_(self.encoder.embeddings.detach())
+        S, Hb, gridtype, align, _ = self.meta
+        _fieldmlp.grid_field_forward(self.xyzs, m.bound, self.table, self.encoder.offsets, S, Hb,
+                                     gridtype, align, self.mlp, self.enc, self.sigma, self.albedo,
+                                     self.m_dev)
+        # compositing (raymarching.py:238-269)
+        _raymarching.composite_rays_train_forward_mixed(
+            self.sigma, self.albedo, self.deltas, self.rays, cap, N, 1e-4, self.ws, self.depth,
+            self.image)
+        # ray head (renderer.py:536-551) and the entropy regulariser (utils.py:386-391)
+        bw = self._bg_weights()
+        call("dfhip_ray_head_forward", N, ptr(self.ws), ptr(self.depth), ptr(self.image),
+             ptr(self.rays_d), ptr(self.nears), ptr(self.fars), *[ptr(w) for w in bw],
+             ptr(self.bg_color), ptr(self.out_image), ptr(self.out_depth), ptr(self.mask),
+             stream())
+        if self.lam > 0:
+            call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss), stream())
+        # backward: SDS gradient at pred_rgb (unscaled), entropy gradient x scale
+        gbw = self._bg_grads()
+        call("dfhip_ray_head_backward", N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d),
+             *[ptr(w) for w in bw], ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws),
+             None, ptr(self.head_partial), *[ptr(g) for g in gbw], stream())
+        if self.lam > 0:
+            call("dfhip_entropy_backward_accumulate", N, ptr(self.ws), ptr(scale), self.lam,
+                 ptr(self.grad_ws), stream())
+        _raymarching.composite_rays_train_backward_mixed(
+            self.grad_ws, self.grad_image, self.sigma, self.albedo, self.deltas, self.rays,
+            self.ws, self.image, cap, N, 1e-4, self.grad_sigma, self.grad_albedo, False)
+        from gridencoder.grid import _parts
+        _fieldmlp.grid_field_backward(
+            self.enc, self.xyzs, m.bound, self.mlp, self.grad_sigma, self.grad_albedo, self.d_enc,
+            self.mlp_partial, [p.grad for p in self.mlp], self.encoder.offsets, self.rows, S, Hb,
+            gridtype, align, None, None, _parts(self.rows, self.C), self.m_dev)
+        return self.loss
+
+    def embedding_backward(self):
+        """Binned embedding-gradient scatter (eager, timed like the autograd
+        path's deferred launch)."""
+        if self._emb_launch is None:
+            m = self.trainer.model
+            S, Hb, gridtype, align, offsets_host = self.meta
+            self._emb_launch = _gridencoder.binned_launcher(
+                self.d_enc, self.xyzs, m.bound, self.encoder.offsets, offsets_host,
+                self.encoder.embeddings.grad, self.cap, self.m_dev, 3, self.C, self.L, S, Hb,
+                gridtype, align, *self.bin_scratch)
+        per = 12 + self.L * self.C * 2
+        with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_dev, per):
+            self._emb_launch()
+
+    def reattach(self):
+        for p, g in self.grads:
+            p.grad = g
+
+    # ------------------------------------------------------------ helpers
+    def _bg_weights(self):
+        if self.bg_layers is None:
+            return [None] * 4
+        l1, l2 = self.bg_layers
+        return [l1.weight, l1.bias, l2.weight, l2.bias]
+
+    def _bg_grads(self):
+        if self.bg_layers is None:
+            return [None] * 4
+        return [w.grad for w in self._bg_weights()]

@@ -236,7 +236,9 @@ class NeRFRenderer(nn.Module):
         # the train path passes no min_near -> the op's default 0.2 (renderer.py:458)
         nears, fars = raymarching.near_far_from_aabb(
             rays_o, rays_d, self.aabb_train if self.training else self.aabb_infer)
-        if light_d is None:
+        if light_d is None and shading != "albedo":
+            # the albedo field never reads the light; the reference draws it
+            # anyway (renderer.py:466), which here would be seven tiny launches
             light_d = safe_normalize(rays_o[0] + torch.randn(3, device=device, dtype=torch.float))
 
         results = {}
@@ -251,7 +253,8 @@ class NeRFRenderer(nn.Module):
                 # per-sample consumers all stop at the live count
                 xyzs, dirs, deltas, rays = raymarching.march_rays_train_dev(
                     rays_o, rays_d, self.bound, self.density_bitfield, self.cascade,
-                    self.grid_size, nears, fars, counter, perturb, dt_gamma, max_steps)
+                    self.grid_size, nears, fars, counter, perturb, dt_gamma, max_steps,
+                    noises=getattr(self, "march_noises", None))
             else:
                 xyzs, dirs, deltas, rays = raymarching.march_rays_train(
                     rays_o, rays_d, self.bound, self.density_bitfield, self.cascade,
@@ -471,9 +474,12 @@ class NeRFRenderer(nn.Module):
         self.iter_density += 1
         total_step = min(16, self.local_step)
         if total_step > 0:
-            # reference: int(sum / total_step) (truncation toward zero)
-            self.mean_count = torch.div(self.step_counter[:total_step, 0].sum(), total_step,
-                                        rounding_mode="trunc")
+            # reference: int(sum / total_step); one native launch (torch's
+            # reductions here would be first-use kernel loads mid-training)
+            mc = torch.empty((), dtype=torch.int64, device=xyzs.device)
+            _dfhip.call("dfhip_mean_count", self.step_counter.data_ptr(), total_step,
+                        mc.data_ptr(), _dfhip.stream())
+            self.mean_count = mc
         self.local_step = 0
 
     def render(self, rays_o, rays_d, staged=False, max_ray_batch=4096, **kwargs):

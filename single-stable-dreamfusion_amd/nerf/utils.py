@@ -445,15 +445,20 @@ class Trainer(object):
         eligible step of each (shading, resolution), replayed afterwards."""
         from .graph import GraphedTrainStep
         model = self.model
-        text_z = self.text_z[data["dir"]] if self.opt.dir_text else self.text_z
         if self._capture_stream is None:
             self._capture_stream = torch.cuda.Stream(device=self.device)
         key = (shading, ambient_ratio, data["H"], data["W"])
         g = self._graphs.get(key)
+        # the prompt embedding of the view class: an index op whose CPU index is
+        # copied from pageable memory (which waits for the stream); the native
+        # step's synthetic guidance does not read it
+        text_z = None
+        if g is None or g.native is None:
+            text_z = self.text_z[data["dir"]] if self.opt.dir_text else self.text_z
         row = model.local_step % 16
         if g is None:
             g = GraphedTrainStep(self, data, shading, ambient_ratio, text_z, self._capture_stream)
-            g.capture()  # run_cuda advanced model.local_step while recording
+            g.capture(data)  # run_cuda advanced model.local_step while recording
             self._graphs[key] = g
         else:
             model.local_step += 1

@@ -213,7 +213,7 @@ def live_rows(t):
 
 @torch.no_grad()
 def march_rays_train_dev(rays_o, rays_d, bound, density_bitfield, C, H, nears, fars, step_counter,
-                         perturb=False, dt_gamma=0, max_steps=1024):
+                         perturb=False, dt_gamma=0, max_steps=1024, noises=None):
     """Native form of march_rays_train(..., force_all_rays=True) with NO host
     synchronisation (so a whole train step can be captured in a HIP graph).
 
@@ -231,7 +231,8 @@ def march_rays_train_dev(rays_o, rays_d, bound, density_bitfield, C, H, nears, f
     rays_d = rays_d.float()
     nears = nears.float().contiguous()
     fars = fars.float().contiguous()
-    noises = (torch.rand(n, device=dev) if perturb else torch.zeros(n, device=dev))
+    if noises is None:  # (given: the draws of another step, tests/test_gpu_native_step.py)
+        noises = (torch.rand(n, device=dev) if perturb else torch.zeros(n, device=dev))
     rays = torch.empty(n, 3, dtype=torch.int32, device=dev)
     block_sums = torch.empty(_backend.march_rays_train_scratch_ints(n), dtype=torch.int32,
                              device=dev)

@@ -114,7 +114,7 @@ def test_graph_step_matches_eager_step(gpu):
 
     _restore(model, snap)
     stream = torch.cuda.Stream()
-    g = GraphedTrainStep(trainer, batch, "albedo", 1.0, text_z, stream)
+    g = GraphedTrainStep(trainer, batch, "albedo", 1.0, text_z, stream, allow_native=False)
     torch.cuda.current_stream().synchronize()
     g.capture()
     torch.cuda.manual_seed(1234)

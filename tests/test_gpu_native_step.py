@@ -1,0 +1,125 @@
+"""GPU tests of the native albedo train step (nerf/native_step.py, csrc/step.hip):
+
+* the prologue's rays / near-far are bit-identical to dfhip_get_rays and
+  near_far_from_aabb (same device code), its draws are deterministic in
+  (seed, step), fresh per step, and distributed as the reference's
+  (U[0, 1) noise, w(t) * N(0, 1) SDS gradient, t in [min_step, max_step]);
+* one native step (prologue -> march -> field -> compositing -> head ->
+  entropy -> backward -> binned embedding backward) gives bit-identical
+  gradients to the autograd step fed the same rays, noise and SDS gradient;
+* graph-replayed native training runs, stays finite and updates every tensor.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(res, seed, graph=False):
+    import bench
+    return bench.make_trainer(res, seed, 0, 1, True, graph=graph)
+
+
+def test_prologue_rays_near_far_and_draws(gpu):
+    import _dfhip
+    import raymarching
+    from nerf.native_step import NativeAlbedoStep, eligible
+    from nerf.utils import get_rays_host_pose
+    trainer, data = _trainer(48, 3)
+    assert eligible(trainer, "albedo")
+    nat = NativeAlbedoStep(trainer, 48, 48)
+    batch = data.collate([0])
+    nat.prologue(batch["pose"], batch["intrinsics"], 5, 17)
+    want = get_rays_host_pose(batch["pose"], batch["intrinsics"], 48, 48, gpu)
+    assert torch.equal(nat.rays_o, want["rays_o"][0]) and torch.equal(nat.rays_d, want["rays_d"][0])
+    ne, fa = raymarching.near_far_from_aabb(want["rays_o"][0], want["rays_d"][0],
+                                            trainer.model.aabb_train)
+    assert torch.equal(nat.nears, ne) and torch.equal(nat.fars, fa)
+    assert int(nat.counter.abs().sum()) == 0
+    noise1, g1 = nat.noises.clone(), nat.g_image.clone()
+    assert 0 <= float(noise1.min()) and float(noise1.max()) < 1
+    assert abs(float(noise1.mean()) - 0.5) < 0.03
+    # w(t) * eps: one w per step; eps ~ N(0, 1)
+    alphas = trainer.guidance.alphas
+    w = float(g1.std())
+    ws_allowed = 1 - alphas[trainer.guidance.min_step:trainer.guidance.max_step + 1]
+    assert float(ws_allowed.min()) * 0.9 < w < float(ws_allowed.max()) * 1.1
+    assert abs(float(g1.mean())) < 0.05 * w
+    nat.prologue(batch["pose"], batch["intrinsics"], 5, 17)
+    assert torch.equal(nat.noises, noise1) and torch.equal(nat.g_image, g1)
+    nat.prologue(batch["pose"], batch["intrinsics"], 5, 18)
+    assert not torch.equal(nat.noises, noise1)
+    nat.prologue(batch["pose"], batch["intrinsics"], 6, 17)
+    assert not torch.equal(nat.noises, noise1)
+    torch.cuda.synchronize()
+    _dfhip.load()
+
+
+def test_native_step_matches_autograd_step(gpu):
+    from nerf.native_step import NativeAlbedoStep
+    res = 64
+    trainer, data = _trainer(res, 7)
+    batch = data.collate([0])
+    for _ in range(3):  # density-grid refresh + a few eager steps
+        trainer.train_iteration(batch)
+    model = trainer.model
+    params = [p for p in model.parameters() if p.requires_grad]
+    snap = [p.detach().clone() for p in params]
+
+    nat = NativeAlbedoStep(trainer, res, res)
+    nat.prologue(batch["pose"], batch["intrinsics"], 11, 1234)
+    nat.body()
+    nat.embedding_backward()
+    torch.cuda.synchronize()
+    got = [p.grad.detach().clone() for p in params]
+    got_count = nat.counter.clone()
+    got_loss = nat.loss.clone()
+    assert int(got_count[0]) > 0
+
+    # the autograd step on the same inputs
+    with torch.no_grad():
+        for p, v in zip(params, snap):
+            p.copy_(v)
+    trainer.optimizer.zero_grad(set_to_none=True)
+    g_img = nat.g_image.view(1, 3, res, res).clone()
+    trainer.guidance.sds_grad = lambda text_z, pred_rgb, *a, **k: (pred_rgb, g_img)
+    model.march_noises = nat.noises.clone()
+    model.device_count_march = True
+    eager = {"H": res, "W": res, "rays_o": nat.rays_o.view(1, -1, 3).clone(),
+             "rays_d": nat.rays_d.view(1, -1, 3).clone(), "dir": batch["dir"]}
+    text_z = trainer.text_z[batch["dir"]]
+    try:
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss = trainer.train_step(eager, "albedo", 1.0, text_z)[2]
+        trainer.backward_only(loss)
+    finally:
+        model.device_count_march = False
+        del model.march_noises
+        del trainer.guidance.sds_grad
+    torch.cuda.synchronize()
+    assert torch.equal(model.last_counter, got_count)
+    assert torch.equal(loss.detach().float(), got_loss)
+    for p, g in zip(params, got):
+        assert p.grad is not None
+        assert torch.equal(p.grad, g), (tuple(p.shape), float((p.grad - g).abs().max()))
+
+
+def test_native_graph_training_runs(gpu):
+    trainer, data = _trainer(64, 9, graph=True)
+    model = trainer.model
+    before = [p.detach().clone() for p in model.parameters() if p.requires_grad]
+    losses = []
+    for i in range(40):
+        loss = trainer.train_iteration(data.collate([i % 4]))
+        losses.append(float(loss))
+    assert len(trainer._graphs) == 1
+    g = next(iter(trainer._graphs.values()))
+    assert g.native is not None
+    assert all(np.isfinite(losses))
+    assert model.mean_density > 0
+    assert int(model.step_counter[:, 0].min()) > 0
+    after = [p.detach() for p in model.parameters() if p.requires_grad]
+    for a, b in zip(after, before):
+        assert torch.isfinite(a).all()
+        assert not torch.equal(a, b)
