@@ -383,15 +383,29 @@ __global__ __launch_bounds__(64) void k_composite_train_bwd(
     }
 }
 
-// ------------------------------------------------------------------ compositing, wave per ray
-// The same arithmetic as k_composite_train_fwd / _bwd in the same order, with a
-// ray's samples spread over the 64 lanes of one wave: each lane loads one
-// sample of the window (coalesced) and computes its alpha, then the wave runs
-// the reference's serial chain (T, the colour / weight / depth sums) over the
-// window with the per-sample values read from their lanes.  Bit-identical to
-// the one-thread-per-ray loop (same f32 operations, same order, same break);
-// 16k rays give 16k waves instead of 256.
-constexpr uint32_t kCompRaysPerBlock = 4;
+// ------------------------------------------------------------------ compositing, row per ray
+// The same arithmetic as k_composite_train_fwd / _bwd in the same order, with
+// one ray per 16-lane row of a wave (4 rays per wave): each lane loads one
+// sample of the ray's 16-sample window (coalesced), computes its alpha, and
+// the row then runs the reference's serial chain (T, the colour / weight /
+// depth sums) over the window, each step reading sample j's values with a DPP
+// row broadcast (row_newbcast:j) that the compiler folds into the consuming
+// VALU instruction.  One VALU instruction thus advances four rays, where a
+// whole-wave chain (readlane per value) spends it on one.  Bit-identical to
+// the one-thread-per-ray loop (same f32 operations, same order, same break).
+//
+// The chain is branch-free inside a window: the reference's
+// `if (T < T_thresh) break` becomes a row-uniform `alive` flag that zeroes the
+// weight of every later sample (fmaf(0, c, x) == x and x + 0 == x, so the sums
+// are unchanged), and lanes past the window's count hold alpha 0, 1 - alpha 1,
+// zero colour and delta (no-ops).  Only the window loop branches (per row).
+constexpr uint32_t kCompRaysPerBlock = 16;   // 4 waves x 4 rows
+
+template <int J>
+__device__ __forceinline__ float row_bcast(float v) {
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + J, 0xF, 0xF, false));
+}
 
 template <typename rgb_t>
 __device__ __forceinline__ void load_rgb3(const rgb_t *c, float &r, float &g, float &b) {
@@ -400,75 +414,115 @@ __device__ __forceinline__ void load_rgb3(const rgb_t *c, float &r, float &g, fl
     b = to_f(c[2]);
 }
 
+struct FwdChain {
+    float T = 1.0f, r = 0.0f, g = 0.0f, b = 0.0f, ws = 0.0f, t = 0.0f, d = 0.0f;
+    bool alive = true;
+    template <int J>
+    __device__ __forceinline__ void step(float a, float om, float cr, float cg, float cb,
+                                         float dl, float T_thresh) {
+        const float w = alive ? row_bcast<J>(a) * T : 0.0f;
+        r = fmaf(w, row_bcast<J>(cr), r);
+        g = fmaf(w, row_bcast<J>(cg), g);
+        b = fmaf(w, row_bcast<J>(cb), b);
+        t += row_bcast<J>(dl);
+        d = fmaf(w, t, d);
+        ws += w;
+        T *= row_bcast<J>(om);
+        alive = alive && !(T < T_thresh);
+    }
+};
+
 // raymarching.cu:500-577
 template <typename scalar_t, typename rgb_t>
-__global__ __launch_bounds__(64 * kCompRaysPerBlock) void k_composite_train_fwd_w(
+__global__ __launch_bounds__(256) void k_composite_train_fwd_w(
     const scalar_t *__restrict__ sigmas, const rgb_t *__restrict__ rgbs,
     const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays, uint32_t M,
     uint32_t N, float T_thresh, scalar_t *weights_sum, scalar_t *depth, scalar_t *image) {
-    const uint32_t n = blockIdx.x * kCompRaysPerBlock + (threadIdx.x >> 6);
-    if (n >= N) return;
-    const int lane = (int)(threadIdx.x & 63);
-    const uint32_t index = (uint32_t)rays[3 * n];
-    const uint32_t offset = (uint32_t)rays[3 * n + 1];
-    const uint32_t num = (uint32_t)rays[3 * n + 2];
-    float T = 1, r = 0, g = 0, b = 0, ws = 0, t = 0, d = 0;
-    if (num != 0 && offset + num <= M) {
-        bool stop = false;
-        for (uint32_t base = 0; base < num && !stop; base += 64) {
-            const uint32_t cnt = min(64u, num - base);
-            float a = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, dl = 0.0f;
-            if ((uint32_t)lane < cnt) {
-                const size_t i = (size_t)offset + base + lane;
-                a = 1.0f - __expf(-to_f(sigmas[i]) * to_f(deltas[2 * i]));
-                dl = to_f(deltas[2 * i + 1]);
-                load_rgb3(rgbs + 3 * i, cr, cg, cb);
-            }
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const float aj = rm::lane_f(a, (int)j);
-                const float w = aj * T;
-                r = fmaf(w, rm::lane_f(cr, (int)j), r);
-                g = fmaf(w, rm::lane_f(cg, (int)j), g);
-                b = fmaf(w, rm::lane_f(cb, (int)j), b);
-                t += rm::lane_f(dl, (int)j);
-                d = fmaf(w, t, d);
-                ws += w;
-                T *= 1.0f - aj;
-                if (T < T_thresh) {
-                    stop = true;
-                    break;
-                }
-            }
-        }
+    const uint32_t n = blockIdx.x * kCompRaysPerBlock + (threadIdx.x >> 4);
+    const int lane = (int)(threadIdx.x & 15);
+    uint32_t index = 0, offset = 0, num = 0;
+    if (n < N) {
+        index = (uint32_t)rays[3 * n];
+        offset = (uint32_t)rays[3 * n + 1];
+        num = (uint32_t)rays[3 * n + 2];
+        if (offset + num > M) num = 0;
     }
-    if (lane == 0) {
-        weights_sum[index] = (scalar_t)ws;
-        depth[index] = (scalar_t)d;
-        image[3 * index + 0] = (scalar_t)r;
-        image[3 * index + 1] = (scalar_t)g;
-        image[3 * index + 2] = (scalar_t)b;
+    FwdChain c;
+    for (uint32_t base = 0; base < num && c.alive; base += 16) {
+        const uint32_t cnt = min(16u, num - base);
+        float a = 0.0f, om = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, dl = 0.0f;
+        if ((uint32_t)lane < cnt) {
+            const size_t i = (size_t)offset + base + lane;
+            a = 1.0f - __expf(-to_f(sigmas[i]) * to_f(deltas[2 * i]));
+            om = 1.0f - a;
+            dl = to_f(deltas[2 * i + 1]);
+            load_rgb3(rgbs + 3 * i, cr, cg, cb);
+        }
+#define DFHIP_FSTEP(J) c.step<J>(a, om, cr, cg, cb, dl, T_thresh);
+        DFHIP_FSTEP(0) DFHIP_FSTEP(1) DFHIP_FSTEP(2) DFHIP_FSTEP(3)
+        DFHIP_FSTEP(4) DFHIP_FSTEP(5) DFHIP_FSTEP(6) DFHIP_FSTEP(7)
+        DFHIP_FSTEP(8) DFHIP_FSTEP(9) DFHIP_FSTEP(10) DFHIP_FSTEP(11)
+        DFHIP_FSTEP(12) DFHIP_FSTEP(13) DFHIP_FSTEP(14) DFHIP_FSTEP(15)
+#undef DFHIP_FSTEP
+    }
+    if (lane == 0 && n < N) {
+        weights_sum[index] = (scalar_t)c.ws;
+        depth[index] = (scalar_t)c.d;
+        image[3 * index + 0] = (scalar_t)c.r;
+        image[3 * index + 1] = (scalar_t)c.g;
+        image[3 * index + 2] = (scalar_t)c.b;
     }
 }
 
+// Backward chain: lane l of the row captures the state after sample l of the
+// window (weight, T, colour sums) and whether the reference loop reached it.
+struct BwdChain {
+    float T = 1.0f, r = 0.0f, g = 0.0f, b = 0.0f;
+    bool alive = true;
+    float wl, Tl, rl, gl, bl;
+    bool taken;
+    template <int J>
+    __device__ __forceinline__ void step(int lane, float a, float om, float cr, float cg,
+                                         float cb, float T_thresh) {
+        const float w = row_bcast<J>(a) * T;
+        r = fmaf(w, row_bcast<J>(cr), r);
+        g = fmaf(w, row_bcast<J>(cg), g);
+        b = fmaf(w, row_bcast<J>(cb), b);
+        T *= row_bcast<J>(om);
+        const bool mine = lane == J;
+        wl = mine ? w : wl;
+        Tl = mine ? T : Tl;
+        rl = mine ? r : rl;
+        gl = mine ? g : gl;
+        bl = mine ? b : bl;
+        taken = mine ? alive : taken;
+        alive = alive && !(T < T_thresh);
+    }
+};
+
 // raymarching.cu:601-682, DENSE as k_composite_train_bwd.
 template <typename scalar_t, bool DENSE, typename rgb_t>
-__global__ __launch_bounds__(64 * kCompRaysPerBlock) void k_composite_train_bwd_w(
+__global__ __launch_bounds__(256) void k_composite_train_bwd_w(
     const scalar_t *__restrict__ grad_ws, const scalar_t *__restrict__ grad_image,
     const scalar_t *__restrict__ sigmas, const rgb_t *__restrict__ rgbs,
     const scalar_t *__restrict__ deltas, const int32_t *__restrict__ rays,
     const scalar_t *__restrict__ weights_sum, const scalar_t *__restrict__ image,
     uint32_t M, uint32_t N, float T_thresh, scalar_t *grad_sigmas, rgb_t *grad_rgbs,
     int tail) {
-    const uint32_t n = blockIdx.x * kCompRaysPerBlock + (threadIdx.x >> 6);
-    if (n >= N) return;
-    const int lane = (int)(threadIdx.x & 63);
-    const uint32_t index = (uint32_t)rays[3 * n];
-    const uint32_t offset = (uint32_t)rays[3 * n + 1];
-    const uint32_t num = (uint32_t)rays[3 * n + 2];
+    const uint32_t n = blockIdx.x * kCompRaysPerBlock + (threadIdx.x >> 4);
+    const int lane = (int)(threadIdx.x & 15);
+    const int row_shift = (int)(threadIdx.x & 48);   // this row's bits in a wave ballot
     const scalar_t zero = (scalar_t)0.0f;
     const rgb_t czero = (rgb_t)0.0f;
+    uint32_t index = 0, offset = 0, num = 0, num_all = 0;
+    if (n < N) {
+        index = (uint32_t)rays[3 * n];
+        offset = (uint32_t)rays[3 * n + 1];
+        num_all = (uint32_t)rays[3 * n + 2];
+        num = (offset + num_all <= M) ? num_all : 0u;
+    }
     uint32_t done = 0;   // samples taken (the reference loop's final i)
-    if (num != 0 && offset + num <= M) {
+    if (num != 0) {
         const float gr = to_f(grad_image[3 * index + 0]);
         const float gg = to_f(grad_image[3 * index + 1]);
         const float gb = to_f(grad_image[3 * index + 2]);
@@ -477,60 +531,47 @@ __global__ __launch_bounds__(64 * kCompRaysPerBlock) void k_composite_train_bwd_
         const float gf = to_f(image[3 * index + 1]);
         const float bf = to_f(image[3 * index + 2]);
         const float wsf = to_f(weights_sum[index]);
-        float T = 1, r = 0, g = 0, b = 0;
-        bool stop = false;
-        for (uint32_t base = 0; base < num && !stop; base += 64) {
-            const uint32_t cnt = min(64u, num - base);
+        BwdChain c;
+        for (uint32_t base = 0; base < num && c.alive; base += 16) {
+            const uint32_t cnt = min(16u, num - base);
             const size_t i = (size_t)offset + base + lane;
-            float a = 0.0f, dt = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+            float a = 0.0f, om = 1.0f, dt = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
             if ((uint32_t)lane < cnt) {
                 dt = to_f(deltas[2 * i]);
                 a = 1.0f - __expf(-to_f(sigmas[i]) * dt);
+                om = 1.0f - a;
                 load_rgb3(rgbs + 3 * i, cr, cg, cb);
             }
-            // this lane's sample: weight, T after it, colour sums including it
-            float wl = 0.0f, Tl = 0.0f, rl = 0.0f, gl = 0.0f, bl = 0.0f;
-            uint32_t end = cnt;
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const float aj = rm::lane_f(a, (int)j);
-                const float w = aj * T;
-                r = fmaf(w, rm::lane_f(cr, (int)j), r);
-                g = fmaf(w, rm::lane_f(cg, (int)j), g);
-                b = fmaf(w, rm::lane_f(cb, (int)j), b);
-                T *= 1.0f - aj;
-                const bool mine = (uint32_t)lane == j;
-                wl = mine ? w : wl;
-                Tl = mine ? T : Tl;
-                rl = mine ? r : rl;
-                gl = mine ? g : gl;
-                bl = mine ? b : bl;
-                if (T < T_thresh) {
-                    stop = true;
-                    end = j + 1;
-                    break;
-                }
-            }
-            if ((uint32_t)lane < end) {
-                grad_rgbs[3 * i + 0] = grad_cast<scalar_t, rgb_t>(gr * wl);
-                grad_rgbs[3 * i + 1] = grad_cast<scalar_t, rgb_t>(gg * wl);
-                grad_rgbs[3 * i + 2] = grad_cast<scalar_t, rgb_t>(gb * wl);
-                float acc = fmaf(gr, fmaf(Tl, cr, -(rf - rl)), gg * fmaf(Tl, cg, -(gf - gl)));
-                acc = fmaf(gb, fmaf(Tl, cb, -(bf - bl)), acc);
+            c.wl = c.Tl = c.rl = c.gl = c.bl = 0.0f;
+            c.taken = false;
+#define DFHIP_BSTEP(J) c.step<J>(lane, a, om, cr, cg, cb, T_thresh);
+            DFHIP_BSTEP(0) DFHIP_BSTEP(1) DFHIP_BSTEP(2) DFHIP_BSTEP(3)
+            DFHIP_BSTEP(4) DFHIP_BSTEP(5) DFHIP_BSTEP(6) DFHIP_BSTEP(7)
+            DFHIP_BSTEP(8) DFHIP_BSTEP(9) DFHIP_BSTEP(10) DFHIP_BSTEP(11)
+            DFHIP_BSTEP(12) DFHIP_BSTEP(13) DFHIP_BSTEP(14) DFHIP_BSTEP(15)
+#undef DFHIP_BSTEP
+            const bool taken = c.taken && (uint32_t)lane < cnt;
+            if (taken) {
+                grad_rgbs[3 * i + 0] = grad_cast<scalar_t, rgb_t>(gr * c.wl);
+                grad_rgbs[3 * i + 1] = grad_cast<scalar_t, rgb_t>(gg * c.wl);
+                grad_rgbs[3 * i + 2] = grad_cast<scalar_t, rgb_t>(gb * c.wl);
+                float acc = fmaf(gr, fmaf(c.Tl, cr, -(rf - c.rl)), gg * fmaf(c.Tl, cg, -(gf - c.gl)));
+                acc = fmaf(gb, fmaf(c.Tl, cb, -(bf - c.bl)), acc);
                 acc = fmaf(gw, 1.0f - wsf, acc);
                 grad_sigmas[i] = (scalar_t)(dt * acc);
             }
-            done = base + end;
+            done = base + (uint32_t)__popcll((__ballot(taken) >> row_shift) & 0xFFFFull);
         }
     }
-    if (DENSE) {
+    if (DENSE && n < N) {
         // rows [offset + done, offset + num) of this ray, clipped to M
-        const uint64_t end = min((uint64_t)offset + num, (uint64_t)M);
-        for (uint64_t row = (uint64_t)offset + done + lane; row < end; row += 64) {
+        const uint64_t end = min((uint64_t)offset + num_all, (uint64_t)M);
+        for (uint64_t row = (uint64_t)offset + done + lane; row < end; row += 16) {
             grad_sigmas[row] = zero;
             grad_rgbs[3 * row] = czero; grad_rgbs[3 * row + 1] = czero; grad_rgbs[3 * row + 2] = czero;
         }
         if (tail && n == N - 1) {
-            for (uint64_t row = (uint64_t)offset + num + lane; row < M; row += 64) {
+            for (uint64_t row = (uint64_t)offset + num_all + lane; row < M; row += 16) {
                 grad_sigmas[row] = zero;
                 grad_rgbs[3 * row] = czero; grad_rgbs[3 * row + 1] = czero; grad_rgbs[3 * row + 2] = czero;
             }
@@ -547,7 +588,7 @@ static void launch_comp_fwd(hipStream_t s, const scalar_t *sig, const rgb_t *rgb
             sig, rgb, dl, rays, M, N, T_thresh, ws, depth, image);
     else
         k_composite_train_fwd_w<scalar_t, rgb_t>
-            <<<ceil_div(N, kCompRaysPerBlock), 64 * kCompRaysPerBlock, 0, s>>>(
+            <<<ceil_div(N, kCompRaysPerBlock), 256, 0, s>>>(
                 sig, rgb, dl, rays, M, N, T_thresh, ws, depth, image);
 }
 
@@ -562,7 +603,7 @@ static void launch_comp_bwd(hipStream_t s, const scalar_t *gws, const scalar_t *
             gws, gimg, sig, rgb, dl, rays, ws, img, M, N, T_thresh, gsig, grgb, tail);
     else
         k_composite_train_bwd_w<scalar_t, DENSE, rgb_t>
-            <<<ceil_div(N, kCompRaysPerBlock), 64 * kCompRaysPerBlock, 0, s>>>(
+            <<<ceil_div(N, kCompRaysPerBlock), 256, 0, s>>>(
                 gws, gimg, sig, rgb, dl, rays, ws, img, M, N, T_thresh, gsig, grgb, tail);
 }
 
