@@ -123,257 +123,268 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
 }
 
 // ------------------------------------------------------------------ backward
-struct Stage {                      // per-wave LDS image of one 32-sample group, [row][sample]
-    half_t x[kIn * kLd32];
-    half_t a1[kHid * kLd32];
-    half_t a2[kHid * kLd32];
-    half_t d1[kHid * kLd32];
-    half_t d2[kHid * kLd32];
-    half_t dO[16 * kLd32];          // rows 4..15 stay zero
+// Workgroup = 4 waves, two workgroups per CU (76 KB of LDS each), persistent
+// over rounds.  Per round each wave takes one 16-sample tile: recomputes the
+// forward from the saved features, runs the three transposed-weight products
+// (sample on the lane, neurons in the accumulator registers), writes the
+// encoder gradient in the [L, cap, C] layout the binned grid backward reads,
+// and stores its activations into a [sample][neuron] LDS image of the tile —
+// each lane's four neurons of one tile as ONE 8-byte write.  After a
+// workgroup barrier the weight gradients of the round's 64 samples are formed
+// with v_mfma_f32_16x16x16_f16, k = sample: both operands (neuron on the lane,
+// four samples in the registers) come straight from the images with
+// ds_read_b64_tr_b16.  The 37 output tiles (W1 8, W2 16, W3 4, and the three
+// bias vectors as products with a ones operand, 9) are split over the four
+// waves, so a wave holds at most 10 accumulator tiles instead of all of them:
+// 2 waves per SIMD instead of 1, no per-element LDS writes, no bias VALU sums.
+// Each partial entry is written by exactly one lane of the workgroup; the
+// fixed-order k_field_wgrad_sum over workgroups keeps the result deterministic.
+constexpr int kBwdWaves = 4;
+constexpr int kStLd = 312;  // stage row stride (halves): 156 dwords = 4 mod 64 -> the
+                            // 32 lanes of an 8-byte write hit 64 distinct banks
+constexpr int kColX = 0, kColA1 = 32, kColA2 = 96, kColD1 = 160, kColD2 = 224, kColDO = 288;
+
+struct StageT {
+    half_t v[16 * kStLd];   // [sample][x | a1 | a2 | d1 | d2 | dO(16, rows 4.. zero)]
 };
 
-constexpr int kBwdWaves = 4;
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
 
-// One wave's inputs for a 32-sample group: encoder features (every lane), and
+// Operand of v_mfma_f32_16x16x16_f16 with the neuron on the lane: lane
+// (g = l >> 4, i = l & 15) gets columns c0 + i of sample rows 4g .. 4g + 3
+// (ds_read_b64_tr_b16: lane 4q + p of the group supplies row 4g + q, columns
+// c0 + 4p .. c0 + 4p + 3).
+__device__ __forceinline__ half4 tr_operand(const StageT &S, int c0, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const half_t *src = S.v + (4 * g + q) * kStLd + c0 + 4 * p;
+    const fp16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+        (__attribute__((address_space(3))) fp16x4_t *)src);
+    half4 out;
+    __builtin_memcpy(&out, &r, sizeof(out));
+    return out;
+}
+
+__device__ __forceinline__ f4 mfma16(half4 a, half4 b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void st_write4(StageT &S, int sample, int col, half_t v0, half_t v1,
+                                          half_t v2, half_t v3) {
+    *reinterpret_cast<half4 *>(S.v + sample * kStLd + col) = half4{v0, v1, v2, v3};
+}
+
+// One wave's inputs for a 16-sample tile: encoder features (every lane), and
 // for the output-layer lanes (h == 0) positions and incoming gradients.
-template <typename rgb_t> struct GroupInT {
-    half8 xb[2];
-    float xyz[2][3], gs[2], grgb[2][3];
+struct TileIn {
+    half8 xb;
+    float xyz[3], gs, grgb[3];
 };
 
 template <typename rgb_t>
-__device__ __forceinline__ void load_group_t(GroupInT<rgb_t> &g, uint32_t grp,
-                                             const half_t *enc, const float *xyz,
-                                             const float *grad_sigma, const rgb_t *grad_rgb,
-                                             uint32_t M, int c, int h) {
+__device__ __forceinline__ void load_tile(TileIn &g, uint32_t tile, const half_t *enc,
+                                          const float *xyz, const float *grad_sigma,
+                                          const rgb_t *grad_rgb, uint32_t M, int c, int h) {
+    const uint32_t sample = tile * 16 + c;
+    g.xb = load_x(enc, sample, M, h);
+    const bool v = (h == 0) && sample < M;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t sample = grp * 32 + 16 * q + c;
-        g.xb[q] = load_x(enc, sample, M, h);
-        const bool v = (h == 0) && sample < M;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            g.xyz[q][d] = v ? xyz[(size_t)sample * 3 + d] : 0.0f;
-            g.grgb[q][d] = v ? (float)grad_rgb[(size_t)sample * 3 + d] : 0.0f;
-        }
-        g.gs[q] = v ? grad_sigma[sample] : 0.0f;
+    for (int d = 0; d < 3; ++d) {
+        g.xyz[d] = v ? xyz[(size_t)sample * 3 + d] : 0.0f;
+        g.grgb[d] = v ? (float)grad_rgb[(size_t)sample * 3 + d] : 0.0f;
     }
+    g.gs = v ? grad_sigma[sample] : 0.0f;
 }
 
 // PERM: enc holds the fused forward's permuted feature order (k_field_fwd_fused);
 // otherwise the natural [M, 32] encoder output.  M = *m_dev (clamped to cap)
 // when m_dev is given; d_enc is [16, cap, 2].
 template <typename rgb_t, bool PERM>
-__global__ __launch_bounds__(256) void k_field_bwd(
+__global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
     const half_t *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
     const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
     const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t cap,
     const int32_t *__restrict__ m_dev,
     half_t *__restrict__ d_enc,     // [16, cap, 2] (level-major)
     float *__restrict__ partial) {  // [gridDim.x, kParams]
-    typedef GroupInT<rgb_t> GroupIn;
-    auto load_group = load_group_t<rgb_t>;
     __shared__ Weights W;
     __shared__ WeightsT T;
-    __shared__ Stage stage[kBwdWaves];
+    __shared__ StageT stage[kBwdWaves];
     load_weights<PERM>(W, &T, w1, b1, w2, b2, w3, b3);
     const uint32_t M = active_count(m_dev, cap);
     const int wave = threadIdx.x >> 6;
-    Stage &S = stage[wave];
-    for (int i = threadIdx.x & 63; i < 16 * kLd32; i += 64) S.dO[i] = (half_t)0.0f;
-    __syncthreads();
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    StageT &S = stage[wave];
+    __syncthreads();
 
-    f4 gw1[4][2], gw2[4][4], gw3[4];
+    // this wave's accumulator tiles (see the ownership table below)
+    f4 acc[10];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        gw3[i] = f4{0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) gw1[i][j] = f4{0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gw2[i][j] = f4{0, 0, 0, 0};
-    }
-    // bias gradients: per-lane sums of the lane's own D-layout values (neuron
-    // 16 t + 4 h + r of sample c), reduced over the 16 sample lanes at the end
-    float gb1[4][4] = {}, gb2[4][4] = {}, gb3[4] = {};
+    for (int i = 0; i < 10; ++i) acc[i] = f4{0, 0, 0, 0};
+    const half4 ones = half4{(half_t)1.0f, (half_t)1.0f, (half_t)1.0f, (half_t)1.0f};
 
-    const uint32_t groups = ceil_div(M, 32u);
-    const uint32_t gstride = gridDim.x * kBwdWaves;
-    // the next group's inputs are loaded while this one is processed (one
-    // wave per SIMD cannot hide HBM latency otherwise)
-    GroupIn cur;
-    const uint32_t grp0 = blockIdx.x * kBwdWaves + wave;
-    if (grp0 < groups) load_group(cur, grp0, enc, xyz, grad_sigma, grad_rgb, M, c, h);
-    for (uint32_t grp = grp0; grp < groups; grp += gstride) {
-        GroupIn nxt;
-        if (grp + gstride < groups)
-            load_group(nxt, grp + gstride, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    const uint32_t tiles = ceil_div(M, 16u);
+    const uint32_t per_round = gridDim.x * kBwdWaves;
+    const uint32_t rounds = ceil_div(tiles, per_round);
+    TileIn cur;
+    uint32_t tile = blockIdx.x * kBwdWaves + wave;
+    load_tile<rgb_t>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    for (uint32_t round = 0; round < rounds; ++round, tile += per_round) {
+        // the next round's inputs are loaded while this one is processed
+        TileIn nxt;
+        load_tile<rgb_t>(nxt, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        const uint32_t sample = tile * 16 + c;
+        const bool valid = sample < M;
+        Fwd F;
+        forward_tile(W, cur.xb, c, h, F);
+        // dL/d(output layer), f16 as autocast's backward produces it
+        half_t dO[4] = {(half_t)0.0f, (half_t)0.0f, (half_t)0.0f, (half_t)0.0f};
+        if (h == 0 && valid) {
+            const float y = (float)(half_t)F.o[0] + gaussian(cur.xyz);
+            // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
+            const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
+            dO[0] = (half_t)(cur.gs * expf(yc));
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int col = 16 * q + c;  // column in the 32-sample stage
-            const uint32_t sample = grp * 32 + col;
-            const bool valid = sample < M;
-            const half8 xb = cur.xb[q];
-            Fwd F;
-            forward_tile(W, xb, c, h, F);
-            // dL/d(output layer), f16 as autocast's backward produces it
-            half8 dob = half8{};
-            if (h == 0) {
-                half_t dO[4] = {(half_t)0.0f, (half_t)0.0f, (half_t)0.0f, (half_t)0.0f};
-                if (valid) {
-                    const float y = (float)(half_t)F.o[0] + gaussian(cur.xyz[q]);
-                    // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
-                    const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
-                    dO[0] = (half_t)(cur.gs[q] * expf(yc));
-#pragma unroll
-                    for (int r = 1; r < 4; ++r) {
-                        const float a = (float)(half_t)(1.0f / (1.0f + expf(-(float)(half_t)F.o[r])));
-                        const float g = (float)(half_t)cur.grgb[q][r - 1];
-                        dO[r] = (half_t)(g * (1.0f - a) * a);  // sigmoid_backward in f16 (opmath f32)
-                    }
-                }
-                dob = half8{dO[0], dO[1], dO[2], dO[3], (half_t)0.0f, (half_t)0.0f, (half_t)0.0f,
-                            (half_t)0.0f};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) S.dO[r * kLd32 + col] = dO[r];
+            for (int r = 1; r < 4; ++r) {
+                const float a = (float)(half_t)(1.0f / (1.0f + expf(-(float)(half_t)F.o[r])));
+                const float g = (float)(half_t)cur.grgb[r - 1];
+                dO[r] = (half_t)(g * (1.0f - a) * a);  // sigmoid_backward in f16 (opmath f32)
             }
-            // hidden layer 2: dA2^T = W3^T dO^T, ReLU mask
-            half_t dz2[4][4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const f4 d = mfma(a_nat(T.w3t, kLd32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    dz2[u][r] = F.a2[u][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
-            }
-            // hidden layer 1: dA1^T = W2^T dZ2^T, ReLU mask
-            half_t dz1[4][4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                f4 d = f4{0, 0, 0, 0};
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    d = mfma(a_perm(T.w2t, kLd64, 16 * t + c, s, h), b_from_tiles(dz2, s), d);
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    dz1[t][r] = F.a1[t][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
-            }
-            // encoder features: dX^T = W1^T dZ1^T -> [L, B, C] directly
-#pragma unroll
-            for (int f = 0; f < 2; ++f) {
-                f4 d = f4{0, 0, 0, 0};
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    d = mfma(a_perm(T.w1t, kLd64, 16 * f + c, s, h), b_from_tiles(dz1, s), d);
-                if (valid) {
-                    // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
-                    const uint32_t lv = 8 * f + 2 * h;
-                    typedef _Float16 half2v __attribute__((ext_vector_type(2)));
-                    *reinterpret_cast<half2v *>(d_enc + ((size_t)lv * cap + sample) * 2) =
-                        half2v{(half_t)d[0], (half_t)d[1]};
-                    *reinterpret_cast<half2v *>(d_enc + ((size_t)(lv + 1) * cap + sample) * 2) =
-                        half2v{(half_t)d[2], (half_t)d[3]};
-                }
-            }
-            // stage [row][sample] images for the weight gradients
-#pragma unroll
-            for (int j = 0; j < 8; ++j) S.x[(8 * h + j) * kLd32 + col] = xb[j];
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = (16 * t + 4 * h + r) * kLd32 + col;
-                    S.a1[row] = F.a1[t][r];
-                    S.a2[row] = F.a2[t][r];
-                    S.d1[row] = dz1[t][r];
-                    S.d2[row] = dz2[t][r];
-                    gb1[t][r] += (float)dz1[t][r];
-                    gb2[t][r] += (float)dz2[t][r];
-                }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) gb3[r] += (float)dob[r];
         }
-        wave_lds_sync();
-        // weight gradients over the group's 32 samples (k = sample)
+        const half8 dob = half8{dO[0], dO[1], dO[2], dO[3], (half_t)0.0f, (half_t)0.0f,
+                                (half_t)0.0f, (half_t)0.0f};
+        // hidden layer 2: dA2^T = W3^T dO^T, ReLU mask
+        half_t dz2[4][4];
 #pragma unroll
-        for (int tn = 0; tn < 4; ++tn) {
-            const half8 a_d1 = a_nat(S.d1, kLd32, 16 * tn + c, 0, h);
-            const half8 a_d2 = a_nat(S.d2, kLd32, 16 * tn + c, 0, h);
+        for (int u = 0; u < 4; ++u) {
+            const f4 d = mfma(a_nat(T.w3t, kLd32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
 #pragma unroll
-            for (int tf = 0; tf < 2; ++tf)
-                gw1[tn][tf] = mfma(a_d1, a_nat(S.x, kLd32, 16 * tf + c, 0, h), gw1[tn][tf]);
-#pragma unroll
-            for (int tm = 0; tm < 4; ++tm)
-                gw2[tn][tm] = mfma(a_d2, a_nat(S.a1, kLd32, 16 * tm + c, 0, h), gw2[tn][tm]);
-            gw3[tn] = mfma(a_nat(S.dO, kLd32, c, 0, h), a_nat(S.a2, kLd32, 16 * tn + c, 0, h), gw3[tn]);
+            for (int r = 0; r < 4; ++r)
+                dz2[u][r] = F.a2[u][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
         }
-        wave_lds_sync();  // the stage is rewritten by the next group
+        // hidden layer 1: dA1^T = W2^T dZ2^T, ReLU mask
+        half_t dz1[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            f4 d = f4{0, 0, 0, 0};
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                d = mfma(a_perm(T.w2t, kLd64, 16 * t + c, s2, h), b_from_tiles(dz2, s2), d);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                dz1[t][r] = F.a1[t][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
+        }
+        // encoder features: dX^T = W1^T dZ1^T -> [L, B, C] directly
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            f4 d = f4{0, 0, 0, 0};
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                d = mfma(a_perm(T.w1t, kLd64, 16 * f + c, s2, h), b_from_tiles(dz1, s2), d);
+            if (valid) {
+                // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
+                const uint32_t lv = 8 * f + 2 * h;
+                typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<half2v *>(d_enc + ((size_t)lv * cap + sample) * 2) =
+                    half2v{(half_t)d[0], (half_t)d[1]};
+                *reinterpret_cast<half2v *>(d_enc + ((size_t)(lv + 1) * cap + sample) * 2) =
+                    half2v{(half_t)d[2], (half_t)d[3]};
+            }
+        }
+        // [sample][neuron] image of the tile (invalid samples: dO = 0 so every
+        // gradient row is zero and they add nothing below)
+        *reinterpret_cast<half8 *>(S.v + c * kStLd + kColX + 8 * h) = cur.xb;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int col = 16 * t + 4 * h;
+            st_write4(S, c, kColA1 + col, F.a1[t][0], F.a1[t][1], F.a1[t][2], F.a1[t][3]);
+            st_write4(S, c, kColA2 + col, F.a2[t][0], F.a2[t][1], F.a2[t][2], F.a2[t][3]);
+            st_write4(S, c, kColD1 + col, dz1[t][0], dz1[t][1], dz1[t][2], dz1[t][3]);
+            st_write4(S, c, kColD2 + col, dz2[t][0], dz2[t][1], dz2[t][2], dz2[t][3]);
+        }
+        st_write4(S, c, kColDO + 4 * h, dO[0], dO[1], dO[2], dO[3]);  // h > 0: zeros
+        __syncthreads();
+        // weight gradients over the round's 4 x 16 samples.  Tile ownership:
+        //   wave 0 / 1: W2 rows tn in {0,1} / {2,3} x 4 column tiles, b2 rows tn
+        //   wave 2 / 3: W1 rows tn in {0,1} / {2,3} x 2 feature tiles, b1 rows tn,
+        //               W3 columns tm in {0,1} / {2,3}; wave 2 also b3
+#pragma unroll
+        for (int st = 0; st < kBwdWaves; ++st) {
+            const StageT &X = stage[st];
+            if (wave < 2) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int tn = 2 * wave + k;
+                    const half4 a = tr_operand(X, kColD2 + 16 * tn, lane);
+#pragma unroll
+                    for (int tm = 0; tm < 4; ++tm)
+                        acc[5 * k + tm] = mfma16(a, tr_operand(X, kColA1 + 16 * tm, lane),
+                                                 acc[5 * k + tm]);
+                    acc[5 * k + 4] = mfma16(a, ones, acc[5 * k + 4]);
+                }
+            } else {
+                const int w2i = wave - 2;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int tn = 2 * w2i + k;
+                    const half4 a = tr_operand(X, kColD1 + 16 * tn, lane);
+#pragma unroll
+                    for (int tf = 0; tf < 2; ++tf)
+                        acc[3 * k + tf] = mfma16(a, tr_operand(X, kColX + 16 * tf, lane),
+                                                 acc[3 * k + tf]);
+                    acc[3 * k + 2] = mfma16(a, ones, acc[3 * k + 2]);
+                }
+                const half4 ao = tr_operand(X, kColDO, lane);
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+                    acc[6 + k] = mfma16(ao, tr_operand(X, kColA2 + 16 * (2 * w2i + k), lane),
+                                        acc[6 + k]);
+                if (wave == 2) acc[8] = mfma16(ao, ones, acc[8]);
+            }
+        }
+        __syncthreads();  // the images are rewritten next round
         cur = nxt;
     }
 
-    // ---- fixed-order workgroup reduction -> partial[blockIdx.x]
-    __syncthreads();
-    float *red = reinterpret_cast<float *>(&stage[0]);  // kParams floats (26 KB) reuse the stage
-    for (int w = 0; w < kBwdWaves; ++w) {
-        if (wave == w) {
-            const bool first = (w == 0);
+    // ---- this workgroup's partial: every entry written by exactly one lane.
+    // Accumulator element r of lane (c, h): row 4h + r, column c of the tile.
+    float *out = partial + (size_t)blockIdx.x * kParams;
+    if (wave < 2) {
 #pragma unroll
-            for (int tn = 0; tn < 4; ++tn) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int n = 16 * tn + 4 * h + r;
-#pragma unroll
-                    for (int tf = 0; tf < 2; ++tf) {
-                        const int p = 16 * tf + c;  // layer-1 input position
-                        float &dst = red[kOffW1 + n * kIn + (PERM ? perm_feature(p) : p)];
-                        dst = first ? gw1[tn][tf][r] : dst + gw1[tn][tf][r];
-                    }
-#pragma unroll
-                    for (int tm = 0; tm < 4; ++tm) {
-                        float &dst = red[kOffW2 + n * kHid + 16 * tm + c];
-                        dst = first ? gw2[tn][tm][r] : dst + gw2[tn][tm][r];
-                    }
-                }
-                if (h == 0)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float &dst = red[kOffW3 + r * kHid + 16 * tn + c];
-                        dst = first ? gw3[tn][r] : dst + gw3[tn][r];
-                    }
-            }
-            // bias: sum over the 16 sample lanes (c) of each lane group
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v1 = gb1[t][r], v2 = gb2[t][r];
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) {
-                        v1 += __shfl_xor(v1, o, 64);
-                        v2 += __shfl_xor(v2, o, 64);
-                    }
-                    if (c == 0) {
-                        float &d1 = red[kOffB1 + 16 * t + 4 * h + r];
-                        d1 = first ? v1 : d1 + v1;
-                        float &d2 = red[kOffB2 + 16 * t + 4 * h + r];
-                        d2 = first ? v2 : d2 + v2;
-                    }
-                }
+        for (int k = 0; k < 2; ++k) {
+            const int tn = 2 * wave + k;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float v3 = gb3[r];
+                const int n = 16 * tn + 4 * h + r;
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) v3 += __shfl_xor(v3, o, 64);
-                if (lane == 0) {
-                    float &d3 = red[kOffB3 + r];
-                    d3 = first ? v3 : d3 + v3;
-                }
+                for (int tm = 0; tm < 4; ++tm)
+                    out[kOffW2 + n * kHid + 16 * tm + c] = acc[5 * k + tm][r];
+                if (c == 0) out[kOffB2 + n] = acc[5 * k + 4][r];
             }
         }
-        __syncthreads();
+    } else {
+        const int w2i = wave - 2;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int tn = 2 * w2i + k;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = 16 * tn + 4 * h + r;
+#pragma unroll
+                for (int tf = 0; tf < 2; ++tf) {
+                    const int p = 16 * tf + c;  // layer-1 input position
+                    out[kOffW1 + n * kIn + (PERM ? perm_feature(p) : p)] = acc[3 * k + tf][r];
+                }
+                if (c == 0) out[kOffB1 + n] = acc[3 * k + 2][r];
+            }
+            if (h == 0)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    out[kOffW3 + r * kHid + 16 * (2 * w2i + k) + c] = acc[6 + k][r];
+        }
+        if (wave == 2 && lane == 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[kOffB3 + r] = acc[8][r];
     }
-    float *out = partial + (size_t)blockIdx.x * kParams;
-    for (int i = threadIdx.x; i < kParams; i += blockDim.x) out[i] = red[i];
 }
 
 // Sum the per-workgroup partials (fixed order) into the six f32 gradients:
@@ -410,8 +421,8 @@ static uint32_t bwd_blocks(uint32_t M) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t want = ceil_div(ceil_div(M, 32u), (uint32_t)kBwdWaves);
-    const uint32_t cap = (uint32_t)cus;
+    const uint32_t want = ceil_div(ceil_div(M, 16u), (uint32_t)kBwdWaves);
+    const uint32_t cap = 2u * (uint32_t)cus;  // two workgroups per CU
     return want < cap ? (want ? want : 1u) : cap;
 }
 
