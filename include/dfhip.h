@@ -407,6 +407,19 @@ int dfhip_grid_encode_backward_binned(int grad_dtype, const void *grad_lbc, cons
                                       uint32_t L, float S, uint32_t H, uint32_t gridtype,
                                       int align_corners, uint32_t *entries, uint32_t *counts,
                                       float *partial, int accumulate, dfhip_stream_t stream);
+/* The same in two phases, so the binning (which reads positions only) can run
+ * on a second stream beside the forward / MLP backward: phase 1 = bin the
+ * samples (entries / counts), 2 = walk + sum (needs phase 1's entries / counts
+ * for the same positions and count), 3 = both (dfhip_grid_encode_backward_binned). */
+int dfhip_grid_encode_backward_binned_phase(int phase, int grad_dtype, const void *grad_lbc,
+                                            const float *inputs, float bound,
+                                            const int32_t *offsets, const int32_t *offsets_host,
+                                            float *grad_embeddings, uint32_t B,
+                                            const int32_t *m_dev, uint32_t D, uint32_t C,
+                                            uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                            int align_corners, uint32_t *entries,
+                                            uint32_t *counts, float *partial, int accumulate,
+                                            dfhip_stream_t stream);
 
 /* nerf/utils.py:708-713 scaler.step(optimizer); scaler.update() for
  * torch.optim.Adam (csrc/optim.hip): non-finite check of every grad, then (if

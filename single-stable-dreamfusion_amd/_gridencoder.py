@@ -124,7 +124,7 @@ def grid_encode_backward_binned(*args, **kw):
 
 def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddings,
                     B, m_dev, D, C, L, S, H, gridtype, align_corners, entries, counts,
-                    partial, accumulate=False):
+                    partial, accumulate=False, phase=3):
     """grad_lbc [L, B, C] (B = capacity), inputs [B, D] raw positions in
     [-bound, bound] (bound > 0) or [0, 1] (bound = 0); rows [0, m_dev[0]) walked
     when m_dev is given.  grad_embeddings [rows, C] f32 is overwritten (or
@@ -142,7 +142,9 @@ def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddi
     if m_dev is not None:
         checked(m_dev, "m_dev", "int")
     off = np.ascontiguousarray(offsets_host, dtype=np.int32)
-    args = (_d.dtype_code(grad_lbc, "grad"), ptr(grad_lbc), ptr(inputs), float(bound),
+    if phase not in (1, 2, 3):
+        raise RuntimeError("phase must be 1 (bin), 2 (walk + sum) or 3 (both)")
+    args = (int(phase), _d.dtype_code(grad_lbc, "grad"), ptr(grad_lbc), ptr(inputs), float(bound),
             ptr(offsets), off.ctypes.data, ptr(grad_embeddings), int(B), ptr(m_dev), int(D),
             int(C), int(L), float(S), int(H), int(gridtype), int(bool(align_corners)),
             ptr(entries), ptr(counts), ptr(partial), int(bool(accumulate)))
@@ -151,5 +153,5 @@ def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddi
     def launch(_keep=keep):
         """Launch on the current stream with the validated, pre-marshalled
         arguments (the graph-replayed step calls this every step)."""
-        call("dfhip_grid_encode_backward_binned", *args, stream())
+        call("dfhip_grid_encode_backward_binned_phase", *args, stream())
     return launch

@@ -418,13 +418,17 @@ extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *o
     return DFHIP_OK;
 }
 
-extern "C" int dfhip_grid_encode_backward_binned(
-    int grad_dtype, const void *grad_lbc, const float *inputs, float bound,
+extern "C" int dfhip_grid_encode_backward_binned_phase(
+    int phase, int grad_dtype, const void *grad_lbc, const float *inputs, float bound,
     const int32_t *offsets, const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
     const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
     uint32_t gridtype, int align_corners, uint32_t *entries, uint32_t *counts, float *partial,
     int accumulate, dfhip_stream_t stream) {
     const char *name = "grid_encode_backward_binned";
+    if (phase < 1 || phase > 3) {
+        set_error("%s: phase must be 1 (bin), 2 (walk + sum) or 3 (both), got %d", name, phase);
+        return DFHIP_EINVAL;
+    }
     if (D != 3 || (C != 1 && C != 2 && C != 4)) {
         set_error("%s: supports D=3 with C in {1,2,4} (got D=%u C=%u)", name, D, C);
         return DFHIP_EINVAL;
@@ -453,8 +457,10 @@ extern "C" int dfhip_grid_encode_backward_binned(
         }
         const uint32_t tiles = ceil_div(B, gb::kTile);
         const uint32_t gbin = tiles < 4096u ? tiles : 4096u;
-        gb::k_bin<3><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype, align_corners, dyn,
-                                          B, counts, entries);
+        if (phase & 1)
+            gb::k_bin<3><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype, align_corners,
+                                              dyn, B, counts, entries);
+        if (!(phase & 2)) return check_launch(name);
         const dim3 g(gb::kXcds * bi.nslots);
         const size_t lds = ((size_t)1 << bi.shift) * C * sizeof(double);
 #define DFHIP_WALK(GT, CC)                                                                      \
@@ -467,10 +473,22 @@ extern "C" int dfhip_grid_encode_backward_binned(
         }
 #undef DFHIP_WALK
     } else {
+        if (!(phase & 2)) return DFHIP_OK;
         (void)hipMemsetAsync(partial, 0, gb::partial_floats(bi, C) * sizeof(float), s);
     }
     const uint64_t want = ceil_div<uint64_t>((uint64_t)total_rows * C, 256);
     gb::k_sum<float><<<(uint32_t)(want < 4096 ? want : 4096), 256, 0, s>>>(
         partial, bi, C, total_rows, grad_embeddings, accumulate);
     return check_launch(name);
+}
+
+extern "C" int dfhip_grid_encode_backward_binned(
+    int grad_dtype, const void *grad_lbc, const float *inputs, float bound,
+    const int32_t *offsets, const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
+    const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+    uint32_t gridtype, int align_corners, uint32_t *entries, uint32_t *counts, float *partial,
+    int accumulate, dfhip_stream_t stream) {
+    return dfhip_grid_encode_backward_binned_phase(
+        3, grad_dtype, grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddings, B, m_dev,
+        D, C, L, S, H, gridtype, align_corners, entries, counts, partial, accumulate, stream);
 }
