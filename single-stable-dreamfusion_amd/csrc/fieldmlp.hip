@@ -398,8 +398,18 @@ __global__ __launch_bounds__(1024) void k_field_wgrad_sum(const float *__restric
     const int col = threadIdx.x & 63, j = threadIdx.x >> 6;
     const int i = blockIdx.x * 64 + col;
     float s = 0.0f;
-    if (i < kParams)
-        for (uint32_t p = j; p < parts; p += 16) s += partial[(size_t)p * kParams + i];
+    if (i < kParams) {
+        // parts j, j + 16, ... added in that order; eight loads in flight
+        uint32_t p = j;
+        for (; p + 7 * 16 < parts; p += 8 * 16) {
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = partial[(size_t)(p + 16 * u) * kParams + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += x[u];
+        }
+        for (; p < parts; p += 16) s += partial[(size_t)p * kParams + i];
+    }
     lane_sum[j][col] = s;
     __syncthreads();
     if (j != 0 || i >= kParams) return;

@@ -362,7 +362,15 @@ __global__ __launch_bounds__(256) void k_sum(const float *__restrict__ partial, 
         const float *src = partial + bi.pbase[l] + (size_t)k * P * srows * C + (size_t)off * C + ch;
         float s = accumulate ? (float)out[i] : 0.0f;
         double t = 0.0;
-        for (uint32_t p = 0; p < P; ++p) t += (double)src[(size_t)p * srows * C];
+        uint32_t p = 0;
+        for (; p + 4 <= P; p += 4) {  // parts added in order, four loads in flight
+            float x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = src[(size_t)(p + u) * srows * C];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t += (double)x[u];
+        }
+        for (; p < P; ++p) t += (double)src[(size_t)p * srows * C];
         out[i] = (out_t)(s + (float)t);
     }
 }

@@ -45,11 +45,14 @@ __device__ __forceinline__ void load_w(W &w, const float *w1, const float *b1, c
     for (int i = threadIdx.x; i < kB2; i += blockDim.x) w.b2[i] = r16(b2[i]);
 }  // (callers __syncthreads before reading)
 
-// The network kernels give each ray kSub = 4 lanes (consecutive threads):
-// sub-lane q makes feature columns q, q + 4, q + 8 and hidden units
-// [16q, 16q + 16), the output layer's partial sums are combined with two
-// xor-shuffles (the same order in all four lanes).  A block is 64 rays.
-constexpr int kSub = 4;
+// The network kernels give each ray kSub = 16 lanes (consecutive threads):
+// sub-lane q makes frequency column q (q < 12) and hidden units
+// [kPer q, kPer q + kPer), the output layer's partial sums are combined with
+// four xor-shuffles (the same order in all sixteen lanes).  A block is 16
+// rays; 16k rays are 4096 waves (4 per SIMD; four lanes per ray left one wave
+// per SIMD to hide every LDS and global latency).
+constexpr int kSub = 16;
+constexpr int kPer = kHid / kSub;  // hidden units per lane
 constexpr int kRays = 256 / kSub;  // rays per 256-thread block
 
 // freqencoder.cu:30-58 for D = 3, degree 6 (same expression as k_freq_fwd),
@@ -59,8 +62,9 @@ __device__ __forceinline__ void features_part(const float *d, int q, float *sx) 
 #pragma unroll
         for (int c = 0; c < 3; ++c) sx[c] = r16(d[c]);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < (12 + kSub - 1) / kSub; ++i) {
         const int col = q + kSub * i;  // 0..11: frequency col >> 1, sin / cos col & 1
+        if (col >= 12) break;
         const float phase = (float)(col & 1) * kHalfPi;
 #pragma unroll
         for (int c = 0; c < 3; ++c) sx[3 + 3 * col + c] = r16(sinf(scalbnf(d[c], col >> 1) + phase));
@@ -69,11 +73,11 @@ __device__ __forceinline__ void features_part(const float *d, int q, float *sx) 
 
 // This sub-lane's 16 hidden units (f16 values) and the full f16 output
 // pre-activation (partials combined across the ray's four lanes).
-__device__ __forceinline__ void mlp_part(const W &w, const float *x, int q, float h[16],
+__device__ __forceinline__ void mlp_part(const W &w, const float *x, int q, float h[kPer],
                                         float o[kOut]) {
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
-        const int j = 16 * q + jj;
+    for (int jj = 0; jj < kPer; ++jj) {
+        const int j = kPer * q + jj;
         float a = 0.0f;
 #pragma unroll
         for (int i = 0; i < kIn; ++i) a = fmaf(x[i], w.w1[j * kIn + i], a);
@@ -84,9 +88,9 @@ __device__ __forceinline__ void mlp_part(const W &w, const float *x, int q, floa
     for (int k = 0; k < kOut; ++k) {
         float a = 0.0f;
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) a = fmaf(h[jj], w.w2[k * kHid + 16 * q + jj], a);
-        a = a + __shfl_xor(a, 1, 64);
-        a = a + __shfl_xor(a, 2, 64);
+        for (int jj = 0; jj < kPer; ++jj) a = fmaf(h[jj], w.w2[k * kHid + kPer * q + jj], a);
+#pragma unroll
+        for (int o2 = 1; o2 < kSub; o2 <<= 1) a = a + __shfl_xor(a, o2, 64);
         o[k] = r16(a + w.b2[k]);
     }
 }
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(256) void k_head_fwd_net(
     const bool live = n < N;
     if (live) features_part(rays_d + 3 * (size_t)n, q, s_x[r]);
     __syncthreads();
-    float x[kIn], h[16], o[kOut];
+    float x[kIn], h[kPer], o[kOut];
 #pragma unroll
     for (int i = 0; i < kIn; ++i) x[i] = live ? s_x[r][i] : 0.0f;
     mlp_part(w, x, q, h, o);
@@ -188,7 +192,7 @@ __global__ __launch_bounds__(256) void k_head_bwd_net(
     else if (q == 0)
         for (int i = 0; i < kIn; ++i) s_x[r][i] = 0.0f;
     __syncthreads();
-    float x[kIn], h[16], o[kOut];
+    float x[kIn], h[kPer], o[kOut];
 #pragma unroll
     for (int i = 0; i < kIn; ++i) x[i] = s_x[r][i];
     mlp_part(w, x, q, h, o);
@@ -216,8 +220,8 @@ __global__ __launch_bounds__(256) void k_head_bwd_net(
         dout[k] = r16(dbg * (1.0f - bg[k]) * bg[k]);  // sigmoid_backward, f16
     }
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
-        const int j = 16 * q + jj;
+    for (int jj = 0; jj < kPer; ++jj) {
+        const int j = kPer * q + jj;
         float a = 0.0f;
 #pragma unroll
         for (int k = 0; k < kOut; ++k) a = fmaf(dout[k], w.w2[k * kHid + j], a);
@@ -257,8 +261,18 @@ __global__ __launch_bounds__(1024) void k_head_wsum(const float *__restrict__ pa
     const int o = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int p = blockIdx.x * 64 + o;
     float s = 0.0f;
-    if (p < kParams)
-        for (uint32_t b = grp; b < blocks; b += 16) s += partial[(size_t)b * kParams + p];
+    if (p < kParams) {
+        // rows grp, grp + 16, ... added in that order; eight loads in flight
+        uint32_t b = grp;
+        for (; b + 7 * 16 < blocks; b += 8 * 16) {
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = partial[(size_t)(b + 16 * u) * kParams + p];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += x[u];
+        }
+        for (; b < blocks; b += 16) s += partial[(size_t)b * kParams + p];
+    }
     red[grp][o] = s;
     __syncthreads();
     if (grp != 0 || p >= kParams) return;

@@ -9,6 +9,9 @@
 //      (torch._amp_foreach_non_finite_check_and_unscale_ with inv_scale 1,
 //      as GradScaler._check_inf_per_device does for a fused optimizer);
 //   2. k_adam: if !found_inf, per element exactly torch's fused Adam
+//      (the bias corrections, per-tensor constants, are evaluated once per
+//      block with the same f32 expressions; blocks map to tensors through a
+//      block table and stream float4s)
 //      (ATen FusedAdamKernel / fused_adam_utils.cuh, ADAM mode, no amsgrad):
 //        g = grad / scale;  g += wd * p
 //        m = b1 * m + (1 - b1) * g;  v = b2 * v + (1 - b2) * g * g
@@ -29,6 +32,8 @@ namespace dfhip {
 namespace opt {
 
 constexpr int kMaxTensors = 24;
+constexpr uint32_t kThreads = 256;
+constexpr uint32_t kPerBlock = kThreads * 4 * 2;  // two float4 per thread
 
 struct Tensor {
     float *p;
@@ -37,63 +42,113 @@ struct Tensor {
     float *v;
     float *step;
     uint64_t n;
-    uint64_t start;  // first element in the concatenated index space
+    uint32_t block0;  // first block of this tensor (blocks of kPerBlock elements)
     float lr, b1, b2, eps, wd;
 };
 
 struct Batch {
     Tensor t[kMaxTensors];
     int count;
-    uint64_t total;
+    uint32_t blocks;
 };
 
-__device__ __forceinline__ int find_tensor(const Batch &B, uint64_t i) {
+// The tensor of this (wave-uniform) block: a scalar scan of the block table.
+__device__ __forceinline__ int block_tensor(const Batch &B) {
     int k = 0;
-    while (k + 1 < B.count && B.t[k + 1].start <= i) ++k;
+    while (k + 1 < B.count && B.t[k + 1].block0 <= blockIdx.x) ++k;
     return k;
 }
 
-__global__ __launch_bounds__(256) void k_nonfinite(Batch B, float *found_inf) {
-    bool bad = false;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.total;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const Tensor &t = B.t[find_tensor(B, i)];
-        bad |= !isfinite(t.g[i - t.start]);
+// Elements [e0, e0 + kPerBlock) of tensor t: vectorised when the tensor's
+// base is 16-byte aligned and the chunk is whole, else element by element.
+template <typename F4, typename F1>
+__device__ __forceinline__ void for_chunk(const Tensor &t, uint64_t e0, F4 f4, F1 f1) {
+    const bool vec = ((reinterpret_cast<uintptr_t>(t.p) | reinterpret_cast<uintptr_t>(t.g) |
+                       reinterpret_cast<uintptr_t>(t.m) | reinterpret_cast<uintptr_t>(t.v)) &
+                      15u) == 0 && e0 + kPerBlock <= t.n;
+    if (vec) {
+#pragma unroll
+        for (uint32_t u = 0; u < kPerBlock / (4 * kThreads); ++u) f4(e0 / 4 + u * kThreads + threadIdx.x);
+    } else {
+        for (uint64_t j = e0 + threadIdx.x; j < t.n && j < e0 + kPerBlock; j += kThreads) f1(j);
     }
+}
+
+__global__ __launch_bounds__(kThreads) void k_nonfinite(Batch B, float *found_inf) {
+    const Tensor &t = B.t[block_tensor(B)];
+    const uint64_t e0 = (uint64_t)(blockIdx.x - t.block0) * kPerBlock;
+    bool bad = false;
+    for_chunk(
+        t, e0,
+        [&](uint64_t q) {
+            const float4 g = reinterpret_cast<const float4 *>(t.g)[q];
+            bad |= !(isfinite(g.x) && isfinite(g.y) && isfinite(g.z) && isfinite(g.w));
+        },
+        [&](uint64_t j) { bad |= !isfinite(t.g[j]); });
     if (__syncthreads_or(bad) && threadIdx.x == 0) *found_inf = 1.0f;
 }
 
-__global__ __launch_bounds__(256) void k_adam(Batch B, const float *scale, const float *found_inf) {
-    if (*found_inf != 0.0f) return;
-    const float s = *scale;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.total;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const Tensor &t = B.t[find_tensor(B, i)];
-        const uint64_t j = i - t.start;
-        const float step = *t.step + 1.0f;
-        float g = t.g[j] / s;
-        float p = t.p[j];
-        if (t.wd != 0.0f) g += t.wd * p;
-        float m = t.m[j], v = t.v[j];
-        m = t.b1 * m + (1.0f - t.b1) * g;
-        v = t.b2 * v + (1.0f - t.b2) * g * g;
-        const float bc1 = 1.0f - powf(t.b1, step);
-        const float step_size = t.lr / bc1;
-        const float bc2 = 1.0f - powf(t.b2, step);
-        const float denom = (sqrtf(v) / sqrtf(bc2)) + t.eps;
-        p -= step_size * m / denom;
-        t.p[j] = p;
-        t.m[j] = m;
-        t.v[j] = v;
-    }
+struct AdamK {
+    float s, step_size, bc2s;
+};
+
+__device__ __forceinline__ float adam1(const Tensor &t, const AdamK &k, float g, float &p,
+                                       float &m, float &v) {
+    g = g / k.s;
+    if (t.wd != 0.0f) g += t.wd * p;
+    m = t.b1 * m + (1.0f - t.b1) * g;
+    v = t.b2 * v + (1.0f - t.b2) * g * g;
+    const float denom = (sqrtf(v) / k.bc2s) + t.eps;
+    p -= k.step_size * m / denom;
+    return p;
 }
 
-__global__ void k_finalize(Batch B, float *scale, int32_t *growth_tracker, float *found_inf,
-                           float growth_factor, float backoff_factor, int growth_interval) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(kThreads) void k_adam(Batch B, const float *scale,
+                                                   const float *found_inf) {
+    if (*found_inf != 0.0f) return;
+    const Tensor &t = B.t[block_tensor(B)];
+    const uint64_t e0 = (uint64_t)(blockIdx.x - t.block0) * kPerBlock;
+    // per-tensor constants (the same f32 expressions torch evaluates per element)
+    const float step = *t.step + 1.0f;
+    AdamK k;
+    k.s = *scale;
+    k.step_size = t.lr / (1.0f - powf(t.b1, step));
+    k.bc2s = sqrtf(1.0f - powf(t.b2, step));
+    for_chunk(
+        t, e0,
+        [&](uint64_t q) {
+            float4 p = reinterpret_cast<float4 *>(t.p)[q];
+            float4 m = reinterpret_cast<float4 *>(t.m)[q];
+            float4 v = reinterpret_cast<float4 *>(t.v)[q];
+            const float4 g = reinterpret_cast<const float4 *>(t.g)[q];
+            adam1(t, k, g.x, p.x, m.x, v.x);
+            adam1(t, k, g.y, p.y, m.y, v.y);
+            adam1(t, k, g.z, p.z, m.z, v.z);
+            adam1(t, k, g.w, p.w, m.w, v.w);
+            reinterpret_cast<float4 *>(t.p)[q] = p;
+            reinterpret_cast<float4 *>(t.m)[q] = m;
+            reinterpret_cast<float4 *>(t.v)[q] = v;
+        },
+        [&](uint64_t j) {
+            float p = t.p[j], m = t.m[j], v = t.v[j];
+            adam1(t, k, t.g[j], p, m, v);
+            t.p[j] = p;
+            t.m[j] = m;
+            t.v[j] = v;
+        });
+}
+
+// One wave: lane k bumps tensor k's step (independent RMWs in parallel, not
+// one thread's serial chain of dependent global round trips), lane 0 updates
+// the scale.
+__global__ __launch_bounds__(64) void k_finalize(Batch B, float *scale, int32_t *growth_tracker,
+                                                 float *found_inf, float growth_factor,
+                                                 float backoff_factor, int growth_interval) {
+    if (blockIdx.x != 0) return;
+    const int k = (int)threadIdx.x;
     const bool inf = *found_inf != 0.0f;
-    if (!inf)
-        for (int k = 0; k < B.count; ++k) *B.t[k].step += 1.0f;
+    if (!inf && k < B.count) *B.t[k].step += 1.0f;
+    if (k != 0) return;
     // ATen amp_update_scale_cuda_kernel
     if (inf) {
         *scale = (*scale) * backoff_factor;
@@ -108,7 +163,7 @@ __global__ void k_finalize(Batch B, float *scale, int32_t *growth_tracker, float
             *growth_tracker = successful;
         }
     }
-    *found_inf = 0.0f;
+    *found_inf = 0.0f;  // every lane read it above; the wave runs in lock step
 }
 
 }  // namespace opt
@@ -136,7 +191,7 @@ extern "C" int dfhip_adam_amp_step(int count, float *const *params, const float 
     }
     opt::Batch B;
     B.count = count;
-    uint64_t total = 0;
+    uint32_t blocks = 0;
     for (int k = 0; k < count; ++k) {
         if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || !steps[k]) {
             set_error("%s: null pointer in tensor %d", name, k);
@@ -149,20 +204,24 @@ extern "C" int dfhip_adam_amp_step(int count, float *const *params, const float 
         t.v = exp_avg_sq[k];
         t.step = steps[k];
         t.n = numel[k];
-        t.start = total;
+        t.block0 = blocks;
         t.lr = lr[k];
         t.b1 = beta1[k];
         t.b2 = beta2[k];
         t.eps = eps[k];
         t.wd = weight_decay[k];
-        total += numel[k];
+        const uint64_t nb = ceil_div<uint64_t>(numel[k], opt::kPerBlock);
+        if (nb > 0x7FFFFFFFull - blocks) {
+            set_error("%s: tensor %d has an unsupported size", name, k);
+            return DFHIP_EINVAL;
+        }
+        blocks += (uint32_t)nb;
     }
-    B.total = total;
+    B.blocks = blocks;
     hipStream_t s = as_stream(stream);
-    const uint64_t want = ceil_div<uint64_t>(total, 256);
-    const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
-    opt::k_nonfinite<<<blocks, 256, 0, s>>>(B, found_inf);
-    opt::k_adam<<<blocks, 256, 0, s>>>(B, scale, found_inf);
+    if (blocks == 0) blocks = 1;  // all tensors empty: one block that finds no work
+    opt::k_nonfinite<<<blocks, opt::kThreads, 0, s>>>(B, found_inf);
+    opt::k_adam<<<blocks, opt::kThreads, 0, s>>>(B, scale, found_inf);
     opt::k_finalize<<<1, 64, 0, s>>>(B, scale, growth_tracker, found_inf, growth_factor,
                                      backoff_factor, growth_interval);
     return check_launch(name);
