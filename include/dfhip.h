@@ -147,6 +147,26 @@ int dfhip_march_rays_train_emit(int dtype, const void *rays_o, const void *rays_
                                 const int32_t *block_sums, int zero_tail,
                                 dfhip_stream_t stream);
 
+/* [scratch] Staged split form (native train step): the count pass also keeps
+ * every sample as f32 (x, y, z, dt, dl) at row i*max_steps + j of `stage`
+ * (dfhip_march_rays_train_stage_floats(N, max_steps) floats), and the emit
+ * pass copies those rows to the ray-ordered outputs (same conversions to
+ * `dtype`, dirs = rays_d) instead of marching each ray a second time.  Same
+ * outputs, zero_tail and block_sums contract as the pair above. */
+uint64_t dfhip_march_rays_train_stage_floats(uint32_t N, uint32_t max_steps);
+int dfhip_march_rays_train_count_staged(int dtype, const void *rays_o, const void *rays_d,
+                                        const uint8_t *grid, float bound, float dt_gamma,
+                                        uint32_t max_steps, uint32_t N, uint32_t C, uint32_t H,
+                                        const void *nears, const void *fars, int32_t *rays,
+                                        int32_t *counter, const void *noises,
+                                        int32_t *block_sums, float *stage,
+                                        dfhip_stream_t stream);
+int dfhip_march_rays_train_emit_staged(int dtype, const void *rays_d, uint32_t max_steps,
+                                       uint32_t N, uint32_t M, void *xyzs, void *dirs,
+                                       void *deltas, int32_t *rays, const int32_t *block_sums,
+                                       int zero_tail, const float *stage,
+                                       dfhip_stream_t stream);
+
 /* raymarching.cu:580 composite_rays_train_forward(sigmas, rgbs, deltas, rays,
  *   M, N, T_thresh, weights_sum, depth, image) */
 int dfhip_composite_rays_train_forward(int dtype, const void *sigmas,

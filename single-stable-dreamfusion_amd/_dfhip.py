@@ -41,6 +41,10 @@ _SIGS = {
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dfhip_march_rays_train_emit": [_i32, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _u32,
                                     _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dfhip_march_rays_train_count_staged": [_i32, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32,
+                                            _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_march_rays_train_emit_staged": [_i32, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp,
+                                           _i32, _vp, _vp],
     "dfhip_composite_rays_train_forward": [_i32, _vp, _vp, _vp, _vp, _u32, _u32, _f32, _vp, _vp,
                                            _vp, _vp],
     "dfhip_composite_rays_train_backward": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32,
@@ -131,6 +135,8 @@ def load() -> ctypes.CDLL:
     lib.dfhip_ray_head_partial_floats.argtypes = [_u32]
     lib.dfhip_grid_backward_partial_floats.restype = ctypes.c_uint64
     lib.dfhip_grid_backward_partial_floats.argtypes = [_u32, _u32, _u32]
+    lib.dfhip_march_rays_train_stage_floats.restype = ctypes.c_uint64
+    lib.dfhip_march_rays_train_stage_floats.argtypes = [_u32, _u32]
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -143,7 +149,7 @@ def exported_symbols() -> list[str]:
     return ["dfhip_abi_version", "dfhip_last_error", "dfhip_march_rays_train_scratch_ints",
             "dfhip_grid_backward_default_parts", "dfhip_grid_backward_partial_floats",
             "dfhip_field_mlp_params", "dfhip_field_mlp_backward_parts",
-            "dfhip_ray_head_partial_floats",
+            "dfhip_ray_head_partial_floats", "dfhip_march_rays_train_stage_floats",
             *_SIGS.keys()]
 
 

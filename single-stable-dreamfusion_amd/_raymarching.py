@@ -85,6 +85,35 @@ def march_rays_train_emit(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C
          ptr(rays), ptr(noises), ptr(block_sums), int(zero_tail), stream())
 
 
+def march_rays_train_stage_floats(N, max_steps):
+    return int(_d.load().dfhip_march_rays_train_stage_floats(int(N), int(max_steps)))
+
+
+def march_rays_train_count_staged(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, nears,
+                                  fars, rays, counter, noises, block_sums, stage):
+    """march_rays_train_count that also keeps every sample in `stage` (f32,
+    march_rays_train_stage_floats(N, max_steps) floats)."""
+    dt = _f(rays_o, "rays_o")
+    checked(grid, "grid", "u8")
+    checked(block_sums, "block_sums", "int")
+    checked(stage, "stage")
+    if stage.dtype != torch.float32 or stage.numel() < march_rays_train_stage_floats(N, max_steps):
+        raise RuntimeError("stage must be float32 with march_rays_train_stage_floats(N, max_steps) "
+                           "elements")
+    call("dfhip_march_rays_train_count_staged", dt, ptr(rays_o), ptr(rays_d), ptr(grid), bound,
+         dt_gamma, max_steps, N, C, H, ptr(nears), ptr(fars), ptr(rays), ptr(counter),
+         ptr(noises), ptr(block_sums), ptr(stage), stream())
+
+
+def march_rays_train_emit_staged(rays_d, max_steps, N, M, xyzs, dirs, deltas, rays, block_sums,
+                                 zero_tail, stage):
+    """march_rays_train_emit from the count pass's stage (no second march)."""
+    dt = _f(rays_d, "rays_d")
+    checked(stage, "stage")
+    call("dfhip_march_rays_train_emit_staged", dt, ptr(rays_d), max_steps, N, M, ptr(xyzs),
+         ptr(dirs), ptr(deltas), ptr(rays), ptr(block_sums), int(zero_tail), ptr(stage), stream())
+
+
 def composite_rays_train_forward(sigmas, rgbs, deltas, rays, M, N, T_thresh, weights_sum, depth,
                                  image):
     dt = _f(sigmas, "sigmas")

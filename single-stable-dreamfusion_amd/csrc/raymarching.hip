@@ -132,15 +132,18 @@ __global__ __launch_bounds__(256) void k_packbits_f32v(const float *__restrict__
 // count pass leaves one total per workgroup in block_sums; the emit pass
 // derives a ray's offset from the preceding totals plus the block's counts.
 constexpr uint32_t kMarchRaysPerBlock = 8;
+constexpr uint32_t kStageFloats = 5;  // x, y, z, dt, dl of a staged sample
 
 // Pass 1 (raymarching.cu:341-400): count occupied samples per ray.
-template <typename scalar_t>
+// STAGE: also keep each sample (x, y, z, dt, dl as f32) at row n * max_steps + i
+// of `stage`, so the emit pass copies instead of marching again.
+template <typename scalar_t, bool STAGE = false>
 __global__ __launch_bounds__(64 * kMarchRaysPerBlock) void k_march_train_count(
     const scalar_t *__restrict__ rays_o, const scalar_t *__restrict__ rays_d,
     const uint8_t *__restrict__ grid, MarchConsts k, uint32_t max_steps, uint32_t N,
     const scalar_t *__restrict__ nears, const scalar_t *__restrict__ fars,
     int32_t *rays, int32_t *counter, const scalar_t *__restrict__ noises,
-    int32_t *block_sums) {
+    int32_t *block_sums, float *__restrict__ stage = nullptr) {
     __shared__ int s_cnt[kMarchRaysPerBlock];
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t n = blockIdx.x * kMarchRaysPerBlock + w;
@@ -150,8 +153,18 @@ __global__ __launch_bounds__(64 * kMarchRaysPerBlock) void k_march_train_count(
         const float near = to_f(nears[n]), far = to_f(fars[n]);
         const float t0 = fmaf(clampf(near * k.dt_gamma, k.dt_min, k.dt_max),
                               to_f(noises[n]), near);
-        cnt = (int)march_wave(k, r, grid, t0, far, max_steps,
-                              [](uint32_t, float, float, float, float, float) {});
+        if constexpr (STAGE) {
+            float *st = stage + (size_t)n * max_steps * kStageFloats;
+            cnt = (int)march_wave(k, r, grid, t0, far, max_steps,
+                                  [&](uint32_t i, float x, float y, float z, float dt, float dl) {
+                                      float *row = st + (size_t)i * kStageFloats;
+                                      row[0] = x; row[1] = y; row[2] = z;
+                                      row[3] = dt; row[4] = dl;
+                                  });
+        } else {
+            cnt = (int)march_wave(k, r, grid, t0, far, max_steps,
+                                  [](uint32_t, float, float, float, float, float) {});
+        }
         if ((threadIdx.x & 63) == 0) {
             rays[3 * n + 0] = (int32_t)n;
             rays[3 * n + 2] = cnt;
@@ -185,14 +198,16 @@ __device__ __forceinline__ void zero_rows(scalar_t *xyzs, scalar_t *dirs, scalar
 // counts of the block's earlier rays; then the wave re-marches its ray and
 // each lane writes the samples it holds (consecutive rows across the wave).
 // Rays whose range would cross M are not written (raymarching.cu:416).
-template <typename scalar_t>
+// STAGED: the samples come from the count pass's stage rows (a copy with
+// the same f32 -> scalar_t conversions) instead of a second march.
+template <typename scalar_t, bool STAGED = false>
 __global__ __launch_bounds__(64 * kMarchRaysPerBlock) void k_march_train_emit(
     const scalar_t *__restrict__ rays_o, const scalar_t *__restrict__ rays_d,
     const uint8_t *__restrict__ grid, MarchConsts k, uint32_t N, uint32_t M,
     const scalar_t *__restrict__ nears, const scalar_t *__restrict__ fars,
     scalar_t *xyzs, scalar_t *dirs, scalar_t *deltas, int32_t *rays,
     const scalar_t *__restrict__ noises, const int32_t *__restrict__ block_sums,
-    int zero_tail) {
+    int zero_tail, const float *__restrict__ stage = nullptr, uint32_t max_steps = 0) {
     __shared__ int s_part[kMarchRaysPerBlock];
     __shared__ int s_cnt[kMarchRaysPerBlock];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -216,7 +231,22 @@ __global__ __launch_bounds__(64 * kMarchRaysPerBlock) void k_march_train_emit(
     const uint32_t off = (uint32_t)(prefix + before);
     if (n < N) {
         if (lane == 0) rays[3 * n + 1] = (int32_t)off;
-        if (cnt > 0 && off + (uint32_t)cnt <= M) {
+        if (STAGED && cnt > 0 && off + (uint32_t)cnt <= M) {
+            const scalar_t d0 = rays_d[3 * n], d1 = rays_d[3 * n + 1], d2 = rays_d[3 * n + 2];
+            const float *st = stage + (size_t)n * max_steps * kStageFloats;
+            for (uint32_t i = lane; i < (uint32_t)cnt; i += 64) {
+                const float *row = st + (size_t)i * kStageFloats;
+                const size_t o = (size_t)off + i;
+                xyzs[3 * o + 0] = from_f<scalar_t>(row[0]);
+                xyzs[3 * o + 1] = from_f<scalar_t>(row[1]);
+                xyzs[3 * o + 2] = from_f<scalar_t>(row[2]);
+                dirs[3 * o + 0] = d0;
+                dirs[3 * o + 1] = d1;
+                dirs[3 * o + 2] = d2;
+                deltas[2 * o + 0] = from_f<scalar_t>(row[3]);
+                deltas[2 * o + 1] = from_f<scalar_t>(row[4]);
+            }
+        } else if (cnt > 0 && off + (uint32_t)cnt <= M) {
             const Ray r = load_ray(rays_o + 3 * n, rays_d + 3 * n);
             const float near = to_f(nears[n]), far = to_f(fars[n]);
             const float t0 = fmaf(clampf(near * k.dt_gamma, k.dt_min, k.dt_max),
@@ -787,6 +817,54 @@ extern "C" int dfhip_march_rays_train_emit(int dtype, const void *rays_o, const 
             (scalar_t *)dirs, (scalar_t *)deltas, rays, (const scalar_t *)noises,
             block_sums, zero_tail));
     return check_launch("march_rays_train_emit");
+}
+
+extern "C" uint64_t dfhip_march_rays_train_stage_floats(uint32_t N, uint32_t max_steps) {
+    return (uint64_t)N * max_steps * kStageFloats;
+}
+
+extern "C" int dfhip_march_rays_train_count_staged(
+    int dtype, const void *rays_o, const void *rays_d, const uint8_t *grid, float bound,
+    float dt_gamma, uint32_t max_steps, uint32_t N, uint32_t C, uint32_t H, const void *nears,
+    const void *fars, int32_t *rays, int32_t *counter, const void *noises, int32_t *block_sums,
+    float *stage, dfhip_stream_t stream) {
+    if (!march_args_ok("march_rays_train_count_staged", C, H, max_steps)) return DFHIP_EINVAL;
+    if (N == 0) return DFHIP_OK;
+    if (!stage) {
+        set_error("march_rays_train_count_staged: null stage");
+        return DFHIP_EINVAL;
+    }
+    const MarchConsts k = make_consts(bound, dt_gamma, max_steps, C, H);
+    DFHIP_DISPATCH(dtype, "march_rays_train_count_staged",
+        (k_march_train_count<scalar_t, true><<<ceil_div(N, kMarchRaysPerBlock),
+                                               64 * kMarchRaysPerBlock, 0, as_stream(stream)>>>(
+            (const scalar_t *)rays_o, (const scalar_t *)rays_d, grid, k, max_steps, N,
+            (const scalar_t *)nears, (const scalar_t *)fars, rays, counter,
+            (const scalar_t *)noises, block_sums, stage)));
+    return check_launch("march_rays_train_count_staged");
+}
+
+extern "C" int dfhip_march_rays_train_emit_staged(
+    int dtype, const void *rays_d, uint32_t max_steps, uint32_t N, uint32_t M, void *xyzs,
+    void *dirs, void *deltas, int32_t *rays, const int32_t *block_sums, int zero_tail,
+    const float *stage, dfhip_stream_t stream) {
+    if (max_steps == 0) {
+        set_error("march_rays_train_emit_staged: max_steps must be > 0");
+        return DFHIP_EINVAL;
+    }
+    if (N == 0) return DFHIP_OK;
+    if (!stage || !rays_d || !rays || !block_sums) {
+        set_error("march_rays_train_emit_staged: null pointer");
+        return DFHIP_EINVAL;
+    }
+    const MarchConsts k{};
+    DFHIP_DISPATCH(dtype, "march_rays_train_emit_staged",
+        (k_march_train_emit<scalar_t, true><<<ceil_div(N, kMarchRaysPerBlock),
+                                              64 * kMarchRaysPerBlock, 0, as_stream(stream)>>>(
+            nullptr, (const scalar_t *)rays_d, nullptr, k, N, M, nullptr, nullptr,
+            (scalar_t *)xyzs, (scalar_t *)dirs, (scalar_t *)deltas, rays, nullptr, block_sums,
+            zero_tail, stage, max_steps)));
+    return check_launch("march_rays_train_emit_staged");
 }
 
 extern "C" int dfhip_march_rays_train(int dtype, const void *rays_o, const void *rays_d,

@@ -100,6 +100,9 @@ class NativeAlbedoStep:
         self.xyzs = torch.empty(cap, 3, **f32)
         self.dirs = torch.empty(cap, 3, **f32)
         self.deltas = torch.empty(cap, 2, **f32)
+        # the count pass keeps each sample here; the emit pass only copies
+        self.stage = torch.empty(_raymarching.march_rays_train_stage_floats(N, self.max_steps),
+                                 **f32)
         self.m_dev = self.counter[:1]
         # field
         enc = m.encoder
@@ -170,14 +173,13 @@ class NativeAlbedoStep:
         sc = self.trainer.scaler
         scale = sc._scale if sc.is_enabled() else self._ones
         # march (raymarching.py:161-235, device count)
-        _raymarching.march_rays_train_count(
+        _raymarching.march_rays_train_count_staged(
             self.rays_o, self.rays_d, m.density_bitfield, m.bound, self.dt_gamma, self.max_steps,
             N, m.cascade, m.grid_size, self.nears, self.fars, self.rays, self.counter,
-            self.noises, self.block_sums)
-        _raymarching.march_rays_train_emit(
-            self.rays_o, self.rays_d, m.density_bitfield, m.bound, self.dt_gamma, self.max_steps,
-            N, m.cascade, m.grid_size, cap, self.nears, self.fars, self.xyzs, self.dirs,
-            self.deltas, self.rays, self.noises, self.block_sums, 0)
+            self.noises, self.block_sums, self.stage)
+        _raymarching.march_rays_train_emit_staged(
+            self.rays_d, self.max_steps, N, cap, self.xyzs, self.dirs, self.deltas, self.rays,
+            self.block_sums, 0, self.stage)
         # field (grid.py:38-39 autocast table, network_grid.py:76-87)
         self.table.copy_(self.encoder.embeddings.detach())
         S, Hb, gridtype, align, _ = self.meta

@@ -111,6 +111,15 @@ def _march_gpu(gpu, rays_o, rays_d, nears, fars, noises, bf, **kw):
     xyzs = torch.full((cap, 3), 7.0, device=gpu)  # poison: every returned row must be written
     dirs = torch.full((cap, 3), 7.0, device=gpu)
     deltas = torch.full((cap, 2), 7.0, device=gpu)
+    if kw.get("staged", False):
+        # count pass keeps the samples, emit pass copies them (native train step)
+        stage = torch.full((_raymarching.march_rays_train_stage_floats(n, max_steps),), 5.0,
+                           device=gpu)
+        _raymarching.march_rays_train_count_staged(o, d, b, 1.0, 0.0, max_steps, n, 1, 128, ne,
+                                                   fa, rays, counter, no, bs, stage)
+        _raymarching.march_rays_train_emit_staged(d, max_steps, n, cap, xyzs, dirs, deltas, rays,
+                                                  bs, zero_tail, stage)
+        return xyzs, dirs, deltas, rays, counter
     _raymarching.march_rays_train_count(o, d, b, 1.0, 0.0, max_steps, n, 1, 128, ne, fa, rays,
                                         counter, no, bs)
     _raymarching.march_rays_train_emit(o, d, b, 1.0, 0.0, max_steps, n, 1, 128, cap, ne, fa, xyzs,
@@ -118,9 +127,11 @@ def _march_gpu(gpu, rays_o, rays_d, nears, fars, noises, bf, **kw):
     return xyzs, dirs, deltas, rays, counter
 
 
-def test_march_rays_train_bitexact_128x128(gpu):
+@pytest.mark.parametrize("staged", [False, True])
+def test_march_rays_train_bitexact_128x128(gpu, staged):
     rays_o, rays_d, nears, fars, noises, bf = march_inputs(128, 128, seed=0)
-    xyzs, dirs, deltas, rays, counter = _march_gpu(gpu, rays_o, rays_d, nears, fars, noises, bf)
+    xyzs, dirs, deltas, rays, counter = _march_gpu(gpu, rays_o, rays_d, nears, fars, noises, bf,
+                                                   staged=staged)
     counts, wx, wd, wl = oracle.march_rays_train(rays_o, rays_d, bf, 1.0, 0.0, 512, 1, 128, nears,
                                                  fars, noises)
     rays = rays.cpu().numpy()
@@ -171,7 +182,8 @@ def test_march_rays_train_edge_cases(gpu):
         np.testing.assert_array_equal(deltas[:total].cpu().numpy(), wl)
 
 
-def test_march_rays_train_capacity_overflow(gpu):
+@pytest.mark.parametrize("staged", [False, True])
+def test_march_rays_train_capacity_overflow(gpu, staged):
     """mean_count mode: rays whose samples do not fit in M are not written and
     their rows read as zero (raymarching.cu:416 + the caller's zero fill)."""
     rays_o, rays_d, nears, fars, noises, bf = march_inputs(32, 32, seed=5, radius=0.7)
@@ -179,7 +191,7 @@ def test_march_rays_train_capacity_overflow(gpu):
                                                fars, noises)
     cap = int(counts.sum()) // 2
     xyzs, _, deltas, rays, _ = _march_gpu(gpu, rays_o, rays_d, nears, fars, noises, bf, cap=cap,
-                                          zero_tail=-1)
+                                          zero_tail=-1, staged=staged)
     offs = oracle.rays_from_counts(counts)[:, 1]
     fit = offs + counts <= cap
     written = int((offs + counts)[fit].max())
