@@ -90,6 +90,50 @@ __device__ __forceinline__ uint32_t row_index(const LevelCtx &c, const uint32_t 
     return c.pow2 ? (idx & (c.hsize - 1)) : (idx % c.hsize);
 }
 
+// Corner rows of one level without the generic per-corner index loop and
+// modulo (same u32 arithmetic as row_index): the tiled index of cell + corner
+// offset o_k is i0 + o_k with i0 = c0 + c1 m1 + c2 m2 (m1 / m2 zero for the
+// dimensions the tiled index stops before), wrapped by a mask when the level
+// is a power of two or the index can never reach hsize, else by % hsize; the
+// hashed form keeps the spatial hash.  Per-level constants are uniform.
+struct LevelRows {
+    uint32_t hsize, wmask, m1, m2, lead;
+    bool hashed, modulo;
+};
+
+template <uint32_t D>
+__device__ __forceinline__ LevelRows level_rows(const LevelCtx &c) {
+    LevelRows r;
+    r.hsize = c.hsize;
+    r.hashed = c.hashed;
+    r.lead = c.hashed ? D : c.used;
+    r.m1 = (D > 1 && r.lead > 1) ? c.smul : 0u;
+    r.m2 = (D > 2 && r.lead > 2) ? c.smul * c.smul : 0u;
+    uint64_t span = 1;  // largest tiled index + 1
+    for (uint32_t d = 0; d < c.used; ++d) span *= c.smul;
+    r.modulo = !c.pow2 && (c.hashed || span > (uint64_t)c.hsize);
+    r.wmask = c.pow2 ? c.hsize - 1u : 0xFFFFFFFFu;
+    return r;
+}
+
+// Row (relative to the level base) of corner k (bit d = +1 along d < lead).
+template <uint32_t D>
+__device__ __forceinline__ uint32_t corner_row(const LevelRows &r, const uint32_t cell[D],
+                                               uint32_t k) {
+    uint32_t idx;
+    if (r.hashed) {
+        uint32_t p[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) p[d] = cell[d] + ((k >> d) & 1u);
+        idx = spatial_hash<D>(p);
+    } else {
+        idx = cell[0] + (k & 1u);
+        if (D > 1) idx += (cell[1] + ((k >> 1) & 1u)) * r.m1;
+        if (D > 2) idx += (cell[D > 2 ? 2 : 0] + ((k >> 2) & 1u)) * r.m2;
+    }
+    return r.modulo ? idx % r.hsize : (idx & r.wmask);
+}
+
 // ------------------------------------------------------------ storage helpers
 // Accumulate one corner contribution into a per-channel register, following
 // the reference's scalar_t arithmetic exactly (gridencoder.cu:142,165).

@@ -158,19 +158,15 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
             if (!load_pos<D>(inputs, dyn, s, x)) continue;
             for (uint32_t l = 0; l < bi.L; ++l) {
                 const LevelCtx c = ge::level_ctx<D>(offsets, lv, l, gridtype, align);
-                const uint32_t lead = (!c.hashed) ? c.used : D;
+                const ge::LevelRows lr = ge::level_rows<D>(c);
                 uint32_t cell[D];
                 float frac[D];
                 locate<D>(c, align, x, cell, frac);
                 uint64_t mask = 0;
 #pragma unroll
                 for (uint32_t k = 0; k < (1u << D); ++k) {
-                    if (k >> lead) continue;
-                    uint32_t p[D];
-#pragma unroll
-                    for (uint32_t d = 0; d < D; ++d)
-                        p[d] = cell[d] + ((d < lead && (k & (1u << d))) ? 1u : 0u);
-                    mask |= 1ull << (ge::row_index<D>(c, p) >> bi.shift);
+                    if (k >> lr.lead) continue;
+                    mask |= 1ull << (ge::corner_row<D>(lr, cell, k) >> bi.shift);
                 }
                 const uint32_t b0 = bi.bin0[l];
                 while (mask) {
@@ -192,15 +188,12 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
 // Flush one cell's merged corner contributions into the LDS slice [r0, r1).
 template <uint32_t D, uint32_t C>
 __device__ __forceinline__ void flush(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
-                                      uint32_t lead, const uint32_t cell[D],
+                                      const ge::LevelRows &lr, const uint32_t cell[D],
                                       const double (&cw)[1u << D][C]) {
 #pragma unroll
     for (uint32_t k = 0; k < (1u << D); ++k) {
-        if (k >> lead) continue;
-        uint32_t p[D];
-#pragma unroll
-        for (uint32_t d = 0; d < D; ++d) p[d] = cell[d] + ((d < lead && (k & (1u << d))) ? 1u : 0u);
-        const uint32_t row = c.base + ge::row_index<D>(c, p);
+        if (k >> lr.lead) continue;
+        const uint32_t row = c.base + ge::corner_row<D>(lr, cell, k);
         if (row >= r0 && row < r1) {
             double *dst = acc + (size_t)(row - r0) * C;
 #pragma unroll
@@ -262,7 +255,8 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     __syncthreads();
     const bool align = align_corners != 0;
     const LevelCtx c = ge::level_ctx<D>(offsets, lv, l, gridtype, align);
-    const uint32_t lead = (!c.hashed) ? c.used : D;
+    const ge::LevelRows lr = ge::level_rows<D>(c);
+    const uint32_t lead = lr.lead;
     const uint32_t M = ge::dyn_count(dyn, B);
     const uint32_t ntiles = ceil_div(M, kTile);
     const uint32_t nb = bi.nbins;
@@ -310,7 +304,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                     for (uint32_t d = 0; d < D; ++d)
                         if (d < lead) same = same && (cell[d] == cur[d]);
                     if (!same) {
-                        if (have) flush<D, C>(acc, r0, r1, c, lead, cur, cw);
+                        if (have) flush<D, C>(acc, r0, r1, c, lr, cur, cw);
 #pragma unroll
                         for (uint32_t kc = 0; kc < (1u << D); ++kc)
 #pragma unroll
@@ -337,7 +331,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                 }
             }
         }
-        if (have) flush<D, C>(acc, r0, r1, c, lead, cur, cw);
+        if (have) flush<D, C>(acc, r0, r1, c, lr, cur, cw);
     }
     __syncthreads();
     float *out = partial + bi.pbase[l] + ((size_t)k * P + part) * ((size_t)srows * C);
