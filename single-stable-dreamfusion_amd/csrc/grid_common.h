@@ -117,6 +117,30 @@ __device__ __forceinline__ LevelRows level_rows(const LevelCtx &c) {
 }
 
 // Row (relative to the level base) of corner k (bit d = +1 along d < lead).
+// MODE fixes the wrap at compile time (0: mask, 1: % hsize, 2: hash, then
+// mask or % by r.modulo); callers branch once per level on row_mode(r), a
+// uniform value, instead of evaluating every form per corner and selecting.
+template <uint32_t D, int MODE>
+__device__ __forceinline__ uint32_t corner_row_m(const LevelRows &r, const uint32_t cell[D],
+                                                 uint32_t k) {
+    uint32_t idx;
+    if (MODE == 2) {
+        uint32_t p[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) p[d] = cell[d] + ((k >> d) & 1u);
+        idx = spatial_hash<D>(p);
+        return r.modulo ? idx % r.hsize : (idx & r.wmask);
+    }
+    idx = cell[0] + (k & 1u);
+    if (D > 1) idx += (cell[1] + ((k >> 1) & 1u)) * r.m1;
+    if (D > 2) idx += (cell[D > 2 ? 2 : 0] + ((k >> 2) & 1u)) * r.m2;
+    return MODE == 1 ? idx % r.hsize : (idx & r.wmask);
+}
+
+__device__ __forceinline__ int row_mode(const LevelRows &r) {
+    return r.hashed ? 2 : (r.modulo ? 1 : 0);
+}
+
 template <uint32_t D>
 __device__ __forceinline__ uint32_t corner_row(const LevelRows &r, const uint32_t cell[D],
                                                uint32_t k) {

@@ -135,6 +135,19 @@ __device__ __forceinline__ bool load_pos(const float *__restrict__ inputs, const
     return !oob;  // out-of-bounds samples contribute nothing (gridencoder.cu:253-258)
 }
 
+// Slices (bits) touched by the corners of a cell at one level.
+template <uint32_t D, int MODE>
+__device__ __forceinline__ uint64_t slice_mask(const ge::LevelRows &lr, const uint32_t cell[D],
+                                               uint32_t shift) {
+    uint64_t mask = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (1u << D); ++k) {
+        if (k >> lr.lead) continue;
+        mask |= 1ull << (ge::corner_row_m<D, MODE>(lr, cell, k) >> shift);
+    }
+    return mask;
+}
+
 // ---------------------------------------------------------------- 1. binning
 template <uint32_t D>
 __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
@@ -163,11 +176,10 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
                 float frac[D];
                 locate<D>(c, align, x, cell, frac);
                 uint64_t mask = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < (1u << D); ++k) {
-                    if (k >> lr.lead) continue;
-                    mask |= 1ull << (ge::corner_row<D>(lr, cell, k) >> bi.shift);
-                }
+                const int mode = ge::row_mode(lr);
+                if (mode == 0) mask = slice_mask<D, 0>(lr, cell, bi.shift);
+                else if (mode == 1) mask = slice_mask<D, 1>(lr, cell, bi.shift);
+                else mask = slice_mask<D, 2>(lr, cell, bi.shift);
                 const uint32_t b0 = bi.bin0[l];
                 while (mask) {
                     const uint32_t k = (uint32_t)__builtin_ctzll(mask);
@@ -186,14 +198,29 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
 
 // ---------------------------------------------------------------- 2. walk
 // Flush one cell's merged corner contributions into the LDS slice [r0, r1).
+template <uint32_t D, uint32_t C, int MODE>
+__device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
+                                        const ge::LevelRows &lr, const uint32_t cell[D],
+                                        const double (&cw)[1u << D][C]);
+
 template <uint32_t D, uint32_t C>
 __device__ __forceinline__ void flush(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
                                       const ge::LevelRows &lr, const uint32_t cell[D],
                                       const double (&cw)[1u << D][C]) {
+    const int mode = ge::row_mode(lr);  // uniform: one scalar branch per flush
+    if (mode == 0) flush_m<D, C, 0>(acc, r0, r1, c, lr, cell, cw);
+    else if (mode == 1) flush_m<D, C, 1>(acc, r0, r1, c, lr, cell, cw);
+    else flush_m<D, C, 2>(acc, r0, r1, c, lr, cell, cw);
+}
+
+template <uint32_t D, uint32_t C, int MODE>
+__device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
+                                        const ge::LevelRows &lr, const uint32_t cell[D],
+                                        const double (&cw)[1u << D][C]) {
 #pragma unroll
     for (uint32_t k = 0; k < (1u << D); ++k) {
         if (k >> lr.lead) continue;
-        const uint32_t row = c.base + ge::corner_row<D>(lr, cell, k);
+        const uint32_t row = c.base + ge::corner_row_m<D, MODE>(lr, cell, k);
         if (row >= r0 && row < r1) {
             double *dst = acc + (size_t)(row - r0) * C;
 #pragma unroll
