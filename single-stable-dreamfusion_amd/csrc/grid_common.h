@@ -5,6 +5,8 @@
 
 #include <math.h>
 
+#include <cmath>
+
 #include "common.h"
 
 namespace dfhip {
@@ -190,6 +192,21 @@ __device__ __forceinline__ uint32_t dyn_count(const SliceDyn &dyn, uint32_t B) {
 
 __device__ __forceinline__ float dyn_map(const SliceDyn &dyn, float x) {
     return dyn.bound > 0.0f ? (x + dyn.bound) / (2.0f * dyn.bound) : x;
+}
+
+// dyn_map for a kernel instantiated knowing that 2 * bound is a power of two
+// (bound 1, the reference default): the quotient is the product with the
+// exact reciprocal `inv`, bit for bit, without the correctly-rounded division.
+inline bool dyn_pow2(float bound) {
+    if (!(bound > 0.0f)) return false;
+    const float d = 2.0f * bound;
+    int e = 0;
+    return std::frexp(d, &e) == 0.5f && d > 1.0e-30f && d < 1.0e30f;
+}
+template <bool POW2>
+__device__ __forceinline__ float dyn_map_t(const SliceDyn &dyn, float inv, float x) {
+    if constexpr (POW2) return (x + dyn.bound) * inv;
+    return dyn_map(dyn, x);
 }
 
 // Host side of dfhip_grid_encode_backward_sliced, shared with the fused

@@ -123,13 +123,13 @@ __device__ __forceinline__ void locate(const LevelCtx &c, bool align, const floa
     }
 }
 
-template <uint32_t D>
+template <uint32_t D, bool POW2>
 __device__ __forceinline__ bool load_pos(const float *__restrict__ inputs, const SliceDyn &dyn,
-                                         uint32_t s, float x[D]) {
+                                         float inv, uint32_t s, float x[D]) {
     bool oob = false;
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) {
-        x[d] = ge::dyn_map(dyn, inputs[(size_t)s * D + d]);
+        x[d] = ge::dyn_map_t<POW2>(dyn, inv, inputs[(size_t)s * D + d]);
         oob |= (x[d] < 0.0f) || (x[d] > 1.0f);
     }
     return !oob;  // out-of-bounds samples contribute nothing (gridencoder.cu:253-258)
@@ -149,11 +149,11 @@ __device__ __forceinline__ uint64_t slice_mask(const ge::LevelRows &lr, const ui
 }
 
 // ---------------------------------------------------------------- 1. binning
-template <uint32_t D>
+template <uint32_t D, bool POW2>
 __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
                                              const int32_t *__restrict__ offsets, Levels lv,
                                              BinInfo bi, uint32_t gridtype, int align_corners,
-                                             SliceDyn dyn, uint32_t B,
+                                             SliceDyn dyn, float inv, uint32_t B,
                                              uint32_t *__restrict__ counts,
                                              uint32_t *__restrict__ entries) {
     __shared__ uint32_t cnt[kMaxBins];
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
         const uint32_t s_end = min(M, (tile + 1) * kTile);
         for (uint32_t s = tile * kTile + threadIdx.x; s < s_end; s += blockDim.x) {
             float x[D];
-            if (!load_pos<D>(inputs, dyn, s, x)) continue;
+            if (!load_pos<D, POW2>(inputs, dyn, inv, s, x)) continue;
             for (uint32_t l = 0; l < bi.L; ++l) {
                 const LevelCtx c = ge::level_ctx<D>(offsets, lv, l, gridtype, align);
                 const ge::LevelRows lr = ge::level_rows<D>(c);
@@ -255,12 +255,12 @@ __device__ __forceinline__ void load_grad(const grad_t *__restrict__ p, float (&
 // LDS atomic instruction rarely has two lanes on a row, and along its run a
 // lane merges consecutive contributions to the same cell in registers (at the
 // coarse levels a cell spans tens of samples of a ray).
-template <typename grad_t, uint32_t D, uint32_t C>
+template <typename grad_t, uint32_t D, uint32_t C, bool POW2>
 __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad,  // [L, B, C]
                                                const float *__restrict__ inputs,
                                                const int32_t *__restrict__ offsets, Levels lv,
                                                BinInfo bi, uint32_t gridtype, int align_corners,
-                                               SliceDyn dyn, uint32_t B,
+                                               SliceDyn dyn, float inv, uint32_t B,
                                                const uint32_t *__restrict__ counts,
                                                const uint32_t *__restrict__ entries,
                                                float *__restrict__ partial) {
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                 if (i < m) {  // guard, not break: keeps the run in registers
                     float x[D];
 #pragma unroll
-                    for (uint32_t d = 0; d < D; ++d) x[d] = ge::dyn_map(dyn, xs[i][d]);
+                    for (uint32_t d = 0; d < D; ++d) x[d] = ge::dyn_map_t<POW2>(dyn, inv, xs[i][d]);
                     uint32_t cell[D];
                     float frac[D];
                     locate<D>(c, align, x, cell, frac);
@@ -416,15 +416,17 @@ static void launch_walk(hipStream_t s, dim3 g, size_t lds, const grad_t *grad,
                         const BinInfo &bi, uint32_t gridtype, int align, SliceDyn dyn,
                         uint32_t B, const uint32_t *counts, const uint32_t *entries,
                         float *partial) {
-    auto kern = k_walk<grad_t, 3, C>;
-    static bool attr = false;
-    if (!attr) {
+    const bool pow2 = ge::dyn_pow2(dyn.bound);
+    const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
+    auto kern = pow2 ? k_walk<grad_t, 3, C, true> : k_walk<grad_t, 3, C, false>;
+    static bool attr[2] = {false, false};
+    if (!attr[pow2]) {
         (void)hipFuncSetAttribute((const void *)kern,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
-        attr = true;
+        attr[pow2] = true;
     }
-    kern<<<g, 1024, lds, s>>>(grad, inputs, offsets, lv, bi, gridtype, align, dyn, B, counts,
-                              entries, partial);
+    kern<<<g, 1024, lds, s>>>(grad, inputs, offsets, lv, bi, gridtype, align, dyn, inv, B,
+                              counts, entries, partial);
 }
 
 }  // namespace gb
@@ -486,9 +488,18 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
         }
         const uint32_t tiles = ceil_div(B, gb::kTile);
         const uint32_t gbin = tiles < 4096u ? tiles : 4096u;
-        if (phase & 1)
-            gb::k_bin<3><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype, align_corners,
-                                              dyn, B, counts, entries);
+        if (phase & 1) {
+            const bool pow2 = ge::dyn_pow2(dyn.bound);
+            const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
+            if (pow2)
+                gb::k_bin<3, true><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype,
+                                                         align_corners, dyn, inv, B, counts,
+                                                         entries);
+            else
+                gb::k_bin<3, false><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype,
+                                                          align_corners, dyn, inv, B, counts,
+                                                          entries);
+        }
         if (!(phase & 2)) return check_launch(name);
         const dim3 g(gb::kXcds * bi.nslots);
         const size_t lds = ((size_t)1 << bi.shift) * C * sizeof(double);
