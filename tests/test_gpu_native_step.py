@@ -123,3 +123,44 @@ def test_native_graph_training_runs(gpu):
     for a, b in zip(after, before):
         assert torch.isfinite(a).all()
         assert not torch.equal(a, b)
+
+
+def test_checkpoint_round_trip_resumes(gpu, tmp_path):
+    """Trainer.save_checkpoint / load_checkpoint (reference utils.py:847-968)
+    after graph-replayed native steps: the reference's keys (model incl. the
+    occupancy state, mean_count / mean_density, optimizer, scaler, scheduler)
+    round-trip exactly into a fresh trainer, which then keeps training."""
+    trainer, data = _trainer(64, 21, graph=True)
+    for i in range(20):
+        trainer.train_iteration(data.collate([i % 4]))
+    torch.cuda.synchronize()
+    trainer.ckpt_path = str(tmp_path)
+    trainer.save_checkpoint("ck", full=True)
+    ck = torch.load(tmp_path / "ck.pth", map_location=gpu, weights_only=True)
+    for key in ("epoch", "global_step", "stats", "mean_count", "mean_density", "optimizer",
+                "lr_scheduler", "scaler", "model"):
+        assert key in ck, key
+    for key in ("encoder.embeddings", "sigma_net.net.0.weight", "density_grid",
+                "density_bitfield", "step_counter", "aabb_train"):
+        assert key in ck["model"], key
+    assert ck["global_step"] == trainer.global_step == 20
+
+    fresh, _ = _trainer(64, 22, graph=True)
+    fresh.ckpt_path = str(tmp_path)
+    fresh.load_checkpoint(str(tmp_path / "ck.pth"))
+    want, got = trainer.model.state_dict(), fresh.model.state_dict()
+    assert want.keys() == got.keys()
+    for k in want:
+        assert torch.equal(want[k], got[k]), k
+    assert fresh.global_step == 20
+    assert int(fresh.model.mean_count) == int(trainer.model.mean_count)
+    assert float(fresh.model.mean_density) == float(trainer.model.mean_density)
+    assert float(fresh.scaler.get_scale()) == float(trainer.scaler.get_scale())
+    so, sf = trainer.optimizer.state_dict()["state"], fresh.optimizer.state_dict()["state"]
+    assert so.keys() == sf.keys()
+    for i in so:
+        for name in ("step", "exp_avg", "exp_avg_sq"):
+            assert torch.equal(so[i][name].to(gpu), sf[i][name].to(gpu)), (i, name)
+    losses = [float(fresh.train_iteration(data.collate([i % 4]))) for i in range(5)]
+    assert all(np.isfinite(losses))
+    assert fresh.global_step == 25

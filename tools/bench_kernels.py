@@ -135,6 +135,19 @@ def main():
         out["field_bwd_us"] = timeit(lambda: _fieldmlp.field_mlp_backward(
             enc16, xw, ws, gsig, galb, denc, part, grads), args.reps)
 
+    # -------------------------------------------------------------- fused grid field
+    if want("fused"):
+        import _fieldmlp
+        torch.manual_seed(0)
+        mlp = [torch.randn(64, 32, device=dev) * 0.2, torch.randn(64, device=dev) * 0.1,
+               torch.randn(64, 64, device=dev) * 0.15, torch.randn(64, device=dev) * 0.1,
+               torch.randn(4, 64, device=dev) * 0.15, torch.randn(4, device=dev) * 0.1]
+        encf = torch.empty(B, 32, dtype=torch.float16, device=dev)
+        sigf = torch.empty(B, device=dev)
+        albf = torch.empty(B, 3, dtype=torch.float16, device=dev)
+        out["fused_field_fwd_us"] = timeit(lambda: _fieldmlp.grid_field_forward(
+            xyzs, 1.0, emb, offs, S, 16, 1, False, mlp, encf, sigf, albf, None), args.reps)
+
     # -------------------------------------------------------------- composite
     if want("composite"):
         sig = torch.rand(B, device=dev) * 30
