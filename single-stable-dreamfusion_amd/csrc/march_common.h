@@ -48,6 +48,7 @@ struct MarchConsts {
     float half_H;   // 0.5f * H (exact product when H is a power of two)
     uint32_t H;
     uint32_t H_pow2;
+    float mip_bound0, rbound0;  // level-0 mip bound min(1, bound) and its reciprocal
 };
 
 inline MarchConsts make_consts(float bound, float dt_gamma, uint32_t max_steps,
@@ -65,6 +66,8 @@ inline MarchConsts make_consts(float bound, float dt_gamma, uint32_t max_steps,
     k.half_H = 0.5f * (float)H;
     k.H = H;
     k.H_pow2 = (H >= 2 && (H & (H - 1)) == 0) ? 1u : 0u;
+    k.mip_bound0 = fminf(1.0f, bound);   // scalbnf(1, 0) clamped as the kernels do
+    k.rbound0 = 1.0f / k.mip_bound0;     // IEEE f32 division, as on the device
     return k;
 }
 
@@ -80,6 +83,28 @@ __device__ __forceinline__ int mip_level(const MarchConsts &k, float x, float y,
     frexpf(md, &ed);
     const float ld = fminf(k.Cf - 1.0f, fmaxf(0.0f, (float)ed));
     return max((int)lp, (int)ld);
+}
+
+// Mip level, its bound and the bound's reciprocal for a point.  With one
+// cascade (the train default, bound <= 1) the level is 0 for every point and
+// the bound and reciprocal are the host-evaluated constants: a uniform branch
+// instead of a per-lane correctly-rounded division.
+struct Mip {
+    int level;
+    float bound, rbound;
+};
+__device__ __forceinline__ Mip mip_of(const MarchConsts &k, float x, float y, float z, float dt) {
+    Mip m;
+    if (k.Cf == 1.0f) {
+        m.level = 0;
+        m.bound = k.mip_bound0;
+        m.rbound = k.rbound0;
+    } else {
+        m.level = mip_level(k, x, y, z, dt);
+        m.bound = fminf(scalbnf(1.0f, m.level), k.bound);
+        m.rbound = 1.0f / m.bound;
+    }
+    return m;
 }
 
 // Grid cell of a clamped coordinate (raymarching.cu:374-376: the product is
@@ -154,9 +179,10 @@ __device__ __forceinline__ uint32_t march(const MarchConsts &k, const Ray &r,
         const float y = clampf(fmaf(t, r.dy, r.oy), -k.bound, k.bound);
         const float z = clampf(fmaf(t, r.dz, r.oz), -k.bound, k.bound);
         const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
-        const int level = mip_level(k, x, y, z, dt);
-        const float mip_bound = fminf(scalbnf(1.0f, level), k.bound);
-        const float rbound = 1.0f / mip_bound;
+        const Mip mp = mip_of(k, x, y, z, dt);
+        const int level = mp.level;
+        const float mip_bound = mp.bound;
+        const float rbound = mp.rbound;
         const int nx = cell_of(k, x, rbound);
         const int ny = cell_of(k, y, rbound);
         const int nz = cell_of(k, z, rbound);
@@ -210,9 +236,10 @@ __device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
         const float y = clampf(fmaf(t, r.dy, r.oy), -k.bound, k.bound);
         const float z = clampf(fmaf(t, r.dz, r.oz), -k.bound, k.bound);
         const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
-        const int level = mip_level(k, x, y, z, dt);
-        const float mip_bound = fminf(scalbnf(1.0f, level), k.bound);
-        const float rbound = 1.0f / mip_bound;
+        const Mip mp = mip_of(k, x, y, z, dt);
+        const int level = mp.level;
+        const float mip_bound = mp.bound;
+        const float rbound = mp.rbound;
         const int nx = cell_of(k, x, rbound);
         const int ny = cell_of(k, y, rbound);
         const int nz = cell_of(k, z, rbound);
@@ -322,9 +349,10 @@ __device__ __forceinline__ uint32_t march_wave(const MarchConsts &k, const Ray &
         const float x = clampf(fmaf(tj, r.dx, r.ox), -k.bound, k.bound);
         const float y = clampf(fmaf(tj, r.dy, r.oy), -k.bound, k.bound);
         const float z = clampf(fmaf(tj, r.dz, r.oz), -k.bound, k.bound);
-        const int level = mip_level(k, x, y, z, dt);
-        const float mip_bound = fminf(scalbnf(1.0f, level), k.bound);
-        const float rbound = 1.0f / mip_bound;
+        const Mip mp = mip_of(k, x, y, z, dt);
+        const int level = mp.level;
+        const float mip_bound = mp.bound;
+        const float rbound = mp.rbound;
         const int nx = cell_of(k, x, rbound);
         const int ny = cell_of(k, y, rbound);
         const int nz = cell_of(k, z, rbound);
