@@ -30,6 +30,9 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "SDS train steps/sec + rays/sec at 128×128, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# ds_add_f64 issue rate measured on gfx950 (tools/micro/lds_atomic.hip):
+# 2.53 lane-ops per CU per clock x 256 CUs x 2.4 GHz
+LDS_F64_ATOMIC_PEAK = 2.53 * 256 * 2.4e9
 ATOMIC_PEAK_GBS = 1300.0     # MI355X_MICROARCH.md: global float atomics ~1.3 TB/s
 
 
@@ -269,7 +272,6 @@ def main():
     if not args.no_kernel_timing:
         timer = _dfhip.new_kernel_timer()
         _dfhip.set_kernel_timer(timer)
-    counts = []
 
     def barrier():
         if world > 1:
@@ -280,7 +282,6 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        counts.append(trainer.model.step_counter[(trainer.model.local_step - 1) % 16, 0].clone())
     host_issue = time.perf_counter() - t0  # host done issuing (no sync inside the loop)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -290,7 +291,11 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    samples = float(torch.stack(counts).float().mean().item())
+    # samples per step: the renderer's per-step counts of the last min(16, K)
+    # steps (read after the timed region; no copy inside the loop)
+    last = min(16, args.steps)
+    rows = [(trainer.model.local_step - 1 - i) % 16 for i in range(last)]
+    samples = float(trainer.model.step_counter[rows, 0].float().mean().item())
     kernels = summarize_kernels(timer.records) if timer else {}
 
     rays_per_step = args.res * args.res
@@ -324,6 +329,15 @@ def main():
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
             "traffic": traffic, "avg_us": kd["avg_us"],
             "bytes_per_launch": kd["bytes_per_launch"]}
+        if dom == "grid_encode_backward":
+            # the binned backward's real ceiling: one f64 LDS add per (sample,
+            # level, corner, channel) before the walk's in-register merging
+            ops = samples * 16 * 8 * 2
+            rate = ops / (kd["avg_us"] * 1e-6)
+            result["lds_atomic_roofline"] = {
+                "achieved": round(rate / 1e12, 4), "peak": round(LDS_F64_ATOMIC_PEAK / 1e12, 4),
+                "unit": "T f64 LDS adds/s", "frac": round(rate / LDS_F64_ATOMIC_PEAK, 4),
+                "ops_per_launch": int(ops)}
         result["kernels"] = kernels
         step_ms = result["ms_per_step"]
         result["kernel_share_of_step"] = {k: round(v["total_ms"] / args.steps / step_ms, 4)
