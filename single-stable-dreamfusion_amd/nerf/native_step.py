@@ -144,10 +144,11 @@ class NativeAlbedoStep:
         if sc.is_enabled() and sc._scale is None:
             sc._lazy_init_scale_growth_tracker(dev)  # what scaler.scale() does on first use
         self._ones = torch.ones(1, **f32)  # upstream gradient of the loss without a scaler
-        # gradients live in persistent buffers, written in place every step
-        for p in m.parameters():
-            if p.requires_grad and p.grad is None:
-                p.grad = torch.zeros_like(p)
+        # gradients live in persistent buffers, written in place every step:
+        # views of one flat bucket, which the data-parallel all-reduce
+        # reduces in place (nerf/utils.py flat_allreduce_)
+        from .utils import flat_grad_bucket_
+        self.grad_bucket = flat_grad_bucket_(m.parameters())
         self.params = [p for p in m.parameters() if p.requires_grad]
         self.grads = [(p, p.grad) for p in self.params]
         self._emb_launch = None

@@ -130,12 +130,54 @@ def seed_everything(seed):
 # data-parallel gradient exchange
 # ----------------------------------------------------------------------------
 
+def flat_grad_bucket_(params):
+    """Make the .grad of every trainable parameter a view of ONE contiguous
+    f32 buffer (in parameter order), so the gradient all-reduce runs in place
+    on it (no cat before / copies after).  Current gradient values are kept.
+    Returns the buffer (also kept on the first parameter)."""
+    params = [p for p in params if p.requires_grad]
+    total = sum(p.numel() for p in params)
+    flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
+    off = 0
+    for p in params:
+        n = p.numel()
+        view = flat[off:off + n].view_as(p)
+        if p.grad is not None:
+            view.copy_(p.grad)
+        p.grad = view
+        off += n
+    params[0]._dfhip_grad_bucket = flat
+    return flat
+
+
+def _grad_bucket(params):
+    """The flat buffer when the grads of `params` are still its consecutive
+    views (flat_grad_bucket_), else None."""
+    flat = getattr(params[0], "_dfhip_grad_bucket", None)
+    if flat is None:
+        return None
+    ptr, off = flat.data_ptr(), 0
+    for p in params:
+        g = p.grad
+        if g is None or g.dtype != torch.float32 or g.data_ptr() != ptr + 4 * off:
+            return None
+        off += g.numel()
+    return flat if off == flat.numel() else None
+
+
 def flat_allreduce_(params, world_size, group=None):
     """Average the .grad of `params` over all ranks with ONE all-reduce of a
     flat buffer (7.27 MB for the grid network: one RCCL ring / tree over xGMI
-    instead of one collective per tensor).  Missing grads count as zeros."""
+    instead of one collective per tensor).  Missing grads count as zeros.
+    When the grads are views of one bucket (flat_grad_bucket_, the native
+    step) the all-reduce and the 1/world scaling run in place on it."""
     params = [p for p in params if p.requires_grad]
     if world_size <= 1 or not params:
+        return
+    bucket = _grad_bucket(params)
+    if bucket is not None:
+        dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
+        bucket.div_(world_size)
         return
     dev = params[0].device
     flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).float()

@@ -79,9 +79,9 @@ def test_sds_math():
     assert torch.allclose(img.grad, g1)
 
 
-def _allreduce_worker(rank, world, port, out):
+def _allreduce_worker(rank, world, port, out, bucket=False):
     import torch.distributed as dist
-    from nerf.utils import flat_allreduce_
+    from nerf.utils import _grad_bucket, flat_allreduce_, flat_grad_bucket_
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
@@ -91,17 +91,27 @@ def _allreduce_worker(rank, world, port, out):
     x = torch.full((2, 4), float(rank + 1))
     lin(x).sum().backward()
     emb.grad = torch.full_like(emb, float(rank))
-    flat_allreduce_(params, world)
+    if bucket:
+        # grads as views of one buffer (the native step): reduced in place
+        flat = flat_grad_bucket_(params)
+        assert _grad_bucket(params) is flat
+        before = [p.grad for p in params]
+        flat_allreduce_(params, world)
+        assert all(p.grad is g for p, g in zip(params, before))
+    else:
+        flat_allreduce_(params, world)
     out[rank] = torch.cat([p.grad.reshape(-1) for p in params]).clone()
     dist.destroy_process_group()
 
 
-def test_flat_allreduce_gloo_two_ranks():
-    port = 29500 + (os.getpid() % 1000)
+@pytest.mark.parametrize("bucket", [False, True])
+def test_flat_allreduce_gloo_two_ranks(bucket):
+    port = 29500 + (os.getpid() % 1000) + (500 if bucket else 0)
     ctx = mp.get_context("spawn")
     with ctx.Manager() as m:
         out = m.dict()
-        procs = [ctx.Process(target=_allreduce_worker, args=(r, 2, port, out)) for r in range(2)]
+        procs = [ctx.Process(target=_allreduce_worker, args=(r, 2, port, out, bucket))
+                 for r in range(2)]
         for p in procs:
             p.start()
         for p in procs:
