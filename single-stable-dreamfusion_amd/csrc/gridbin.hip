@@ -30,6 +30,8 @@
 // order of the LDS atomics.
 #include "grid_common.h"
 
+#include <type_traits>
+
 namespace dfhip {
 namespace gb {
 
@@ -301,63 +303,73 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         double cw[1u << D][C];
         uint32_t cur[D];
         bool have = false;
-        for (uint32_t e = e0; e < e1; e += kRun) {
-            const uint32_t m = min(e1 - e, kRun);
-            // every load of the batch is issued before the first use: clamped
-            // indices instead of guarded loads (a guarded load is a branch
-            // with its own wait)
-            uint32_t sid[kRun];
-            float xs[kRun][D];
-            float gs[kRun][C];
+        // a lane walks a run of Q entries in batches of RUN loads; segments
+        // with Q == 1 (the fine levels) take single-entry batches instead of
+        // eight clamped duplicate loads per entry
+        auto walk = [&](auto run_c) {
+            constexpr uint32_t RUN = decltype(run_c)::value;
+            for (uint32_t e = e0; e < e1; e += RUN) {
+                const uint32_t m = min(e1 - e, RUN);
+                // every load of the batch is issued before the first use: clamped
+                // indices instead of guarded loads (a guarded load is a branch
+                // with its own wait)
+                uint32_t sid[RUN];
+                float xs[RUN][D];
+                float gs[RUN][C];
 #pragma unroll
-            for (uint32_t i = 0; i < kRun; ++i) sid[i] = seg[min(e + i, e1 - 1)];
+                for (uint32_t i = 0; i < RUN; ++i) sid[i] = seg[min(e + i, e1 - 1)];
 #pragma unroll
-            for (uint32_t i = 0; i < kRun; ++i) {
+                for (uint32_t i = 0; i < RUN; ++i) {
 #pragma unroll
-                for (uint32_t d = 0; d < D; ++d) xs[i][d] = inputs[(size_t)sid[i] * D + d];
-                load_grad<grad_t, C>(gl + (size_t)sid[i] * C, gs[i]);
-            }
+                    for (uint32_t d = 0; d < D; ++d) xs[i][d] = inputs[(size_t)sid[i] * D + d];
+                    load_grad<grad_t, C>(gl + (size_t)sid[i] * C, gs[i]);
+                }
 #pragma unroll
-            for (uint32_t i = 0; i < kRun; ++i) {
-                if (i < m) {  // guard, not break: keeps the run in registers
-                    float x[D];
+                for (uint32_t i = 0; i < RUN; ++i) {
+                    if (i < m) {  // guard, not break: keeps the run in registers
+                        float x[D];
 #pragma unroll
-                    for (uint32_t d = 0; d < D; ++d) x[d] = ge::dyn_map_t<POW2>(dyn, inv, xs[i][d]);
-                    uint32_t cell[D];
-                    float frac[D];
-                    locate<D>(c, align, x, cell, frac);
-                    bool same = have;
-#pragma unroll
-                    for (uint32_t d = 0; d < D; ++d)
-                        if (d < lead) same = same && (cell[d] == cur[d]);
-                    if (!same) {
-                        if (have) flush<D, C>(acc, r0, r1, c, lr, cur, cw);
-#pragma unroll
-                        for (uint32_t kc = 0; kc < (1u << D); ++kc)
-#pragma unroll
-                            for (uint32_t ch = 0; ch < C; ++ch) cw[kc][ch] = 0.0;
-#pragma unroll
-                        for (uint32_t d = 0; d < D; ++d) cur[d] = cell[d];
-                        have = true;
-                    }
-                    float tw = 1.0f;  // trailing dims dropped from the index: corners coincide
-#pragma unroll
-                    for (uint32_t d = 0; d < D; ++d)
-                        if (d >= lead) tw *= (1.0f - frac[d]) + frac[d];
-#pragma unroll
-                    for (uint32_t kc = 0; kc < (1u << D); ++kc) {
-                        if (kc >> lead) continue;
-                        float w = tw;
+                        for (uint32_t d = 0; d < D; ++d) x[d] = ge::dyn_map_t<POW2>(dyn, inv, xs[i][d]);
+                        uint32_t cell[D];
+                        float frac[D];
+                        locate<D>(c, align, x, cell, frac);
+                        bool same = have;
 #pragma unroll
                         for (uint32_t d = 0; d < D; ++d)
-                            if (d < lead) w *= (kc & (1u << d)) ? frac[d] : 1.0f - frac[d];
+                            if (d < lead) same = same && (cell[d] == cur[d]);
+                        if (!same) {
+                            if (have) flush<D, C>(acc, r0, r1, c, lr, cur, cw);
 #pragma unroll
-                        for (uint32_t ch = 0; ch < C; ++ch)
-                            cw[kc][ch] = fma((double)w, (double)gs[i][ch], cw[kc][ch]);
+                            for (uint32_t kc = 0; kc < (1u << D); ++kc)
+#pragma unroll
+                                for (uint32_t ch = 0; ch < C; ++ch) cw[kc][ch] = 0.0;
+#pragma unroll
+                            for (uint32_t d = 0; d < D; ++d) cur[d] = cell[d];
+                            have = true;
+                        }
+                        float tw = 1.0f;  // trailing dims dropped from the index: corners coincide
+#pragma unroll
+                        for (uint32_t d = 0; d < D; ++d)
+                            if (d >= lead) tw *= (1.0f - frac[d]) + frac[d];
+#pragma unroll
+                        for (uint32_t kc = 0; kc < (1u << D); ++kc) {
+                            if (kc >> lead) continue;
+                            float w = tw;
+#pragma unroll
+                            for (uint32_t d = 0; d < D; ++d)
+                                if (d < lead) w *= (kc & (1u << d)) ? frac[d] : 1.0f - frac[d];
+#pragma unroll
+                            for (uint32_t ch = 0; ch < C; ++ch)
+                                cw[kc][ch] = fma((double)w, (double)gs[i][ch], cw[kc][ch]);
+                        }
                     }
                 }
             }
-        }
+        };
+        if (Q <= 1)
+            walk(std::integral_constant<uint32_t, 1>{});
+        else
+            walk(std::integral_constant<uint32_t, kRun>{});
         if (have) flush<D, C>(acc, r0, r1, c, lr, cur, cw);
     }
     __syncthreads();
