@@ -214,57 +214,64 @@ __device__ __forceinline__ half8 grid_features(const half_t *__restrict__ table,
     if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
         return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
     const uint32_t *tab = reinterpret_cast<const uint32_t *>(table);
-    float frac[4][3];
-    uint32_t row[4][8];
+    // two batches of two levels: 16 row loads in flight per lane per batch
+    // (32 at once held 64 VGPRs of rows and bits and capped the kernel at 4
+    // waves per SIMD)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const LevelK k = lk[4 * q + h];
-        uint32_t cell[3];
+    for (int half = 0; half < 2; ++half) {
+        float frac[2][3];
+        uint32_t row[2][8];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const float p = fmaf(x[d], k.scale, align ? 0.0f : 0.5f);
-            cell[d] = (uint32_t)floorf(p);
-            frac[q][d] = p - (float)cell[d];
-        }
-        if (k.flags == 0u) {
-            // tiled / dense: corner offsets {0, 1, m1, m1 + 1, m2, ...}
-            const uint32_t i0 = cell[0] + cell[1] * k.m1 + cell[2] * k.m2;
-            const uint32_t o[8] = {0u, 1u, k.m1, k.m1 + 1u, k.m2, k.m2 + 1u, k.m2 + k.m1,
-                                   k.m2 + k.m1 + 1u};
+        for (int qq = 0; qq < 2; ++qq) {
+            const LevelK k = lk[4 * (2 * half + qq) + h];
+            uint32_t cell[3];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) row[q][c] = k.base + ((i0 + o[c]) & k.wmask);
-        } else {
+            for (int d = 0; d < 3; ++d) {
+                const float p = fmaf(x[d], k.scale, align ? 0.0f : 0.5f);
+                cell[d] = (uint32_t)floorf(p);
+                frac[qq][d] = p - (float)cell[d];
+            }
+            if (k.flags == 0u) {
+                // tiled / dense: corner offsets {0, 1, m1, m1 + 1, m2, ...}
+                const uint32_t i0 = cell[0] + cell[1] * k.m1 + cell[2] * k.m2;
+                const uint32_t o[8] = {0u, 1u, k.m1, k.m1 + 1u, k.m2, k.m2 + 1u, k.m2 + k.m1,
+                                       k.m2 + k.m1 + 1u};
 #pragma unroll
-            for (uint32_t c = 0; c < 8; ++c) {
-                const uint32_t px = cell[0] + (c & 1u), py = cell[1] + ((c >> 1) & 1u),
-                               pz = cell[2] + ((c >> 2) & 1u);
-                uint32_t idx = (k.flags & 2u) ? (px ^ (py * 2654435761u) ^ (pz * 805459861u))
-                                              : px + py * k.m1 + pz * k.m2;
-                idx = (k.flags & 1u) ? idx % k.hsize : (idx & k.wmask);
-                row[q][c] = k.base + idx;
+                for (int c = 0; c < 8; ++c) row[qq][c] = k.base + ((i0 + o[c]) & k.wmask);
+            } else {
+#pragma unroll
+                for (uint32_t c = 0; c < 8; ++c) {
+                    const uint32_t px = cell[0] + (c & 1u), py = cell[1] + ((c >> 1) & 1u),
+                                   pz = cell[2] + ((c >> 2) & 1u);
+                    uint32_t idx = (k.flags & 2u) ? (px ^ (py * 2654435761u) ^ (pz * 805459861u))
+                                                  : px + py * k.m1 + pz * k.m2;
+                    idx = (k.flags & 1u) ? idx % k.hsize : (idx & k.wmask);
+                    row[qq][c] = k.base + idx;
+                }
             }
         }
-    }
-    uint32_t bits[4][8];
+        uint32_t bits[2][8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+        for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) bits[q][c] = tab[row[q][c]];
+            for (int c = 0; c < 8; ++c) bits[qq][c] = tab[row[qq][c]];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        half_t a0 = (half_t)0.0f, a1 = (half_t)0.0f;
+        for (int qq = 0; qq < 2; ++qq) {
+            half_t a0 = (half_t)0.0f, a1 = (half_t)0.0f;
 #pragma unroll
-        for (uint32_t c = 0; c < 8; ++c) {
-            float w = 1.0f;
+            for (uint32_t c = 0; c < 8; ++c) {
+                float w = 1.0f;
 #pragma unroll
-            for (int d = 0; d < 3; ++d) w *= (c & (1u << d)) ? frac[q][d] : 1.0f - frac[q][d];
-            half_t v[2];
-            __builtin_memcpy(v, &bits[q][c], 4);
-            ge::acc_corner(a0, w, v[0]);
-            ge::acc_corner(a1, w, v[1]);
+                for (int d = 0; d < 3; ++d) w *= (c & (1u << d)) ? frac[qq][d] : 1.0f - frac[qq][d];
+                half_t v[2];
+                __builtin_memcpy(v, &bits[qq][c], 4);
+                ge::acc_corner(a0, w, v[0]);
+                ge::acc_corner(a1, w, v[1]);
+            }
+            const int q = 2 * half + qq;
+            out[2 * q] = a0;
+            out[2 * q + 1] = a1;
         }
-        out[2 * q] = a0;
-        out[2 * q + 1] = a1;
     }
     return out;
 }

@@ -39,7 +39,7 @@ namespace fm {
 // B operand, and are also written (permuted order, 16 B per lane) for the
 // backward.  xyz in [-bound, bound] is mapped to [0, 1] as grid.py:142 does.
 template <typename rgb_t>
-__global__ __launch_bounds__(256) void k_field_fwd_fused(
+__global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
     const float *__restrict__ xyz, float bound, const half_t *__restrict__ table,
     const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
