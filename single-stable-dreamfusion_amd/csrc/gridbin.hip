@@ -39,7 +39,7 @@ using ge::Levels;
 using ge::LevelCtx;
 using ge::SliceDyn;
 
-constexpr uint32_t kTile = 2048;     // samples per binning tile (ids per segment)
+constexpr uint32_t kTile = 1024;     // samples per binning tile (ids per segment)
 constexpr uint32_t kMaxBins = 1024;
 constexpr uint32_t kLdsBytes = 160 * 1024;
 
