@@ -86,7 +86,7 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     // each sample's position / gradient is read by the workgroups of one XCD
     // only (its L2).  Per XCD, each slice of level l gets q_l workgroups, q_l
     // chosen so that every level gets about 2 * CUs / L workgroups in total.
-    const uint32_t per_level = (2u * cus + L - 1) / L;
+    const uint32_t per_level = (4u * cus + L - 1) / L;
     (void)maxslices;
     uint64_t pf = 0;
     uint32_t slots = 0;
