@@ -85,7 +85,8 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     // XCD-aware walk: XCD x owns the x-th contiguous eighth of the tiles, so
     // each sample's position / gradient is read by the workgroups of one XCD
     // only (its L2).  Per XCD, each slice of level l gets q_l workgroups, q_l
-    // chosen so that every level gets about 2 * CUs / L workgroups in total.
+    // chosen so that every level gets about 4 * CUs / L workgroups in total
+    // (2 * CUs / L left the coarse levels' long walks as the tail: +4 %).
     const uint32_t per_level = (4u * cus + L - 1) / L;
     (void)maxslices;
     uint64_t pf = 0;
