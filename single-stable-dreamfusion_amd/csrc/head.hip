@@ -292,12 +292,21 @@ __global__ __launch_bounds__(1024) void k_entropy_fwd(uint32_t N, const float *_
                                                       float lambda, float *__restrict__ loss) {
     __shared__ double part[16];
     double s = 0.0;
-    for (uint32_t n = threadIdx.x; n < N; n += blockDim.x) {
-        float a = ws[n];
+    // elements n, n + blockDim, ... added in that order; eight loads in flight
+    // (one dependent load per element left this single block latency-bound)
+    auto term = [](float a) {
         a = a < kLo ? kLo : (a > kHi ? kHi : a);
-        const float e = -a * log2f(a) - (1.0f - a) * log2f(1.0f - a);
-        s += (double)e;
+        return -a * log2f(a) - (1.0f - a) * log2f(1.0f - a);
+    };
+    uint32_t n = threadIdx.x;
+    for (; n + 7 * blockDim.x < N; n += 8 * blockDim.x) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ws[n + u * blockDim.x];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += (double)term(v[u]);
     }
+    for (; n < N; n += blockDim.x) s += (double)term(ws[n]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
