@@ -427,6 +427,23 @@ __global__ __launch_bounds__(1024) void k_field_wgrad_sum(const float *__restric
     dst[k] = accumulate ? dst[k] + s : s;
 }
 
+// Workgroups of 256 threads that fit on the whole device at once for `kern`.
+template <typename K>
+static uint32_t resident_blocks(K kern) {
+    static uint32_t cached = 0;  // one per kernel instantiation
+    if (cached == 0) {
+        int dev = 0, cus = 256, per_cu = 0;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, 256, 0) !=
+                hipSuccess ||
+            per_cu <= 0)
+            per_cu = 4;
+        cached = (uint32_t)(per_cu * cus);
+    }
+    return cached;
+}
+
 static uint32_t bwd_blocks(uint32_t M) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
@@ -549,9 +566,13 @@ extern "C" int dfhip_grid_field_forward(const float *xyz, float bound, const voi
     }
     hipStream_t s = as_stream(stream);
     const ge::Levels lv = ge::make_levels(L, S, H);
-    // persistent waves: enough to fill the chip, each walks 16-sample tiles
+    // persistent waves: exactly one resident wave per slot of the chip (each
+    // walks ~M / (16 * waves) tiles); more blocks than fit leave a partial
+    // last round of blocks (4096 blocks at 5 waves/SIMD were 3.2 rounds)
     const uint32_t tiles = ceil_div(cap, 16u);
-    const uint32_t blocks = ceil_div(tiles, 4u) < 4096u ? ceil_div(tiles, 4u) : 4096u;
+    const uint32_t fit = rgb_dtype == DFHIP_F16 ? resident_blocks(k_field_fwd_fused<half_t>)
+                                                : resident_blocks(k_field_fwd_fused<float>);
+    const uint32_t blocks = ceil_div(tiles, 4u) < fit ? ceil_div(tiles, 4u) : fit;
     if (rgb_dtype == DFHIP_F32)
         k_field_fwd_fused<float><<<blocks, 256, 0, s>>>(
             xyz, bound, (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2,
