@@ -479,6 +479,18 @@ int dfhip_ray_head_backward(uint32_t N, const float *g_image, const float *ws,
                             float *grad_image, float *grad_ws, float *grad_bg, float *partial,
                             float *gw1, float *gb1, float *gw2, float *gb2,
                             dfhip_stream_t stream);
+/* The same with the entropy regulariser's backward fused (utils.py:386-391):
+ * grad_ws = -(sum_c g_c bg_c) + grad_loss[0] * lambda / N * log2((1 - a) / a)
+ * (zero where the clamp to [1e-5, 1 - 1e-5] is active), i.e. what
+ * dfhip_ray_head_backward followed by dfhip_entropy_backward_accumulate write,
+ * bit for bit, in one pass (native train step). */
+int dfhip_ray_head_backward_entropy(uint32_t N, const float *g_image, const float *ws,
+                                    const float *rays_d, const float *w1, const float *b1,
+                                    const float *w2, const float *b2, const float *bg_color,
+                                    float *grad_image, float *grad_ws, float *grad_bg,
+                                    float *partial, float *gw1, float *gb1, float *gw2,
+                                    float *gb2, const float *grad_loss, float lambda,
+                                    dfhip_stream_t stream);
 
 /* nerf/utils.py:386-391 entropy regulariser: loss[0] = lambda * mean(-a log2 a
  * - (1 - a) log2(1 - a)), a = clamp(ws, 1e-5, 1 - 1e-5) (f64 sum); backward

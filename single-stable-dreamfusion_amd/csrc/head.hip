@@ -170,6 +170,15 @@ __global__ __launch_bounds__(256) void k_head_bwd_plain(
     grad_ws[n] = -sw;
 }
 
+constexpr float kLo = 1e-5f, kHi = 1.0f - 1e-5f;
+
+// d loss / d ws of lambda * mean(entropy(clamp(ws))) for upstream gradient g:
+// g * lambda / N * log2((1 - a) / a), zero where the clamp is active.
+__device__ __forceinline__ float entropy_grad(uint32_t N, float a, const float *g, float lambda) {
+    const float scale = g[0] * lambda / (float)N;
+    return (a >= kLo && a <= kHi) ? scale * (log2f(1.0f - a) - log2f(a)) : 0.0f;
+}
+
 // Network backward: the forward is recomputed (four lanes per ray), then the
 // sigmoid and the two f16 Linear layers are run backward and this block's
 // weight-gradient partials (f32 sums over its 64 rays of f16 products) formed
@@ -178,7 +187,7 @@ __global__ __launch_bounds__(256) void k_head_bwd_net(
     uint32_t N, const float *__restrict__ g_image /* [3, N] */, const float *__restrict__ ws,
     const float *__restrict__ rays_d, const float *w1, const float *b1, const float *w2,
     const float *b2, float *__restrict__ grad_image, float *__restrict__ grad_ws,
-    float *__restrict__ partial) {
+    float *__restrict__ partial, const float *__restrict__ ent_grad_loss, float ent_lambda) {
     __shared__ W w;
     __shared__ float s_x[kRays][kIn + 1];
     __shared__ half_t s_dh[kRays][kHid];  // relu-masked hidden grads (f16 values)
@@ -210,7 +219,10 @@ __global__ __launch_bounds__(256) void k_head_bwd_net(
             grad_image[3 * (size_t)n + k] = g[k];
             sw = sw + g[k] * bg[k];
         }
-        grad_ws[n] = -sw;
+        // the entropy regulariser's gradient added as autograd sums the two
+        // uses of ws (k_entropy_bwd's value, same f32 arithmetic)
+        grad_ws[n] = ent_grad_loss ? -sw + entropy_grad(N, ws[n], ent_grad_loss, ent_lambda)
+                                   : -sw;
     }
     const float t = live ? 1.0f - ws[n] : 0.0f;
     float dout[3];
@@ -286,8 +298,6 @@ __global__ __launch_bounds__(1024) void k_head_wsum(const float *__restrict__ pa
 }
 
 // ---------------------------------------------------------------- entropy
-constexpr float kLo = 1e-5f, kHi = 1.0f - 1e-5f;
-
 __global__ __launch_bounds__(1024) void k_entropy_fwd(uint32_t N, const float *__restrict__ ws,
                                                       float lambda, float *__restrict__ loss) {
     __shared__ double part[16];
@@ -326,9 +336,7 @@ __global__ __launch_bounds__(256) void k_entropy_bwd(uint32_t N, const float *__
                                                      float *__restrict__ grad_ws) {
     const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
-    const float a = ws[n];
-    const float scale = g[0] * lambda / (float)N;
-    const float v = (a >= kLo && a <= kHi) ? scale * (log2f(1.0f - a) - log2f(a)) : 0.0f;
+    const float v = entropy_grad(N, ws[n], g, lambda);
     grad_ws[n] = ACC ? grad_ws[n] + v : v;
 }
 
@@ -369,12 +377,13 @@ extern "C" int dfhip_ray_head_forward(uint32_t N, const float *ws, const float *
     return check_launch(name);
 }
 
-extern "C" int dfhip_ray_head_backward(uint32_t N, const float *g_image, const float *ws,
-                                       const float *rays_d, const float *w1, const float *b1,
-                                       const float *w2, const float *b2, const float *bg_color,
-                                       float *grad_image, float *grad_ws, float *grad_bg,
-                                       float *partial, float *gw1, float *gb1, float *gw2,
-                                       float *gb2, dfhip_stream_t stream) {
+static int ray_head_backward(uint32_t N, const float *g_image, const float *ws,
+                             const float *rays_d, const float *w1, const float *b1,
+                             const float *w2, const float *b2, const float *bg_color,
+                             float *grad_image, float *grad_ws, float *grad_bg, float *partial,
+                             float *gw1, float *gb1, float *gw2, float *gb2,
+                             const float *ent_grad_loss, float ent_lambda,
+                             dfhip_stream_t stream) {
     const char *name = "ray_head_backward";
     if (N == 0) return DFHIP_OK;
     if (!g_image || !ws || !grad_image || !grad_ws) {
@@ -391,14 +400,43 @@ extern "C" int dfhip_ray_head_backward(uint32_t N, const float *g_image, const f
     if (net) {
         const uint32_t blocks = ceil_div(N, (uint32_t)hd::kRays);
         hd::k_head_bwd_net<<<blocks, 256, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
-                                                  grad_image, grad_ws, partial);
+                                                  grad_image, grad_ws, partial, ent_grad_loss,
+                                                  ent_lambda);
         hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u), 1024, 0, s>>>(
             partial, blocks, gw1, gb1, gw2, gb2);
     } else {
         hd::k_head_bwd_plain<<<ceil_div(N, 256u), 256, 0, s>>>(N, g_image, ws, bg_color,
                                                                grad_image, grad_ws, grad_bg);
+        if (ent_grad_loss)
+            hd::k_entropy_bwd<true><<<ceil_div(N, 256u), 256, 0, s>>>(N, ws, ent_grad_loss,
+                                                                     ent_lambda, grad_ws);
     }
     return check_launch(name);
+}
+
+extern "C" int dfhip_ray_head_backward(uint32_t N, const float *g_image, const float *ws,
+                                       const float *rays_d, const float *w1, const float *b1,
+                                       const float *w2, const float *b2, const float *bg_color,
+                                       float *grad_image, float *grad_ws, float *grad_bg,
+                                       float *partial, float *gw1, float *gb1, float *gw2,
+                                       float *gb2, dfhip_stream_t stream) {
+    return ray_head_backward(N, g_image, ws, rays_d, w1, b1, w2, b2, bg_color, grad_image,
+                             grad_ws, grad_bg, partial, gw1, gb1, gw2, gb2, nullptr, 0.0f,
+                             stream);
+}
+
+extern "C" int dfhip_ray_head_backward_entropy(
+    uint32_t N, const float *g_image, const float *ws, const float *rays_d, const float *w1,
+    const float *b1, const float *w2, const float *b2, const float *bg_color, float *grad_image,
+    float *grad_ws, float *grad_bg, float *partial, float *gw1, float *gb1, float *gw2,
+    float *gb2, const float *grad_loss, float lambda, dfhip_stream_t stream) {
+    if (N > 0 && !grad_loss) {
+        set_error("ray_head_backward_entropy: null grad_loss");
+        return DFHIP_EINVAL;
+    }
+    return ray_head_backward(N, g_image, ws, rays_d, w1, b1, w2, b2, bg_color, grad_image,
+                             grad_ws, grad_bg, partial, gw1, gb1, gw2, gb2, grad_loss, lambda,
+                             stream);
 }
 
 extern "C" int dfhip_entropy_forward(uint32_t N, const float *ws, float lambda, float *loss,

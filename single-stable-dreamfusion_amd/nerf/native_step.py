@@ -15,8 +15,8 @@ the step is, with the same kernels and the same arithmetic:
       pred_rgb, step counter = 0
   graph: march count / emit -> f16 table copy -> fused grid field ->
       compositing -> ray head (background MLP, mix, depth, mask) -> entropy
-      loss -> ray head backward -> entropy backward (accumulated into the
-      weights-sum gradient) -> compositing backward -> field MLP backward
+      loss -> ray head backward with the entropy gradient fused into the
+      weights-sum gradient -> compositing backward -> field MLP backward
   eager (timed): binned embedding backward -> GradScaler + Adam
 
 Gradients are bit-identical to the autograd step given the same draws
@@ -201,12 +201,14 @@ class NativeAlbedoStep:
             call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss), stream())
         # backward: SDS gradient at pred_rgb (unscaled), entropy gradient x scale
         gbw = self._bg_grads()
-        call("dfhip_ray_head_backward", N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d),
-             *[ptr(w) for w in bw], ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws),
-             None, ptr(self.head_partial), *[ptr(g) for g in gbw], stream())
+        head_args = (N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d), *[ptr(w) for w in bw],
+                     ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws), None,
+                     ptr(self.head_partial), *[ptr(g) for g in gbw])
         if self.lam > 0:
-            call("dfhip_entropy_backward_accumulate", N, ptr(self.ws), ptr(scale), self.lam,
-                 ptr(self.grad_ws), stream())
+            # head backward + the entropy term's gradient (upstream: the scale)
+            call("dfhip_ray_head_backward_entropy", *head_args, ptr(scale), self.lam, stream())
+        else:
+            call("dfhip_ray_head_backward", *head_args, stream())
         _raymarching.composite_rays_train_backward_mixed(
             self.grad_ws, self.grad_image, self.sigma, self.albedo, self.deltas, self.rays,
             self.ws, self.image, cap, N, 1e-4, self.grad_sigma, self.grad_albedo, False)
