@@ -352,3 +352,35 @@ def test_grid_backward_binned_empty(gpu):
     gemb = _binned(e, torch.zeros(100, 3, device=gpu), 1.0, offs, rows, 100, m_dev, 3, 2, 16, S,
                    16, 1, gpu)
     assert torch.all(gemb == 0)
+
+
+def test_grid_backward_binned_phases(gpu):
+    """The phase-split entry point: bin (phase 1) then walk + sum (phase 2),
+    as two launches, equals the one-call form (phase 3) bit for bit."""
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    x = T(_samples(30000, 31), gpu)
+    B = x.shape[0]
+    g = (np.random.default_rng(32).normal(size=(B, 32)) * 0.1).astype(np.float16)
+    glbc = T(g, gpu).view(B, 16, 2).transpose(0, 1).contiguous()
+    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, 16, 2)
+    out = {}
+    for mode in ("split", "whole"):
+        ent = torch.empty(ne, dtype=torch.int32, device=gpu)
+        cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
+        part = torch.full((npf,), float("nan"), device=gpu)
+        gemb = torch.full((rows, 2), float("nan"), device=gpu)
+        args = (glbc, x, 0.0, T(offs, gpu), offs, gemb, B, None, 3, 2, 16, S, 16, 1, False, ent,
+                cnt, part)
+        if mode == "split":
+            _gridencoder.binned_launcher(*args, phase=1)()
+            _gridencoder.binned_launcher(*args, phase=2)()
+        else:
+            _gridencoder.binned_launcher(*args, phase=3)()
+        out[mode] = gemb
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["whole"]).all()
+    assert torch.equal(out["split"], out["whole"])
+    with pytest.raises(RuntimeError):
+        _gridencoder.binned_launcher(*args, phase=4)
