@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-infer", action="store_true",
                    help="skip the C4 inference-render measurement")
     p.add_argument("--infer-res", type=int, default=800)
+    p.add_argument("--launcher-selftest", action="store_true",
+                   help="CPU/gloo check of the N-rank launch only (no GPU work)")
     return p.parse_args()
 
 
@@ -246,11 +248,65 @@ def load_pmc(name):
     return total
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv=None):
+    """`bench.py --gpus N` without a torch.distributed launcher: start N child
+    processes (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their env,
+    rendezvous on 127.0.0.1) and return the worst exit code.  Called before
+    anything in this process touches the GPU, and it never exec()s: the
+    children are fresh interpreters running this same file."""
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()),
+                                       *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def launcher_selftest(args, rank, world):
+    """CPU check of the N-rank launch (gloo): every rank joins, the all-reduced
+    payload is the same everywhere and rank 0 prints the bench line's
+    world-derived fields.  No GPU work."""
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(args.seed)               # identical replica init
+    w = torch.randn(1024)
+    g = torch.full((1024,), float(rank + 1))   # per-rank gradient
+    dist.all_reduce(g)
+    g /= world
+    w -= 0.1 * g
+    digest = torch.tensor([float(w.double().sum())], dtype=torch.float64)
+    lo, hi = digest.clone(), digest.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "config": {"parallelism": f"dp{world}"},
+                          "replicas_identical": bool(lo.item() == hi.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launcher_selftest:
+        return launcher_selftest(args, rank, world)
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:

@@ -181,3 +181,24 @@ def test_rand_poses_host():
         phis = torch.from_numpy(np.where(phis < 0, phis + 2 * np.pi, phis).astype(np.float32))
         want = get_view_direction(thetas, phis, np.deg2rad(30), np.deg2rad(60))
         assert (want == dirs).float().mean() >= 0.75  # boundary rounding may differ
+
+
+def test_bench_launches_n_ranks_itself():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts two ranks itself
+    (gloo self-test: no GPU work) and rank 0 reports n_gpus 2 / dp2 with
+    bit-identical replicas after one all-reduced update."""
+    import json
+    import subprocess
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2",
+                        "--launcher-selftest"], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["replicas_identical"]
