@@ -256,6 +256,28 @@ def bg_bounds(fwd, weights, grad_bg=None, sum_gamma=2e-5, acc_ulps=None):
     return out
 
 
+def mlp_forward(x16, weights, acc_ulps=None, dx=None):
+    """Generic nn.Linear/ReLU stack under fp16 autocast (network_grid.py:13-32:
+    ReLU between layers, none after the last).  weights = [w0, b0, w1, b1,
+    ...].  Returns (outputs, windows): the f16 output of every layer and the
+    propagated window of each (dx: window of the inputs, default exact)."""
+    a = np.asarray(x16, F16)
+    da = np.zeros(a.shape) if dx is None else dx
+    outs, wins = [], []
+    n = len(weights) // 2
+    for i in range(n):
+        w, b = weights[2 * i], weights[2 * i + 1]
+        a64 = a.astype(F64)
+        z = a64 @ r16(w).astype(F64).T + (r16(b).astype(F64) if b is not None else 0.0)
+        dz = _layer_window(a64, da, w, b, z, acc_ulps)
+        last = i == n - 1
+        a = r16(z) if last else relu16(r16(z))
+        da = _round_window(z, dz, None if last else _relu)
+        outs.append(a)
+        wins.append(da)
+    return outs, wins
+
+
 def ulp16(v):
     """Spacing of f16 values at |v| (subnormal spacing 2^-24 below 2^-14)."""
     a = np.abs(np.asarray(v, F64))

@@ -1,10 +1,8 @@
-"""Fused field head (csrc/fieldmlp.hip + nerf/field.py) against the unfused
-reference composition (GridEncoder -> nn.Linear/ReLU stack under fp16
-autocast -> trunc_exp(h0 + gaussian) / sigmoid), network_grid.py:13-32,76-87.
-
-fp16 tolerance: the fused kernel accumulates each layer on MFMA in a different
-order than hipBLASLt and keeps f32 weight-gradient sums (the reference rounds
-the weight gradients to f16 before the f32 cast)."""
+"""Fused field head (csrc/fieldmlp.hip + nerf/field.py, the product autograd
+path) against the CPU oracle of the reference composition (GridEncoder ->
+nn.Linear/ReLU stack under fp16 autocast -> trunc_exp(h0 + gaussian) /
+sigmoid, network_grid.py:13-32,76-87): oracle/field.py with its propagated
+f16-rounding windows (tests/oracle_checks.py), forward and all gradients."""
 import numpy as np
 import pytest
 import torch
@@ -24,40 +22,30 @@ def _field(gpu, seed=0, emb_scale=0.5):
     return enc, layers
 
 
-def _reference(x, enc, layers):
-    h = enc(x, bound=1.0)
-    for i, lin in enumerate(layers):
-        h = lin(h)
-        if i < 2:
-            h = torch.relu(h)
-    g = 5 * torch.exp(-(x ** 2).sum(-1) / (2 * 0.2 ** 2))
-    from activation import trunc_exp
-    return trunc_exp(h[..., 0] + g), torch.sigmoid(h[..., 1:])
-
-
 @pytest.mark.parametrize("M", [1, 31, 50_003])
-def test_fused_field_matches_unfused(gpu, M):
+def test_fused_field_matches_oracle(gpu, M):
     from nerf.field import eligible, grid_field
+    from oracle_checks import check_field
     enc, layers = _field(gpu)
     g = torch.Generator(device="cpu").manual_seed(1)
     x = (torch.rand(M, 3, generator=g) * 2 - 1).mul_(0.9).to(gpu)
-    gs = torch.randn(M, generator=g).to(gpu)
-    ga = torch.randn(M, 3, generator=g).to(gpu)
+    gs = (torch.randn(M, generator=g) * 1e-2).to(gpu)
+    ga = (torch.randn(M, 3, generator=g) * 1e-2).to(gpu)
     with torch.autocast("cuda", dtype=torch.float16):
         assert eligible(enc, layers, x)
         s1, a1 = grid_field(x, 1.0, enc, layers)
-        s0, a0 = _reference(x, enc, layers)
-    assert s1.dtype == torch.float32 and a1.dtype == torch.float16 and a0.dtype == torch.float16
-    torch.testing.assert_close(s1, s0.float(), rtol=2e-2, atol=1e-3)
-    torch.testing.assert_close(a1.float(), a0.float(), rtol=0, atol=4e-3)
+    assert s1.dtype == torch.float32 and a1.dtype == torch.float16
     params = [enc.embeddings] + list(layers.parameters())
     g1 = torch.autograd.grad((s1 * gs).sum() + (a1.float() * ga).sum(), params)
-    g0 = torch.autograd.grad((s0.float() * gs).sum() + (a0.float() * ga).sum(), params)
-    for i, (a, b) in enumerate(zip(g1, g0)):
-        assert a.dtype == torch.float32 and a.shape == b.shape
-        b = b.float()
-        err = (a - b).norm() / b.norm().clamp(min=1e-12)
-        assert err < 2e-2, f"param {i}: rel err {err:.3e}"
+    for t in g1:
+        assert t.dtype == torch.float32
+    ws = [p.detach().float().cpu().numpy() for p in layers.parameters()]
+    stats = check_field(x.cpu().numpy(), enc.embeddings.detach().cpu().numpy(),
+                        enc.offsets.cpu().numpy(), float(np.log2(enc.per_level_scale)), 16, ws,
+                        s1.detach().cpu().numpy(), a1.detach().cpu().numpy(),
+                        gs.cpu().numpy(), ga.cpu().numpy().astype(np.float16),
+                        [t.cpu().numpy() for t in g1[1:]], g1[0].cpu().numpy(), label=f"M={M}")
+    print(stats)
 
 
 def test_fused_field_deterministic(gpu):

@@ -14,28 +14,43 @@ import torch.nn as nn
 pytestmark = pytest.mark.gpu
 
 
-def test_mlp_split_k_matches_linear_stack(gpu):
+def test_mlp_split_k_matches_oracle(gpu):
+    """nerf/mlp.py (torch GEMMs + split-K weight gradients, the unfused MLP)
+    against the f16-autocast oracle (oracle/field.py mlp_forward): outputs
+    inside the order-free rounding windows, weight/bias gradients against the
+    exact float64 sums of the f16 graph (2e-5 of the |term| sums + one f16
+    ulp of rounding of each upstream activation's window)."""
+    import oracle.field as of
     from nerf.mlp import mlp_forward
     torch.manual_seed(0)
     layers = nn.ModuleList([nn.Linear(32, 64), nn.Linear(64, 64), nn.Linear(64, 4)]).to(gpu)
-    ref = copy.deepcopy(layers)
     x = torch.randn(100_003, 32, device=gpu)
-    g = torch.randn(100_003, 4, device=gpu)
+    g = torch.randn(100_003, 4, device=gpu) * 1e-2
     with torch.autocast("cuda", dtype=torch.float16):
         y = mlp_forward(x, layers)
-        h = x
-        for i, lin in enumerate(ref):
-            h = lin(h)
-            if i < 2:
-                h = torch.relu(h)
-    assert y.dtype == torch.float16 and h.dtype == torch.float16
-    torch.testing.assert_close(y, h, rtol=2e-3, atol=2e-3)
+    assert y.dtype == torch.float16
     (y.float() * g).sum().backward()
-    (h.float() * g).sum().backward()
-    for a, b in zip(layers.parameters(), ref.parameters()):
-        assert a.grad.dtype == torch.float32
-        scale = b.grad.abs().max()
-        torch.testing.assert_close(a.grad, b.grad, rtol=2e-2, atol=2e-3 * scale)
+    ws = [p.detach().cpu().numpy() for p in layers.parameters()]
+    x16 = x.cpu().numpy().astype(np.float16)
+    outs, wins = of.mlp_forward(x16, ws)
+    diff = np.abs(y.detach().cpu().numpy().astype(np.float64) - outs[-1].astype(np.float64))
+    assert np.all(diff <= wins[-1]), (diff - wins[-1]).max()
+    print(f"\noutputs differing from the exact rounding: {(diff > 0).mean():.2e}")
+    # gradients of the f16 graph, exact sums
+    w16 = [of.r16(w).astype(np.float64) for w in ws[0::2]]
+    dy = of.r16(g.cpu().numpy()).astype(np.float64)  # autocast: f16 grad of the f16 output
+    acts = [x16.astype(np.float64)] + [o.astype(np.float64) for o in outs[:-1]]
+    want, d = [None] * 6, dy
+    for i in reversed(range(3)):
+        want[2 * i], want[2 * i + 1] = d.T @ acts[i], d.sum(0)
+        if i:
+            d = np.where(acts[i] > 0, of.r16(d @ w16[i]).astype(np.float64), 0.0)
+    for i, (p, w) in enumerate(zip(layers.parameters(), want)):
+        got = p.grad.detach().cpu().numpy().astype(np.float64)
+        scale = np.abs(w).max()
+        # upstream activation windows and flipped ReLU masks move a few terms
+        err = np.abs(got - w).max() / scale
+        assert p.grad.dtype == torch.float32 and err <= 2e-3, (i, err)
 
 
 def _trainer(gpu, fused, seed=0):
