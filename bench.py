@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-infer", action="store_true",
                    help="skip the C4 inference-render measurement")
     p.add_argument("--infer-res", type=int, default=800)
+    p.add_argument("--no-alt-backward", action="store_true",
+                   help="skip timing the other backward structure (two-pass / fused)")
     p.add_argument("--launcher-selftest", action="store_true",
                    help="CPU/gloo check of the N-rank launch only (no GPU work)")
     return p.parse_args()
@@ -315,8 +317,7 @@ def main():
     import _dfhip
     _dfhip.load()
     trainer, data = make_trainer(args.res, args.seed, rank, world, not args.two_pass_backward,
-                                 graph=not (args.eager or args.two_pass_backward),
-                                 mock_sds=args.mock_sds)
+                                 graph=not args.eager, mock_sds=args.mock_sds)
 
     def step():
         trainer.train_iteration(data.collate([0]))
@@ -398,6 +399,23 @@ def main():
         step_ms = result["ms_per_step"]
         result["kernel_share_of_step"] = {k: round(v["total_ms"] / args.steps / step_ms, 4)
                                           for k, v in kernels.items()}
+    if world == 1 and not args.no_alt_backward:
+        # the other backward structure, same workload and launch mode: the
+        # reference's two passes (sd.py:115 + utils.py:708) beside the fused
+        # headline (or the fused one beside a --two-pass-backward headline)
+        alt, alt_data = make_trainer(args.res, args.seed, rank, world, args.two_pass_backward,
+                                     graph=not args.eager, mock_sds=args.mock_sds)
+        for _ in range(args.warmup):
+            alt.train_iteration(alt_data.collate([0]))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            alt.train_iteration(alt_data.collate([0]))
+        torch.cuda.synchronize()
+        key = "fused_ms_per_step" if args.two_pass_backward else "two_pass_ms_per_step"
+        result[key] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
+        del alt, alt_data
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_infer:
         result["inference"] = bench_inference(device, args.infer_res)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -406,6 +406,18 @@ int dfhip_grid_field_backward(const void *enc, const float *xyz, float bound, co
                               uint32_t total_rows, uint32_t L, float S, uint32_t H,
                               uint32_t gridtype, int align_corners, float *grad_embeddings,
                               float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream);
+/* Same, but the weight gradients (and grad_embeddings when given) are ADDED
+ * into (dst + new, f32): the second backward of the reference's two-pass step
+ * (SDS latents.backward, sd.py:115, then scaler.scale(loss).backward(),
+ * utils.py:708), where autograd accumulates each parameter's .grad. */
+int dfhip_grid_field_backward_accumulate(
+    const void *enc, const float *xyz, float bound, const float *w1, const float *b1,
+    const float *w2, const float *b2, const float *w3, const float *b3, const float *grad_sigma,
+    const void *grad_rgb, int grad_rgb_dtype, uint32_t cap, const int32_t *m_dev,
+    void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1, float *gb1, float *gw2,
+    float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
+    float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
+    float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream);
 
 /* Binned owner-computes form of grid_encode_backward (gridencoder.cu:226-313,
  * csrc/gridbin.hip) for D = 3, C in {1, 2, 4}: (sample, level) pairs are binned

@@ -87,6 +87,10 @@ _SIGS = {
     "dfhip_grid_field_backward": [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                   _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32, _vp],
+    "dfhip_grid_field_backward_accumulate": [
+        _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp, _vp, _vp, _u32,
+        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32,
+        _vp],
     "dfhip_adam_amp_step": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                             _vp, _vp, _f32, _f32, _i32, _vp],
     "dfhip_ray_head_forward": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -93,7 +93,9 @@ def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners
 
 def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lbc, mlp_partial,
                         grads, offsets, total_rows, S, H, gridtype, align_corners,
-                        grad_embeddings, grid_partial, grid_parts, m_dev=None):
+                        grad_embeddings, grid_partial, grid_parts, m_dev=None, accumulate=False):
+    """accumulate: add into grads (and grad_embeddings) instead of overwriting
+    (the second backward of the reference's two-pass step)."""
     cap = xyz.shape[0]
     for t, n in ((enc, "enc"), (grad_rgb, "grad_rgb"), (d_enc_lbc, "d_enc")):
         checked(t, n)
@@ -106,7 +108,8 @@ def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lb
     if m_dev is not None:
         checked(m_dev, "m_dev", "int")
     gp = _weights(grads)
-    call("dfhip_grid_field_backward", ptr(enc), ptr(xyz), float(bound), *_weights(weights),
+    call("dfhip_grid_field_backward_accumulate" if accumulate else "dfhip_grid_field_backward",
+         ptr(enc), ptr(xyz), float(bound), *_weights(weights),
          ptr(grad_sigma), ptr(grad_rgb), _d.dtype_code(grad_rgb, "grad_rgb"), cap, ptr(m_dev),
          ptr(d_enc_lbc), ptr(mlp_partial), backward_parts(cap) if cap else 1, *gp,
          ptr(offsets), int(total_rows), offsets.shape[0] - 1, float(S), int(H), int(gridtype),

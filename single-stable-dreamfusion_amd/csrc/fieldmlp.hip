@@ -588,15 +588,15 @@ extern "C" int dfhip_grid_field_forward(const float *xyz, float bound, const voi
     return check_launch(name);
 }
 
-extern "C" int dfhip_grid_field_backward(
-    const void *enc, const float *xyz, float bound, const float *w1, const float *b1,
-    const float *w2, const float *b2, const float *w3, const float *b3, const float *grad_sigma,
-    const void *grad_rgb, int grad_rgb_dtype, uint32_t cap, const int32_t *m_dev,
-    void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1, float *gb1, float *gw2,
-    float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
-    float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
-    float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream) {
-    const char *name = "grid_field_backward";
+static int grid_field_backward(
+    const char *name, const void *enc, const float *xyz, float bound, const float *w1,
+    const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
+    const float *grad_sigma, const void *grad_rgb, int grad_rgb_dtype, uint32_t cap,
+    const int32_t *m_dev, void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1,
+    float *gb1, float *gw2, float *gb2, float *gw3, float *gb3, const int32_t *offsets,
+    uint32_t total_rows, uint32_t L, float S, uint32_t H, uint32_t gridtype, int align_corners,
+    float *grad_embeddings, float *grid_partial, uint32_t grid_parts, int accumulate,
+    dfhip_stream_t stream) {
     if (!check_field_grid(name, L)) return DFHIP_EINVAL;
     if (!(bound > 0.0f)) {
         set_error("%s: bound must be > 0", name);
@@ -635,11 +635,41 @@ extern "C" int dfhip_grid_field_backward(
         (void)hipMemsetAsync(mlp_partial, 0, kParams * sizeof(float), s);
     }
     k_field_wgrad_sum<<<ceil_div((uint32_t)kParams, 64u), 1024, 0, s>>>(
-        mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, 0);
+        mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, accumulate);
     int rc = check_launch(name);
     if (rc != DFHIP_OK || grad_embeddings == nullptr) return rc;
     return ge::grid_backward_sliced(name, DFHIP_F16, DFHIP_F32, d_enc_lbc, xyz, offsets,
                                     grad_embeddings, total_rows, cap, 3, 2, L, S, H, gridtype,
-                                    align_corners, grid_partial, grid_parts, 0,
+                                    align_corners, grid_partial, grid_parts, accumulate,
                                     ge::SliceDyn{m_dev, bound}, s);
+}
+
+extern "C" int dfhip_grid_field_backward(
+    const void *enc, const float *xyz, float bound, const float *w1, const float *b1,
+    const float *w2, const float *b2, const float *w3, const float *b3, const float *grad_sigma,
+    const void *grad_rgb, int grad_rgb_dtype, uint32_t cap, const int32_t *m_dev,
+    void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1, float *gb1, float *gw2,
+    float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
+    float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
+    float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream) {
+    return grid_field_backward("grid_field_backward", enc, xyz, bound, w1, b1, w2, b2, w3, b3,
+                               grad_sigma, grad_rgb, grad_rgb_dtype, cap, m_dev, d_enc_lbc,
+                               mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, offsets,
+                               total_rows, L, S, H, gridtype, align_corners, grad_embeddings,
+                               grid_partial, grid_parts, 0, stream);
+}
+
+extern "C" int dfhip_grid_field_backward_accumulate(
+    const void *enc, const float *xyz, float bound, const float *w1, const float *b1,
+    const float *w2, const float *b2, const float *w3, const float *b3, const float *grad_sigma,
+    const void *grad_rgb, int grad_rgb_dtype, uint32_t cap, const int32_t *m_dev,
+    void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1, float *gb1, float *gw2,
+    float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
+    float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
+    float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream) {
+    return grid_field_backward("grid_field_backward_accumulate", enc, xyz, bound, w1, b1, w2, b2,
+                               w3, b3, grad_sigma, grad_rgb, grad_rgb_dtype, cap, m_dev, d_enc_lbc,
+                               mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, offsets,
+                               total_rows, L, S, H, gridtype, align_corners, grad_embeddings,
+                               grid_partial, grid_parts, 1, stream);
 }

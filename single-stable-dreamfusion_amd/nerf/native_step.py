@@ -24,6 +24,11 @@ Gradients are bit-identical to the autograd step given the same draws
 autograd puts it (the entropy term's upstream gradient is the scale; the SDS
 gradient is not scaled, the reference quirk kept by Trainer.backward_only).
 
+With trainer.fused_backward off the step keeps the reference's two backward
+passes (SDS latents.backward, sd.py:115, then scaler.scale(loss).backward(),
+utils.py:708): the compositing / field backwards run once per pass and the
+second pass adds into the parameter gradients, as autograd accumulates them.
+
 Applies to the albedo shading with the InjectedSDS guidance, the
 reference's grid network (16 x 2 tiled grid, 32 -> 64 -> 64 -> 4 MLP), a
 background MLP (bg_radius > 0) or a random background colour, and
@@ -45,7 +50,7 @@ def eligible(trainer, shading):
     m, opt = trainer.model, trainer.opt
     if shading != "albedo" or not isinstance(trainer.guidance, InjectedSDS):
         return False
-    if not (trainer.fp16 and m.cuda_ray and trainer.fused_backward):
+    if not (trainer.fp16 and m.cuda_ray):
         return False
     if opt.lambda_opacity > 0:
         return False
@@ -149,6 +154,13 @@ class NativeAlbedoStep:
         # reduces in place (nerf/utils.py flat_allreduce_)
         from .utils import flat_grad_bucket_
         self.grad_bucket = flat_grad_bucket_(m.parameters())
+        # the reference's two backward passes (SDS, then the scaled loss)
+        self.two_pass = not trainer.fused_backward
+        if self.two_pass:
+            self.d_enc2 = torch.empty_like(self.d_enc)
+            self.zero_image = torch.zeros(N, 3, **f32)
+            self.grad_ws2 = torch.empty(N, **f32)
+            self._emb_launch2 = None
         self.params = [p for p in m.parameters() if p.requires_grad]
         self.grads = [(p, p.grad) for p in self.params]
         self._emb_launch = None
@@ -200,6 +212,9 @@ class NativeAlbedoStep:
         if self.lam > 0:
             call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss), stream())
         # backward: SDS gradient at pred_rgb (unscaled), entropy gradient x scale
+        if self.two_pass:
+            self._backward_two_pass(bw, scale)
+            return self.loss
         gbw = self._bg_grads()
         head_args = (N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d), *[ptr(w) for w in bw],
                      ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws), None,
@@ -219,6 +234,34 @@ class NativeAlbedoStep:
             gridtype, align, None, None, _parts(self.rows, self.C), self.m_dev)
         return self.loss
 
+    def _backward_two_pass(self, bw, scale):
+        """Pass 1: the SDS gradient alone (pred_rgb -> head -> compositing ->
+        field); pass 2: the scaled entropy loss alone (weights_sum ->
+        compositing -> field, no image gradient), adding into the gradients."""
+        m = self.trainer.model
+        N, cap = self.N, self.cap
+        S, Hb, gridtype, align, _ = self.meta
+        from gridencoder.grid import _parts
+        gbw = self._bg_grads()
+        call("dfhip_ray_head_backward", N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d),
+             *[ptr(w) for w in bw], ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws),
+             None, ptr(self.head_partial), *[ptr(g) for g in gbw], stream())
+        passes = [(self.grad_ws, self.grad_image, self.d_enc, False)]
+        if self.lam > 0:
+            passes.append((self.grad_ws2, self.zero_image, self.d_enc2, True))
+        for i, (g_ws, g_img, d_enc, acc) in enumerate(passes):
+            if i == 1:
+                call("dfhip_entropy_backward", N, ptr(self.ws), ptr(scale), self.lam,
+                     ptr(self.grad_ws2), stream())
+            _raymarching.composite_rays_train_backward_mixed(
+                g_ws, g_img, self.sigma, self.albedo, self.deltas, self.rays, self.ws,
+                self.image, cap, N, 1e-4, self.grad_sigma, self.grad_albedo, False)
+            _fieldmlp.grid_field_backward(
+                self.enc, self.xyzs, m.bound, self.mlp, self.grad_sigma, self.grad_albedo, d_enc,
+                self.mlp_partial, [p.grad for p in self.mlp], self.encoder.offsets, self.rows, S,
+                Hb, gridtype, align, None, None, _parts(self.rows, self.C), self.m_dev,
+                accumulate=acc)
+
     def embedding_backward(self):
         """Binned embedding-gradient scatter (eager, timed like the autograd
         path's deferred launch)."""
@@ -232,6 +275,16 @@ class NativeAlbedoStep:
         per = 12 + self.L * self.C * 2
         with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_dev, per):
             self._emb_launch()
+        if self.two_pass and self.lam > 0:
+            if self._emb_launch2 is None:
+                m = self.trainer.model
+                S, Hb, gridtype, align, offsets_host = self.meta
+                self._emb_launch2 = _gridencoder.binned_launcher(
+                    self.d_enc2, self.xyzs, m.bound, self.encoder.offsets, offsets_host,
+                    self.encoder.embeddings.grad, self.cap, self.m_dev, 3, self.C, self.L, S,
+                    Hb, gridtype, align, *self.bin_scratch, accumulate=True)
+            with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_dev, per):
+                self._emb_launch2()
 
     def reattach(self):
         for p, g in self.grads:

@@ -478,6 +478,13 @@ class Trainer(object):
 
     # ------------------------------------------------------------ graph step
     def _graph_eligible(self, shading):
+        if not (self.graph_step and self.fp16 and self.model.cuda_ray and shading == "albedo"
+                and hasattr(self.guidance, "sds_grad")):
+            return False
+        if not self.fused_backward:
+            # the reference's two-pass backward is graphed only as the native step
+            from . import native_step as _native
+            return _native.eligible(self, shading)
         return (self.graph_step and self.fp16 and self.model.cuda_ray and shading == "albedo"
                 and self.fused_backward and hasattr(self.guidance, "sds_grad")
                 and self.device.type == "cuda")

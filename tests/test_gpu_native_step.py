@@ -16,9 +16,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(res, seed, graph=False):
+def _trainer(res, seed, graph=False, fused=True):
     import bench
-    return bench.make_trainer(res, seed, 0, 1, True, graph=graph)
+    return bench.make_trainer(res, seed, 0, 1, fused, graph=graph)
 
 
 def test_prologue_rays_near_far_and_draws(gpu):
@@ -56,10 +56,13 @@ def test_prologue_rays_near_far_and_draws(gpu):
     _dfhip.load()
 
 
-def test_native_step_matches_autograd_step(gpu):
+@pytest.mark.parametrize("fused", [True, False])
+def test_native_step_matches_autograd_step(gpu, fused):
+    """fused: one backward of SDS + scaled loss; not fused: the reference's two
+    passes (sd.py:115 then utils.py:708), gradients accumulated."""
     from nerf.native_step import NativeAlbedoStep
     res = 64
-    trainer, data = _trainer(res, 7)
+    trainer, data = _trainer(res, 7, fused=fused)
     batch = data.collate([0])
     for _ in range(3):  # density-grid refresh + a few eager steps
         trainer.train_iteration(batch)
@@ -105,8 +108,9 @@ def test_native_step_matches_autograd_step(gpu):
         assert torch.equal(p.grad, g), (tuple(p.shape), float((p.grad - g).abs().max()))
 
 
-def test_native_graph_training_runs(gpu):
-    trainer, data = _trainer(64, 9, graph=True)
+@pytest.mark.parametrize("fused", [True, False])
+def test_native_graph_training_runs(gpu, fused):
+    trainer, data = _trainer(64, 9, graph=True, fused=fused)
     model = trainer.model
     before = [p.detach().clone() for p in model.parameters() if p.requires_grad]
     losses = []
