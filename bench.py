@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-infer", action="store_true",
                    help="skip the C4 inference-render measurement")
     p.add_argument("--infer-res", type=int, default=800)
+    p.add_argument("--no-shading", action="store_true",
+                   help="skip timing the textureless / lambertian steps")
     p.add_argument("--no-alt-backward", action="store_true",
                    help="skip timing the other backward structure (two-pass / fused)")
     p.add_argument("--launcher-selftest", action="store_true",
@@ -416,6 +418,32 @@ def main():
         result[key] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
         del alt, alt_data
         torch.cuda.empty_cache()
+    if world == 1 and not args.no_shading:
+        # the steps after albedo_iters (utils.py:346-359): 20 % albedo, 40 %
+        # textureless, 40 % lambertian (ambient 0.1), finite-difference normals
+        shade = {}
+        for kind in ("textureless", "lambertian"):
+            tr, dat = make_trainer(args.res, args.seed, rank, world, True, graph=not args.eager,
+                                   mock_sds=args.mock_sds)
+            tr.pick_shading = (lambda k: (lambda: (k, 0.1)))(kind)
+            for _ in range(args.warmup):
+                tr.train_iteration(dat.collate([0]))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                tr.train_iteration(dat.collate([0]))
+            torch.cuda.synchronize()
+            shade[f"{kind}_ms_per_step"] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
+            del tr, dat
+            torch.cuda.empty_cache()
+        base = result["ms_per_step"] if not args.two_pass_backward else result.get(
+            "fused_ms_per_step", result["ms_per_step"])
+        shade["albedo_ms_per_step"] = base
+        shade["schedule_ms_per_step"] = round(0.2 * base + 0.4 * shade["textureless_ms_per_step"]
+                                              + 0.4 * shade["lambertian_ms_per_step"], 3)
+        shade["note"] = ("steps >= albedo_iters: 0.2 albedo + 0.4 textureless + 0.4 lambertian "
+                         "(utils.py:346-359), native graph-replayed, fused backward")
+        result["shading"] = shade
     if rank == 0 and world == 1 and not args.no_infer:
         result["inference"] = bench_inference(device, args.infer_res)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -38,6 +38,8 @@ extern "C" {
 typedef void *dfhip_stream_t; /* hipStream_t */
 
 enum dfhip_dtype { DFHIP_F32 = 0, DFHIP_F16 = 1, DFHIP_F64 = 2 };
+/* Shadings of the non-albedo train steps (nerf/network_grid.py:124-144). */
+enum dfhip_shading { DFHIP_SHADING_TEXTURELESS = 1, DFHIP_SHADING_LAMBERTIAN = 2 };
 
 enum dfhip_status {
     DFHIP_OK = 0,
@@ -564,6 +566,44 @@ int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d
                             const float *b1, const float *w2, const float *b2, const float *w3,
                             const float *b3, float *weights_sum, float *depth, float *image,
                             uint32_t *work, dfhip_stream_t stream);
+
+/* ---- non-albedo shading of the train step (csrc/shade.hip) ------------------
+ * Replaces, for the `textureless` / `lambertian` steps, network_grid.py:90-144
+ * (finite_difference_normal: six common_forward calls at the clamped stencil
+ * points, safe_normalize, NaN -> 0, lambertian = ratio + (1 - ratio) *
+ * clamp(normal @ l, min=0), colour) and renderer.py:485-489 (orientation
+ * loss).  The stencil evaluations are extra rows of one field launch: xyz is a
+ * [7 cap, 3] buffer whose rows [0, M) are the march's samples (M = *m_dev).
+ *
+ * dfhip_shading_stencil writes rows M + a M + i (a = 0..5: +x, -x, +y, -y,
+ *   +z, -z) = clamp(x_i + eps e, -bound, bound) and *m7_dev = 7 M. */
+int dfhip_shading_stencil(float *xyz, const int32_t *m_dev, uint32_t cap, float eps, float bound,
+                          int32_t *m7_dev, dfhip_stream_t stream);
+/* Scratch doubles for dfhip_shading_forward's orientation partial sums. */
+uint32_t dfhip_shading_partial_doubles(uint32_t cap);
+/* sigma [7 cap] f32 / albedo [7 cap, 3] f16 of the field on the 7 M rows,
+ * dirs [cap, 3], light [3] f32 (device) -> color [cap, 3] f16 (compositing
+ * input), normal [cap, 3] f32, orientation mean over the march's padded row
+ * count M' (raymarching.py:224-227) into *orient (nullable), and
+ * *loss += lambda_orient * orient (nullable). */
+int dfhip_shading_forward(const float *sigma, const void *albedo, const float *dirs,
+                          const float *light, float ratio, float eps, int shading,
+                          const int32_t *m_dev, uint32_t cap, void *color, float *normal,
+                          double *partial, float lambda_orient, float *orient, float *loss,
+                          dfhip_stream_t stream);
+/* grad_color [cap, 3] f16 (compositing backward) and the loss scale
+ * grad_loss[0] (upstream of lambda_orient * orient) -> grad_sigma of the
+ * stencil rows [M, 7 M) and grad_albedo [7 cap, 3] f16 of all 7 M rows
+ * (grad_sigma rows [0, M) are left as the compositing wrote them). */
+int dfhip_shading_backward(const float *sigma, const void *albedo, const float *dirs,
+                           const float *light, float ratio, float eps, int shading,
+                           const int32_t *m_dev, uint32_t cap, const void *grad_color,
+                           const float *grad_loss, float lambda_orient, float *grad_sigma,
+                           void *grad_albedo, dfhip_stream_t stream);
+/* The step's light direction safe_normalize(rays_o[0] + randn(3))
+ * (renderer.py:462-464), drawn from Philox keyed by (seed, step). */
+int dfhip_shading_light(const float *rays_o, uint64_t seed, uint64_t step, float *light,
+                        dfhip_stream_t stream);
 
 #ifdef __cplusplus
 }

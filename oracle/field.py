@@ -390,3 +390,91 @@ def entropy(ws, lam):
     inside = (w >= 1e-5) & (w <= 1 - 1e-5)
     g = np.where(inside, lam / w.size * (np.log2(1 - a) - np.log2(a)), 0.0)
     return lam * e.mean(), g
+
+
+# ----------------------------------------------------------------- shading (non-albedo steps)
+
+def fd_normal(sig_pm, eps=1e-2):
+    """network_grid.py:90-121 in f32: sig_pm [6, M] = sigma at x + eps e_a
+    (rows +x, -x, +y, -y, +z, -z) -> (v [M, 3], normal [M, 3], |v|^2, r, nan
+    mask): v = -(0.5 (s+ - s-) / eps), normal = v / sqrt(clamp(|v|^2, 1e-20)),
+    NaN -> 0."""
+    s = np.asarray(sig_pm, F32)
+    e = F32(eps)
+    v = np.stack([-((F32(0.5) * (s[2 * a] - s[2 * a + 1])) / e) for a in range(3)], -1)
+    v = v.astype(F32)
+    ss = ((v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2]).astype(F32)
+    r = np.sqrt(np.maximum(ss, F32(1e-20))).astype(F32)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        n = (v / r[:, None]).astype(F32)
+    nan = np.isnan(n)
+    return v, np.where(nan, F32(0), n).astype(F32), ss, r, nan
+
+
+def shade_forward(sigma, sig_pm, albedo16, dirs, light, ratio, shading, eps=1e-2):
+    """network_grid.py:124-144 + renderer.py:485-489 under autocast: returns a
+    dict with normal [M, 3] f32, dot16 / lam16 [M] f16, color [M, 3] f16 and
+    the per-sample orientation terms [M] f32 (w.detach() * clamp(n.d, 0)^2)."""
+    v, n, ss, r, nan = fd_normal(sig_pm, eps)
+    l16 = r16(light).astype(F64)
+    # normal @ l: f16 operands (products exact), f32 sum, f16 result
+    p = r16(n).astype(F64) * l16[None, :]
+    d16 = r16(((p[:, 0] + p[:, 1]) + p[:, 2]).astype(F32))
+    c16 = np.maximum(d16, F16(0)).astype(F32)
+    omr = F32(1.0 - float(ratio))
+    lam16 = r16(F32(ratio) + r16(c16 * omr).astype(F32))
+    if shading == "textureless":
+        color = np.repeat(lam16[:, None], 3, 1)
+    else:  # lambertian
+        color = r16(np.asarray(albedo16, F16).astype(F32) * lam16.astype(F32)[:, None])
+    w = (F32(1) - np.exp(-np.asarray(sigma, F32).astype(F64)).astype(F32)).astype(F32)
+    d = np.asarray(dirs, F32)
+    nd = ((n[:, 0] * d[:, 0] + n[:, 1] * d[:, 1]) + n[:, 2] * d[:, 2]).astype(F32)
+    c = np.maximum(nd, F32(0))
+    orient = (w * (c * c)).astype(F32)
+    return {"v": v, "normal": n, "ss": ss, "r": r, "nan": nan, "d16": d16, "lam16": lam16,
+            "color": color.astype(F16), "w": w, "nd": nd, "orient": orient, "l16": l16}
+
+
+def padded_rows(m):
+    """The march's returned row count M' (raymarching.py:224-227)."""
+    return m + 128 - m % 128
+
+
+def shade_backward(fwd, albedo16, dirs, grad_color16, grad_loss, lam_orient, m_rows, ratio,
+                   shading, eps=1e-2):
+    """Autograd of shade_forward for the f16 colour gradient grad_color16
+    [M, 3] and the loss-scale upstream grad_loss of lam_orient * mean(orient)
+    over m_rows (= M').  Returns (grad_sig_pm [6, M] f32, grad_albedo16 [M, 3]
+    f16 or None)."""
+    g = np.asarray(grad_color16, F16).astype(F32)
+    lam = fwd["lam16"].astype(F32)
+    ga = None
+    if shading == "textureless":
+        glam = r16((g[:, 0] + g[:, 1]) + g[:, 2]).astype(F32)
+    else:
+        a = np.asarray(albedo16, F16).astype(F32)
+        ga = r16(g * lam[:, None])
+        gl = r16(g * a).astype(F32)
+        glam = r16((gl[:, 0] + gl[:, 1]) + gl[:, 2]).astype(F32)
+    gc = r16(glam * F32(1.0 - float(ratio))).astype(F32)
+    gd = np.where(fwd["d16"] >= 0, gc, F32(0)).astype(F32)
+    gn = r16(gd[:, None] * fwd["l16"].astype(F32)[None, :]).astype(F32)
+    go = F32((F32(grad_loss) * F32(lam_orient)) / F32(m_rows))
+    d = np.asarray(dirs, F32)
+    g2 = np.where(fwd["nd"] >= 0, (go * fwd["w"]) * (F32(2) * np.maximum(fwd["nd"], F32(0))),
+                  F32(0)).astype(F32)
+    gn = (gn + g2[:, None] * d).astype(F32)
+    gn = np.where(fwd["nan"], F32(0), gn)
+    v, r, ss = fwd["v"], fwd["r"], fwd["ss"]
+    r2 = (r * r).astype(F32)
+    gr = ((((-gn[:, 0] * v[:, 0]) / r2) + ((-gn[:, 1] * v[:, 1]) / r2)) +
+          ((-gn[:, 2] * v[:, 2]) / r2)).astype(F32)
+    gs = np.where(ss >= F32(1e-20), gr / (F32(2) * r), F32(0)).astype(F32)
+    gv = (gn / r[:, None] + (gs[:, None] * v + gs[:, None] * v)).astype(F32)
+    gdiff = (F32(0.5) * (-gv / F32(eps))).astype(F32)
+    out = np.empty((6, gv.shape[0]), F32)
+    for a in range(3):
+        out[2 * a] = gdiff[:, a]
+        out[2 * a + 1] = -gdiff[:, a]
+    return out, ga

@@ -23,6 +23,7 @@ F32, F16, F64 = 0, 1, 2
 _DTYPE = {torch.float32: F32, torch.float16: F16, torch.float64: F64}
 
 _vp, _u32, _i32, _f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
+_u64 = ctypes.c_uint64
 
 # name -> argtypes (stream is always the trailing c_void_p)
 _SIGS = {
@@ -87,6 +88,12 @@ _SIGS = {
     "dfhip_grid_field_backward": [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                   _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32, _vp],
+    "dfhip_shading_stencil": [_vp, _vp, _u32, _f32, _f32, _vp, _vp],
+    "dfhip_shading_forward": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp, _vp,
+                              _f32, _vp, _vp, _vp],
+    "dfhip_shading_backward": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp, _f32,
+                               _vp, _vp, _vp],
+    "dfhip_shading_light": [_vp, _u64, _u64, _vp, _vp],
     "dfhip_grid_field_backward_accumulate": [
         _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp, _vp, _vp, _u32,
         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32,
@@ -141,6 +148,8 @@ def load() -> ctypes.CDLL:
     lib.dfhip_ray_head_partial_floats.argtypes = [_u32]
     lib.dfhip_grid_backward_partial_floats.restype = ctypes.c_uint64
     lib.dfhip_grid_backward_partial_floats.argtypes = [_u32, _u32, _u32]
+    lib.dfhip_shading_partial_doubles.restype = _u32
+    lib.dfhip_shading_partial_doubles.argtypes = [_u32]
     lib.dfhip_march_rays_train_stage_floats.restype = ctypes.c_uint64
     lib.dfhip_march_rays_train_stage_floats.argtypes = [_u32, _u32]
     for name, args in _SIGS.items():
@@ -156,6 +165,7 @@ def exported_symbols() -> list[str]:
             "dfhip_grid_backward_default_parts", "dfhip_grid_backward_partial_floats",
             "dfhip_field_mlp_params", "dfhip_field_mlp_backward_parts",
             "dfhip_ray_head_partial_floats", "dfhip_march_rays_train_stage_floats",
+            "dfhip_shading_partial_doubles",
             *_SIGS.keys()]
 
 

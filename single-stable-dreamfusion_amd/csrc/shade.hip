@@ -1,0 +1,380 @@
+// Non-albedo shading of the grid NeRF train step on the device (the
+// `textureless` and `lambertian` steps, 80 % of the reference's steps after
+// albedo_iters: nerf/utils.py:346-359):
+//
+//   normal  = safe_normalize(-(sigma(x + eps e_a) - sigma(x - eps e_a)) * 0.5 / eps)
+//             (network_grid.py:90-121: six extra common_forward calls at the
+//              clamped stencil points, NaN -> 0)
+//   lam     = ratio + (1 - ratio) * clamp(normal @ l, min=0)       (:135, f16 under autocast)
+//   color   = lam.repeat(3) (textureless) | albedo * lam (lambertian)   (:137-142)
+//   orient  = mean(w.detach() * clamp(normal . d, min=0)^2), w = 1 - exp(-sigma)
+//             (renderer.py:485-489, mean over the march's M' rows)
+//
+// The six stencil evaluations are extra rows of ONE fused field launch: the
+// stencil kernel writes the stencil points of the M live samples behind them
+// (rows M + a M + i, a = 0..5: +x, -x, +y, -y, +z, -z) and the live row count
+// 7 M, so the field forward, the field backward and the embedding backward
+// each run once over 7 M rows.  The shading kernels keep the reference's
+// dtypes and rounding points: the normal and the orientation loss in f32, the
+// light product, lambertian and colour as f16 values (autocast casts normal @ l
+// to f16), the gradients of the f16 tensors rounded to f16 where autograd
+// would hold them in f16.  Loss-scale handling follows autograd: the
+// orientation term's gradient carries the GradScaler scale, as the entropy
+// term's does.
+#include "common.h"
+
+#include <math.h>
+
+namespace dfhip {
+namespace shd {
+
+constexpr int kStencil = 6;
+constexpr uint32_t kThreads = 256;
+
+__device__ __forceinline__ float r16(float x) { return (float)(half_t)f32_rounded(x); }
+
+__device__ __forceinline__ uint32_t live(const int32_t *m_dev, uint32_t cap) {
+    const int32_t m = *m_dev;
+    return m < 0 ? 0u : ((uint32_t)m < cap ? (uint32_t)m : cap);
+}
+
+// March rows M' of the reference (raymarching.py:224-227: m += align - m % align)
+__device__ __forceinline__ float padded_rows(uint32_t m) {
+    return (float)(m + 128u - m % 128u);
+}
+
+// Stencil points of the live samples behind them + the live count 7 M.
+__global__ __launch_bounds__(kThreads) void k_stencil(float *__restrict__ xyz,
+                                                      const int32_t *__restrict__ m_dev,
+                                                      uint32_t cap, float eps, float bound,
+                                                      int32_t *__restrict__ m7_dev) {
+    const uint32_t M = live(m_dev, cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *m7_dev = (int32_t)(7u * M);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+        float x[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) x[d] = xyz[3 * (size_t)i + d];
+#pragma unroll
+        for (int s = 0; s < kStencil; ++s) {
+            const int a = s >> 1;
+            const float off = (s & 1) ? -eps : eps;
+            float *dst = xyz + 3 * ((size_t)(1 + s) * M + i);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                // x + tensor([[eps, 0, 0]]) then clamp(-bound, bound)
+                const float v = x[d] + (d == a ? off : 0.0f);
+                dst[d] = fminf(fmaxf(v, -bound), bound);
+            }
+        }
+    }
+}
+
+struct Normal {
+    float v[3], n[3], r, ss;
+    bool nan[3];
+};
+
+// network_grid.py:90-121 (f32): v = -(0.5 * (s+ - s-) / eps), n = v / sqrt(clamp(|v|^2, 1e-20))
+__device__ __forceinline__ Normal fd_normal(const float *__restrict__ sigma, uint32_t M,
+                                            uint32_t i, float eps) {
+    Normal o;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float sp = sigma[(size_t)(1 + 2 * a) * M + i];
+        const float sn = sigma[(size_t)(2 + 2 * a) * M + i];
+        o.v[a] = -((0.5f * (sp - sn)) / eps);
+    }
+    o.ss = (o.v[0] * o.v[0] + o.v[1] * o.v[1]) + o.v[2] * o.v[2];
+    o.r = sqrtf(fmaxf(o.ss, 1e-20f));
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float q = o.v[a] / o.r;
+        o.nan[a] = q != q;
+        o.n[a] = o.nan[a] ? 0.0f : q;
+    }
+    return o;
+}
+
+// (normal @ l) under autocast: f16 operands, f32 accumulation, f16 result
+__device__ __forceinline__ float dot16(const float n[3], const float l16[3]) {
+    const float p0 = r16(n[0]) * l16[0], p1 = r16(n[1]) * l16[1], p2 = r16(n[2]) * l16[2];
+    return r16((p0 + p1) + p2);
+}
+
+struct Shade {
+    float d16, lam16;
+};
+
+__device__ __forceinline__ Shade lambert(const float n[3], const float l16[3], float ratio,
+                                         float omr) {
+    Shade s;
+    s.d16 = dot16(n, l16);
+    const float c16 = s.d16 > 0.0f ? s.d16 : 0.0f;  // clamp(min=0)
+    s.lam16 = r16(ratio + r16(c16 * omr));          // ratio + (1 - ratio) * c
+    return s;
+}
+
+// Forward: colour (f16, for the compositing), the normal (f32, kept for the
+// backward) and per-block partial sums of the orientation term (f64).
+__global__ __launch_bounds__(kThreads) void k_shade_fwd(
+    const float *__restrict__ sigma, const half_t *__restrict__ albedo,
+    const float *__restrict__ dirs, const float *__restrict__ light, float ratio, float omr,
+    float eps, int lambertian, const int32_t *__restrict__ m_dev, uint32_t cap,
+    half_t *__restrict__ color, float *__restrict__ normal, double *__restrict__ part) {
+    __shared__ double red[kThreads / 64];
+    const uint32_t M = live(m_dev, cap);
+    float l16[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) l16[d] = r16(light[d]);
+    double acc = 0.0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+        const Normal nm = fd_normal(sigma, M, i, eps);
+        const Shade sh = lambert(nm.n, l16, ratio, omr);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            normal[3 * (size_t)i + d] = nm.n[d];
+            const float c = lambertian ? r16((float)albedo[3 * (size_t)i + d] * sh.lam16)
+                                       : sh.lam16;
+            color[3 * (size_t)i + d] = (half_t)c;
+        }
+        // orientation term: (1 - exp(-sigma)) * clamp(n . d, min=0)^2
+        const float w = 1.0f - expf(-sigma[i]);
+        const float nd = (nm.n[0] * dirs[3 * (size_t)i] + nm.n[1] * dirs[3 * (size_t)i + 1]) +
+                         nm.n[2] * dirs[3 * (size_t)i + 2];
+        const float c = nd > 0.0f ? nd : 0.0f;
+        acc += (double)(w * (c * c));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int w = 0; w < (int)(kThreads / 64); ++w) s += red[w];
+        part[blockIdx.x] = s;
+    }
+}
+
+// loss += lambda * sum / M' (fixed-order sum of the block partials)
+__global__ __launch_bounds__(64) void k_orient_finish(const double *__restrict__ part,
+                                                      uint32_t parts, const int32_t *m_dev,
+                                                      uint32_t cap, float lambda,
+                                                      float *__restrict__ orient,
+                                                      float *__restrict__ loss) {
+    double s = 0.0;
+    for (uint32_t p = threadIdx.x; p < parts; p += 64) s += part[p];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (threadIdx.x == 0) {
+        const float mean = (float)s / padded_rows(live(m_dev, cap));
+        if (orient) *orient = mean;
+        if (loss) *loss = *loss + lambda * mean;
+    }
+}
+
+// Backward.  grad_color [cap, 3] f16: d loss / d colour from the compositing
+// backward.  Writes grad_albedo for the 7 M field rows (main rows: the albedo
+// gradient of the lambertian product, else 0; stencil rows 0) and grad_sigma
+// for the stencil rows (the main rows keep the compositing's gradient).
+__global__ __launch_bounds__(kThreads) void k_shade_bwd(
+    const float *__restrict__ sigma, const half_t *__restrict__ albedo,
+    const float *__restrict__ dirs, const float *__restrict__ light, float ratio, float omr,
+    float eps, int lambertian, const int32_t *__restrict__ m_dev, uint32_t cap,
+    const half_t *__restrict__ grad_color, const float *__restrict__ grad_loss, float lambda,
+    float *__restrict__ grad_sigma, half_t *__restrict__ grad_albedo) {
+    const uint32_t M = live(m_dev, cap);
+    float l16[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) l16[d] = r16(light[d]);
+    // d loss / d orient_i: (scale * lambda) / M' (MulBackward, MeanBackward)
+    const float go = (grad_loss[0] * lambda) / padded_rows(M);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+        const Normal nm = fd_normal(sigma, M, i, eps);
+        const Shade sh = lambert(nm.n, l16, ratio, omr);
+        float g[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) g[d] = (float)grad_color[3 * (size_t)i + d];
+        float glam;
+        if (lambertian) {
+            float gl[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const float a = (float)albedo[3 * (size_t)i + d];
+                grad_albedo[3 * (size_t)i + d] = (half_t)r16(g[d] * sh.lam16);
+                gl[d] = r16(g[d] * a);
+            }
+            glam = r16((gl[0] + gl[1]) + gl[2]);  // sum over the broadcast dim
+        } else {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) grad_albedo[3 * (size_t)i + d] = (half_t)0.0f;
+            glam = r16((g[0] + g[1]) + g[2]);  // RepeatBackward
+        }
+        const float gc = r16(glam * omr);                 // (1 - ratio) * c
+        const float gd = sh.d16 >= 0.0f ? gc : 0.0f;      // clamp(min=0)
+        float gn[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) gn[d] = r16(gd * l16[d]);  // mv backward (f16), cast back
+        // orientation term: d/dn of go * w * clamp(n . d, 0)^2
+        const float w = 1.0f - expf(-sigma[i]);
+        const float dx = dirs[3 * (size_t)i], dy = dirs[3 * (size_t)i + 1],
+                    dz = dirs[3 * (size_t)i + 2];
+        const float nd = (nm.n[0] * dx + nm.n[1] * dy) + nm.n[2] * dz;
+        const float c = nd > 0.0f ? nd : 0.0f;
+        const float g2 = nd >= 0.0f ? (go * w) * (2.0f * c) : 0.0f;
+        gn[0] = gn[0] + g2 * dx;
+        gn[1] = gn[1] + g2 * dy;
+        gn[2] = gn[2] + g2 * dz;
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            if (nm.nan[d]) gn[d] = 0.0f;  // normal[isnan] = 0
+        // n = v / r, r = sqrt(clamp(ss, 1e-20)), ss = sum v^2
+        const float r2 = nm.r * nm.r;
+        const float gr = ((-gn[0] * nm.v[0]) / r2 + (-gn[1] * nm.v[1]) / r2) +
+                         (-gn[2] * nm.v[2]) / r2;
+        const float gs = nm.ss >= 1e-20f ? gr / (2.0f * nm.r) : 0.0f;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float gv = gn[a] / nm.r + (gs * nm.v[a] + gs * nm.v[a]);
+            // v = -((0.5 * (s+ - s-)) / eps)
+            const float gdiff = 0.5f * (-gv / eps);
+            grad_sigma[(size_t)(1 + 2 * a) * M + i] = gdiff;
+            grad_sigma[(size_t)(2 + 2 * a) * M + i] = -gdiff;
+        }
+    }
+    // the stencil rows carry no albedo gradient
+    const size_t n6 = 3 * (size_t)6 * M;
+    half_t *ga = grad_albedo + 3 * (size_t)M;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n6;
+         k += (size_t)gridDim.x * blockDim.x)
+        ga[k] = (half_t)0.0f;
+}
+
+// Light direction of the step (renderer.py:462-464): safe_normalize(rays_o[0]
+// + randn(3)), the normal draws from Philox keyed like the step prologue.
+struct U4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
+        const uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__global__ void k_light(const float *__restrict__ rays_o, uint32_t seed_lo, uint32_t seed_hi,
+                        uint32_t step_lo, uint32_t step_hi, float *__restrict__ light) {
+    if (threadIdx.x != 0) return;
+    const U4 r = philox(U4{0xFFFFFFFEu, step_lo, step_hi, 3u}, seed_lo, seed_hi);
+    auto u = [](uint32_t v) { return (float)(v >> 8) * 0x1p-24f; };
+    const float ra = sqrtf(-2.0f * logf((float)((r.x >> 8) + 1u) * 0x1p-24f));
+    const float rb = sqrtf(-2.0f * logf((float)((r.z >> 8) + 1u) * 0x1p-24f));
+    float s0, c0, s1, c1;
+    sincosf(6.283185307179586f * u(r.y), &s0, &c0);
+    sincosf(6.283185307179586f * u(r.w), &s1, &c1);
+    const float z[3] = {ra * c0, ra * s0, rb * c1};
+    float v[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) v[d] = rays_o[d] + z[d];
+    const float ss = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
+    const float rr = sqrtf(fmaxf(ss, 1e-20f));
+#pragma unroll
+    for (int d = 0; d < 3; ++d) light[d] = v[d] / rr;
+}
+
+}  // namespace shd
+}  // namespace dfhip
+
+using namespace dfhip;
+
+static uint32_t shade_blocks(uint32_t cap) {
+    // grid-stride: enough workgroups for 4 per CU, never more than the rows need
+    uint32_t b = ceil_div(cap, shd::kThreads);
+    return b < 1024u ? (b ? b : 1u) : 1024u;
+}
+
+extern "C" uint32_t dfhip_shading_partial_doubles(uint32_t cap) { return shade_blocks(cap); }
+
+extern "C" int dfhip_shading_stencil(float *xyz, const int32_t *m_dev, uint32_t cap, float eps,
+                                     float bound, int32_t *m7_dev, dfhip_stream_t stream) {
+    if (!xyz || !m_dev || !m7_dev) {
+        set_error("shading_stencil: null pointer");
+        return DFHIP_EINVAL;
+    }
+    if (!(bound > 0.0f)) {
+        set_error("shading_stencil: bound must be > 0");
+        return DFHIP_EINVAL;
+    }
+    shd::k_stencil<<<shade_blocks(cap), shd::kThreads, 0, as_stream(stream)>>>(xyz, m_dev, cap,
+                                                                               eps, bound, m7_dev);
+    return check_launch("shading_stencil");
+}
+
+static bool shading_mode(const char *name, int shading, int &lambertian) {
+    if (shading == DFHIP_SHADING_TEXTURELESS) lambertian = 0;
+    else if (shading == DFHIP_SHADING_LAMBERTIAN) lambertian = 1;
+    else {
+        set_error("%s: shading must be DFHIP_SHADING_TEXTURELESS or _LAMBERTIAN", name);
+        return false;
+    }
+    return true;
+}
+
+extern "C" int dfhip_shading_forward(const float *sigma, const void *albedo, const float *dirs,
+                                     const float *light, float ratio, float eps, int shading,
+                                     const int32_t *m_dev, uint32_t cap, void *color,
+                                     float *normal, double *partial, float lambda_orient,
+                                     float *orient, float *loss, dfhip_stream_t stream) {
+    const char *name = "shading_forward";
+    int lam = 0;
+    if (!shading_mode(name, shading, lam)) return DFHIP_EINVAL;
+    if (!sigma || !albedo || !dirs || !light || !m_dev || !color || !normal || !partial) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const uint32_t blocks = shade_blocks(cap);
+    const float omr = (float)(1.0 - (double)ratio);
+    shd::k_shade_fwd<<<blocks, shd::kThreads, 0, s>>>(sigma, (const half_t *)albedo, dirs, light,
+                                                      ratio, omr, eps, lam, m_dev, cap,
+                                                      (half_t *)color, normal, partial);
+    shd::k_orient_finish<<<1, 64, 0, s>>>(partial, blocks, m_dev, cap, lambda_orient, orient,
+                                          loss);
+    return check_launch(name);
+}
+
+extern "C" int dfhip_shading_backward(const float *sigma, const void *albedo, const float *dirs,
+                                      const float *light, float ratio, float eps, int shading,
+                                      const int32_t *m_dev, uint32_t cap, const void *grad_color,
+                                      const float *grad_loss, float lambda_orient,
+                                      float *grad_sigma, void *grad_albedo,
+                                      dfhip_stream_t stream) {
+    const char *name = "shading_backward";
+    int lam = 0;
+    if (!shading_mode(name, shading, lam)) return DFHIP_EINVAL;
+    if (!sigma || !albedo || !dirs || !light || !m_dev || !grad_color || !grad_loss ||
+        !grad_sigma || !grad_albedo) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    const float omr = (float)(1.0 - (double)ratio);
+    shd::k_shade_bwd<<<shade_blocks(cap), shd::kThreads, 0, as_stream(stream)>>>(
+        sigma, (const half_t *)albedo, dirs, light, ratio, omr, eps, lam, m_dev, cap,
+        (const half_t *)grad_color, grad_loss, lambda_orient, grad_sigma, (half_t *)grad_albedo);
+    return check_launch(name);
+}
+
+extern "C" int dfhip_shading_light(const float *rays_o, uint64_t seed, uint64_t step,
+                                   float *light, dfhip_stream_t stream) {
+    if (!rays_o || !light) {
+        set_error("shading_light: null pointer");
+        return DFHIP_EINVAL;
+    }
+    shd::k_light<<<1, 64, 0, as_stream(stream)>>>(rays_o, (uint32_t)seed, (uint32_t)(seed >> 32),
+                                                  (uint32_t)step, (uint32_t)(step >> 32), light);
+    return check_launch("shading_light");
+}

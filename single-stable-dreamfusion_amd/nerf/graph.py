@@ -19,9 +19,8 @@ replayed:
   gradient all-reduce (multi-GPU), GradScaler + fused Adam and the LR
   schedule run as in the eager step.
 
-Only the albedo shading is captured (the reference's first `albedo_iters`
-steps and 20 % of the later ones): the finite-difference normal paths run
-eagerly.  RNG draws inside the graph (march noise, background colour, light
+The albedo shading is captured in both forms; the textureless / lambertian
+steps (finite-difference normals, csrc/shade.hip) only as the native step.  RNG draws inside the graph (march noise, background colour, light
 direction, timestep, SDS noise) use torch's graph-safe Philox offsets, so
 every replay draws fresh numbers.
 """
@@ -46,7 +45,8 @@ class GraphedTrainStep:
         self.native = None
         if (_NATIVE and allow_native and "pose" in data and "intrinsics" in data
                 and _native.eligible(trainer, shading)):
-            self.native = _native.NativeAlbedoStep(trainer, self.H, self.W)
+            self.native = _native.NativeAlbedoStep(trainer, self.H, self.W, shading,
+                                                   ambient_ratio)
             self.rays_o = self.native.rays_o.view(1, -1, 3)
             self.rays_d = self.native.rays_d.view(1, -1, 3)
         else:

@@ -44,12 +44,19 @@ import _raymarching
 from _dfhip import call, ptr, stream
 
 
+# shading -> dfhip_shading code (csrc/shade.hip); albedo needs no shading kernel
+SHADINGS = {"albedo": 0, "textureless": 1, "lambertian": 2}
+FD_EPS = 1e-2  # network_grid.py:90 finite_difference_normal epsilon
+
+
 def eligible(trainer, shading):
     """True when NativeAlbedoStep reproduces trainer.train_step for `shading`."""
     from .sd import InjectedSDS
     m, opt = trainer.model, trainer.opt
-    if shading != "albedo" or not isinstance(trainer.guidance, InjectedSDS):
+    if shading not in SHADINGS or not isinstance(trainer.guidance, InjectedSDS):
         return False
+    if shading != "albedo" and not trainer.fused_backward:
+        return False  # the two-pass form is built for the albedo step only
     if not (trainer.fp16 and m.cuda_ray):
         return False
     if opt.lambda_opacity > 0:
@@ -70,9 +77,14 @@ def eligible(trainer, shading):
 
 
 class NativeAlbedoStep:
-    """Buffers and launches of one albedo train step at resolution H x W."""
+    """Buffers and launches of one train step at resolution H x W.
 
-    def __init__(self, trainer, H, W):
+    shading "albedo" (the default), or "textureless" / "lambertian" with the
+    ambient ratio: the finite-difference normals' six stencil evaluations are
+    rows [M, 7 M) of the same field launches (csrc/shade.hip), so every
+    per-sample field buffer holds 7 x the march capacity."""
+
+    def __init__(self, trainer, H, W, shading="albedo", ratio=1.0):
         self.trainer = trainer
         m, opt = trainer.model, trainer.opt
         dev = trainer.device
@@ -80,6 +92,11 @@ class NativeAlbedoStep:
         N = self.N = self.H * self.W
         self.max_steps = int(opt.max_steps)
         cap = self.cap = N * self.max_steps
+        self.shading, self.ratio = shading, float(ratio)
+        self.shade_code = SHADINGS[shading]
+        self.rows_per = 1 if self.shade_code == 0 else 7  # field rows per march sample
+        fcap = self.fcap = cap * self.rows_per            # field-row capacity
+        self.lam_orient = float(opt.lambda_orient) if self.shade_code else 0.0
         self.dt_gamma = float(opt.dt_gamma)
         self.lam = float(opt.lambda_entropy)
         f32 = dict(device=dev, dtype=torch.float32)
@@ -102,7 +119,7 @@ class NativeAlbedoStep:
         # march
         self.rays = torch.empty(N, 3, **i32)
         self.block_sums = torch.empty(_raymarching.march_rays_train_scratch_ints(N), **i32)
-        self.xyzs = torch.empty(cap, 3, **f32)
+        self.xyzs = torch.empty(fcap, 3, **f32)  # march rows [0, M), stencil rows behind
         self.dirs = torch.empty(cap, 3, **f32)
         self.deltas = torch.empty(cap, 2, **f32)
         # the count pass keeps each sample here; the emit pass only copies
@@ -120,9 +137,21 @@ class NativeAlbedoStep:
         self.mlp = []
         for lin in m.sigma_net.net:
             self.mlp += [lin.weight, lin.bias]
-        self.enc = torch.empty(cap, self.L * self.C, **f16)
-        self.sigma = torch.empty(cap, **f32)
-        self.albedo = torch.empty(cap, 3, **f16)
+        self.enc = torch.empty(fcap, self.L * self.C, **f16)
+        self.sigma = torch.empty(fcap, **f32)
+        self.albedo = torch.empty(fcap, 3, **f16)
+        self.m_field = self.m_dev  # live field rows: M, or 7 M with the stencil
+        if self.shade_code:
+            self.m7 = torch.zeros(1, **i32)
+            self.m_field = self.m7
+            self.light = torch.empty(3, **f32)
+            self.color = torch.empty(cap, 3, **f16)
+            self.normal = torch.empty(cap, 3, **f32)
+            self.orient = torch.zeros((), **f32)
+            self.orient_partial = torch.empty(
+                int(_dfhip.load().dfhip_shading_partial_doubles(cap)), device=dev,
+                dtype=torch.float64)
+            self.grad_color = torch.empty(cap, 3, **f16)
         # compositing + head
         self.ws = torch.empty(N, **f32)
         self.depth = torch.empty(N, **f32)
@@ -136,12 +165,12 @@ class NativeAlbedoStep:
         self.grad_ws = torch.empty(N, **f32)
         self.head_partial = (torch.empty(int(_dfhip.load().dfhip_ray_head_partial_floats(N)),
                                          **f32) if self.bg_layers is not None else None)
-        self.grad_sigma = torch.empty(cap, **f32)
-        self.grad_albedo = torch.empty(cap, 3, **f16)
-        self.d_enc = torch.empty(self.L, cap, self.C, **f16)
-        self.mlp_partial = torch.empty(_fieldmlp.backward_parts(cap) * _fieldmlp.params_count(),
+        self.grad_sigma = torch.empty(fcap, **f32)
+        self.grad_albedo = torch.empty(fcap, 3, **f16)
+        self.d_enc = torch.empty(self.L, fcap, self.C, **f16)
+        self.mlp_partial = torch.empty(_fieldmlp.backward_parts(fcap) * _fieldmlp.params_count(),
                                        **f32)
-        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, enc.offsets_host, self.L,
+        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(fcap, enc.offsets_host, self.L,
                                                                 self.C)
         self.bin_scratch = (torch.empty(ne, **i32), torch.empty(nc, **i32),
                             torch.empty(npf, **f32))
@@ -177,6 +206,10 @@ class NativeAlbedoStep:
              int(step) & 0xFFFFFFFFFFFFFFFF, 1, ptr(self.alphas), lo, hi, ptr(self.rays_o),
              ptr(self.rays_d), ptr(self.nears), ptr(self.fars), ptr(self.noises),
              ptr(self.bg_color), ptr(self.g_image), ptr(self.counter), stream())
+        if self.shade_code:
+            # the light direction (renderer.py:462-464), same (seed, step) key
+            call("dfhip_shading_light", ptr(self.rays_o), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                 int(step) & 0xFFFFFFFFFFFFFFFF, ptr(self.light), stream())
 
     def body(self):
         """Forward and backward down to the feature / network gradients (the
@@ -193,15 +226,29 @@ class NativeAlbedoStep:
         _raymarching.march_rays_train_emit_staged(
             self.rays_d, self.max_steps, N, cap, self.xyzs, self.dirs, self.deltas, self.rays,
             self.block_sums, 0, self.stage)
-        # field (grid.py:38-39 autocast table, network_grid.py:76-87)
+        # field (grid.py:38-39 autocast table, network_grid.py:76-87); with a
+        # shading, the six finite-difference stencil points of every sample are
+        # field rows too (network_grid.py:90-114)
         self.table.copy_(self.encoder.embeddings.detach())
         S, Hb, gridtype, align, _ = self.meta
+        if self.shade_code:
+            call("dfhip_shading_stencil", ptr(self.xyzs), ptr(self.m_dev), cap, FD_EPS,
+                 float(m.bound), ptr(self.m7), stream())
         _fieldmlp.grid_field_forward(self.xyzs, m.bound, self.table, self.encoder.offsets, S, Hb,
                                      gridtype, align, self.mlp, self.enc, self.sigma, self.albedo,
-                                     self.m_dev)
+                                     self.m_field)
+        rgb = self.albedo
+        if self.shade_code:
+            # normals, lambertian, colour, orientation loss (network_grid.py:116-144,
+            # renderer.py:485-489)
+            call("dfhip_shading_forward", ptr(self.sigma), ptr(self.albedo), ptr(self.dirs),
+                 ptr(self.light), self.ratio, FD_EPS, self.shade_code, ptr(self.m_dev), cap,
+                 ptr(self.color), ptr(self.normal), ptr(self.orient_partial), self.lam_orient,
+                 ptr(self.orient), None, stream())
+            rgb = self.color
         # compositing (raymarching.py:238-269)
         _raymarching.composite_rays_train_forward_mixed(
-            self.sigma, self.albedo, self.deltas, self.rays, cap, N, 1e-4, self.ws, self.depth,
+            self.sigma, rgb, self.deltas, self.rays, cap, N, 1e-4, self.ws, self.depth,
             self.image)
         # ray head (renderer.py:536-551) and the entropy regulariser (utils.py:386-391)
         bw = self._bg_weights()
@@ -211,6 +258,8 @@ class NativeAlbedoStep:
              stream())
         if self.lam > 0:
             call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss), stream())
+        if self.lam_orient > 0:
+            self.loss.add_(self.orient, alpha=self.lam_orient)  # utils.py:398-400
         # backward: SDS gradient at pred_rgb (unscaled), entropy gradient x scale
         if self.two_pass:
             self._backward_two_pass(bw, scale)
@@ -225,13 +274,20 @@ class NativeAlbedoStep:
         else:
             call("dfhip_ray_head_backward", *head_args, stream())
         _raymarching.composite_rays_train_backward_mixed(
-            self.grad_ws, self.grad_image, self.sigma, self.albedo, self.deltas, self.rays,
-            self.ws, self.image, cap, N, 1e-4, self.grad_sigma, self.grad_albedo, False)
+            self.grad_ws, self.grad_image, self.sigma, rgb, self.deltas, self.rays,
+            self.ws, self.image, cap, N, 1e-4, self.grad_sigma,
+            self.grad_color if self.shade_code else self.grad_albedo, False)
+        if self.shade_code:
+            # colour / orientation gradients -> albedo and stencil sigma gradients
+            call("dfhip_shading_backward", ptr(self.sigma), ptr(self.albedo), ptr(self.dirs),
+                 ptr(self.light), self.ratio, FD_EPS, self.shade_code, ptr(self.m_dev), cap,
+                 ptr(self.grad_color), ptr(scale), self.lam_orient, ptr(self.grad_sigma),
+                 ptr(self.grad_albedo), stream())
         from gridencoder.grid import _parts
         _fieldmlp.grid_field_backward(
             self.enc, self.xyzs, m.bound, self.mlp, self.grad_sigma, self.grad_albedo, self.d_enc,
             self.mlp_partial, [p.grad for p in self.mlp], self.encoder.offsets, self.rows, S, Hb,
-            gridtype, align, None, None, _parts(self.rows, self.C), self.m_dev)
+            gridtype, align, None, None, _parts(self.rows, self.C), self.m_field)
         return self.loss
 
     def _backward_two_pass(self, bw, scale):
@@ -270,10 +326,10 @@ class NativeAlbedoStep:
             S, Hb, gridtype, align, offsets_host = self.meta
             self._emb_launch = _gridencoder.binned_launcher(
                 self.d_enc, self.xyzs, m.bound, self.encoder.offsets, offsets_host,
-                self.encoder.embeddings.grad, self.cap, self.m_dev, 3, self.C, self.L, S, Hb,
+                self.encoder.embeddings.grad, self.fcap, self.m_field, 3, self.C, self.L, S, Hb,
                 gridtype, align, *self.bin_scratch)
         per = 12 + self.L * self.C * 2
-        with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_dev, per):
+        with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_field, per):
             self._emb_launch()
         if self.two_pass and self.lam > 0:
             if self._emb_launch2 is None:

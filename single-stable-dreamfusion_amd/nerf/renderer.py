@@ -256,11 +256,13 @@ class NeRFRenderer(nn.Module):
                     self.grid_size, nears, fars, counter, perturb, dt_gamma, max_steps,
                     noises=getattr(self, "march_noises", None))
             else:
+                noises = getattr(self, "march_noises", None)  # given draws (tests)
                 xyzs, dirs, deltas, rays = raymarching.march_rays_train(
                     rays_o, rays_d, self.bound, self.density_bitfield, self.cascade,
                     self.grid_size, nears, fars, counter,
                     -1 if force_all_rays else self.mean_count,  # unused with force_all_rays
-                    perturb, 128, force_all_rays, dt_gamma, max_steps)
+                    noises if (perturb and noises is not None) else perturb, 128, force_all_rays,
+                    dt_gamma, max_steps)
             sigmas, rgbs, normals = self(xyzs, dirs, light_d, ratio=ambient_ratio, shading=shading)
             weights_sum, depth, image = raymarching.composite_rays_train(sigmas, rgbs, deltas, rays,
                                                                          T_thresh)

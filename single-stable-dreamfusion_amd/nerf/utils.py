@@ -465,7 +465,9 @@ class Trainer(object):
         self.local_step += 1
         self.global_step += 1
         shading, ambient_ratio = self.pick_shading()
-        if self._graph_eligible(shading):
+        native_only = shading != "albedo" or not self.fused_backward
+        if self._graph_eligible(shading) and (not native_only or
+                                              ("pose" in data and "intrinsics" in data)):
             return self._graph_iteration(data, shading, ambient_ratio)
         self.optimizer.zero_grad()
         with torch.autocast("cuda", enabled=self.fp16):
@@ -478,11 +480,12 @@ class Trainer(object):
 
     # ------------------------------------------------------------ graph step
     def _graph_eligible(self, shading):
-        if not (self.graph_step and self.fp16 and self.model.cuda_ray and shading == "albedo"
-                and hasattr(self.guidance, "sds_grad")):
+        if not (self.graph_step and self.fp16 and self.model.cuda_ray
+                and hasattr(self.guidance, "sds_grad") and self.device.type == "cuda"):
             return False
-        if not self.fused_backward:
-            # the reference's two-pass backward is graphed only as the native step
+        if not self.fused_backward or shading != "albedo":
+            # the two-pass backward and the normal-shaded steps are graphed only
+            # as the native step
             from . import native_step as _native
             return _native.eligible(self, shading)
         return (self.graph_step and self.fp16 and self.model.cuda_ray and shading == "albedo"

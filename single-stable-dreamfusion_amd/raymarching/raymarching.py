@@ -147,7 +147,8 @@ class _march_rays_train(Function):
         rays [N, 3] int32 = (ray id, first sample row, sample count).  With
         force_all_rays (or mean_count <= 0) M is the emitted count rounded up
         by `align`; otherwise M = mean_count rounded up and rays that do not fit
-        are dropped (here: the last rays in id order)."""
+        are dropped (here: the last rays in id order).  `perturb` may also be
+        an [N] f32 tensor: the noises to use (replaying another step's draws)."""
         rays_o = _flat3(_to_gpu(rays_o))
         rays_d = _flat3(_to_gpu(rays_d))
         density_bitfield = _to_gpu(density_bitfield).contiguous()
@@ -158,8 +159,11 @@ class _march_rays_train(Function):
 
         if step_counter is None:
             step_counter = torch.zeros(2, dtype=torch.int32, device=dev)
-        noises = (torch.rand(n, dtype=dt, device=dev) if perturb
-                  else torch.zeros(n, dtype=dt, device=dev))
+        if torch.is_tensor(perturb):
+            noises = perturb.to(dt).contiguous()
+        else:
+            noises = (torch.rand(n, dtype=dt, device=dev) if perturb
+                      else torch.zeros(n, dtype=dt, device=dev))
         rays = torch.empty(n, 3, dtype=torch.int32, device=dev)
         block_sums = torch.empty(_backend.march_rays_train_scratch_ints(n), dtype=torch.int32,
                                  device=dev)
