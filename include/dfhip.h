@@ -429,7 +429,8 @@ int dfhip_grid_field_backward_accumulate(
  * positions mapped (x + bound) / (2 bound) when bound > 0, else already in
  * [0, 1].  offsets_host is a HOST copy of the L + 1 offsets (slice layout);
  * offsets the device copy.  grad_embeddings [rows, C] f32 is overwritten, or
- * added into when accumulate != 0.  [scratch] entries / counts (u32) and
+ * added into when accumulate != 0.  [scratch] entries (u16 tile-relative ids,
+ * sized in u32 words) / counts (u32) and
  * partial (f32) sized by dfhip_grid_backward_binned_scratch for capacity B. */
 int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host, uint32_t L,
                                        uint32_t C, uint64_t *entries_u32, uint64_t *counts_u32,
@@ -572,34 +573,36 @@ int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d
  * (finite_difference_normal: six common_forward calls at the clamped stencil
  * points, safe_normalize, NaN -> 0, lambertian = ratio + (1 - ratio) *
  * clamp(normal @ l, min=0), colour) and renderer.py:485-489 (orientation
- * loss).  The stencil evaluations are extra rows of one field launch: xyz is a
- * [7 cap, 3] buffer whose rows [0, M) are the march's samples (M = *m_dev).
+ * loss).  The stencil evaluations are extra rows of one field launch over a
+ * [7 cap, 3] position buffer: row 7 i = sample i (of the M = *m_dev march
+ * samples), rows 7 i + 1 + a = its stencil point a (+x, -x, +y, -y, +z, -z).
  *
- * dfhip_shading_stencil writes rows M + a M + i (a = 0..5: +x, -x, +y, -y,
- *   +z, -z) = clamp(x_i + eps e, -bound, bound) and *m7_dev = 7 M. */
-int dfhip_shading_stencil(float *xyz, const int32_t *m_dev, uint32_t cap, float eps, float bound,
-                          int32_t *m7_dev, dfhip_stream_t stream);
+ * dfhip_shading_stencil: xyz [cap, 3] (march samples) -> xyz7 [7 cap, 3] rows
+ *   7 i + k (clamp(x_i + eps e, -bound, bound)) and *m7_dev = 7 M. */
+int dfhip_shading_stencil(const float *xyz, const int32_t *m_dev, uint32_t cap, float eps,
+                          float bound, float *xyz7, int32_t *m7_dev, dfhip_stream_t stream);
 /* Scratch doubles for dfhip_shading_forward's orientation partial sums. */
 uint32_t dfhip_shading_partial_doubles(uint32_t cap);
-/* sigma [7 cap] f32 / albedo [7 cap, 3] f16 of the field on the 7 M rows,
- * dirs [cap, 3], light [3] f32 (device) -> color [cap, 3] f16 (compositing
- * input), normal [cap, 3] f32, orientation mean over the march's padded row
- * count M' (raymarching.py:224-227) into *orient (nullable), and
+/* sigma7 [7 cap] f32 / albedo7 [7 cap, 3] f16 = the field on the 7 M rows,
+ * dirs [cap, 3], light [3] f32 (device) -> sigma [cap] f32 and color [cap, 3]
+ * f16 of the samples (compositing inputs), normal [cap, 3] f32, the
+ * orientation mean over the march's padded row count M'
+ * (raymarching.py:224-227) into *orient (nullable), and
  * *loss += lambda_orient * orient (nullable). */
-int dfhip_shading_forward(const float *sigma, const void *albedo, const float *dirs,
+int dfhip_shading_forward(const float *sigma7, const void *albedo7, const float *dirs,
                           const float *light, float ratio, float eps, int shading,
-                          const int32_t *m_dev, uint32_t cap, void *color, float *normal,
-                          double *partial, float lambda_orient, float *orient, float *loss,
-                          dfhip_stream_t stream);
-/* grad_color [cap, 3] f16 (compositing backward) and the loss scale
- * grad_loss[0] (upstream of lambda_orient * orient) -> grad_sigma of the
- * stencil rows [M, 7 M) and grad_albedo [7 cap, 3] f16 of all 7 M rows
- * (grad_sigma rows [0, M) are left as the compositing wrote them). */
-int dfhip_shading_backward(const float *sigma, const void *albedo, const float *dirs,
+                          const int32_t *m_dev, uint32_t cap, float *sigma, void *color,
+                          float *normal, double *partial, float lambda_orient, float *orient,
+                          float *loss, dfhip_stream_t stream);
+/* grad_sigma [cap] f32 / grad_color [cap, 3] f16 (compositing backward) and the
+ * loss scale grad_loss[0] (upstream of lambda_orient * orient) -> the field-row
+ * gradients grad_sigma7 [7 cap] f32 and grad_albedo7 [7 cap, 3] f16 of all 7 M
+ * rows. */
+int dfhip_shading_backward(const float *sigma7, const void *albedo7, const float *dirs,
                            const float *light, float ratio, float eps, int shading,
-                           const int32_t *m_dev, uint32_t cap, const void *grad_color,
-                           const float *grad_loss, float lambda_orient, float *grad_sigma,
-                           void *grad_albedo, dfhip_stream_t stream);
+                           const int32_t *m_dev, uint32_t cap, const float *grad_sigma,
+                           const void *grad_color, const float *grad_loss, float lambda_orient,
+                           float *grad_sigma7, void *grad_albedo7, dfhip_stream_t stream);
 /* The step's light direction safe_normalize(rays_o[0] + randn(3))
  * (renderer.py:462-464), drawn from Philox keyed by (seed, step). */
 int dfhip_shading_light(const float *rays_o, uint64_t seed, uint64_t step, float *light,

@@ -88,11 +88,11 @@ _SIGS = {
     "dfhip_grid_field_backward": [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                   _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32, _vp],
-    "dfhip_shading_stencil": [_vp, _vp, _u32, _f32, _f32, _vp, _vp],
+    "dfhip_shading_stencil": [_vp, _vp, _u32, _f32, _f32, _vp, _vp, _vp],
     "dfhip_shading_forward": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp, _vp,
-                              _f32, _vp, _vp, _vp],
-    "dfhip_shading_backward": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp, _f32,
-                               _vp, _vp, _vp],
+                              _vp, _f32, _vp, _vp, _vp],
+    "dfhip_shading_backward": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp, _vp,
+                               _f32, _vp, _vp, _vp],
     "dfhip_shading_light": [_vp, _u64, _u64, _vp, _vp],
     "dfhip_grid_field_backward_accumulate": [
         _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp, _vp, _vp, _u32,

@@ -10,8 +10,9 @@
 //
 //   1. k_bin: per tile of kTile consecutive samples (one workgroup), every
 //      in-bounds sample derives, level by level, the slices of its 2^D corner
-//      rows and appends its id to the (tile, slice) segment (LDS counters give
-//      the slot; segments hold kTile ids, so no scan is needed).
+//      rows and appends its tile-relative id (u16) to the (tile, slice)
+//      segment (LDS counters give the slot; segments hold kTile ids, so no
+//      scan is needed).
 //   2. k_walk: workgroup (slice, part) zeroes the slice's f64 accumulators in
 //      LDS, walks the segments of its part's tiles (one wave per segment,
 //      gathering the sample's position and feature gradient), adds the
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
                                              BinInfo bi, uint32_t gridtype, int align_corners,
                                              SliceDyn dyn, float inv, uint32_t B,
                                              uint32_t *__restrict__ counts,
-                                             uint32_t *__restrict__ entries) {
+                                             uint16_t *__restrict__ entries) {
     __shared__ uint32_t cnt[kMaxBins];
     const bool align = align_corners != 0;
     const uint32_t M = ge::dyn_count(dyn, B);
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
         __syncthreads();
-        uint32_t *seg = entries + (size_t)tile * nb * kTile;
+        uint16_t *seg = entries + (size_t)tile * nb * kTile;
         const uint32_t s_end = min(M, (tile + 1) * kTile);
         for (uint32_t s = tile * kTile + threadIdx.x; s < s_end; s += blockDim.x) {
             float x[D];
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
                     mask &= mask - 1;
                     const uint32_t b = b0 + k;
                     const uint32_t slot = atomicAdd(&cnt[b], 1u);
-                    seg[(size_t)b * kTile + slot] = s;
+                    seg[(size_t)b * kTile + slot] = (uint16_t)(s - tile * kTile);
                 }
             }
         }
@@ -234,6 +235,23 @@ __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, c
 
 constexpr uint32_t kRun = 8;  // entries gathered per lane before they are walked
 
+// One sample's position as one 12-byte load (global_load_dwordx3) for D = 3:
+// one L1 line lookup per lane instead of three.
+typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+template <uint32_t D>
+__device__ __forceinline__ void load_pos3(const float *__restrict__ inputs, uint32_t s,
+                                          float (&x)[D]) {
+    if constexpr (D == 3) {
+        const f3u v = *reinterpret_cast<const f3u *>(inputs + (size_t)s * 3);
+        x[0] = v.x;
+        x[1] = v.y;
+        x[2] = v.z;
+    } else {
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) x[d] = inputs[(size_t)s * D + d];
+    }
+}
+
 // One sample's C gradient channels as one load where the row is 4 or 8 bytes.
 template <typename grad_t, uint32_t C>
 __device__ __forceinline__ void load_grad(const grad_t *__restrict__ p, float (&g)[C]) {
@@ -265,7 +283,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                                                BinInfo bi, uint32_t gridtype, int align_corners,
                                                SliceDyn dyn, float inv, uint32_t B,
                                                const uint32_t *__restrict__ counts,
-                                               const uint32_t *__restrict__ entries,
+                                               const uint16_t *__restrict__ entries,
                                                float *__restrict__ partial) {
     extern __shared__ double acc[];
     // workgroup -> (XCD x, slot) -> (level, slice k, sub-part q)
@@ -298,7 +316,8 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     const uint32_t t1 = (uint32_t)(((uint64_t)ntiles * (x + 1)) / kXcds);
     for (uint32_t t = t0 + q + Q * wave; t < t1; t += Q * waves) {
         const uint32_t cnt = counts[(size_t)t * nb + b];
-        const uint32_t *seg = entries + ((size_t)t * nb + b) * kTile;
+        const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile;
+        const uint32_t tbase = t * kTile;
         const uint32_t Q = (cnt + 63) >> 6;
         const uint32_t e0 = min(lane * Q, cnt), e1 = min(e0 + Q, cnt);
         double cw[1u << D][C];
@@ -318,11 +337,10 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                 float xs[RUN][D];
                 float gs[RUN][C];
 #pragma unroll
-                for (uint32_t i = 0; i < RUN; ++i) sid[i] = seg[min(e + i, e1 - 1)];
+                for (uint32_t i = 0; i < RUN; ++i) sid[i] = tbase + seg[min(e + i, e1 - 1)];
 #pragma unroll
                 for (uint32_t i = 0; i < RUN; ++i) {
-#pragma unroll
-                    for (uint32_t d = 0; d < D; ++d) xs[i][d] = inputs[(size_t)sid[i] * D + d];
+                    load_pos3<D>(inputs, sid[i], xs[i]);
                     load_grad<grad_t, C>(gl + (size_t)sid[i] * C, gs[i]);
                 }
 #pragma unroll
@@ -427,7 +445,7 @@ template <typename grad_t, uint32_t C>
 static void launch_walk(hipStream_t s, dim3 g, size_t lds, const grad_t *grad,
                         const float *inputs, const int32_t *offsets, const Levels &lv,
                         const BinInfo &bi, uint32_t gridtype, int align, SliceDyn dyn,
-                        uint32_t B, const uint32_t *counts, const uint32_t *entries,
+                        uint32_t B, const uint32_t *counts, const uint16_t *entries,
                         float *partial) {
     const bool pow2 = ge::dyn_pow2(dyn.bound);
     const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
@@ -456,7 +474,8 @@ extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *o
         return DFHIP_EINVAL;
     }
     const uint64_t tiles = ceil_div<uint64_t>(cap ? cap : 1, gb::kTile);
-    if (entries_u32) *entries_u32 = tiles * bi.nbins * gb::kTile;
+    // tile-relative sample ids, u16 (kTile <= 65536), counted in u32 words
+    if (entries_u32) *entries_u32 = (tiles * bi.nbins * gb::kTile + 1) / 2;
     if (counts_u32) *counts_u32 = tiles * bi.nbins;
     if (partial_f32) *partial_f32 = gb::partial_floats(bi, C);
     return DFHIP_OK;
@@ -507,18 +526,18 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
             if (pow2)
                 gb::k_bin<3, true><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype,
                                                          align_corners, dyn, inv, B, counts,
-                                                         entries);
+                                                         (uint16_t *)entries);
             else
                 gb::k_bin<3, false><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype,
                                                           align_corners, dyn, inv, B, counts,
-                                                          entries);
+                                                          (uint16_t *)entries);
         }
         if (!(phase & 2)) return check_launch(name);
         const dim3 g(gb::kXcds * bi.nslots);
         const size_t lds = ((size_t)1 << bi.shift) * C * sizeof(double);
 #define DFHIP_WALK(GT, CC)                                                                      \
     gb::launch_walk<GT, CC>(s, g, lds, (const GT *)grad_lbc, inputs, offsets, lv, bi, gridtype, \
-                            align_corners, dyn, B, counts, entries, partial)
+                            align_corners, dyn, B, counts, (const uint16_t *)entries, partial)
         if (grad_dtype == DFHIP_F16) {
             if (C == 1) DFHIP_WALK(half_t, 1); else if (C == 2) DFHIP_WALK(half_t, 2); else DFHIP_WALK(half_t, 4);
         } else {

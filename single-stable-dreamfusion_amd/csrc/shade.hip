@@ -11,11 +11,16 @@
 //             (renderer.py:485-489, mean over the march's M' rows)
 //
 // The six stencil evaluations are extra rows of ONE fused field launch: the
-// stencil kernel writes the stencil points of the M live samples behind them
-// (rows M + a M + i, a = 0..5: +x, -x, +y, -y, +z, -z) and the live row count
-// 7 M, so the field forward, the field backward and the embedding backward
-// each run once over 7 M rows.  The shading kernels keep the reference's
-// dtypes and rounding points: the normal and the orientation loss in f32, the
+// stencil kernel lays out the M live samples with their stencil points
+// interleaved (row 7 i = sample i, rows 7 i + 1 + a, a = 0..5: +x, -x, +y,
+// -y, +z, -z) and writes the live row count 7 M, so the field forward, the
+// field backward and the embedding backward each run once over 7 M rows.  The
+// interleaving keeps a sample's seven points adjacent: at the coarse grid
+// levels (cells wider than the 2 eps stencil) they fall in one cell, and the
+// binned embedding backward merges their contributions in registers before
+// its LDS atomics; their table gathers hit the same lines.
+//
+// The shading kernels keep the reference's dtypes and rounding points: the normal and the orientation loss in f32, the
 // light product, lambertian and colour as f16 values (autocast casts normal @ l
 // to f16), the gradients of the f16 tensors rounded to f16 where autograd
 // would hold them in f16.  Loss-scale handling follows autograd: the
@@ -43,10 +48,11 @@ __device__ __forceinline__ float padded_rows(uint32_t m) {
     return (float)(m + 128u - m % 128u);
 }
 
-// Stencil points of the live samples behind them + the live count 7 M.
-__global__ __launch_bounds__(kThreads) void k_stencil(float *__restrict__ xyz,
+// Samples and their stencil points, interleaved, + the live count 7 M.
+__global__ __launch_bounds__(kThreads) void k_stencil(const float *__restrict__ xyz,
                                                       const int32_t *__restrict__ m_dev,
                                                       uint32_t cap, float eps, float bound,
+                                                      float *__restrict__ xyz7,
                                                       int32_t *__restrict__ m7_dev) {
     const uint32_t M = live(m_dev, cap);
     if (blockIdx.x == 0 && threadIdx.x == 0) *m7_dev = (int32_t)(7u * M);
@@ -54,16 +60,18 @@ __global__ __launch_bounds__(kThreads) void k_stencil(float *__restrict__ xyz,
         float x[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) x[d] = xyz[3 * (size_t)i + d];
+        float *dst = xyz7 + 21 * (size_t)i;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) dst[d] = x[d];
 #pragma unroll
         for (int s = 0; s < kStencil; ++s) {
             const int a = s >> 1;
             const float off = (s & 1) ? -eps : eps;
-            float *dst = xyz + 3 * ((size_t)(1 + s) * M + i);
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
                 // x + tensor([[eps, 0, 0]]) then clamp(-bound, bound)
                 const float v = x[d] + (d == a ? off : 0.0f);
-                dst[d] = fminf(fmaxf(v, -bound), bound);
+                dst[3 * (1 + s) + d] = fminf(fmaxf(v, -bound), bound);
             }
         }
     }
@@ -75,13 +83,13 @@ struct Normal {
 };
 
 // network_grid.py:90-121 (f32): v = -(0.5 * (s+ - s-) / eps), n = v / sqrt(clamp(|v|^2, 1e-20))
-__device__ __forceinline__ Normal fd_normal(const float *__restrict__ sigma, uint32_t M,
-                                            uint32_t i, float eps) {
+__device__ __forceinline__ Normal fd_normal(const float *__restrict__ sigma7, uint32_t i,
+                                            float eps) {
     Normal o;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float sp = sigma[(size_t)(1 + 2 * a) * M + i];
-        const float sn = sigma[(size_t)(2 + 2 * a) * M + i];
+        const float sp = sigma7[7 * (size_t)i + 1 + 2 * a];
+        const float sn = sigma7[7 * (size_t)i + 2 + 2 * a];
         o.v[a] = -((0.5f * (sp - sn)) / eps);
     }
     o.ss = (o.v[0] * o.v[0] + o.v[1] * o.v[1]) + o.v[2] * o.v[2];
@@ -114,13 +122,15 @@ __device__ __forceinline__ Shade lambert(const float n[3], const float l16[3], f
     return s;
 }
 
-// Forward: colour (f16, for the compositing), the normal (f32, kept for the
-// backward) and per-block partial sums of the orientation term (f64).
+// Forward: the samples' density (f32) and colour (f16) for the compositing,
+// the normal (f32, kept for the backward) and per-block partial sums of the
+// orientation term (f64).  sigma7 / albedo7: the field on the 7 M rows.
 __global__ __launch_bounds__(kThreads) void k_shade_fwd(
-    const float *__restrict__ sigma, const half_t *__restrict__ albedo,
+    const float *__restrict__ sigma7, const half_t *__restrict__ albedo7,
     const float *__restrict__ dirs, const float *__restrict__ light, float ratio, float omr,
     float eps, int lambertian, const int32_t *__restrict__ m_dev, uint32_t cap,
-    half_t *__restrict__ color, float *__restrict__ normal, double *__restrict__ part) {
+    float *__restrict__ sigma, half_t *__restrict__ color, float *__restrict__ normal,
+    double *__restrict__ part) {
     __shared__ double red[kThreads / 64];
     const uint32_t M = live(m_dev, cap);
     float l16[3];
@@ -128,17 +138,19 @@ __global__ __launch_bounds__(kThreads) void k_shade_fwd(
     for (int d = 0; d < 3; ++d) l16[d] = r16(light[d]);
     double acc = 0.0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
-        const Normal nm = fd_normal(sigma, M, i, eps);
+        const Normal nm = fd_normal(sigma7, i, eps);
         const Shade sh = lambert(nm.n, l16, ratio, omr);
+        const float sg = sigma7[7 * (size_t)i];
+        sigma[i] = sg;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             normal[3 * (size_t)i + d] = nm.n[d];
-            const float c = lambertian ? r16((float)albedo[3 * (size_t)i + d] * sh.lam16)
+            const float c = lambertian ? r16((float)albedo7[21 * (size_t)i + d] * sh.lam16)
                                        : sh.lam16;
             color[3 * (size_t)i + d] = (half_t)c;
         }
         // orientation term: (1 - exp(-sigma)) * clamp(n . d, min=0)^2
-        const float w = 1.0f - expf(-sigma[i]);
+        const float w = 1.0f - expf(-sg);
         const float nd = (nm.n[0] * dirs[3 * (size_t)i] + nm.n[1] * dirs[3 * (size_t)i + 1]) +
                          nm.n[2] * dirs[3 * (size_t)i + 2];
         const float c = nd > 0.0f ? nd : 0.0f;
@@ -172,16 +184,18 @@ __global__ __launch_bounds__(64) void k_orient_finish(const double *__restrict__
     }
 }
 
-// Backward.  grad_color [cap, 3] f16: d loss / d colour from the compositing
-// backward.  Writes grad_albedo for the 7 M field rows (main rows: the albedo
-// gradient of the lambertian product, else 0; stencil rows 0) and grad_sigma
-// for the stencil rows (the main rows keep the compositing's gradient).
+// Backward.  grad_sigma [cap] f32 / grad_color [cap, 3] f16: d loss / d
+// (density, colour) from the compositing backward.  Writes the field-row
+// gradients grad_sigma7 [7 M] (sample rows: the compositing's, stencil rows:
+// through the normal) and grad_albedo7 [7 M, 3] (sample rows: the lambertian
+// product's albedo gradient, else 0; stencil rows 0).
 __global__ __launch_bounds__(kThreads) void k_shade_bwd(
-    const float *__restrict__ sigma, const half_t *__restrict__ albedo,
+    const float *__restrict__ sigma7, const half_t *__restrict__ albedo7,
     const float *__restrict__ dirs, const float *__restrict__ light, float ratio, float omr,
     float eps, int lambertian, const int32_t *__restrict__ m_dev, uint32_t cap,
-    const half_t *__restrict__ grad_color, const float *__restrict__ grad_loss, float lambda,
-    float *__restrict__ grad_sigma, half_t *__restrict__ grad_albedo) {
+    const float *__restrict__ grad_sigma, const half_t *__restrict__ grad_color,
+    const float *__restrict__ grad_loss, float lambda, float *__restrict__ grad_sigma7,
+    half_t *__restrict__ grad_albedo7) {
     const uint32_t M = live(m_dev, cap);
     float l16[3];
 #pragma unroll
@@ -189,8 +203,9 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
     // d loss / d orient_i: (scale * lambda) / M' (MulBackward, MeanBackward)
     const float go = (grad_loss[0] * lambda) / padded_rows(M);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
-        const Normal nm = fd_normal(sigma, M, i, eps);
+        const Normal nm = fd_normal(sigma7, i, eps);
         const Shade sh = lambert(nm.n, l16, ratio, omr);
+        half_t *ga = grad_albedo7 + 21 * (size_t)i;
         float g[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) g[d] = (float)grad_color[3 * (size_t)i + d];
@@ -199,14 +214,14 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
             float gl[3];
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
-                const float a = (float)albedo[3 * (size_t)i + d];
-                grad_albedo[3 * (size_t)i + d] = (half_t)r16(g[d] * sh.lam16);
+                const float a = (float)albedo7[21 * (size_t)i + d];
+                ga[d] = (half_t)r16(g[d] * sh.lam16);
                 gl[d] = r16(g[d] * a);
             }
             glam = r16((gl[0] + gl[1]) + gl[2]);  // sum over the broadcast dim
         } else {
 #pragma unroll
-            for (int d = 0; d < 3; ++d) grad_albedo[3 * (size_t)i + d] = (half_t)0.0f;
+            for (int d = 0; d < 3; ++d) ga[d] = (half_t)0.0f;
             glam = r16((g[0] + g[1]) + g[2]);  // RepeatBackward
         }
         const float gc = r16(glam * omr);                 // (1 - ratio) * c
@@ -215,7 +230,7 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
 #pragma unroll
         for (int d = 0; d < 3; ++d) gn[d] = r16(gd * l16[d]);  // mv backward (f16), cast back
         // orientation term: d/dn of go * w * clamp(n . d, 0)^2
-        const float w = 1.0f - expf(-sigma[i]);
+        const float w = 1.0f - expf(-sigma7[7 * (size_t)i]);
         const float dx = dirs[3 * (size_t)i], dy = dirs[3 * (size_t)i + 1],
                     dz = dirs[3 * (size_t)i + 2];
         const float nd = (nm.n[0] * dx + nm.n[1] * dy) + nm.n[2] * dz;
@@ -232,21 +247,20 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
         const float gr = ((-gn[0] * nm.v[0]) / r2 + (-gn[1] * nm.v[1]) / r2) +
                          (-gn[2] * nm.v[2]) / r2;
         const float gs = nm.ss >= 1e-20f ? gr / (2.0f * nm.r) : 0.0f;
+        float *gs7 = grad_sigma7 + 7 * (size_t)i;
+        gs7[0] = grad_sigma[i];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             const float gv = gn[a] / nm.r + (gs * nm.v[a] + gs * nm.v[a]);
             // v = -((0.5 * (s+ - s-)) / eps)
             const float gdiff = 0.5f * (-gv / eps);
-            grad_sigma[(size_t)(1 + 2 * a) * M + i] = gdiff;
-            grad_sigma[(size_t)(2 + 2 * a) * M + i] = -gdiff;
+            gs7[1 + 2 * a] = gdiff;
+            gs7[2 + 2 * a] = -gdiff;
         }
+        // the stencil rows carry no albedo gradient
+#pragma unroll
+        for (int k = 3; k < 21; ++k) ga[k] = (half_t)0.0f;
     }
-    // the stencil rows carry no albedo gradient
-    const size_t n6 = 3 * (size_t)6 * M;
-    half_t *ga = grad_albedo + 3 * (size_t)M;
-    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n6;
-         k += (size_t)gridDim.x * blockDim.x)
-        ga[k] = (half_t)0.0f;
 }
 
 // Light direction of the step (renderer.py:462-464): safe_normalize(rays_o[0]
@@ -299,9 +313,10 @@ static uint32_t shade_blocks(uint32_t cap) {
 
 extern "C" uint32_t dfhip_shading_partial_doubles(uint32_t cap) { return shade_blocks(cap); }
 
-extern "C" int dfhip_shading_stencil(float *xyz, const int32_t *m_dev, uint32_t cap, float eps,
-                                     float bound, int32_t *m7_dev, dfhip_stream_t stream) {
-    if (!xyz || !m_dev || !m7_dev) {
+extern "C" int dfhip_shading_stencil(const float *xyz, const int32_t *m_dev, uint32_t cap,
+                                     float eps, float bound, float *xyz7, int32_t *m7_dev,
+                                     dfhip_stream_t stream) {
+    if (!xyz || !m_dev || !xyz7 || !m7_dev) {
         set_error("shading_stencil: null pointer");
         return DFHIP_EINVAL;
     }
@@ -309,8 +324,8 @@ extern "C" int dfhip_shading_stencil(float *xyz, const int32_t *m_dev, uint32_t 
         set_error("shading_stencil: bound must be > 0");
         return DFHIP_EINVAL;
     }
-    shd::k_stencil<<<shade_blocks(cap), shd::kThreads, 0, as_stream(stream)>>>(xyz, m_dev, cap,
-                                                                               eps, bound, m7_dev);
+    shd::k_stencil<<<shade_blocks(cap), shd::kThreads, 0, as_stream(stream)>>>(
+        xyz, m_dev, cap, eps, bound, xyz7, m7_dev);
     return check_launch("shading_stencil");
 }
 
@@ -324,47 +339,51 @@ static bool shading_mode(const char *name, int shading, int &lambertian) {
     return true;
 }
 
-extern "C" int dfhip_shading_forward(const float *sigma, const void *albedo, const float *dirs,
+extern "C" int dfhip_shading_forward(const float *sigma7, const void *albedo7, const float *dirs,
                                      const float *light, float ratio, float eps, int shading,
-                                     const int32_t *m_dev, uint32_t cap, void *color,
-                                     float *normal, double *partial, float lambda_orient,
-                                     float *orient, float *loss, dfhip_stream_t stream) {
+                                     const int32_t *m_dev, uint32_t cap, float *sigma,
+                                     void *color, float *normal, double *partial,
+                                     float lambda_orient, float *orient, float *loss,
+                                     dfhip_stream_t stream) {
     const char *name = "shading_forward";
     int lam = 0;
     if (!shading_mode(name, shading, lam)) return DFHIP_EINVAL;
-    if (!sigma || !albedo || !dirs || !light || !m_dev || !color || !normal || !partial) {
+    if (!sigma7 || !albedo7 || !dirs || !light || !m_dev || !sigma || !color || !normal ||
+        !partial) {
         set_error("%s: null pointer", name);
         return DFHIP_EINVAL;
     }
     hipStream_t s = as_stream(stream);
     const uint32_t blocks = shade_blocks(cap);
     const float omr = (float)(1.0 - (double)ratio);
-    shd::k_shade_fwd<<<blocks, shd::kThreads, 0, s>>>(sigma, (const half_t *)albedo, dirs, light,
-                                                      ratio, omr, eps, lam, m_dev, cap,
-                                                      (half_t *)color, normal, partial);
+    shd::k_shade_fwd<<<blocks, shd::kThreads, 0, s>>>(sigma7, (const half_t *)albedo7, dirs,
+                                                      light, ratio, omr, eps, lam, m_dev, cap,
+                                                      sigma, (half_t *)color, normal, partial);
     shd::k_orient_finish<<<1, 64, 0, s>>>(partial, blocks, m_dev, cap, lambda_orient, orient,
                                           loss);
     return check_launch(name);
 }
 
-extern "C" int dfhip_shading_backward(const float *sigma, const void *albedo, const float *dirs,
-                                      const float *light, float ratio, float eps, int shading,
-                                      const int32_t *m_dev, uint32_t cap, const void *grad_color,
+extern "C" int dfhip_shading_backward(const float *sigma7, const void *albedo7,
+                                      const float *dirs, const float *light, float ratio,
+                                      float eps, int shading, const int32_t *m_dev, uint32_t cap,
+                                      const float *grad_sigma, const void *grad_color,
                                       const float *grad_loss, float lambda_orient,
-                                      float *grad_sigma, void *grad_albedo,
+                                      float *grad_sigma7, void *grad_albedo7,
                                       dfhip_stream_t stream) {
     const char *name = "shading_backward";
     int lam = 0;
     if (!shading_mode(name, shading, lam)) return DFHIP_EINVAL;
-    if (!sigma || !albedo || !dirs || !light || !m_dev || !grad_color || !grad_loss ||
-        !grad_sigma || !grad_albedo) {
+    if (!sigma7 || !albedo7 || !dirs || !light || !m_dev || !grad_sigma || !grad_color ||
+        !grad_loss || !grad_sigma7 || !grad_albedo7) {
         set_error("%s: null pointer", name);
         return DFHIP_EINVAL;
     }
     const float omr = (float)(1.0 - (double)ratio);
     shd::k_shade_bwd<<<shade_blocks(cap), shd::kThreads, 0, as_stream(stream)>>>(
-        sigma, (const half_t *)albedo, dirs, light, ratio, omr, eps, lam, m_dev, cap,
-        (const half_t *)grad_color, grad_loss, lambda_orient, grad_sigma, (half_t *)grad_albedo);
+        sigma7, (const half_t *)albedo7, dirs, light, ratio, omr, eps, lam, m_dev, cap, grad_sigma,
+        (const half_t *)grad_color, grad_loss, lambda_orient, grad_sigma7,
+        (half_t *)grad_albedo7);
     return check_launch(name);
 }
 

@@ -119,7 +119,7 @@ class NativeAlbedoStep:
         # march
         self.rays = torch.empty(N, 3, **i32)
         self.block_sums = torch.empty(_raymarching.march_rays_train_scratch_ints(N), **i32)
-        self.xyzs = torch.empty(fcap, 3, **f32)  # march rows [0, M), stencil rows behind
+        self.xyzs = torch.empty(cap, 3, **f32)
         self.dirs = torch.empty(cap, 3, **f32)
         self.deltas = torch.empty(cap, 2, **f32)
         # the count pass keeps each sample here; the emit pass only copies
@@ -138,10 +138,15 @@ class NativeAlbedoStep:
         for lin in m.sigma_net.net:
             self.mlp += [lin.weight, lin.bias]
         self.enc = torch.empty(fcap, self.L * self.C, **f16)
-        self.sigma = torch.empty(fcap, **f32)
+        # field rows: the samples, or (shading) each sample followed by its six
+        # stencil points (csrc/shade.hip); the compositing reads self.sigma
+        self.sigma = torch.empty(cap, **f32)
         self.albedo = torch.empty(fcap, 3, **f16)
+        self.xyz_field, self.sigma_field = self.xyzs, self.sigma
         self.m_field = self.m_dev  # live field rows: M, or 7 M with the stencil
         if self.shade_code:
+            self.xyz_field = torch.empty(fcap, 3, **f32)
+            self.sigma_field = torch.empty(fcap, **f32)
             self.m7 = torch.zeros(1, **i32)
             self.m_field = self.m7
             self.light = torch.empty(3, **f32)
@@ -165,8 +170,10 @@ class NativeAlbedoStep:
         self.grad_ws = torch.empty(N, **f32)
         self.head_partial = (torch.empty(int(_dfhip.load().dfhip_ray_head_partial_floats(N)),
                                          **f32) if self.bg_layers is not None else None)
-        self.grad_sigma = torch.empty(fcap, **f32)
+        self.grad_sigma = torch.empty(cap, **f32)
         self.grad_albedo = torch.empty(fcap, 3, **f16)
+        self.grad_sigma_field = (torch.empty(fcap, **f32) if self.shade_code
+                                 else self.grad_sigma)
         self.d_enc = torch.empty(self.L, fcap, self.C, **f16)
         self.mlp_partial = torch.empty(_fieldmlp.backward_parts(fcap) * _fieldmlp.params_count(),
                                        **f32)
@@ -233,18 +240,18 @@ class NativeAlbedoStep:
         S, Hb, gridtype, align, _ = self.meta
         if self.shade_code:
             call("dfhip_shading_stencil", ptr(self.xyzs), ptr(self.m_dev), cap, FD_EPS,
-                 float(m.bound), ptr(self.m7), stream())
-        _fieldmlp.grid_field_forward(self.xyzs, m.bound, self.table, self.encoder.offsets, S, Hb,
-                                     gridtype, align, self.mlp, self.enc, self.sigma, self.albedo,
-                                     self.m_field)
+                 float(m.bound), ptr(self.xyz_field), ptr(self.m7), stream())
+        _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table, self.encoder.offsets,
+                                     S, Hb, gridtype, align, self.mlp, self.enc,
+                                     self.sigma_field, self.albedo, self.m_field)
         rgb = self.albedo
         if self.shade_code:
             # normals, lambertian, colour, orientation loss (network_grid.py:116-144,
             # renderer.py:485-489)
-            call("dfhip_shading_forward", ptr(self.sigma), ptr(self.albedo), ptr(self.dirs),
-                 ptr(self.light), self.ratio, FD_EPS, self.shade_code, ptr(self.m_dev), cap,
-                 ptr(self.color), ptr(self.normal), ptr(self.orient_partial), self.lam_orient,
-                 ptr(self.orient), None, stream())
+            call("dfhip_shading_forward", ptr(self.sigma_field), ptr(self.albedo),
+                 ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
+                 ptr(self.m_dev), cap, ptr(self.sigma), ptr(self.color), ptr(self.normal),
+                 ptr(self.orient_partial), self.lam_orient, ptr(self.orient), None, stream())
             rgb = self.color
         # compositing (raymarching.py:238-269)
         _raymarching.composite_rays_train_forward_mixed(
@@ -278,16 +285,17 @@ class NativeAlbedoStep:
             self.ws, self.image, cap, N, 1e-4, self.grad_sigma,
             self.grad_color if self.shade_code else self.grad_albedo, False)
         if self.shade_code:
-            # colour / orientation gradients -> albedo and stencil sigma gradients
-            call("dfhip_shading_backward", ptr(self.sigma), ptr(self.albedo), ptr(self.dirs),
-                 ptr(self.light), self.ratio, FD_EPS, self.shade_code, ptr(self.m_dev), cap,
-                 ptr(self.grad_color), ptr(scale), self.lam_orient, ptr(self.grad_sigma),
-                 ptr(self.grad_albedo), stream())
+            # density / colour / orientation gradients -> the field rows' gradients
+            call("dfhip_shading_backward", ptr(self.sigma_field), ptr(self.albedo),
+                 ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
+                 ptr(self.m_dev), cap, ptr(self.grad_sigma), ptr(self.grad_color), ptr(scale),
+                 self.lam_orient, ptr(self.grad_sigma_field), ptr(self.grad_albedo), stream())
         from gridencoder.grid import _parts
         _fieldmlp.grid_field_backward(
-            self.enc, self.xyzs, m.bound, self.mlp, self.grad_sigma, self.grad_albedo, self.d_enc,
-            self.mlp_partial, [p.grad for p in self.mlp], self.encoder.offsets, self.rows, S, Hb,
-            gridtype, align, None, None, _parts(self.rows, self.C), self.m_field)
+            self.enc, self.xyz_field, m.bound, self.mlp, self.grad_sigma_field, self.grad_albedo,
+            self.d_enc, self.mlp_partial, [p.grad for p in self.mlp], self.encoder.offsets,
+            self.rows, S, Hb, gridtype, align, None, None, _parts(self.rows, self.C),
+            self.m_field)
         return self.loss
 
     def _backward_two_pass(self, bw, scale):
@@ -325,7 +333,7 @@ class NativeAlbedoStep:
             m = self.trainer.model
             S, Hb, gridtype, align, offsets_host = self.meta
             self._emb_launch = _gridencoder.binned_launcher(
-                self.d_enc, self.xyzs, m.bound, self.encoder.offsets, offsets_host,
+                self.d_enc, self.xyz_field, m.bound, self.encoder.offsets, offsets_host,
                 self.encoder.embeddings.grad, self.fcap, self.m_field, 3, self.C, self.L, S, Hb,
                 gridtype, align, *self.bin_scratch)
         per = 12 + self.L * self.C * 2

@@ -7,8 +7,8 @@ launches, nerf/native_step.py)
   shade_backward) on the step's own field values: normals to f32 rounding,
   colours bit-exact up to f16 boundary flips, orientation loss, stencil and
   albedo gradients;
-* the stencil rows equal clamp(x +- eps e_a, -bound, bound) bit for bit and
-  the field on them equals the fused field evaluated on those points;
+* the stencil rows (interleaved: row 7 i = sample i, 7 i + 1 + a = its
+  stencil point a) equal clamp(x +- eps e_a, -bound, bound) bit for bit;
 * against the autograd shading step (the reference's composition of
   common_forward x 7 + safe_normalize + lambertian + orientation loss, on the
   same kernels) fed the same rays, noise, light and SDS gradient;
@@ -49,17 +49,19 @@ def test_shading_kernels_match_oracle(gpu, shading, ratio):
     M = int(nat.counter[0])
     assert M > 1000 and int(nat.m7) == 7 * M
     x = nat.xyzs[:M].cpu().numpy()
-    st = nat.xyzs[M:7 * M].view(6, M, 3).cpu().numpy()
+    x7 = nat.xyz_field[:7 * M].view(M, 7, 3).cpu().numpy()
+    np.testing.assert_array_equal(x7[:, 0], x)
     for a in range(6):
         want = x.copy()
         want[:, a // 2] = want[:, a // 2] + np.float32(-1e-2 if a & 1 else 1e-2)
-        np.testing.assert_array_equal(st[a], np.clip(want, -1, 1))
-    sig = nat.sigma[:7 * M].cpu().numpy()
-    alb = nat.albedo[:M].cpu().numpy()
+        np.testing.assert_array_equal(x7[:, 1 + a], np.clip(want, -1, 1))
+    sig7 = nat.sigma_field[:7 * M].view(M, 7).cpu().numpy()
+    np.testing.assert_array_equal(nat.sigma[:M].cpu().numpy(), sig7[:, 0])
+    alb = nat.albedo[:7 * M].view(M, 7, 3)[:, 0].cpu().numpy()
     dirs = nat.dirs[:M].cpu().numpy()
     light = nat.light.cpu().numpy()
     np.testing.assert_allclose(np.linalg.norm(light), 1.0, rtol=1e-6)
-    fo = of.shade_forward(sig[:M], sig[M:].reshape(6, M), alb, dirs, light, ratio, shading)
+    fo = of.shade_forward(sig7[:, 0], sig7[:, 1:].T, alb, dirs, light, ratio, shading)
     np.testing.assert_allclose(nat.normal[:M].cpu().numpy(), fo["normal"], rtol=2e-6, atol=2e-7)
     col = nat.color[:M].cpu().numpy()
     flips = (col != fo["color"]).any(1)
@@ -74,17 +76,19 @@ def test_shading_kernels_match_oracle(gpu, shading, ratio):
     scale = float(trainer.scaler._scale) if trainer.scaler.is_enabled() else 1.0
     gsp, ga = of.shade_backward(fo, alb, dirs, nat.grad_color[:M].cpu().numpy(), scale,
                                 trainer.opt.lambda_orient, of.padded_rows(M), ratio, shading)
-    got = nat.grad_sigma[M:7 * M].view(6, M).cpu().numpy()
+    g7 = nat.grad_sigma_field[:7 * M].view(M, 7).cpu().numpy()
+    np.testing.assert_array_equal(g7[:, 0], nat.grad_sigma[:M].cpu().numpy())
+    got = g7[:, 1:].T
     clean = ~flips
     np.testing.assert_allclose(got[:, clean], gsp[:, clean], rtol=1e-4,
                                atol=1e-6 * np.abs(gsp).max())
-    ga_got = nat.grad_albedo[:7 * M].cpu().numpy()
-    assert not ga_got[M:].any()  # stencil rows carry no albedo gradient
+    ga_got = nat.grad_albedo[:7 * M].view(M, 7, 3).cpu().numpy()
+    assert not ga_got[:, 1:].any()  # stencil rows carry no albedo gradient
     if shading == "lambertian":
-        np.testing.assert_allclose(ga_got[:M][clean].astype(np.float32),
+        np.testing.assert_allclose(ga_got[:, 0][clean].astype(np.float32),
                                    ga[clean].astype(np.float32), rtol=2e-3, atol=1e-7)
     else:
-        assert not ga_got[:M].any()
+        assert not ga_got[:, 0].any()
 
 
 def _autograd_grads(trainer, nat, batch, shading, ratio, res):
@@ -127,7 +131,7 @@ def test_native_shaded_step_matches_autograd_step(gpu, shading, ratio):
             p.copy_(v)
     loss = _autograd_grads(trainer, nat, batch, shading, ratio, res)
     assert int(trainer.model.last_counter[0]) == int(nat.counter[0])
-    np.testing.assert_allclose(float(loss), got_loss, rtol=1e-5)
+    np.testing.assert_allclose(float(loss.detach()), got_loss, rtol=1e-5)
     for p, g in zip(params, got):
         assert p.grad is not None
         ref = p.grad.double()
