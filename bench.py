@@ -52,7 +52,9 @@ def parse():
                    help="launch every kernel eagerly (no HIP-graph replay of the step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=1)
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--c1-steps", type=int, default=10,
+                   help="timed CPU iterations of BASELINE configs[0] (64x64), 0 to skip")
     p.add_argument("--no-infer", action="store_true",
                    help="skip the C4 inference-render measurement")
     p.add_argument("--infer-res", type=int, default=800)
@@ -93,19 +95,29 @@ def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False):
     return trainer, data
 
 
-def cpu_baseline(res, steps):
+def cpu_baseline(res, steps, c1_steps=10, c1_warmup=3):
     """The oracle's pure-PyTorch CPU restatement of the --cuda_ray-off train
-    step, on this host's cores, over a bounded sample."""
+    step (renderer.py:301-443 run() + sample_pdf, grid network, entropy, Adam)
+    on this host's cores, with the GPU leg's guidance (w(t) N(0,1) injected at
+    pred_rgb): `steps` timed steps (+1 warm-up) at the GPU workload's res x res
+    (the reported value), and BASELINE configs[0] = C1, 64x64 with c1_steps
+    timed iterations after c1_warmup warm-up ones."""
     import oracle.cpu_render as cr
     cores = len(os.sched_getaffinity(0))
     threads = int(os.environ.get("OMP_NUM_THREADS", cores))
     torch.set_num_threads(max(1, min(cores, threads)))
-    step = cr.CPUTrainStep(res, res, seed=0)
-    step.step()  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step.step()
-    dt = time.perf_counter() - t0
+
+    def timed(r, k, w):
+        step = cr.CPUTrainStep(r, r, seed=0, guidance="injected")
+        for _ in range(w):
+            step.step()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step.step()
+        return (time.perf_counter() - t0) / k
+
+    dt = timed(res, steps, 1)
+    c1 = timed(64, c1_steps, c1_warmup) if c1_steps > 0 else None
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -114,10 +126,16 @@ def cpu_baseline(res, steps):
                 break
     except OSError:
         pass
-    return {"value": res * res * steps / dt, "unit": "rays/s", "steps_per_sec": steps / dt,
-            "cores": torch.get_num_threads(), "kind": "port", "cpu_model": model,
-            "sample": f"{steps} timed + 1 warm-up --cuda_ray-off train steps at {res}x{res} "
-                      f"(64 coarse + 64 importance samples/ray, fp32, synthetic SDS, Adam)"}
+    out = {"value": res * res / dt, "unit": "rays/s", "steps_per_sec": 1.0 / dt,
+           "cores": torch.get_num_threads(), "kind": "port", "cpu_model": model,
+           "sample": f"{steps} timed + 1 warm-up --cuda_ray-off train steps at {res}x{res} "
+                     f"(64 coarse + 64 importance samples/ray, fp32, w(t) N(0,1) SDS gradient "
+                     f"injected at pred_rgb as on the GPU, entropy, Adam)"}
+    if c1 is not None:
+        out["c1"] = {"workload": "C1: main.py -O off, 64x64, run() 64+64 samples, fp32, CPU",
+                     "steps": c1_steps, "warmup": c1_warmup, "ms_per_step": round(c1 * 1e3, 1),
+                     "steps_per_sec": round(1.0 / c1, 4), "rays_per_sec": round(4096 / c1, 1)}
+    return out
 
 
 def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1):
@@ -447,7 +465,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_infer:
         result["inference"] = bench_inference(device, args.infer_res)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.res, args.cpu_steps)
+        result["cpu_baseline"] = cpu_baseline(args.res, args.cpu_steps, args.c1_steps)
         result["gpu_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -118,8 +118,9 @@ class CPUNeRF(nn.Module):
         g = 5 * torch.exp(-(x ** 2).sum(-1) / (2 * 0.2 ** 2))
         return torch.exp(h[..., 0] + g), torch.sigmoid(h[..., 1:])
 
-    def run(self, rays_o, rays_d, num_steps=64, upsample_steps=64, perturb=True):
-        """renderer.py:301-443 (albedo shading, bg net) -> image [N,3], weights_sum [N]."""
+    def run(self, rays_o, rays_d, num_steps=64, upsample_steps=64, perturb=True, det=False):
+        """renderer.py:301-443 (albedo shading, bg net) -> image [N,3], weights_sum [N].
+        det: sample_pdf's deterministic u (renderer.py:28-30, eval mode)."""
         N = rays_o.shape[0]
         nears, fars = near_far_from_aabb(rays_o, rays_d, self.aabb, self.min_near)
         nears, fars = nears[:, None], fars[:, None]
@@ -139,7 +140,11 @@ class CPUNeRF(nn.Module):
             wts = w[:, 1:-1] + 1e-5
             pdf = wts / wts.sum(-1, keepdim=True)
             cdf = torch.cat([torch.zeros_like(pdf[:, :1]), torch.cumsum(pdf, -1)], -1)
-            u = torch.rand(N, upsample_steps).contiguous()
+            if det:
+                u = torch.linspace(0.5 / upsample_steps, 1 - 0.5 / upsample_steps,
+                                   upsample_steps).expand(N, upsample_steps).contiguous()
+            else:
+                u = torch.rand(N, upsample_steps).contiguous()
             inds = torch.searchsorted(cdf, u, right=True)
             lo, hi = (inds - 1).clamp(min=0), inds.clamp(max=cdf.shape[-1] - 1)
             cl, ch = torch.gather(cdf, 1, lo), torch.gather(cdf, 1, hi)
@@ -165,10 +170,13 @@ class CPUNeRF(nn.Module):
 
 
 class CPUTrainStep:
-    """One --cuda_ray-off SDS train step on CPU: render, synthetic SDS grad at
-    the 512^2-upsampled image, entropy regulariser, one backward, Adam."""
+    """One --cuda_ray-off SDS train step on CPU: render, SDS gradient, entropy
+    regulariser, one backward, Adam.  guidance "injected" (the GPU bench's
+    InjectedSDS: w(t) * N(0, 1) at pred_rgb) or "synthetic" (SDS arithmetic
+    around stand-in VAE / UNet convolutions at 512^2)."""
 
-    def __init__(self, H, W, seed=0, lr=1e-3):
+    def __init__(self, H, W, seed=0, lr=1e-3, guidance="injected"):
+        self.guidance = guidance
         torch.manual_seed(seed)
         self.H, self.W = H, W
         self.model = CPUNeRF()
@@ -198,6 +206,14 @@ class CPUTrainStep:
         self.opt.zero_grad()
         image, ws = self.model.run(rays_o, rays_d)
         pred = image.view(1, self.H, self.W, 3).permute(0, 3, 1, 2)
+        a = ws.clamp(1e-5, 1 - 1e-5)
+        loss = 1e-4 * (-a * torch.log2(a) - (1 - a) * torch.log2(1 - a)).mean()
+        if self.guidance == "injected":
+            t = int(torch.randint(20, 981, ()))
+            grad = (1 - self.alphas[t]) * torch.randn_like(pred)
+            torch.autograd.backward([pred, loss], [grad, None])
+            self.opt.step()
+            return float(loss.detach())
         x = F.avg_pool2d(2 * F.interpolate(pred, (512, 512), mode="bilinear",
                                            align_corners=False) - 1, 8)
         lat = F.conv2d(x, self.enc_w) * 0.18215
@@ -207,8 +223,6 @@ class CPUTrainStep:
             noisy = self.alphas[t].sqrt() * lat + (1 - self.alphas[t]).sqrt() * noise
             eps = F.conv2d(noisy, self.eps_w)
             grad = (1 - self.alphas[t]) * (eps - noise)
-        a = ws.clamp(1e-5, 1 - 1e-5)
-        loss = 1e-4 * (-a * torch.log2(a) - (1 - a) * torch.log2(1 - a)).mean()
         torch.autograd.backward([lat, loss], [grad, None])
         self.opt.step()
         return float(loss.detach())
