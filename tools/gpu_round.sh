@@ -1,0 +1,24 @@
+#!/bin/bash
+# Full round check: GPU parity tests, smoke, a default bench line, and a
+# rocprofv3 kernel-stats pass of a short bench.  Each GPU step has its own
+# time limit; the script stops at the first failing step.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-round}
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+    > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+    || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 2; }
+tail -1 $OUT/smoke.log
+timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 \
+    || { echo "bench failed"; tail -30 $OUT/bench.log; exit 3; }
+grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
+python -c "import json; d=json.load(open('$OUT/bench.json')); print('ms/step', d['ms_per_step'], 'value', d['value'], 'roof', d.get('roofline',{}).get('frac'), 'infer', d.get('inference',{}).get('ms_per_frame'))"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
+    -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing --no-alt-backward --no-shading \
+    > $OUT/bench_prof.log 2>&1 || { echo "prof failed"; tail -20 $OUT/bench_prof.log; exit 4; }
+python tools/prof_top.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/rocprof_top.txt
+cat $OUT/rocprof_top.txt
