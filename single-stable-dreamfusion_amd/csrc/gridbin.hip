@@ -2,33 +2,37 @@
 // (reference gridencoder/src/gridencoder.cu:226-313 kernel_grid_backward,
 // restructured for gfx950).
 //
-// The LDS-sliced backward (gridencoder.hip k_grid_bwd_sliced) lets every
-// slice walk every sample of its level: a 2^16-row level cut into 7-8 slices
-// re-reads and re-derives each sample's corners 7-8 times, although a sample's
-// corners touch only 1-3 of them.  Here the (sample, level) pairs are first
-// binned by the slices their corners touch, so every walk is useful:
+// The reference issues one half2 global atomic per (sample, level, corner).
+// Here every table row is owned by one LDS slice image at a time:
 //
 //   1. k_bin: per tile of kTile consecutive samples (one workgroup), every
-//      in-bounds sample derives, level by level, the slices of its 2^D corner
+//      in-bounds sample derives, level by level, the slices of its corner
 //      rows and appends its tile-relative id (u16) to the (tile, slice)
 //      segment (LDS counters give the slot; segments hold kTile ids, so no
-//      scan is needed).
-//   2. k_walk: workgroup (slice, part) zeroes the slice's f64 accumulators in
-//      LDS, walks the segments of its part's tiles (one wave per segment,
+//      scan is needed).  Per-(bin, tile) counts are stored bin-major, and
+//      each bin's total is accumulated.
+//   2. k_walk: G walk workgroups are dealt out to the bins in proportion to
+//      their entries (every non-empty bin gets at least one: P_b = 1 +
+//      E_b (G - nonempty) / T), so every workgroup walks about T / G entries
+//      however the occupancy loads individual slices.  Part j of bin b's P_b
+//      walks tiles j, j + P_b, j + 2 P_b, ...: it zeroes the slice's f64
+//      accumulators in LDS, walks the segments (one wave per segment,
 //      gathering the sample's position and feature gradient), adds the
 //      contributions of the corners inside the slice with ds_add_f64, and
-//      writes the slice to its partial buffer (f32, plain coalesced stores).
-//   3. k_sum: every table row sums its slice's partials in a fixed order.
+//      writes the slice to its f32 image (one per workgroup).
+//   3. k_sum: every table row sums its bin's P_b images in a fixed order.
 //
 // Slices are 2^shift rows of one level (8192 rows x 2 channels x f64 =
-// 128 KiB of LDS).  The walk is XCD-aware: the tiles are cut into 8
-// contiguous ranges, one per XCD, and every slice gets workgroups on every
-// XCD, so a sample's position and gradient are only ever read through one
-// XCD's L2.  Levels with fewer slices get more workgroups per slice, so every
-// level gets about the same number of workgroups.
-// Products w * g are formed in f64 (exact) and summed in f64; the result is
-// the f64 sum rounded to f32 once.  Deterministic up to the f64 summation
-// order of the LDS atomics.
+// 128 KiB of LDS, one walk workgroup per CU at a time; G = 4 per CU).
+// Measured on gfx950 (tools/walk_trace.py): the walk is bound by per-entry
+// issue and gather latency, not by the LDS atomics (removing all of them
+// gained 6 %); an XCD-local tile split bought nothing (the same per-entry
+// rate without it) while piling a hot slice's entries onto few workgroups;
+// and lanes must stay on nearby samples (one wave per tile segment, short
+// runs per lane): equal long runs per thread cost 1.8x per entry.
+// Products w * g are formed in f64 (exact) and summed in f64; each image is
+// rounded to f32 once and the images are added in a fixed order (the
+// reference: f16 / f32 global atomics in arbitrary order).
 #include "grid_common.h"
 
 #include <type_traits>
@@ -39,80 +43,105 @@ namespace gb {
 using ge::Levels;
 using ge::LevelCtx;
 using ge::SliceDyn;
+typedef unsigned long long u64;
 
-constexpr uint32_t kTile = 1024;     // samples per binning tile (ids per segment)
-constexpr uint32_t kMaxBins = 1024;
-constexpr uint32_t kLdsBytes = 160 * 1024;
-
-constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, workgroup i dispatched to XCD i % 8
+constexpr uint32_t kTile = 1024;              // samples per binning tile (ids per segment)
+constexpr uint32_t kMaxBins = 4096;
+constexpr uint32_t kMaxSlices = 128;          // slices per level (k_bin's 128-bit masks)
+constexpr uint32_t kSliceBytes = 128 * 1024;  // f64 accumulators of one walk workgroup
+constexpr uint32_t kTotSplit = 16;            // bin totals as 16 partial sums (tile % 16)
 
 struct BinInfo {
-    uint32_t L, nbins, shift, nslots;
+    uint32_t L, nbins, shift, tcap;      // tcap: tiles of the capacity (counts row stride)
+    uint32_t G;                          // walk workgroups
+    uint32_t o_totals, o_plan;           // word offsets into `counts` (layout below)
     uint32_t bin0[ge::kMaxLevels + 1];   // first bin of level l (bin0[L] = nbins)
-    uint32_t parts[ge::kMaxLevels];      // walk workgroups per slice of level l (kXcds * q)
-    uint32_t q[ge::kMaxLevels];          // ... of which on one XCD
-    uint32_t slot0[ge::kMaxLevels + 1];  // first per-XCD work slot of level l
     uint32_t base[ge::kMaxLevels];       // first row of level l
     uint32_t rows[ge::kMaxLevels];       // rows of level l
-    uint64_t pbase[ge::kMaxLevels];      // first partial float of level l
+    uint64_t *trace;                     // debug: per-workgroup walk timeline (null: off)
 };
+
+static uint64_t *g_walk_trace = nullptr;  // set by dfhip_debug_walk_trace (tools only)
 
 static uint32_t slice_shift(uint32_t C) {
     uint32_t shift = 0;
-    while ((2ull << shift) * 8ull * C <= kLdsBytes) ++shift;
-    return shift;  // largest 2^shift rows with 2^shift * C doubles <= LDS
+    while ((2ull << shift) * 8ull * C <= kSliceBytes) ++shift;
+    return shift;  // largest 2^shift rows with 2^shift * C doubles <= kSliceBytes
 }
 
-// Host: bins / parts / partial layout from the HOST copy of the offsets.
-static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint32_t cus,
+static uint32_t device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            v > 0)
+            cus = v;
+        else
+            cus = 256;
+    }
+    return (uint32_t)cus;
+}
+
+// scratch layout (u32 words of `counts`):
+//   [tcap][nbins]  per-(tile, bin) counts          (k_bin)
+//   [nbins][16]    totals, as 16 partial sums      (k_bin; zeroed before it)
+//   [nbins][2]     first image slot, parts         (k_walk; zeroed before k_bin)
+// Host: bins and layout from the HOST copy of the offsets.
+static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint32_t cap,
                       BinInfo &bi) {
-    if (L == 0 || L > ge::kMaxLevels) return false;
+    if (L == 0 || L > ge::kMaxLevels || C == 0) return false;
     bi.L = L;
+    bi.trace = g_walk_trace;
     bi.shift = slice_shift(C);
-    uint32_t nb = 0, maxslices = 1;
+    bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, kTile);
+    bi.G = 4 * device_cus();
+    uint32_t nb = 0;
     for (uint32_t l = 0; l < L; ++l) {
         const uint32_t rows = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
         const uint32_t ns = rows ? ((rows - 1) >> bi.shift) + 1 : 0;
-        if (ns > 64) return false;  // slice masks are 64-bit
+        if (ns > kMaxSlices) return false;
         bi.bin0[l] = nb;
         bi.base[l] = (uint32_t)offsets_host[l];
         bi.rows[l] = rows;
         nb += ns;
-        if (ns > maxslices) maxslices = ns;
     }
     bi.bin0[L] = nb;
     bi.nbins = nb;
     if (nb == 0 || nb > kMaxBins) return false;
-    // XCD-aware walk: XCD x owns the x-th contiguous eighth of the tiles, so
-    // each sample's position / gradient is read by the workgroups of one XCD
-    // only (its L2).  Per XCD, each slice of level l gets q_l workgroups, q_l
-    // chosen so that every level gets about 4 * CUs / L workgroups in total
-    // (2 * CUs / L left the coarse levels' long walks as the tail: +4 %).
-    const uint32_t per_level = (4u * cus + L - 1) / L;
-    (void)maxslices;
-    uint64_t pf = 0;
-    uint32_t slots = 0;
-    for (uint32_t l = 0; l < L; ++l) {
-        const uint32_t ns = bi.bin0[l + 1] - bi.bin0[l];
-        uint32_t q = ns ? per_level / (kXcds * ns) : 1;
-        if (q < 1) q = 1;
-        if (q > 16) q = 16;
-        bi.q[l] = q;
-        bi.parts[l] = kXcds * q;
-        bi.slot0[l] = slots;
-        slots += ns * q;
-        bi.pbase[l] = pf;
-        pf += (uint64_t)ns * bi.parts[l] * (1ull << bi.shift) * C;
-    }
-    bi.slot0[L] = slots;
-    bi.nslots = slots;
+    if (bi.G < nb) bi.G = nb;  // every bin can get a workgroup
+    const uint64_t tot = (uint64_t)nb * bi.tcap;
+    if (tot + (kTotSplit + 2ull) * nb >= (1ull << 32)) return false;
+    bi.o_totals = (uint32_t)tot;
+    bi.o_plan = bi.o_totals + nb * kTotSplit;
     return true;
 }
+static uint64_t counts_words(const BinInfo &bi) { return (uint64_t)bi.o_plan + 2ull * bi.nbins; }
 
+__device__ __forceinline__ uint32_t bin_total(const uint32_t *__restrict__ totals, uint32_t b) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(totals + (size_t)b * kTotSplit);
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kTotSplit / 4; ++i) {
+        const uint4 v = p[i];
+        t += v.x + v.y + v.z + v.w;
+    }
+    return t;
+}
 static uint64_t partial_floats(const BinInfo &bi, uint32_t C) {
-    const uint32_t l = bi.L - 1;
-    return bi.pbase[l] + (uint64_t)(bi.bin0[l + 1] - bi.bin0[l]) * bi.parts[l] *
-                             (1ull << bi.shift) * C;
+    return (uint64_t)bi.G * ((uint64_t)1 << bi.shift) * C;
+}
+
+// Exclusive prefix over a wave (64 lanes) and the wave total.
+__device__ __forceinline__ u64 wave_excl_scan(u64 v, uint32_t lane, u64 *total) {
+    u64 inc = v;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const u64 u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+    }
+    *total = __shfl(inc, 63, 64);
+    return inc - v;
 }
 
 // Cell and fractional position of x at level c (gridencoder.cu:146-154).
@@ -139,17 +168,40 @@ __device__ __forceinline__ bool load_pos(const float *__restrict__ inputs, const
     return !oob;  // out-of-bounds samples contribute nothing (gridencoder.cu:253-258)
 }
 
-// Slices (bits) touched by the corners of a cell at one level.
-template <uint32_t D, int MODE>
-__device__ __forceinline__ uint64_t slice_mask(const ge::LevelRows &lr, const uint32_t cell[D],
-                                               uint32_t shift) {
-    uint64_t mask = 0;
+// Slices touched by the corners of a cell at one level, as a bit mask of
+// W words (W = 1 for levels of at most 64 slices, else 2).
+template <uint32_t D, int MODE, uint32_t W>
+__device__ __forceinline__ void slice_mask(const ge::LevelRows &lr, const uint32_t cell[D],
+                                           uint32_t shift, uint64_t (&mask)[W]) {
+#pragma unroll
+    for (uint32_t h = 0; h < W; ++h) mask[h] = 0;
 #pragma unroll
     for (uint32_t k = 0; k < (1u << D); ++k) {
         if (k >> lr.lead) continue;
-        mask |= 1ull << (ge::corner_row_m<D, MODE>(lr, cell, k) >> shift);
+        const uint32_t v = ge::corner_row_m<D, MODE>(lr, cell, k) >> shift;
+        if constexpr (W == 1) {
+            mask[0] |= 1ull << v;
+        } else {
+            if (v < 64) mask[0] |= 1ull << v;
+            else mask[1] |= 1ull << (v - 64);
+        }
     }
-    return mask;
+}
+
+// Append sample s (tile-relative id) to the segments of the slices in mask.
+template <uint32_t W>
+__device__ __forceinline__ void append(const uint64_t (&mask)[W], uint32_t b0, uint32_t *cnt,
+                                       uint16_t *seg, uint16_t id) {
+#pragma unroll
+    for (uint32_t h = 0; h < W; ++h) {
+        uint64_t mk = mask[h];
+        while (mk) {
+            const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mk) + 64u * h;
+            mk &= mk - 1;
+            const uint32_t slot = atomicAdd(&cnt[b], 1u);
+            seg[(size_t)b * kTile + slot] = id;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- 1. binning
@@ -179,23 +231,30 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
                 uint32_t cell[D];
                 float frac[D];
                 locate<D>(c, align, x, cell, frac);
-                uint64_t mask = 0;
                 const int mode = ge::row_mode(lr);
-                if (mode == 0) mask = slice_mask<D, 0>(lr, cell, bi.shift);
-                else if (mode == 1) mask = slice_mask<D, 1>(lr, cell, bi.shift);
-                else mask = slice_mask<D, 2>(lr, cell, bi.shift);
                 const uint32_t b0 = bi.bin0[l];
-                while (mask) {
-                    const uint32_t k = (uint32_t)__builtin_ctzll(mask);
-                    mask &= mask - 1;
-                    const uint32_t b = b0 + k;
-                    const uint32_t slot = atomicAdd(&cnt[b], 1u);
-                    seg[(size_t)b * kTile + slot] = (uint16_t)(s - tile * kTile);
+                const uint16_t id = (uint16_t)(s - tile * kTile);
+                if (bi.bin0[l + 1] - b0 <= 64) {  // uniform: one mask word
+                    uint64_t mask[1];
+                    if (mode == 0) slice_mask<D, 0, 1>(lr, cell, bi.shift, mask);
+                    else if (mode == 1) slice_mask<D, 1, 1>(lr, cell, bi.shift, mask);
+                    else slice_mask<D, 2, 1>(lr, cell, bi.shift, mask);
+                    append<1>(mask, b0, cnt, seg, id);
+                } else {
+                    uint64_t mask[2];
+                    if (mode == 0) slice_mask<D, 0, 2>(lr, cell, bi.shift, mask);
+                    else if (mode == 1) slice_mask<D, 1, 2>(lr, cell, bi.shift, mask);
+                    else slice_mask<D, 2, 2>(lr, cell, bi.shift, mask);
+                    append<2>(mask, b0, cnt, seg, id);
                 }
             }
         }
         __syncthreads();
-        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(size_t)tile * nb + b] = cnt[b];
+        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+            const uint32_t v = cnt[b];
+            counts[(size_t)tile * nb + b] = v;
+            if (v) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], v);
+        }
         __syncthreads();
     }
 }
@@ -207,14 +266,20 @@ __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, c
                                         const ge::LevelRows &lr, const uint32_t cell[D],
                                         const double (&cw)[1u << D][C]);
 
-template <uint32_t D, uint32_t C>
+constexpr int kModeAny = 3;  // MODE: the corner-row wrap fixed at compile time, or any
+
+template <uint32_t D, uint32_t C, int MODE>
 __device__ __forceinline__ void flush(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
                                       const ge::LevelRows &lr, const uint32_t cell[D],
                                       const double (&cw)[1u << D][C]) {
-    const int mode = ge::row_mode(lr);  // uniform: one scalar branch per flush
-    if (mode == 0) flush_m<D, C, 0>(acc, r0, r1, c, lr, cell, cw);
-    else if (mode == 1) flush_m<D, C, 1>(acc, r0, r1, c, lr, cell, cw);
-    else flush_m<D, C, 2>(acc, r0, r1, c, lr, cell, cw);
+    if constexpr (MODE != kModeAny) {
+        flush_m<D, C, MODE>(acc, r0, r1, c, lr, cell, cw);
+    } else {
+        const int mode = ge::row_mode(lr);  // uniform: one scalar branch per flush
+        if (mode == 0) flush_m<D, C, 0>(acc, r0, r1, c, lr, cell, cw);
+        else if (mode == 1) flush_m<D, C, 1>(acc, r0, r1, c, lr, cell, cw);
+        else flush_m<D, C, 2>(acc, r0, r1, c, lr, cell, cw);
+    }
 }
 
 template <uint32_t D, uint32_t C, int MODE>
@@ -276,25 +341,62 @@ __device__ __forceinline__ void load_grad(const grad_t *__restrict__ p, float (&
 // LDS atomic instruction rarely has two lanes on a row, and along its run a
 // lane merges consecutive contributions to the same cell in registers (at the
 // coarse levels a cell spans tens of samples of a ray).
-template <typename grad_t, uint32_t D, uint32_t C, bool POW2>
+template <typename grad_t, uint32_t D, uint32_t C, bool POW2, int MODE>
 __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad,  // [L, B, C]
                                                const float *__restrict__ inputs,
                                                const int32_t *__restrict__ offsets, Levels lv,
                                                BinInfo bi, uint32_t gridtype, int align_corners,
                                                SliceDyn dyn, float inv, uint32_t B,
-                                               const uint32_t *__restrict__ counts,
+                                               uint32_t *counts,
                                                const uint16_t *__restrict__ entries,
                                                float *__restrict__ partial) {
     extern __shared__ double acc[];
-    // workgroup -> (XCD x, slot) -> (level, slice k, sub-part q)
-    const uint32_t x = blockIdx.x % kXcds, slot = blockIdx.x / kXcds;
+    __shared__ uint32_t sh_b, sh_j, sh_p;
+    __shared__ uint32_t n_seen;
+    uint64_t tr0 = 0;
+    if (bi.trace) tr0 = wall_clock64();
+    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
+    const uint32_t *totals = counts + bi.o_totals;
+    if (threadIdx.x < 64) {  // plan (wave 0): this workgroup's bin b and part j of P_b
+        const uint32_t ln = threadIdx.x;
+        u64 T = 0, nz = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t e = b0 + ln < nb ? bin_total(totals, b0 + ln) : 0u;
+            u64 t, z;
+            (void)wave_excl_scan(e, ln, &t);
+            (void)wave_excl_scan(e ? 1u : 0u, ln, &z);
+            T += t;
+            nz += z;
+        }
+        const u64 extra = G > nz ? G - nz : 0;
+        uint32_t carry = 0;
+        if (ln == 0) sh_p = 0;  // none: an idle workgroup
+        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t b = b0 + ln;
+            const uint32_t e = b < nb ? bin_total(totals, b) : 0u;
+            const uint32_t p = e ? 1u + (uint32_t)((u64)e * extra / (T ? T : 1)) : 0u;
+            u64 tot;
+            const uint32_t s = carry + (uint32_t)wave_excl_scan(p, ln, &tot);
+            if (b < nb && p && slot >= s && slot < s + p) {
+                sh_b = b;
+                sh_j = slot - s;
+                sh_p = p;
+            }
+            if (b < nb && p && slot == s) {  // part 0 records the bin's images for k_sum
+                counts[bi.o_plan + 2 * b] = s;
+                counts[bi.o_plan + 2 * b + 1] = p;
+            }
+            carry += (uint32_t)tot;
+        }
+        if (ln == 0) n_seen = 0;
+    }
+    __syncthreads();
+    const uint32_t P = sh_p;
+    if (P == 0) return;  // uniform: more workgroups than parts
+    const uint32_t b = sh_b, part = sh_j;
     uint32_t l = 0;
-    while (l + 1 < bi.L && bi.slot0[l + 1] <= slot) ++l;
-    const uint32_t Q = bi.q[l];
-    const uint32_t k = (slot - bi.slot0[l]) / Q, q = (slot - bi.slot0[l]) - k * Q;
-    const uint32_t b = bi.bin0[l] + k;
-    const uint32_t P = bi.parts[l];
-    const uint32_t part = x * Q + q;
+    while (l + 1 < bi.L && bi.bin0[l + 1] <= b) ++l;
+    const uint32_t k = b - bi.bin0[l];
     const uint32_t srows = 1u << bi.shift;
     const uint32_t r0 = bi.base[l] + (k << bi.shift);
     const uint32_t r1 = min(r0 + srows, bi.base[l] + bi.rows[l]);
@@ -307,15 +409,12 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     const uint32_t lead = lr.lead;
     const uint32_t M = ge::dyn_count(dyn, B);
     const uint32_t ntiles = ceil_div(M, kTile);
-    const uint32_t nb = bi.nbins;
     const grad_t *gl = grad + (size_t)l * B * C;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
-    // XCD x: tiles [t0, t1); sub-part q: t0 + q, t0 + q + Q, ...; wave w takes
-    // every waves-th of those
-    const uint32_t t0 = (uint32_t)(((uint64_t)ntiles * x) / kXcds);
-    const uint32_t t1 = (uint32_t)(((uint64_t)ntiles * (x + 1)) / kXcds);
-    for (uint32_t t = t0 + q + Q * wave; t < t1; t += Q * waves) {
+    // part j of P: tiles j, j + P, ...; wave w takes every waves-th of those
+    for (uint32_t t = part + P * wave; t < ntiles; t += P * waves) {
         const uint32_t cnt = counts[(size_t)t * nb + b];
+        if (bi.trace && lane == 0) atomicAdd(&n_seen, cnt);
         const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile;
         const uint32_t tbase = t * kTile;
         const uint32_t Q = (cnt + 63) >> 6;
@@ -357,7 +456,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                         for (uint32_t d = 0; d < D; ++d)
                             if (d < lead) same = same && (cell[d] == cur[d]);
                         if (!same) {
-                            if (have) flush<D, C>(acc, r0, r1, c, lr, cur, cw);
+                            if (have) flush<D, C, MODE>(acc, r0, r1, c, lr, cur, cw);
 #pragma unroll
                             for (uint32_t kc = 0; kc < (1u << D); ++kc)
 #pragma unroll
@@ -389,75 +488,109 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
             walk(std::integral_constant<uint32_t, 1>{});
         else
             walk(std::integral_constant<uint32_t, kRun>{});
-        if (have) flush<D, C>(acc, r0, r1, c, lr, cur, cw);
+        if (have) flush<D, C, MODE>(acc, r0, r1, c, lr, cur, cw);
     }
     __syncthreads();
-    float *out = partial + bi.pbase[l] + ((size_t)k * P + part) * ((size_t)srows * C);
+    float *out = partial + (size_t)slot * ((size_t)srows * C);
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = (float)acc[i];
+    if (bi.trace) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t *r = bi.trace + (size_t)blockIdx.x * 8;
+            r[0] = b;
+            r[1] = b + 1;
+            r[2] = P;
+            r[3] = n_seen;
+            r[4] = tr0;
+            r[5] = tr0;
+            r[6] = part;
+            r[7] = wall_clock64();
+        }
+    }
 }
 
 // ---------------------------------------------------------------- 3. sum
+// Every (row, channel) of the table sums its bin's P_b images (slots
+// S_b .. S_b + P_b - 1, recorded by k_walk) in order.
 template <typename out_t>
 __global__ __launch_bounds__(256) void k_sum(const float *__restrict__ partial, BinInfo bi,
                                              uint32_t C, uint32_t total_rows,
+                                             const uint32_t *__restrict__ counts,
                                              out_t *__restrict__ out, int accumulate) {
-    const uint64_t n = (uint64_t)total_rows * C;
     const uint32_t srows = 1u << bi.shift;
+    const size_t img = (size_t)srows * C;
+    const uint64_t n = (uint64_t)total_rows * C;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t row = (uint32_t)(i / C), ch = (uint32_t)(i - (uint64_t)row * C);
         uint32_t l = 0;
         while (l + 1 < bi.L && bi.base[l + 1] <= row) ++l;
         const uint32_t rel = row - bi.base[l];
-        const uint32_t k = rel >> bi.shift, off = rel & (srows - 1);
-        const uint32_t P = bi.parts[l];
-        const float *src = partial + bi.pbase[l] + (size_t)k * P * srows * C + (size_t)off * C + ch;
-        float s = accumulate ? (float)out[i] : 0.0f;
+        const uint32_t b = bi.bin0[l] + (rel >> bi.shift);
+        const uint32_t S = counts[bi.o_plan + 2 * b], P = counts[bi.o_plan + 2 * b + 1];
+        const float *src = partial + (size_t)S * img + (size_t)(rel & (srows - 1)) * C + ch;
         double t = 0.0;
         uint32_t p = 0;
         for (; p + 4 <= P; p += 4) {  // parts added in order, four loads in flight
-            float x[4];
+            float v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) x[u] = src[(size_t)(p + u) * srows * C];
+            for (int u = 0; u < 4; ++u) v[u] = src[(size_t)(p + u) * img];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) t += (double)x[u];
+            for (int u = 0; u < 4; ++u) t += (double)v[u];
         }
-        for (; p < P; ++p) t += (double)src[(size_t)p * srows * C];
+        for (; p < P; ++p) t += (double)src[(size_t)p * img];
+        const float s = accumulate ? (float)out[i] : 0.0f;
         out[i] = (out_t)(s + (float)t);
     }
 }
 
-static uint32_t device_cus() {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            v > 0)
-            cus = v;
-        else
-            cus = 256;
+// Corner-row wrap mode shared by every level (0 mask, 1 modulo, 2 hash; the
+// host restatement of ge::level_ctx / level_rows / row_mode), or kModeAny.
+static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t L, uint32_t D,
+                        uint32_t gridtype, bool align) {
+    int mode = -1;
+    for (uint32_t l = 0; l < L; ++l) {
+        const uint64_t hsize = (uint64_t)(offsets_host[l + 1] - offsets_host[l]);
+        const uint64_t smul = align ? lv.res[l] : lv.res[l] + 1u;
+        uint64_t stride = 1, span = 1;
+        for (uint32_t d = 0; d < D; ++d) {
+            if (stride <= hsize) {
+                stride *= smul;
+                span *= smul;
+            }
+        }
+        const bool hashed = gridtype == 0 && stride > hsize;
+        const bool pow2 = (hsize & (hsize - 1)) == 0;
+        const bool modulo = !pow2 && (hashed || span > hsize);
+        const int m = hashed ? 2 : (modulo ? 1 : 0);
+        if (mode < 0) mode = m;
+        else if (mode != m) return kModeAny;
     }
-    return (uint32_t)cus;
+    return mode == 0 ? 0 : kModeAny;  // only the mask form is specialised
 }
 
 template <typename grad_t, uint32_t C>
-static void launch_walk(hipStream_t s, dim3 g, size_t lds, const grad_t *grad,
-                        const float *inputs, const int32_t *offsets, const Levels &lv,
+static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const float *inputs,
+                        const int32_t *offsets, const int32_t *offsets_host, const Levels &lv,
                         const BinInfo &bi, uint32_t gridtype, int align, SliceDyn dyn,
-                        uint32_t B, const uint32_t *counts, const uint16_t *entries,
-                        float *partial) {
+                        uint32_t B, uint32_t *counts, const uint16_t *entries, float *partial) {
     const bool pow2 = ge::dyn_pow2(dyn.bound);
     const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-    auto kern = pow2 ? k_walk<grad_t, 3, C, true> : k_walk<grad_t, 3, C, false>;
-    static bool attr[2] = {false, false};
-    if (!attr[pow2]) {
-        (void)hipFuncSetAttribute((const void *)kern,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
-        attr[pow2] = true;
+    const bool m0 = uniform_mode(offsets_host, lv, bi.L, 3, gridtype, align != 0) == 0;
+    typedef void (*walk_fn)(const grad_t *, const float *, const int32_t *, Levels, BinInfo,
+                            uint32_t, int, SliceDyn, float, uint32_t, uint32_t *,
+                            const uint16_t *, float *);
+    walk_fn kern;
+    if (pow2) kern = m0 ? k_walk<grad_t, 3, C, true, 0> : k_walk<grad_t, 3, C, true, kModeAny>;
+    else kern = m0 ? k_walk<grad_t, 3, C, false, 0> : k_walk<grad_t, 3, C, false, kModeAny>;
+    static bool attr[2][2] = {{false, false}, {false, false}};
+    if (!attr[pow2][m0]) {
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kSliceBytes);
+        attr[pow2][m0] = true;
     }
-    kern<<<g, 1024, lds, s>>>(grad, inputs, offsets, lv, bi, gridtype, align, dyn, inv, B,
-                              counts, entries, partial);
+    kern<<<bi.G, 1024, lds, s>>>(grad, inputs, offsets, lv, bi, gridtype, align, dyn, inv, B,
+                                 counts, entries, partial);
 }
 
 }  // namespace gb
@@ -465,18 +598,25 @@ static void launch_walk(hipStream_t s, dim3 g, size_t lds, const grad_t *grad,
 
 using namespace dfhip;
 
+// Debug: per-workgroup walk timeline {first bin, end bin, 0, entries, t0,
+// t_planned, range start, t_end} (wall clock ticks) into `trace` (8 u64 per
+// walk workgroup); null turns it off.  Used by tools/walk_trace.py only.
+extern "C" int dfhip_debug_walk_trace(uint64_t *trace) {
+    gb::g_walk_trace = trace;
+    return DFHIP_OK;
+}
+
 extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host,
                                                   uint32_t L, uint32_t C, uint64_t *entries_u32,
                                                   uint64_t *counts_u32, uint64_t *partial_f32) {
     gb::BinInfo bi;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, gb::device_cus(), bi)) {
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, bi)) {
         set_error("grid_backward_binned_scratch: unsupported level layout");
         return DFHIP_EINVAL;
     }
-    const uint64_t tiles = ceil_div<uint64_t>(cap ? cap : 1, gb::kTile);
     // tile-relative sample ids, u16 (kTile <= 65536), counted in u32 words
-    if (entries_u32) *entries_u32 = (tiles * bi.nbins * gb::kTile + 1) / 2;
-    if (counts_u32) *counts_u32 = tiles * bi.nbins;
+    if (entries_u32) *entries_u32 = ((uint64_t)bi.tcap * bi.nbins * gb::kTile + 1) / 2;
+    if (counts_u32) *counts_u32 = gb::counts_words(bi);
     if (partial_f32) *partial_f32 = gb::partial_floats(bi, C);
     return DFHIP_OK;
 }
@@ -497,7 +637,7 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
         return DFHIP_EINVAL;
     }
     gb::BinInfo bi;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, gb::device_cus(), bi)) {
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, B, bi)) {
         set_error("%s: unsupported level layout", name);
         return DFHIP_EINVAL;
     }
@@ -509,18 +649,19 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
         set_error("%s: grad dtype must be f16 or f32", name);
         return DFHIP_EDTYPE;
     }
+    if (B > 0 && (!grad_lbc || !inputs)) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
     hipStream_t s = as_stream(stream);
-    const uint32_t total_rows = (uint32_t)offsets_host[L];
     const ge::Levels lv = ge::make_levels(L, S, H);
     const ge::SliceDyn dyn{m_dev, bound};
-    if (B > 0) {
-        if (!grad_lbc || !inputs) {
-            set_error("%s: null pointer", name);
-            return DFHIP_EINVAL;
-        }
-        const uint32_t tiles = ceil_div(B, gb::kTile);
-        const uint32_t gbin = tiles < 4096u ? tiles : 4096u;
-        if (phase & 1) {
+    if (phase & 1) {
+        // totals (k_bin adds) and the plan (k_walk sets; P = 0: no images)
+        (void)hipMemsetAsync(counts + bi.o_totals, 0,
+                             (size_t)bi.nbins * (gb::kTotSplit + 2) * sizeof(uint32_t), s);
+        if (B > 0) {
+            const uint32_t gbin = bi.tcap < 4096u ? bi.tcap : 4096u;
             const bool pow2 = ge::dyn_pow2(dyn.bound);
             const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
             if (pow2)
@@ -532,25 +673,27 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
                                                           align_corners, dyn, inv, B, counts,
                                                           (uint16_t *)entries);
         }
-        if (!(phase & 2)) return check_launch(name);
-        const dim3 g(gb::kXcds * bi.nslots);
+    }
+    if (!(phase & 2)) return check_launch(name);
+    if (B > 0) {
         const size_t lds = ((size_t)1 << bi.shift) * C * sizeof(double);
-#define DFHIP_WALK(GT, CC)                                                                      \
-    gb::launch_walk<GT, CC>(s, g, lds, (const GT *)grad_lbc, inputs, offsets, lv, bi, gridtype, \
-                            align_corners, dyn, B, counts, (const uint16_t *)entries, partial)
+#define DFHIP_WALK(GT, CC)                                                                    \
+    gb::launch_walk<GT, CC>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
+                            bi, gridtype, align_corners, dyn, B, counts,                     \
+                            (const uint16_t *)entries, partial)
         if (grad_dtype == DFHIP_F16) {
             if (C == 1) DFHIP_WALK(half_t, 1); else if (C == 2) DFHIP_WALK(half_t, 2); else DFHIP_WALK(half_t, 4);
         } else {
             if (C == 1) DFHIP_WALK(float, 1); else if (C == 2) DFHIP_WALK(float, 2); else DFHIP_WALK(float, 4);
         }
 #undef DFHIP_WALK
-    } else {
-        if (!(phase & 2)) return DFHIP_OK;
-        (void)hipMemsetAsync(partial, 0, gb::partial_floats(bi, C) * sizeof(float), s);
     }
+    // every row is written: rows of bins no walk touched get zero (or keep
+    // their value when accumulating)
+    const uint32_t total_rows = (uint32_t)offsets_host[L];
     const uint64_t want = ceil_div<uint64_t>((uint64_t)total_rows * C, 256);
     gb::k_sum<float><<<(uint32_t)(want < 4096 ? want : 4096), 256, 0, s>>>(
-        partial, bi, C, total_rows, grad_embeddings, accumulate);
+        partial, bi, C, total_rows, counts, grad_embeddings, accumulate);
     return check_launch(name);
 }
 

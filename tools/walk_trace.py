@@ -1,0 +1,97 @@
+"""Per-workgroup timeline of the binned grid backward's walk (k_walk) on the
+samples of a real 128x128 march: which levels' workgroups take how long, how
+many entries each walks, and how the launch's span splits into zeroing,
+walking and write-out.  python tools/walk_trace.py [--reps 3]"""
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (str(ROOT), str(ROOT / "single-stable-dreamfusion_amd"), str(ROOT / "tests"),
+          str(ROOT / "tools")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--radius", type=float, default=0.56)
+    args = ap.parse_args()
+    import _dfhip
+    import _gridencoder
+    import raymarching
+    from gridencoder.grid import level_offsets
+    from scenes import march_inputs
+    lib = _dfhip.load()
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    rays_o, rays_d, nears, fars, _, bf = march_inputs(128, 128, seed=0, radius=args.radius,
+                                                      noise=0.0)
+    o, d, ne, fa, b = map(T, (rays_o, rays_d, nears, fars, bf))
+    counter = torch.zeros(2, dtype=torch.int32, device=dev)
+    xyzs, _, _, _ = raymarching.march_rays_train(o, d, 1.0, b, 1, 128, ne, fa, counter, -1, True,
+                                                 128, True, 0.0, 512)
+    B = xyzs.shape[0]
+    x01 = ((xyzs + 1) / 2).contiguous()
+    pls = np.exp2(np.log2(2048 / 16) / 15)
+    S = float(np.log2(pls))
+    offs = level_offsets(16, 2, 3, 16, pls, 16, False).astype(np.int32)
+    L = 16
+    g = (torch.randn(L, B, 2, device=dev) * 0.01).half()
+    gemb = torch.empty(int(offs[-1]), 2, device=dev)
+    ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2)
+    ent = torch.empty(ne_, dtype=torch.int32, device=dev)
+    cnt = torch.empty(nc, dtype=torch.int32, device=dev)
+    part = torch.empty(npf, device=dev)
+    ot = T(offs)
+    trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
+    lib.dfhip_debug_walk_trace.argtypes = [ctypes.c_void_p]
+    for rep in range(args.reps + 1):
+        trace.zero_()
+        lib.dfhip_debug_walk_trace(trace.data_ptr())
+        _gridencoder.grid_encode_backward_binned(g, x01, 0.0, ot, offs, gemb, B, None, 3, 2, L,
+                                                 S, 16, 1, False, ent, cnt, part)
+        lib.dfhip_debug_walk_trace(None)
+        torch.cuda.synchronize()
+    report(trace, B, L, offs)
+
+
+def report(trace, B, L, offs=None, shift=13):
+    tr = trace.view(-1, 8).cpu().numpy()
+    tr = tr[tr[:, 7] != 0]
+    t0 = tr[:, 4].min()
+    us = lambda v: (v - t0) / 100.0  # noqa: E731  wall clock: 100 MHz
+    span = us(tr[:, 7].max())
+    dur = (tr[:, 7] - tr[:, 4]) / 100.0
+    plan = (tr[:, 5] - tr[:, 4]) / 100.0
+    print(f"B={B} walk workgroups={len(tr)} span={span:.1f} us")
+    print(f"workgroup duration mean {dur.mean():.1f} max {dur.max():.1f} min {dur.min():.1f} us; "
+          f"plan mean {plan.mean():.2f} us; start max {us(tr[:, 4]).max():.1f} us")
+    print(f"entries/workgroup mean {tr[:, 3].mean():.0f} max {tr[:, 3].max()}; "
+          f"bins/workgroup mean {(tr[:, 1] - tr[:, 0]).mean():.2f}")
+    order = np.argsort(-dur)[:8]
+    for i in order:
+        print(f"  slow wg: bins {tr[i, 0]}..{tr[i, 1] - 1} xcd {tr[i, 2]} entries {tr[i, 3]} "
+              f"dur {dur[i]:.1f} us")
+    ends = np.sort(us(tr[:, 7]))
+    print("end-time quantiles (us):", [round(float(np.quantile(ends, q)), 1)
+                                      for q in (0.1, 0.25, 0.5, 0.75, 0.9, 1.0)])
+    print(f"total entries {tr[:, 3].sum()} ({tr[:, 3].sum() / B:.2f} per sample)")
+    if offs is not None:  # per-level entry rate of single-bin workgroups
+        bin0 = [0]
+        for lv in range(L):
+            rows = int(offs[lv + 1] - offs[lv])
+            bin0.append(bin0[-1] + ((rows - 1) >> shift) + 1)
+        lvl = np.searchsorted(np.array(bin0), tr[:, 0], side="right") - 1
+        one = (tr[:, 1] - tr[:, 0]) == 1
+        print("level: entries/us per workgroup (single-bin workgroups)")
+        print("  " + "  ".join(f"{lv}:{(tr[one & (lvl == lv), 3] / dur[one & (lvl == lv)]).mean():.0f}"
+                               for lv in range(L) if (one & (lvl == lv)).any()))
+
+
+if __name__ == "__main__":
+    main()
