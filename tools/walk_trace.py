@@ -49,6 +49,8 @@ def main():
     part = torch.empty(npf, device=dev)
     ot = T(offs)
     trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
+    import os
+    win = os.environ.get("DFHIP_GRID_NOWIN") is None
     lib.dfhip_debug_walk_trace.argtypes = [ctypes.c_void_p]
     for rep in range(args.reps + 1):
         trace.zero_()
@@ -57,7 +59,7 @@ def main():
                                                  S, 16, 1, False, ent, cnt, part)
         lib.dfhip_debug_walk_trace(None)
         torch.cuda.synchronize()
-    report(trace, B, L, offs)
+    report(trace, B, L, offs, shift=0 if win else 13)
 
 
 def report(trace, B, L, offs=None, shift=13):
@@ -73,7 +75,7 @@ def report(trace, B, L, offs=None, shift=13):
           f"plan mean {plan.mean():.2f} us; start max {us(tr[:, 4]).max():.1f} us")
     print(f"entries/workgroup mean {tr[:, 3].mean():.0f} max {tr[:, 3].max()}; "
           f"bins/workgroup mean {(tr[:, 1] - tr[:, 0]).mean():.2f}")
-    order = np.argsort(-dur)[:8]
+    order = np.argsort(-dur)[:16]
     for i in order:
         print(f"  slow wg: bins {tr[i, 0]}..{tr[i, 1] - 1} xcd {tr[i, 2]} entries {tr[i, 3]} "
               f"dur {dur[i]:.1f} us")
@@ -81,7 +83,13 @@ def report(trace, B, L, offs=None, shift=13):
     print("end-time quantiles (us):", [round(float(np.quantile(ends, q)), 1)
                                       for q in (0.1, 0.25, 0.5, 0.75, 0.9, 1.0)])
     print(f"total entries {tr[:, 3].sum()} ({tr[:, 3].sum() / B:.2f} per sample)")
-    if offs is not None:  # per-level entry rate of single-bin workgroups
+    rate = {}
+    for i in range(len(tr)):
+        rate.setdefault(int(tr[i, 0]), []).append(tr[i, 3] / dur[i])
+    print("bin: mean entries/us over its workgroups (ascending, first 12)")
+    print("  " + "  ".join(f"{b}:{np.mean(v):.0f}" for b, v in
+                           sorted(rate.items(), key=lambda kv: np.mean(kv[1]))[:12]))
+    if offs is not None and shift:  # per-level entry rate of single-bin workgroups
         bin0 = [0]
         for lv in range(L):
             rows = int(offs[lv + 1] - offs[lv])
