@@ -62,6 +62,8 @@ def parse():
                    help="skip timing the textureless / lambertian steps")
     p.add_argument("--no-alt-backward", action="store_true",
                    help="skip timing the other backward structure (two-pass / fused)")
+    p.add_argument("--no-traffic", action="store_true",
+                   help="skip the live rocprofv3 PMC passes for roofline.traffic")
     p.add_argument("--launcher-selftest", action="store_true",
                    help="CPU/gloo check of the N-rank launch only (no GPU work)")
     return p.parse_args()
@@ -214,6 +216,31 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1)
     return out
 
 
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA
+
+
+def field_mlp_report(trainer):
+    """MFMA throughput of the fused field kernels of the train step (the
+    sigma MLP): the last step's fused forward (grid gather
+    + 32-64-64-4 MLP) and MLP backward re-launched eagerly and timed with
+    events.  Algorithmic FLOPs per field row: forward 2 x (32x64 + 64x64 +
+    64x4) = 12,800; backward 2 x that for the input and weight
+    gradients = 25,600 (the kernel's recompute of the forward is not
+    counted)."""
+    g = next(iter(trainer._graphs.values()), None) if getattr(trainer, "_graphs", None) else None
+    nat = getattr(g, "native", None)
+    if nat is None:
+        return None
+    fwd_us, bwd_us, rows = nat.time_field()
+    out = {"rows": rows}
+    for name, us, per in (("forward", fwd_us, 12800.0), ("backward", bwd_us, 25600.0)):
+        tf = per * rows / (us * 1e-6) / 1e12
+        out[name] = {"avg_us": round(us, 2), "flops_per_row": per,
+                     "mfma": {"achieved": round(tf, 2), "peak": MFMA_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TFLOPS, 5)}}
+    return out
+
+
 def summarize_kernels(records):
     torch.cuda.synchronize()
     per = {}
@@ -248,26 +275,60 @@ REGION_KERNELS = {
 }
 
 
-def load_pmc(name):
-    """Per-launch HBM bytes of timed region `name` (sum over its kernels) from
-    the committed rocprofv3 PMC summary (profiles/pmc_summary.json, made by
-    tools/gpu_pmc_bench.sh + tools/pmc_summary.py), or None."""
-    path = ROOT / "profiles" / "pmc_summary.json"
-    if not path.exists():
-        return None
-    try:
-        data = json.loads(path.read_text())
-    except ValueError:
-        return None
-    kernels = data.get("kernels", {})
-    total = 0
-    for pats in REGION_KERNELS.get(name, (name,)):
-        pats = (pats,) if isinstance(pats, str) else pats
-        hit = next((v for k, v in kernels.items() if any(p in k for p in pats)), None)
-        if hit is None:
-            return None  # a kernel of the region was not profiled
-        total += hit["hbm_bytes_per_dispatch"]
-    return total
+def measure_traffic(region, timeout=180):
+    """HBM bytes per launch of timed region `region`, measured now: two
+    rocprofv3 passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE, kernel-trace
+    only, each its own run, as MI355X_MICROARCH.md prescribes) over a short
+    child run of this same bench (3 + 3 steps, no extras).  FETCH_SIZE is
+    doubled (the gfx950 correction for wide reads; the guide leaves gathers
+    uncalibrated), both are KiB.  Returns (bytes or None, note)."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    import csv
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not on PATH"
+    child = [sys.executable, str(Path(__file__).resolve()), "--steps", "3", "--warmup", "3",
+             "--no-cpu-baseline", "--no-kernel-timing", "--no-alt-backward", "--no-shading",
+             "--no-infer", "--no-traffic"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
+    env["TMPDIR"] = "/tmp"
+    tmp = tempfile.mkdtemp(prefix="dfhip_pmc_", dir="/tmp")
+    pats = REGION_KERNELS.get(region, (region,))
+    per = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(tmp, counter)
+        cmd = [rp, "--kernel-trace", "--pmc", counter, "--output-format", "csv", "-d", d, "-o",
+               "run", "--"] + child
+        proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                env=env, start_new_session=True)
+        try:
+            rc = proc.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
+            proc.wait()
+            return None, f"{counter} pass timed out"
+        if rc != 0:
+            return None, f"{counter} pass exited {rc}"
+        sums = {}
+        for f in Path(d).rglob("*counter_collection.csv"):
+            for r in csv.DictReader(open(f)):
+                for i, alts in enumerate(pats):
+                    alts = (alts,) if isinstance(alts, str) else alts
+                    if any(a in r["Kernel_Name"] for a in alts):
+                        sums.setdefault(i, []).append(float(r["Counter_Value"]))
+        if len(sums) != len(pats):
+            return None, f"{counter}: not every kernel of {region} was profiled"
+        scale = 2.0 if counter == "FETCH_SIZE" else 1.0
+        per[counter] = sum(scale * 1024.0 * sum(v) / len(v) for v in sums.values())
+    shutil.rmtree(tmp, ignore_errors=True)
+    return int(per["FETCH_SIZE"] + per["WRITE_SIZE"]), (
+        "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs) of "
+        "a 3+3-step child bench; FETCH_SIZE x2 (gfx950), KiB -> bytes, summed over the region's "
+        "kernels, mean per launch")
 
 
 def _free_port():
@@ -400,11 +461,13 @@ def main():
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         kd = kernels[dom]
-        traffic = load_pmc(dom)
+        traffic, note = (None, "skipped (--no-traffic or N > 1)")
+        if world == 1 and not args.no_traffic:
+            traffic, note = measure_traffic(dom)
         result["roofline"] = {
             "kernel": dom, "bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
-            "traffic": traffic, "avg_us": kd["avg_us"],
+            "traffic": traffic, "traffic_source": note, "avg_us": kd["avg_us"],
             "bytes_per_launch": kd["bytes_per_launch"]}
         if dom == "grid_encode_backward":
             # the binned backward's real ceiling: one f64 LDS add per (sample,
@@ -419,6 +482,8 @@ def main():
         step_ms = result["ms_per_step"]
         result["kernel_share_of_step"] = {k: round(v["total_ms"] / args.steps / step_ms, 4)
                                           for k, v in kernels.items()}
+    if world == 1 and not args.no_kernel_timing:
+        result["field_mlp"] = field_mlp_report(trainer)
     if world == 1 and not args.no_alt_backward:
         # the other backward structure, same workload and launch mode: the
         # reference's two passes (sd.py:115 + utils.py:708) beside the fused

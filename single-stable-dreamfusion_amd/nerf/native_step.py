@@ -350,6 +350,40 @@ class NativeAlbedoStep:
             with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_dev, per):
                 self._emb_launch2()
 
+    def time_field(self, reps=5):
+        """Eager re-launches of the last step's fused field forward and MLP
+        backward on its own buffers (both overwrite their outputs), timed with
+        events on torch's current stream (the launch stream): average
+        microseconds of each and the live field rows.  Measurement only: the
+        step's results are unchanged."""
+        m = self.trainer.model
+        S, Hb, gridtype, align, _ = self.meta
+        from gridencoder.grid import _parts
+
+        def fwd():
+            _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table,
+                                         self.encoder.offsets, S, Hb, gridtype, align, self.mlp,
+                                         self.enc, self.sigma_field, self.albedo, self.m_field)
+
+        def bwd():
+            _fieldmlp.grid_field_backward(
+                self.enc, self.xyz_field, m.bound, self.mlp, self.grad_sigma_field,
+                self.grad_albedo, self.d_enc, self.mlp_partial, [p.grad for p in self.mlp],
+                self.encoder.offsets, self.rows, S, Hb, gridtype, align, None, None,
+                _parts(self.rows, self.C), self.m_field)
+
+        out = []
+        for fn in (fwd, bwd):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            out.append(e0.elapsed_time(e1) * 1e3 / reps)
+        return out[0], out[1], int(self.m_field.item())
+
     def reattach(self):
         for p, g in self.grads:
             p.grad = g
