@@ -62,6 +62,9 @@ def parse():
                    help="skip timing the textureless / lambertian steps")
     p.add_argument("--no-alt-backward", action="store_true",
                    help="skip timing the other backward structure (two-pass / fused)")
+    p.add_argument("--no-c5", action="store_true",
+                   help="skip the C5 leg (256x256 bf16 renderer step)")
+    p.add_argument("--c5-res", type=int, default=256)
     p.add_argument("--no-traffic", action="store_true",
                    help="skip the live rocprofv3 PMC passes for roofline.traffic")
     p.add_argument("--launcher-selftest", action="store_true",
@@ -69,7 +72,8 @@ def parse():
     return p.parse_args()
 
 
-def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False):
+def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False, bf16=False):
+    """bf16: BASELINE configs[4] (C5) — bf16 autocast, SD-2.1-base text width."""
     import main
     from nerf.network_grid import NeRFNetwork
     from nerf.provider import NeRFDataset
@@ -77,18 +81,22 @@ def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False):
     from nerf.utils import Trainer, make_adam, seed_everything
 
     opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res),
-                          "--guidance", "synthetic", "--seed", str(seed)])
+                          "--guidance", "synthetic", "--seed", str(seed)]
+                         + (["--bf16", "--sd_version", "2.1-base"] if bf16 else []))
     # identical model initialisation on every rank; per-rank RNG (cameras,
     # march noise, background, SDS draws) from here on
     seed_everything(seed)
     device = torch.device("cuda", torch.cuda.current_device())
     model = NeRFNetwork(opt)
     seed_everything(seed + rank)
-    guidance = SyntheticSDS(device) if mock_sds else InjectedSDS(device)
+    text_dim = 1024 if bf16 else 768
+    guidance = (SyntheticSDS(device, text_dim=text_dim) if mock_sds
+                else InjectedSDS(device, text_dim=text_dim))
     optimizer = lambda m: make_adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)  # noqa
     sched = lambda o: torch.optim.lr_scheduler.LambdaLR(o, lambda it: 0.1 ** min(it / opt.iters, 1))  # noqa
     trainer = Trainer("df", opt, model, guidance, device=device, workspace=None,
-                      optimizer=optimizer, ema_decay=None, fp16=True, lr_scheduler=sched,
+                      optimizer=optimizer, ema_decay=None, fp16=not bf16, bf16=bf16,
+                      lr_scheduler=sched,
                       use_checkpoint="scratch", scheduler_update_every_step=True,
                       local_rank=rank, world_size=world, mute=True, fused_backward=fused,
                       graph_step=graph)
@@ -216,6 +224,50 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1)
     return out
 
 
+def bench_c5(args, rank, world):
+    """BASELINE configs[4] (C5), renderer leg: the same train step at
+    c5_res x c5_res (65,536 rays) under bf16 autocast — bf16 table, features,
+    activations and colours (csrc/fieldmlp.hip bf16 instantiations on
+    v_mfma_f32_16x16x32_bf16), no GradScaler — graph-replayed, with the
+    injected w(t) N(0,1) guidance of SD-2.1-base's text width (1024); the
+    SD-2.1-base UNet / VAE cannot be loaded offline, so the full SDS step is
+    not timed."""
+    import _dfhip
+    tr, dat = make_trainer(args.c5_res, args.seed, rank, world, True, graph=not args.eager,
+                           mock_sds=args.mock_sds, bf16=True)
+    for _ in range(args.warmup):
+        tr.train_iteration(dat.collate([0]))
+    timer = _dfhip.new_kernel_timer()
+    _dfhip.set_kernel_timer(timer)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_iteration(dat.collate([0]))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    _dfhip.set_kernel_timer(None)
+    last = min(16, args.steps)
+    rows = [(tr.model.local_step - 1 - i) % 16 for i in range(last)]
+    samples = float(tr.model.step_counter[rows, 0].float().mean().item())
+    n = args.c5_res * args.c5_res
+    g = next(iter(tr._graphs.values()), None)
+    out = {"workload": f"C5 renderer leg: {args.c5_res}x{args.c5_res} render, bf16 autocast "
+                       "(bf16 field on v_mfma_f32_16x16x32_bf16, no GradScaler), cuda_ray, "
+                       "max_steps 512, injected w(t)*N(0,1) guidance (SD-2.1-base weights "
+                       "not available offline)",
+           "dtype": "bf16+f32", "rays_per_step": n, "steps": args.steps,
+           "ms_per_step": round(dt * 1e3, 3), "steps_per_sec": round(1.0 / dt, 3),
+           "rays_per_sec": round(n / dt, 1), "mean_samples_per_step": round(samples, 1),
+           "native_step": bool(g is not None and g.native is not None),
+           "kernels": summarize_kernels(timer.records)}
+    fm = field_mlp_report(tr)
+    if fm:
+        out["field_mlp"] = fm
+    del tr, dat
+    torch.cuda.empty_cache()
+    return out
+
+
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA
 
 
@@ -292,7 +344,7 @@ def measure_traffic(region, timeout=180):
         return None, "rocprofv3 not on PATH"
     child = [sys.executable, str(Path(__file__).resolve()), "--steps", "3", "--warmup", "3",
              "--no-cpu-baseline", "--no-kernel-timing", "--no-alt-backward", "--no-shading",
-             "--no-infer", "--no-traffic"]
+             "--no-infer", "--no-traffic", "--no-c5"]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
     env["TMPDIR"] = "/tmp"
@@ -527,6 +579,8 @@ def main():
         shade["note"] = ("steps >= albedo_iters: 0.2 albedo + 0.4 textureless + 0.4 lambertian "
                          "(utils.py:346-359), native graph-replayed, fused backward")
         result["shading"] = shade
+    if world == 1 and not args.no_c5:
+        result["c5"] = bench_c5(args, rank, world)
     if rank == 0 and world == 1 and not args.no_infer:
         result["inference"] = bench_inference(device, args.infer_res)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

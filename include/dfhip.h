@@ -37,7 +37,9 @@ extern "C" {
 
 typedef void *dfhip_stream_t; /* hipStream_t */
 
-enum dfhip_dtype { DFHIP_F32 = 0, DFHIP_F16 = 1, DFHIP_F64 = 2 };
+/* DFHIP_BF16: bfloat16 storage (the C5 bf16 option; no reference counterpart,
+ * the reference dispatches f32 / f16 / f64 only). */
+enum dfhip_dtype { DFHIP_F32 = 0, DFHIP_F16 = 1, DFHIP_F64 = 2, DFHIP_BF16 = 3 };
 /* Shadings of the non-albedo train steps (nerf/network_grid.py:124-144). */
 enum dfhip_shading { DFHIP_SHADING_TEXTURELESS = 1, DFHIP_SHADING_LAMBERTIAN = 2 };
 
@@ -207,7 +209,7 @@ int dfhip_composite_rays_train_backward_dense(int dtype, const void *grad_weight
 
 /* Native mixed-precision form of the two calls above for the fp16 train step:
  * sigmas, deltas, weights_sum, depth, image and their gradients are f32, the
- * colours `rgbs` and `grad_rgbs` are `rgb_dtype` (DFHIP_F32 or DFHIP_F16).
+ * colours `rgbs` and `grad_rgbs` are `rgb_dtype` (DFHIP_F32, DFHIP_F16 or DFHIP_BF16).
  * Same arithmetic as the reference, whose custom_fwd casts f16 colours to f32
  * (exact) and whose autograd casts the f32 colour gradient back to f16 once.
  * The backward is the dense form (needs ray-ordered contiguous rays);
@@ -393,6 +395,18 @@ int dfhip_grid_field_forward(const float *xyz, float bound, const void *table,
                              const float *b1, const float *w2, const float *b2, const float *w3,
                              const float *b3, void *enc, float *sigma, void *rgb, int rgb_dtype,
                              uint32_t cap, const int32_t *m_dev, dfhip_stream_t stream);
+/* bf16 form (BASELINE configs[4], bf16 autocast; new capability — the
+ * reference's kernels have no bf16): table [rows, 2] bf16, enc [cap, 32] bf16,
+ * hidden activations bf16, v_mfma_f32_16x16x32_bf16 with f32 accumulation,
+ * rgb f32 or DFHIP_BF16.  Grid features accumulate in f32 (fmaf per corner,
+ * corner order) and are rounded to bf16 once. */
+int dfhip_grid_field_forward_bf16(const float *xyz, float bound, const void *table,
+                                  const int32_t *offsets, uint32_t L, float S, uint32_t H,
+                                  uint32_t gridtype, int align_corners, const float *w1,
+                                  const float *b1, const float *w2, const float *b2,
+                                  const float *w3, const float *b3, void *enc, float *sigma,
+                                  void *rgb, int rgb_dtype, uint32_t cap, const int32_t *m_dev,
+                                  dfhip_stream_t stream);
 /* Backward of dfhip_grid_field_forward: MLP backward (d_enc_lbc [16, cap, 2] f16
  * scratch, mlp_partial: dfhip_field_mlp_backward_parts(cap) * params floats),
  * f32 weight gradients (overwritten), then the sliced embedding backward into
@@ -420,6 +434,19 @@ int dfhip_grid_field_backward_accumulate(
     float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
     float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
     float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream);
+
+/* bf16 backward of dfhip_grid_field_forward_bf16: enc and d_enc_lbc
+ * [16, cap, 2] are bf16, grad_rgb f32 or DFHIP_BF16; weight gradients f32,
+ * overwritten (accumulate == 0) or added into.  The embedding gradient is
+ * dfhip_grid_encode_backward_binned with grad_dtype DFHIP_BF16. */
+int dfhip_grid_field_backward_bf16(const void *enc, const float *xyz, float bound,
+                                   const float *w1, const float *b1, const float *w2,
+                                   const float *b2, const float *w3, const float *b3,
+                                   const float *grad_sigma, const void *grad_rgb,
+                                   int grad_rgb_dtype, uint32_t cap, const int32_t *m_dev,
+                                   void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts,
+                                   float *gw1, float *gb1, float *gw2, float *gb2, float *gw3,
+                                   float *gb3, int accumulate, dfhip_stream_t stream);
 
 /* Binned owner-computes form of grid_encode_backward (gridencoder.cu:226-313,
  * csrc/gridbin.hip) for D = 3, C in {1, 2, 4}: (sample, level) pairs are binned

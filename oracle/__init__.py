@@ -177,36 +177,68 @@ def composite_rays(n_alive, n_step, T_thresh, rays_alive, rays_t, sigmas, rgbs, 
 # ---------------------------------------------------------------- gridencoder
 
 _ST = {np.dtype(np.float32): 0, np.dtype(np.float16): 1, np.dtype(np.float64): 2}
+_ST_BF16 = 3  # uint16 arrays holding bfloat16 bits (numpy has no bfloat16)
+
+
+def to_bf16_bits(x):
+    """f32 -> bfloat16 bits (uint16), round to nearest even (torch.bfloat16)."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    nan = ((u & 0x7F800000) == 0x7F800000) & ((u & 0x7FFFFF) != 0)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return np.where(nan, ((u >> 16) | 0x40).astype(np.uint16), r)
+
+
+def bf16_bits_to_f32(b):
+    return (np.ascontiguousarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def round_bf16(x):
+    """Round f32 values to bfloat16 (result as f32)."""
+    return bf16_bits_to_f32(to_bf16_bits(x))
+
+
+def _st(a, bf16):
+    if bf16:
+        if a.dtype != np.uint16:
+            raise TypeError("bf16 arrays are passed as uint16 bfloat16 bits")
+        return _ST_BF16
+    return _ST[a.dtype]
 
 
 def grid_encode_forward(inputs, embeddings, offsets, S, H, gridtype=1, align_corners=False,
-                        calc_dy_dx=False, blc=True):
+                        calc_dy_dx=False, blc=True, bf16=False):
     """inputs [B, D] f32 in [0,1]; embeddings [rows, C] f32/f16/f64 ->
-    outputs [B, L*C] (blc) or [L, B, C] in the embeddings' dtype, dy_dx or None."""
+    outputs [B, L*C] (blc) or [L, B, C] in the embeddings' dtype, dy_dx or None.
+    bf16=True: embeddings are uint16 bfloat16 bits, f32 accumulation rounded
+    to bf16 once (csrc/field_common.h grid_features); outputs are bf16 bits."""
     x = _f32(inputs)
     emb = np.ascontiguousarray(embeddings)
+    st = _st(emb, bf16)
     off = _i32(offsets)
     B, D = x.shape
     C = emb.shape[1]
     L = off.shape[0] - 1
     out = np.zeros((B, L * C) if blc else (L, B, C), emb.dtype)
     dy = np.zeros((B, L * D * C), emb.dtype) if calc_dy_dx else None
-    lib().orc_grid_encode_forward(_p(x), _p(emb), ctypes.c_int(_ST[emb.dtype]), _p(off), _p(out),
+    lib().orc_grid_encode_forward(_p(x), _p(emb), ctypes.c_int(st), _p(off), _p(out),
                                   _u32(B), _u32(D), _u32(C), _u32(L), _f(S), _u32(H), _p(dy),
                                   _u32(gridtype), ctypes.c_int(int(align_corners)),
                                   ctypes.c_int(int(blc)))
     return out, dy
 
 
-def grid_encode_backward(grad, inputs, offsets, C, S, H, gridtype=1, align_corners=False, blc=True):
-    """Exact (float64, fixed order) embedding gradient [rows, C]."""
+def grid_encode_backward(grad, inputs, offsets, C, S, H, gridtype=1, align_corners=False, blc=True,
+                         bf16=False):
+    """Exact (float64, fixed order) embedding gradient [rows, C] (bf16=True:
+    grad holds uint16 bfloat16 bits)."""
     g = np.ascontiguousarray(grad)
+    st = _st(g, bf16)
     x = _f32(inputs)
     off = _i32(offsets)
     B, D = x.shape
     L = off.shape[0] - 1
     out = np.zeros((int(off[-1]), C), np.float64)
-    lib().orc_grid_encode_backward(_p(g), ctypes.c_int(_ST[g.dtype]), _p(x), _p(off), _p(out),
+    lib().orc_grid_encode_backward(_p(g), ctypes.c_int(st), _p(x), _p(off), _p(out),
                                    _u32(B), _u32(D), _u32(C), _u32(L), _f(S), _u32(H),
                                    _u32(gridtype), ctypes.c_int(int(align_corners)),
                                    ctypes.c_int(int(blc)))

@@ -30,21 +30,54 @@ Restates, in numpy, what the reference computes when `common_forward`
   rounds them to f16 before autocast's cast back to f32; the product path keeps
   f32 — both lie within one f16 ulp of this value).
 
+The same restatement under bf16 autocast (the C5 option; the reference has
+no bf16 path) is selected with `with precision("bf16"):` — every rounding
+point above rounds to bfloat16 instead (values kept as f32 arrays holding
+bf16 numbers), the grid features accumulate in f32 and round once
+(`encode_bf16`), and the windows use bf16's spacing (2^-7 relative).
+
 The background network (network_grid.py:158-167: FreqEncoder -> 39 -> 64 -> 3
 MLP -> sigmoid) and the per-ray tail of run_cuda (renderer.py:536-551) are
 restated the same way.
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 
-from . import freq_encode_forward, grid_encode_forward
+from . import (bf16_bits_to_f32, freq_encode_forward, grid_encode_forward, round_bf16,
+               to_bf16_bits)
 
 F16, F32, F64 = np.float16, np.float32, np.float64
 
+# the autocast element type of the field restatement: "f16" (the reference's
+# fp16 autocast) or "bf16" (values stored as f32 arrays of bf16 numbers)
+_ELEM = {"name": "f16"}
+
+
+@contextlib.contextmanager
+def precision(name):
+    """Select the element type ("f16" or "bf16") of r16 / relu16 / ulp16 and
+    the field forward / backward / window functions built on them."""
+    if name not in ("f16", "bf16"):
+        raise ValueError(name)
+    prev, _ELEM["name"] = _ELEM["name"], name
+    try:
+        yield
+    finally:
+        _ELEM["name"] = prev
+
+
+def _vd():
+    return F16 if _ELEM["name"] == "f16" else F32
+
 
 def r16(x):
-    """Round to f16 (round-to-nearest-even), via f32 like an f32 accumulator."""
+    """Round to the element type (f16, or bf16 under precision("bf16")),
+    round-to-nearest-even, via f32 like an f32 accumulator."""
+    if _ELEM["name"] == "bf16":
+        return round_bf16(np.asarray(x).astype(F32))
     return np.asarray(x).astype(F32).astype(F16)
 
 
@@ -64,11 +97,11 @@ def linear16(x16, w, b, chunk=None):
     acc = np.broadcast_to(np.asarray(b16, F64), (x.shape[0], w16.shape[0])).astype(F32)
     for k0 in range(0, x.shape[1], chunk):
         acc = (acc.astype(F64) + x[:, k0:k0 + chunk] @ w16[:, k0:k0 + chunk].T).astype(F32)
-    return acc.astype(F16)
+    return r16(acc)
 
 
 def relu16(z16):
-    return np.where(z16 > 0, z16, F16(0)).astype(F16)
+    return np.where(z16 > 0, z16, 0).astype(_vd())
 
 
 def gaussian(x):
@@ -89,6 +122,15 @@ def encode(xyz, bound, embeddings, offsets, S, H):
     x01 = ((np.asarray(xyz, F32) + F32(bound)) / F32(2 * bound)).astype(F32)
     out, _ = grid_encode_forward(x01, np.asarray(embeddings).astype(F16), offsets, S, H)
     return out
+
+
+def encode_bf16(xyz, bound, embeddings, offsets, S, H):
+    """bf16 grid features [M, 32] (as f32 values): the f32 embeddings rounded to
+    bf16, f32 accumulation per corner (fmaf, corner order), one rounding."""
+    x01 = ((np.asarray(xyz, F32) + F32(bound)) / F32(2 * bound)).astype(F32)
+    out, _ = grid_encode_forward(x01, to_bf16_bits(np.asarray(embeddings, F32)), offsets, S, H,
+                                 bf16=True)
+    return bf16_bits_to_f32(out)
 
 
 def field_forward(xyz, weights, enc16, chunk=None):
@@ -116,13 +158,13 @@ def field_backward(fwd, weights, grad_sigma, grad_albedo16):
     yc = np.clip(y, F32(-15), F32(15))
     d0 = r16(np.asarray(grad_sigma, F32) * np.exp(yc.astype(F64)).astype(F32))
     a = fwd["albedo"].astype(F32)
-    g = np.asarray(grad_albedo16, F16).astype(F32)
+    g = np.asarray(grad_albedo16).astype(_vd()).astype(F32)
     drgb = r16((g * (F32(1) - a)) * a)
-    dO = np.concatenate([d0[:, None], drgb], axis=1).astype(F16)
+    dO = np.concatenate([d0[:, None], drgb], axis=1).astype(_vd())
     dA2 = dO.astype(F64) @ w3
-    dz2 = np.where(fwd["a2"] > 0, r16(dA2), F16(0)).astype(F16)
+    dz2 = np.where(fwd["a2"] > 0, r16(dA2), 0).astype(_vd())
     dA1 = dz2.astype(F64) @ w2
-    dz1 = np.where(fwd["a1"] > 0, r16(dA1), F16(0)).astype(F16)
+    dz1 = np.where(fwd["a1"] > 0, r16(dA1), 0).astype(_vd())
     dX = dz1.astype(F64) @ w1
     x64, a1, a2 = fwd["x"].astype(F64), fwd["a1"].astype(F64), fwd["a2"].astype(F64)
     dO64, dz2_64, dz1_64 = dO.astype(F64), dz2.astype(F64), dz1.astype(F64)
@@ -279,8 +321,11 @@ def mlp_forward(x16, weights, acc_ulps=None, dx=None):
 
 
 def ulp16(v):
-    """Spacing of f16 values at |v| (subnormal spacing 2^-24 below 2^-14)."""
+    """Spacing of f16 values at |v| (subnormal spacing 2^-24 below 2^-14); of
+    bf16 values (2^-7 relative) under precision("bf16")."""
     a = np.abs(np.asarray(v, F64))
+    if _ELEM["name"] == "bf16":
+        return np.exp2(np.floor(np.log2(np.maximum(a, 2.0 ** -126)))) * 2.0 ** -7
     e = np.floor(np.log2(np.maximum(a, 2.0 ** -14)))
     return np.exp2(e) * 2.0 ** -10
 

@@ -106,6 +106,23 @@ static float h2f_(uint16_t h) {
     return f;
 }
 float orc_round_half(float f) { return h2f_(f2h_(f)); }
+
+/* bfloat16 <-> float, round to nearest even (torch.bfloat16 / v_cvt_pk_bf16_f32) */
+static uint16_t f2bf_(float f) {
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    if ((x & 0x7f800000u) == 0x7f800000u && (x & 0x7fffffu))
+        return (uint16_t)((x >> 16) | 0x40u); /* quiet NaN */
+    x += 0x7fffu + ((x >> 16) & 1u);
+    return (uint16_t)(x >> 16);
+}
+static float bf2f_(uint16_t h) {
+    const uint32_t x = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &x, 4);
+    return f;
+}
+float orc_round_bf16(float f) { return bf2f_(f2bf_(f)); }
 void orc_f32_to_f16(const float *src, uint16_t *dst, int64_t n) {
     for (int64_t i = 0; i < n; ++i) dst[i] = f2h_(src[i]);
 }
@@ -458,19 +475,23 @@ static float level_scale_(uint32_t l, float S, uint32_t H) {
 }
 
 /* storage: 0 = f32, 1 = f16 (uint16 bits), 2 = f64 */
+/* storage types: 0 f32, 1 f16, 2 f64, 3 bf16 (the C5 option; no reference
+ * counterpart: accumulated in f32 like st 0, rounded to bf16 once on store) */
 static double load_(const void *p, int st, size_t i) {
     if (st == 0) return ((const float *)p)[i];
     if (st == 1) return h2f_(((const uint16_t *)p)[i]);
+    if (st == 3) return bf2f_(((const uint16_t *)p)[i]);
     return ((const double *)p)[i];
 }
 static void store_(void *p, int st, size_t i, double v) {
     if (st == 0) ((float *)p)[i] = (float)v;
     else if (st == 1) ((uint16_t *)p)[i] = f2h_((float)v);
+    else if (st == 3) ((uint16_t *)p)[i] = f2bf_((float)v);
     else ((double *)p)[i] = v;
 }
 /* one corner contribution in the storage type's arithmetic (gridencoder.cu:165) */
 static double acc_(int st, double r, float w, double g) {
-    if (st == 0) return fmaf(w, (float)g, (float)r);
+    if (st == 0 || st == 3) return fmaf(w, (float)g, (float)r);
     if (st == 1) {
         const float p = h2f_(f2h_(w * (float)g));   /* Half(w * float(g)) */
         return h2f_(f2h_((float)r + p));             /* Half(float(r) + float(p)) */

@@ -19,8 +19,8 @@ import torch
 
 LIB_PATH = Path(os.environ.get("DFHIP_LIB", Path(__file__).resolve().parent / "lib" / "libdfhip.so"))
 
-F32, F16, F64 = 0, 1, 2
-_DTYPE = {torch.float32: F32, torch.float16: F16, torch.float64: F64}
+F32, F16, F64, BF16 = 0, 1, 2, 3
+_DTYPE = {torch.float32: F32, torch.float16: F16, torch.float64: F64, torch.bfloat16: BF16}
 
 _vp, _u32, _i32, _f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
 _u64 = ctypes.c_uint64
@@ -94,6 +94,12 @@ _SIGS = {
     "dfhip_shading_backward": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp, _vp,
                                _f32, _vp, _vp, _vp],
     "dfhip_shading_light": [_vp, _u64, _u64, _vp, _vp],
+    "dfhip_grid_field_forward_bf16": [_vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp,
+                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,
+                                      _vp],
+    "dfhip_grid_field_backward_bf16": [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _i32, _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _i32, _vp],
     "dfhip_grid_field_backward_accumulate": [
         _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp, _vp, _vp, _u32,
         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _u32,
@@ -265,7 +271,8 @@ def dtype_code(t: torch.Tensor, what: str) -> int:
     try:
         return _DTYPE[t.dtype]
     except KeyError:
-        raise RuntimeError(f"{what} must be a floating tensor (float32/float16/float64), got {t.dtype}")
+        raise RuntimeError(f"{what} must be a floating tensor (float32/float16/bfloat16/float64), "
+                           f"got {t.dtype}")
 
 
 def check_cuda(t: torch.Tensor, what: str) -> None:

@@ -69,15 +69,20 @@ def field_mlp_backward(enc, xyz, weights, grad_sigma, grad_rgb, d_enc_lbc, parti
 
 def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners, weights, enc,
                        sigma, rgb, m_dev=None):
-    """xyz [cap, 3] f32 in [-bound, bound]; table [rows, 2] f16; offsets [17]
-    int32.  Writes sigma [cap] f32, rgb [cap, 3] (f16/f32) and, when given,
-    enc [cap, 32] f16 (permuted feature order, for grid_field_backward).  Only
-    rows [0, m_dev[0]) are computed when m_dev (int32 device tensor) is given."""
+    """xyz [cap, 3] f32 in [-bound, bound]; table [rows, 2] f16 (fp16 autocast,
+    the reference's -O) or bf16 (the C5 bf16 option: features and activations
+    bf16 too); offsets [17] int32.  Writes sigma [cap] f32, rgb [cap, 3] (the
+    table's dtype or f32) and, when given, enc [cap, 32] in the table's dtype
+    (permuted feature order, for grid_field_backward).  Only rows
+    [0, m_dev[0]) are computed when m_dev (int32 device tensor) is given."""
     cap = xyz.shape[0]
     _f32(xyz, "xyz")
     checked(table, "table")
-    if table.dtype != torch.float16 or table.dim() != 2 or table.shape[1] != 2:
-        raise RuntimeError("table must be a [rows, 2] float16 tensor")
+    if table.dtype not in (torch.float16, torch.bfloat16) or table.dim() != 2 or \
+            table.shape[1] != 2:
+        raise RuntimeError("table must be a [rows, 2] float16 or bfloat16 tensor")
+    if enc is not None and enc.dtype != table.dtype:
+        raise RuntimeError("enc must have the table's dtype")
     checked(offsets, "offsets", "int")
     _f32(sigma, "sigma")
     checked(rgb, "rgb")
@@ -85,7 +90,9 @@ def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners
         checked(enc, "enc")
     if m_dev is not None:
         checked(m_dev, "m_dev", "int")
-    call("dfhip_grid_field_forward", ptr(xyz), float(bound), ptr(table), ptr(offsets),
+    fn = "dfhip_grid_field_forward_bf16" if table.dtype == torch.bfloat16 else \
+        "dfhip_grid_field_forward"
+    call(fn, ptr(xyz), float(bound), ptr(table), ptr(offsets),
          offsets.shape[0] - 1, float(S), int(H), int(gridtype), int(bool(align_corners)),
          *_weights(weights), ptr(enc), ptr(sigma), ptr(rgb), _d.dtype_code(rgb, "rgb"), cap,
          ptr(m_dev), stream())
@@ -108,6 +115,19 @@ def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lb
     if m_dev is not None:
         checked(m_dev, "m_dev", "int")
     gp = _weights(grads)
+    if enc.dtype == torch.bfloat16:
+        # bf16 field: the embedding gradient is the binned backward's (bf16 grads)
+        if grad_embeddings is not None:
+            raise RuntimeError("bf16 field: grad_embeddings must be None (use the binned "
+                               "embedding backward on d_enc_lbc)")
+        if d_enc_lbc.dtype != torch.bfloat16:
+            raise RuntimeError("bf16 field: d_enc must be bfloat16")
+        call("dfhip_grid_field_backward_bf16", ptr(enc), ptr(xyz), float(bound),
+             *_weights(weights), ptr(grad_sigma), ptr(grad_rgb),
+             _d.dtype_code(grad_rgb, "grad_rgb"), cap, ptr(m_dev), ptr(d_enc_lbc),
+             ptr(mlp_partial), backward_parts(cap) if cap else 1, *gp, int(bool(accumulate)),
+             stream())
+        return
     call("dfhip_grid_field_backward_accumulate" if accumulate else "dfhip_grid_field_backward",
          ptr(enc), ptr(xyz), float(bound), *_weights(weights),
          ptr(grad_sigma), ptr(grad_rgb), _d.dtype_code(grad_rgb, "grad_rgb"), cap, ptr(m_dev),

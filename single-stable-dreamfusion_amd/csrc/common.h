@@ -34,6 +34,7 @@ __host__ __device__ inline T ceil_div(T a, T b) { return (a + b - 1) / b; }
 // f16 storage uses the compiler's native _Float16 (IEEE binary16, RNE casts),
 // bit-identical to torch.half.
 typedef _Float16 half_t;
+typedef __bf16 bf16_t;  // the C5 bf16 option (DFHIP_BF16)
 
 template <typename T> __device__ __forceinline__ float to_f(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f(float v) { return (T)v; }

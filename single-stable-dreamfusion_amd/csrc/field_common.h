@@ -8,11 +8,15 @@
 #include "common.h"
 #include "grid_common.h"
 
+#include <type_traits>
+
 namespace dfhip {
 namespace fm {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kIn = 32, kHid = 64, kOut = 4;
@@ -21,8 +25,19 @@ constexpr int kOffW1 = 0, kOffB1 = kOffW1 + kHid * kIn, kOffW2 = kOffB1 + kHid,
               kOffB2 = kOffW2 + kHid * kHid, kOffW3 = kOffB2 + kHid, kOffB3 = kOffW3 + kOut * kHid,
               kParams = kOffB3 + kOut;  // 6532
 
+// Field element type T: f16 (the reference's fp16 autocast, C2) or bf16 (the
+// C5 option: bf16 autocast, new in this build).  Operand vectors of T and
+// the matching gfx950 MFMAs (v_mfma_f32_16x16x32_{f16,bf16}).
+template <typename T> struct Elem;
+template <> struct Elem<half_t> { typedef half8 v8; typedef half4 v4; };
+template <> struct Elem<bf16_t> { typedef bf8 v8; typedef bf4 v4; };
+template <typename T> struct Id { typedef T type; };  // non-deduced context
+
 __device__ __forceinline__ f4 mfma(half8 a, half8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 mfma(bf8 a, bf8 b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 // Make this wave's LDS writes visible to its other lanes before they read.
@@ -39,18 +54,22 @@ __device__ __forceinline__ void wave_lds_sync() {
 constexpr int kLd32 = 40;  // rows of 32 halves (+8)
 constexpr int kLd64 = 72;  // rows of 64 halves (+8)
 
-// Weights as f16 (autocast's cast of the f32 parameters), in LDS.
-struct Weights {
-    half_t w1[kHid * kLd32];  // [n1][f]
-    half_t w2[kHid * kLd64];  // [n2][n1]
-    half_t w3[16 * kLd64];    // [o][n2], rows 4..15 zero
-    float b1[kHid], b2[kHid], b3[16];  // f32 of the f16-rounded biases; b3 rows 4.. zero
+// Weights as T (autocast's cast of the f32 parameters), in LDS.
+template <typename T>
+struct WeightsG {
+    T w1[kHid * kLd32];  // [n1][f]
+    T w2[kHid * kLd64];  // [n2][n1]
+    T w3[16 * kLd64];    // [o][n2], rows 4..15 zero
+    float b1[kHid], b2[kHid], b3[16];  // f32 of the T-rounded biases; b3 rows 4.. zero
 };
-struct WeightsT {             // backward only
-    half_t w1t[kIn * kLd64];  // [f][n1]
-    half_t w2t[kHid * kLd64]; // [n1][n2]
-    half_t w3t[kHid * kLd32]; // [n2][o], o 4..31 zero
+template <typename T>
+struct WeightsTG {       // backward only
+    T w1t[kIn * kLd64];  // [f][n1]
+    T w2t[kHid * kLd64]; // [n1][n2]
+    T w3t[kHid * kLd32]; // [n2][o], o 4..31 zero
 };
+typedef WeightsG<half_t> Weights;
+typedef WeightsTG<half_t> WeightsT;
 
 // Feature order of the fused path: position p = 8h + j of the layer-1 B
 // operand holds level 4 (j >> 1) + h, channel j & 1, so that for each j the
@@ -61,70 +80,80 @@ __host__ __device__ constexpr int perm_feature(int p) {
 }
 
 // PERM: layer-1 weights stored in the fused path's permuted feature order.
-template <bool PERM>
-__device__ void load_weights(Weights &W, WeightsT *T, const float *w1, const float *b1,
-                             const float *w2, const float *b2, const float *w3, const float *b3) {
+template <bool PERM, typename E>
+__device__ void load_weights(WeightsG<E> &W, typename Id<WeightsTG<E>>::type *T, const float *w1,
+                             const float *b1, const float *w2, const float *b2, const float *w3,
+                             const float *b3) {
     for (int i = threadIdx.x; i < kHid * kIn; i += blockDim.x) {
         const int n = i / kIn, p = i % kIn;
-        W.w1[n * kLd32 + p] = (half_t)w1[n * kIn + (PERM ? perm_feature(p) : p)];
-        if (T) T->w1t[(i % kIn) * kLd64 + i / kIn] = (half_t)w1[i];  // natural: rows = features
+        W.w1[n * kLd32 + p] = (E)w1[n * kIn + (PERM ? perm_feature(p) : p)];
+        if (T) T->w1t[(i % kIn) * kLd64 + i / kIn] = (E)w1[i];  // natural: rows = features
     }
     for (int i = threadIdx.x; i < kHid * kHid; i += blockDim.x) {
-        const half_t v = (half_t)w2[i];
+        const E v = (E)w2[i];
         W.w2[(i / kHid) * kLd64 + i % kHid] = v;
         if (T) T->w2t[(i % kHid) * kLd64 + i / kHid] = v;
     }
     for (int i = threadIdx.x; i < 16 * kHid; i += blockDim.x)
-        W.w3[(i / kHid) * kLd64 + i % kHid] = i < kOut * kHid ? (half_t)w3[i] : (half_t)0.0f;
+        W.w3[(i / kHid) * kLd64 + i % kHid] = i < kOut * kHid ? (E)w3[i] : (E)0.0f;
     if (T)
         for (int i = threadIdx.x; i < kHid * 32; i += blockDim.x) {
             const int n2 = i / 32, o = i % 32;
-            T->w3t[n2 * kLd32 + o] = o < kOut ? (half_t)w3[o * kHid + n2] : (half_t)0.0f;
+            T->w3t[n2 * kLd32 + o] = o < kOut ? (E)w3[o * kHid + n2] : (E)0.0f;
         }
     for (int i = threadIdx.x; i < kHid; i += blockDim.x) {
-        W.b1[i] = (float)(half_t)b1[i];
-        W.b2[i] = (float)(half_t)b2[i];
+        W.b1[i] = (float)(E)b1[i];
+        W.b2[i] = (float)(E)b2[i];
     }
-    for (int i = threadIdx.x; i < 16; i += blockDim.x) W.b3[i] = i < kOut ? (float)(half_t)b3[i] : 0.0f;
+    for (int i = threadIdx.x; i < 16; i += blockDim.x) W.b3[i] = i < kOut ? (float)(E)b3[i] : 0.0f;
 }
 
 // A operand, natural k order: row `row` of a row-major [*, ld] f16 matrix,
 // k = 8h .. 8h+7 (+ koff).
-__device__ __forceinline__ half8 a_nat(const half_t *m, int ld, int row, int koff, int h) {
-    return *reinterpret_cast<const half8 *>(m + row * ld + koff + 8 * h);
+template <typename E>
+__device__ __forceinline__ typename Elem<E>::v8 a_nat(const E *m, int ld, int row, int koff, int h) {
+    return *reinterpret_cast<const typename Elem<E>::v8 *>(m + row * ld + koff + 8 * h);
 }
 // A operand, permuted k order of k-step s (see header).
-__device__ __forceinline__ half8 a_perm(const half_t *m, int ld, int row, int s, int h) {
-    const half4 lo = *reinterpret_cast<const half4 *>(m + row * ld + 32 * s + 4 * h);
-    const half4 hi = *reinterpret_cast<const half4 *>(m + row * ld + 32 * s + 16 + 4 * h);
-    return half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+template <typename E>
+__device__ __forceinline__ typename Elem<E>::v8 a_perm(const E *m, int ld, int row, int s, int h) {
+    typedef typename Elem<E>::v4 v4;
+    const v4 lo = *reinterpret_cast<const v4 *>(m + row * ld + 32 * s + 4 * h);
+    const v4 hi = *reinterpret_cast<const v4 *>(m + row * ld + 32 * s + 16 + 4 * h);
+    return typename Elem<E>::v8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 // B operand of k-step s from four accumulator tiles' f16 values v[tile][reg].
-__device__ __forceinline__ half8 b_from_tiles(const half_t (&v)[4][4], int s) {
-    return half8{v[2 * s][0], v[2 * s][1], v[2 * s][2], v[2 * s][3],
-                 v[2 * s + 1][0], v[2 * s + 1][1], v[2 * s + 1][2], v[2 * s + 1][3]};
+template <typename E>
+__device__ __forceinline__ typename Elem<E>::v8 b_from_tiles(const E (&v)[4][4], int s) {
+    return typename Elem<E>::v8{v[2 * s][0], v[2 * s][1], v[2 * s][2], v[2 * s][3],
+                                v[2 * s + 1][0], v[2 * s + 1][1], v[2 * s + 1][2],
+                                v[2 * s + 1][3]};
 }
 __device__ __forceinline__ f4 bias4(const float *b, int row0) {
     return f4{b[row0], b[row0 + 1], b[row0 + 2], b[row0 + 3]};
 }
 
 // One 16-sample tile through the MLP.  xb: B operand of the encoder features
-// (lane: sample c, features 8h..8h+7).  Outputs the post-ReLU f16 activations
+// (lane: sample c, features 8h..8h+7).  Outputs the post-ReLU activations (T)
 // of both hidden layers and the f32 accumulators of the output layer.
-struct Fwd {
-    half_t a1[4][4], a2[4][4];  // [tile][reg]: neuron 16 t + 4 h + r of sample c
-    f4 o;                       // rows 4h + r (only h == 0 valid: outputs 0..3)
+template <typename E>
+struct FwdG {
+    E a1[4][4], a2[4][4];  // [tile][reg]: neuron 16 t + 4 h + r of sample c
+    f4 o;                  // rows 4h + r (only h == 0 valid: outputs 0..3)
 };
+typedef FwdG<half_t> Fwd;
 
-__device__ __forceinline__ void forward_tile(const Weights &W, half8 xb, int c, int h, Fwd &F) {
+template <typename E>
+__device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem<E>::v8 xb, int c,
+                                             int h, FwdG<E> &F) {
     f4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         acc[t] = mfma(a_nat(W.w1, kLd32, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const half_t v = (half_t)acc[t][r];
-            F.a1[t][r] = v > (half_t)0.0f ? v : (half_t)0.0f;
+            const E v = (E)acc[t][r];
+            F.a1[t][r] = v > (E)0.0f ? v : (E)0.0f;
         }
     }
 #pragma unroll
@@ -134,8 +163,8 @@ __device__ __forceinline__ void forward_tile(const Weights &W, half8 xb, int c, 
         for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kLd64, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const half_t v = (half_t)a[r];
-            F.a2[u][r] = v > (half_t)0.0f ? v : (half_t)0.0f;
+            const E v = (E)a[r];
+            F.a2[u][r] = v > (E)0.0f ? v : (E)0.0f;
         }
     }
     f4 o = bias4(W.b3, 4 * h);
@@ -150,9 +179,12 @@ __device__ __forceinline__ float gaussian(const float *x) {
     return 5.0f * expf(-s / 0.08f);
 }
 
-__device__ __forceinline__ half8 load_x(const half_t *enc, uint32_t sample, uint32_t M, int h) {
-    if (sample >= M) return half8{};
-    return *reinterpret_cast<const half8 *>(enc + (size_t)sample * kIn + 8 * h);
+template <typename E>
+__device__ __forceinline__ typename Elem<E>::v8 load_x(const E *enc, uint32_t sample, uint32_t M,
+                                                       int h) {
+    typedef typename Elem<E>::v8 v8;
+    if (sample >= M) return v8{};
+    return *reinterpret_cast<const v8 *>(enc + (size_t)sample * kIn + 8 * h);
 }
 
 // Per-level constants of the 16-level 3-D grid, staged once per workgroup
@@ -202,15 +234,19 @@ __device__ __forceinline__ void stage_levels(LevelK *lk, const int32_t *__restri
 }
 
 // Grid features of one sample at levels 4(j >> 1) + h (j = 0..7, channel
-// j & 1) in the permuted order above: exactly k_grid_fwd<half, 3, 2>'s
+// j & 1) in the permuted order above.  f16: exactly k_grid_fwd<half, 3, 2>'s
 // arithmetic (gridencoder.cu:75-178: half accumulators rounded per corner, in
-// corner order).  All 32 row loads of the four levels are issued before the
+// corner order).  bf16 (no reference counterpart: its kernels dispatch f32 /
+// f16 / f64 only): f32 accumulators, fmaf per corner in corner order, ONE
+// rounding to bf16 — per-corner bf16 rounding would lose 3 more bits than the
+// f16 path's.  All 32 row loads of the four levels are issued before the
 // first accumulation (the corners of z-dropped tiled levels load the row of
 // their z = 0 twin, an L1 hit), so a lane has 32 gathers in flight.
-__device__ __forceinline__ half8 grid_features(const half_t *__restrict__ table,
-                                               const LevelK *lk, bool align,
-                                               const float (&x)[3], int h) {
-    half8 out{};
+template <typename E>
+__device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restrict__ table,
+                                                              const LevelK *lk, bool align,
+                                                              const float (&x)[3], int h) {
+    typename Elem<E>::v8 out{};
     if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
         return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
     const uint32_t *tab = reinterpret_cast<const uint32_t *>(table);
@@ -257,20 +293,28 @@ __device__ __forceinline__ half8 grid_features(const half_t *__restrict__ table,
             for (int c = 0; c < 8; ++c) bits[qq][c] = tab[row[qq][c]];
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) {
-            half_t a0 = (half_t)0.0f, a1 = (half_t)0.0f;
+            // f16: half accumulators (the reference's scalar_t); bf16: f32
+            typedef typename std::conditional<std::is_same<E, half_t>::value, half_t, float>::type
+                acc_t;
+            acc_t a0 = (acc_t)0.0f, a1 = (acc_t)0.0f;
 #pragma unroll
             for (uint32_t c = 0; c < 8; ++c) {
                 float w = 1.0f;
 #pragma unroll
                 for (int d = 0; d < 3; ++d) w *= (c & (1u << d)) ? frac[qq][d] : 1.0f - frac[qq][d];
-                half_t v[2];
+                E v[2];
                 __builtin_memcpy(v, &bits[qq][c], 4);
-                ge::acc_corner(a0, w, v[0]);
-                ge::acc_corner(a1, w, v[1]);
+                if constexpr (std::is_same<E, half_t>::value) {
+                    ge::acc_corner(a0, w, v[0]);
+                    ge::acc_corner(a1, w, v[1]);
+                } else {
+                    a0 = fmaf(w, (float)v[0], a0);
+                    a1 = fmaf(w, (float)v[1], a1);
+                }
             }
             const int q = 2 * half + qq;
-            out[2 * q] = a0;
-            out[2 * q + 1] = a1;
+            out[2 * q] = (E)a0;
+            out[2 * q + 1] = (E)a1;
         }
     }
     return out;

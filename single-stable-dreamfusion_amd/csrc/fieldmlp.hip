@@ -38,14 +38,15 @@ namespace fm {
 // table loads in flight per lane), the features go straight into the MLP's
 // B operand, and are also written (permuted order, 16 B per lane) for the
 // backward.  xyz in [-bound, bound] is mapped to [0, 1] as grid.py:142 does.
-template <typename rgb_t>
+template <typename E, typename rgb_t>
 __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
-    const float *__restrict__ xyz, float bound, const half_t *__restrict__ table,
+    const float *__restrict__ xyz, float bound, const E *__restrict__ table,
     const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
-    const float *b3, half_t *__restrict__ enc, float *__restrict__ sigma,
+    const float *b3, E *__restrict__ enc, float *__restrict__ sigma,
     rgb_t *__restrict__ rgb, uint32_t cap, const int32_t *__restrict__ m_dev) {
-    __shared__ Weights W;
+    typedef typename Elem<E>::v8 v8;
+    __shared__ WeightsG<E> W;
     __shared__ LevelK LK[kLevels];
     const bool align = align_corners != 0;
     load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
@@ -66,18 +67,17 @@ __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
                 x[d] = xyz[(size_t)sample * 3 + d];
                 x01[d] = (x[d] + bound) / (2.0f * bound);
             }
-        const half8 xb = valid ? grid_features(table, LK, align, x01, h)
-                               : half8{};
-        if (enc && valid) *reinterpret_cast<half8 *>(enc + (size_t)sample * kIn + 8 * h) = xb;
-        Fwd F;
+        const v8 xb = valid ? grid_features(table, LK, align, x01, h) : v8{};
+        if (enc && valid) *reinterpret_cast<v8 *>(enc + (size_t)sample * kIn + 8 * h) = xb;
+        FwdG<E> F;
         forward_tile(W, xb, c, h, F);
         if (h == 0 && valid) {
-            const float y = (float)(half_t)F.o[0] + gaussian(x);
+            const float y = (float)(E)F.o[0] + gaussian(x);
             sigma[sample] = expf(y);
 #pragma unroll
             for (int r = 1; r < 4; ++r) {
-                const float v = (float)(half_t)F.o[r];
-                rgb[(size_t)sample * 3 + r - 1] = (rgb_t)(half_t)(1.0f / (1.0f + expf(-v)));
+                const float v = (float)(E)F.o[r];
+                rgb[(size_t)sample * 3 + r - 1] = (rgb_t)(E)(1.0f / (1.0f + expf(-v)));
             }
         }
     }
@@ -144,44 +144,61 @@ constexpr int kStLd = 312;  // stage row stride (halves): 156 dwords = 4 mod 64 
                             // 32 lanes of an 8-byte write hit 64 distinct banks
 constexpr int kColX = 0, kColA1 = 32, kColA2 = 96, kColD1 = 160, kColD2 = 224, kColDO = 288;
 
+template <typename E>
 struct StageT {
-    half_t v[16 * kStLd];   // [sample][x | a1 | a2 | d1 | d2 | dO(16, rows 4.. zero)]
+    E v[16 * kStLd];   // [sample][x | a1 | a2 | d1 | d2 | dO(16, rows 4.. zero)]
 };
 
 typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
 
-// Operand of v_mfma_f32_16x16x16_f16 with the neuron on the lane: lane
+// Operand of v_mfma_f32_16x16x16_{f16,bf16} with the neuron on the lane: lane
 // (g = l >> 4, i = l & 15) gets columns c0 + i of sample rows 4g .. 4g + 3
 // (ds_read_b64_tr_b16: lane 4q + p of the group supplies row 4g + q, columns
 // c0 + 4p .. c0 + 4p + 3).
-__device__ __forceinline__ half4 tr_operand(const StageT &S, int c0, int lane) {
+template <typename E>
+__device__ __forceinline__ typename Elem<E>::v4 tr_operand(const StageT<E> &S, int c0, int lane) {
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const half_t *src = S.v + (4 * g + q) * kStLd + c0 + 4 * p;
-    const fp16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
-        (__attribute__((address_space(3))) fp16x4_t *)src);
-    half4 out;
-    __builtin_memcpy(&out, &r, sizeof(out));
+    const E *src = S.v + (4 * g + q) * kStLd + c0 + 4 * p;
+    typename Elem<E>::v4 out;
+    if constexpr (std::is_same<E, half_t>::value) {
+        const fp16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+            (__attribute__((address_space(3))) fp16x4_t *)src);
+        __builtin_memcpy(&out, &r, sizeof(out));
+    } else {
+        out = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) bf4 *)src);
+    }
     return out;
 }
 
 __device__ __forceinline__ f4 mfma16(half4 a, half4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f4 mfma16(bf4 a, bf4 b, f4 c) {
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    s4 x, y;
+    __builtin_memcpy(&x, &a, sizeof(x));
+    __builtin_memcpy(&y, &b, sizeof(y));
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(x, y, c, 0, 0, 0);
+}
 
-__device__ __forceinline__ void st_write4(StageT &S, int sample, int col, half_t v0, half_t v1,
-                                          half_t v2, half_t v3) {
-    *reinterpret_cast<half4 *>(S.v + sample * kStLd + col) = half4{v0, v1, v2, v3};
+template <typename E>
+__device__ __forceinline__ void st_write4(StageT<E> &S, int sample, int col, E v0, E v1, E v2,
+                                          E v3) {
+    *reinterpret_cast<typename Elem<E>::v4 *>(S.v + sample * kStLd + col) =
+        typename Elem<E>::v4{v0, v1, v2, v3};
 }
 
 // One wave's inputs for a 16-sample tile: encoder features (every lane), and
 // for the output-layer lanes (h == 0) positions and incoming gradients.
+template <typename E>
 struct TileIn {
-    half8 xb;
+    typename Elem<E>::v8 xb;
     float xyz[3], gs, grgb[3];
 };
 
-template <typename rgb_t>
-__device__ __forceinline__ void load_tile(TileIn &g, uint32_t tile, const half_t *enc,
+template <typename E, typename rgb_t>
+__device__ __forceinline__ void load_tile(TileIn<E> &g, uint32_t tile, const E *enc,
                                           const float *xyz, const float *grad_sigma,
                                           const rgb_t *grad_rgb, uint32_t M, int c, int h) {
     const uint32_t sample = tile * 16 + c;
@@ -198,71 +215,72 @@ __device__ __forceinline__ void load_tile(TileIn &g, uint32_t tile, const half_t
 // PERM: enc holds the fused forward's permuted feature order (k_field_fwd_fused);
 // otherwise the natural [M, 32] encoder output.  M = *m_dev (clamped to cap)
 // when m_dev is given; d_enc is [16, cap, 2].
-template <typename rgb_t, bool PERM>
+template <typename E, typename rgb_t, bool PERM>
 __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
-    const half_t *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
+    const E *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
     const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
     const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t cap,
     const int32_t *__restrict__ m_dev,
-    half_t *__restrict__ d_enc,     // [16, cap, 2] (level-major)
+    E *__restrict__ d_enc,          // [16, cap, 2] (level-major)
     float *__restrict__ partial) {  // [gridDim.x, kParams]
-    __shared__ Weights W;
-    __shared__ WeightsT T;
-    __shared__ StageT stage[kBwdWaves];
+    typedef typename Elem<E>::v8 v8;
+    typedef typename Elem<E>::v4 v4;
+    __shared__ WeightsG<E> W;
+    __shared__ WeightsTG<E> T;
+    __shared__ StageT<E> stage[kBwdWaves];
     load_weights<PERM>(W, &T, w1, b1, w2, b2, w3, b3);
     const uint32_t M = active_count(m_dev, cap);
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
-    StageT &S = stage[wave];
+    StageT<E> &S = stage[wave];
     __syncthreads();
 
     // this wave's accumulator tiles (see the ownership table below)
     f4 acc[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) acc[i] = f4{0, 0, 0, 0};
-    const half4 ones = half4{(half_t)1.0f, (half_t)1.0f, (half_t)1.0f, (half_t)1.0f};
+    const v4 ones = v4{(E)1.0f, (E)1.0f, (E)1.0f, (E)1.0f};
 
     const uint32_t tiles = ceil_div(M, 16u);
     const uint32_t per_round = gridDim.x * kBwdWaves;
     const uint32_t rounds = ceil_div(tiles, per_round);
-    TileIn cur;
+    TileIn<E> cur;
     uint32_t tile = blockIdx.x * kBwdWaves + wave;
-    load_tile<rgb_t>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    load_tile<E, rgb_t>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
     for (uint32_t round = 0; round < rounds; ++round, tile += per_round) {
         // the next round's inputs are loaded while this one is processed
-        TileIn nxt;
-        load_tile<rgb_t>(nxt, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        TileIn<E> nxt;
+        load_tile<E, rgb_t>(nxt, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
         const uint32_t sample = tile * 16 + c;
         const bool valid = sample < M;
-        Fwd F;
+        FwdG<E> F;
         forward_tile(W, cur.xb, c, h, F);
-        // dL/d(output layer), f16 as autocast's backward produces it
-        half_t dO[4] = {(half_t)0.0f, (half_t)0.0f, (half_t)0.0f, (half_t)0.0f};
+        // dL/d(output layer), in E as autocast's backward produces it
+        E dO[4] = {(E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
         if (h == 0 && valid) {
-            const float y = (float)(half_t)F.o[0] + gaussian(cur.xyz);
+            const float y = (float)(E)F.o[0] + gaussian(cur.xyz);
             // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
             const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
-            dO[0] = (half_t)(cur.gs * expf(yc));
+            dO[0] = (E)(cur.gs * expf(yc));
 #pragma unroll
             for (int r = 1; r < 4; ++r) {
-                const float a = (float)(half_t)(1.0f / (1.0f + expf(-(float)(half_t)F.o[r])));
-                const float g = (float)(half_t)cur.grgb[r - 1];
-                dO[r] = (half_t)(g * (1.0f - a) * a);  // sigmoid_backward in f16 (opmath f32)
+                const float a = (float)(E)(1.0f / (1.0f + expf(-(float)(E)F.o[r])));
+                const float g = (float)(E)cur.grgb[r - 1];
+                dO[r] = (E)(g * (1.0f - a) * a);  // sigmoid_backward in E (opmath f32)
             }
         }
-        const half8 dob = half8{dO[0], dO[1], dO[2], dO[3], (half_t)0.0f, (half_t)0.0f,
-                                (half_t)0.0f, (half_t)0.0f};
+        const v8 dob = v8{dO[0], dO[1], dO[2], dO[3], (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
         // hidden layer 2: dA2^T = W3^T dO^T, ReLU mask
-        half_t dz2[4][4];
+        E dz2[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const f4 d = mfma(a_nat(T.w3t, kLd32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                dz2[u][r] = F.a2[u][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
+                dz2[u][r] = F.a2[u][r] > (E)0.0f ? (E)d[r] : (E)0.0f;
         }
         // hidden layer 1: dA1^T = W2^T dZ2^T, ReLU mask
-        half_t dz1[4][4];
+        E dz1[4][4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             f4 d = f4{0, 0, 0, 0};
@@ -271,7 +289,7 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
                 d = mfma(a_perm(T.w2t, kLd64, 16 * t + c, s2, h), b_from_tiles(dz2, s2), d);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                dz1[t][r] = F.a1[t][r] > (half_t)0.0f ? (half_t)d[r] : (half_t)0.0f;
+                dz1[t][r] = F.a1[t][r] > (E)0.0f ? (E)d[r] : (E)0.0f;
         }
         // encoder features: dX^T = W1^T dZ1^T -> [L, B, C] directly
 #pragma unroll
@@ -283,16 +301,16 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             if (valid) {
                 // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
                 const uint32_t lv = 8 * f + 2 * h;
-                typedef _Float16 half2v __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<half2v *>(d_enc + ((size_t)lv * cap + sample) * 2) =
-                    half2v{(half_t)d[0], (half_t)d[1]};
-                *reinterpret_cast<half2v *>(d_enc + ((size_t)(lv + 1) * cap + sample) * 2) =
-                    half2v{(half_t)d[2], (half_t)d[3]};
+                typedef E e2v __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<e2v *>(d_enc + ((size_t)lv * cap + sample) * 2) =
+                    e2v{(E)d[0], (E)d[1]};
+                *reinterpret_cast<e2v *>(d_enc + ((size_t)(lv + 1) * cap + sample) * 2) =
+                    e2v{(E)d[2], (E)d[3]};
             }
         }
         // [sample][neuron] image of the tile (invalid samples: dO = 0 so every
         // gradient row is zero and they add nothing below)
-        *reinterpret_cast<half8 *>(S.v + c * kStLd + kColX + 8 * h) = cur.xb;
+        *reinterpret_cast<v8 *>(S.v + c * kStLd + kColX + 8 * h) = cur.xb;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int col = 16 * t + 4 * h;
@@ -309,12 +327,12 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
         //               W3 columns tm in {0,1} / {2,3}; wave 2 also b3
 #pragma unroll
         for (int st = 0; st < kBwdWaves; ++st) {
-            const StageT &X = stage[st];
+            const StageT<E> &X = stage[st];
             if (wave < 2) {
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int tn = 2 * wave + k;
-                    const half4 a = tr_operand(X, kColD2 + 16 * tn, lane);
+                    const v4 a = tr_operand(X, kColD2 + 16 * tn, lane);
 #pragma unroll
                     for (int tm = 0; tm < 4; ++tm)
                         acc[5 * k + tm] = mfma16(a, tr_operand(X, kColA1 + 16 * tm, lane),
@@ -326,14 +344,14 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int tn = 2 * w2i + k;
-                    const half4 a = tr_operand(X, kColD1 + 16 * tn, lane);
+                    const v4 a = tr_operand(X, kColD1 + 16 * tn, lane);
 #pragma unroll
                     for (int tf = 0; tf < 2; ++tf)
                         acc[3 * k + tf] = mfma16(a, tr_operand(X, kColX + 16 * tf, lane),
                                                  acc[3 * k + tf]);
                     acc[3 * k + 2] = mfma16(a, ones, acc[3 * k + 2]);
                 }
-                const half4 ao = tr_operand(X, kColDO, lane);
+                const v4 ao = tr_operand(X, kColDO, lane);
 #pragma unroll
                 for (int k = 0; k < 2; ++k)
                     acc[6 + k] = mfma16(ao, tr_operand(X, kColA2 + 16 * (2 * w2i + k), lane),
@@ -516,11 +534,11 @@ extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const
             return DFHIP_EINVAL;
         }
         if (grad_rgb_dtype == DFHIP_F32)
-            k_field_bwd<float, false><<<parts, 256, 0, s>>>(
+            k_field_bwd<half_t, float, false><<<parts, 256, 0, s>>>(
                 (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
                 (const float *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
         else if (grad_rgb_dtype == DFHIP_F16)
-            k_field_bwd<half_t, false><<<parts, 256, 0, s>>>(
+            k_field_bwd<half_t, half_t, false><<<parts, 256, 0, s>>>(
                 (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
                 (const half_t *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
         else {
@@ -546,14 +564,31 @@ static bool check_field_grid(const char *name, uint32_t L) {
     return true;
 }
 
-extern "C" int dfhip_grid_field_forward(const float *xyz, float bound, const void *table,
-                                        const int32_t *offsets, uint32_t L, float S, uint32_t H,
-                                        uint32_t gridtype, int align_corners, const float *w1,
-                                        const float *b1, const float *w2, const float *b2,
-                                        const float *w3, const float *b3, void *enc,
-                                        float *sigma, void *rgb, int rgb_dtype, uint32_t cap,
-                                        const int32_t *m_dev, dfhip_stream_t stream) {
-    const char *name = "grid_field_forward";
+template <typename E, typename rgb_t>
+static void launch_field_fwd(hipStream_t s, const float *xyz, float bound, const void *table,
+                             const int32_t *offsets, const ge::Levels &lv, uint32_t gridtype,
+                             int align_corners, const float *w1, const float *b1, const float *w2,
+                             const float *b2, const float *w3, const float *b3, void *enc,
+                             float *sigma, void *rgb, uint32_t cap, const int32_t *m_dev) {
+    // persistent waves: exactly one resident wave per slot of the chip (each
+    // walks ~M / (16 * waves) tiles); more blocks than fit leave a partial
+    // last round of blocks (4096 blocks at 5 waves/SIMD were 3.2 rounds)
+    const uint32_t tiles = ceil_div(cap, 16u);
+    const uint32_t fit = resident_blocks(k_field_fwd_fused<E, rgb_t>);
+    const uint32_t blocks = ceil_div(tiles, 4u) < fit ? ceil_div(tiles, 4u) : fit;
+    k_field_fwd_fused<E, rgb_t><<<blocks, 256, 0, s>>>(
+        xyz, bound, (const E *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3,
+        b3, (E *)enc, sigma, (rgb_t *)rgb, cap, m_dev);
+}
+
+// elem: DFHIP_F16 (table, features, activations in f16: the reference's fp16
+// autocast) or DFHIP_BF16 (all of them bf16: bf16 autocast, the C5 option).
+static int grid_field_forward(const char *name, int elem, const float *xyz, float bound,
+                              const void *table, const int32_t *offsets, uint32_t L, float S,
+                              uint32_t H, uint32_t gridtype, int align_corners, const float *w1,
+                              const float *b1, const float *w2, const float *b2, const float *w3,
+                              const float *b3, void *enc, float *sigma, void *rgb, int rgb_dtype,
+                              uint32_t cap, const int32_t *m_dev, dfhip_stream_t stream) {
     if (!check_field_grid(name, L)) return DFHIP_EINVAL;
     if (!(bound > 0.0f)) {
         set_error("%s: bound must be > 0", name);
@@ -566,30 +601,48 @@ extern "C" int dfhip_grid_field_forward(const float *xyz, float bound, const voi
     }
     hipStream_t s = as_stream(stream);
     const ge::Levels lv = ge::make_levels(L, S, H);
-    // persistent waves: exactly one resident wave per slot of the chip (each
-    // walks ~M / (16 * waves) tiles); more blocks than fit leave a partial
-    // last round of blocks (4096 blocks at 5 waves/SIMD were 3.2 rounds)
-    const uint32_t tiles = ceil_div(cap, 16u);
-    const uint32_t fit = rgb_dtype == DFHIP_F16 ? resident_blocks(k_field_fwd_fused<half_t>)
-                                                : resident_blocks(k_field_fwd_fused<float>);
-    const uint32_t blocks = ceil_div(tiles, 4u) < fit ? ceil_div(tiles, 4u) : fit;
-    if (rgb_dtype == DFHIP_F32)
-        k_field_fwd_fused<float><<<blocks, 256, 0, s>>>(
-            xyz, bound, (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2,
-            b2, w3, b3, (half_t *)enc, sigma, (float *)rgb, cap, m_dev);
-    else if (rgb_dtype == DFHIP_F16)
-        k_field_fwd_fused<half_t><<<blocks, 256, 0, s>>>(
-            xyz, bound, (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2,
-            b2, w3, b3, (half_t *)enc, sigma, (half_t *)rgb, cap, m_dev);
+#define DFHIP_FWD(E, R)                                                                       \
+    launch_field_fwd<E, R>(s, xyz, bound, table, offsets, lv, gridtype, align_corners, w1, b1, \
+                           w2, b2, w3, b3, enc, sigma, rgb, cap, m_dev)
+    if (elem == DFHIP_F16 && rgb_dtype == DFHIP_F32) DFHIP_FWD(half_t, float);
+    else if (elem == DFHIP_F16 && rgb_dtype == DFHIP_F16) DFHIP_FWD(half_t, half_t);
+    else if (elem == DFHIP_BF16 && rgb_dtype == DFHIP_F32) DFHIP_FWD(bf16_t, float);
+    else if (elem == DFHIP_BF16 && rgb_dtype == DFHIP_BF16) DFHIP_FWD(bf16_t, bf16_t);
     else {
-        set_error("%s: rgb dtype must be f32 or f16", name);
+        set_error("%s: rgb dtype must be f32 or the field's element type", name);
         return DFHIP_EDTYPE;
     }
+#undef DFHIP_FWD
     return check_launch(name);
 }
 
+extern "C" int dfhip_grid_field_forward(const float *xyz, float bound, const void *table,
+                                        const int32_t *offsets, uint32_t L, float S, uint32_t H,
+                                        uint32_t gridtype, int align_corners, const float *w1,
+                                        const float *b1, const float *w2, const float *b2,
+                                        const float *w3, const float *b3, void *enc,
+                                        float *sigma, void *rgb, int rgb_dtype, uint32_t cap,
+                                        const int32_t *m_dev, dfhip_stream_t stream) {
+    return grid_field_forward("grid_field_forward", DFHIP_F16, xyz, bound, table, offsets, L, S,
+                              H, gridtype, align_corners, w1, b1, w2, b2, w3, b3, enc, sigma,
+                              rgb, rgb_dtype, cap, m_dev, stream);
+}
+
+extern "C" int dfhip_grid_field_forward_bf16(const float *xyz, float bound, const void *table,
+                                             const int32_t *offsets, uint32_t L, float S,
+                                             uint32_t H, uint32_t gridtype, int align_corners,
+                                             const float *w1, const float *b1, const float *w2,
+                                             const float *b2, const float *w3, const float *b3,
+                                             void *enc, float *sigma, void *rgb, int rgb_dtype,
+                                             uint32_t cap, const int32_t *m_dev,
+                                             dfhip_stream_t stream) {
+    return grid_field_forward("grid_field_forward_bf16", DFHIP_BF16, xyz, bound, table, offsets,
+                              L, S, H, gridtype, align_corners, w1, b1, w2, b2, w3, b3, enc,
+                              sigma, rgb, rgb_dtype, cap, m_dev, stream);
+}
+
 static int grid_field_backward(
-    const char *name, const void *enc, const float *xyz, float bound, const float *w1,
+    const char *name, int elem, const void *enc, const float *xyz, float bound, const float *w1,
     const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
     const float *grad_sigma, const void *grad_rgb, int grad_rgb_dtype, uint32_t cap,
     const int32_t *m_dev, void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1,
@@ -618,18 +671,19 @@ static int grid_field_backward(
                       name, bwd_blocks(cap), mlp_parts);
             return DFHIP_EINVAL;
         }
-        if (grad_rgb_dtype == DFHIP_F32)
-            k_field_bwd<float, true><<<mlp_parts, 256, 0, s>>>(
-                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                (const float *)grad_rgb, cap, m_dev, (half_t *)d_enc_lbc, mlp_partial);
-        else if (grad_rgb_dtype == DFHIP_F16)
-            k_field_bwd<half_t, true><<<mlp_parts, 256, 0, s>>>(
-                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                (const half_t *)grad_rgb, cap, m_dev, (half_t *)d_enc_lbc, mlp_partial);
+#define DFHIP_BWD(E, R)                                                                       \
+    k_field_bwd<E, R, true><<<mlp_parts, 256, 0, s>>>(                                        \
+        (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, cap,     \
+        m_dev, (E *)d_enc_lbc, mlp_partial)
+        if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(half_t, float);
+        else if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F16) DFHIP_BWD(half_t, half_t);
+        else if (elem == DFHIP_BF16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(bf16_t, float);
+        else if (elem == DFHIP_BF16 && grad_rgb_dtype == DFHIP_BF16) DFHIP_BWD(bf16_t, bf16_t);
         else {
-            set_error("%s: grad_rgb dtype must be f32 or f16", name);
+            set_error("%s: grad_rgb dtype must be f32 or the field's element type", name);
             return DFHIP_EDTYPE;
         }
+#undef DFHIP_BWD
     } else {
         mlp_parts = 1;
         (void)hipMemsetAsync(mlp_partial, 0, kParams * sizeof(float), s);
@@ -638,6 +692,11 @@ static int grid_field_backward(
         mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, accumulate);
     int rc = check_launch(name);
     if (rc != DFHIP_OK || grad_embeddings == nullptr) return rc;
+    if (elem != DFHIP_F16) {
+        set_error("%s: the sliced embedding backward takes f16 feature gradients; pass "
+                  "grad_embeddings = NULL and use dfhip_grid_encode_backward_binned", name);
+        return DFHIP_EDTYPE;
+    }
     return ge::grid_backward_sliced(name, DFHIP_F16, DFHIP_F32, d_enc_lbc, xyz, offsets,
                                     grad_embeddings, total_rows, cap, 3, 2, L, S, H, gridtype,
                                     align_corners, grid_partial, grid_parts, accumulate,
@@ -652,7 +711,7 @@ extern "C" int dfhip_grid_field_backward(
     float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
     float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
     float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream) {
-    return grid_field_backward("grid_field_backward", enc, xyz, bound, w1, b1, w2, b2, w3, b3,
+    return grid_field_backward("grid_field_backward", DFHIP_F16, enc, xyz, bound, w1, b1, w2, b2, w3, b3,
                                grad_sigma, grad_rgb, grad_rgb_dtype, cap, m_dev, d_enc_lbc,
                                mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, offsets,
                                total_rows, L, S, H, gridtype, align_corners, grad_embeddings,
@@ -667,9 +726,22 @@ extern "C" int dfhip_grid_field_backward_accumulate(
     float *gb2, float *gw3, float *gb3, const int32_t *offsets, uint32_t total_rows, uint32_t L,
     float S, uint32_t H, uint32_t gridtype, int align_corners, float *grad_embeddings,
     float *grid_partial, uint32_t grid_parts, dfhip_stream_t stream) {
-    return grid_field_backward("grid_field_backward_accumulate", enc, xyz, bound, w1, b1, w2, b2,
+    return grid_field_backward("grid_field_backward_accumulate", DFHIP_F16, enc, xyz, bound, w1, b1, w2, b2,
                                w3, b3, grad_sigma, grad_rgb, grad_rgb_dtype, cap, m_dev, d_enc_lbc,
                                mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3, offsets,
                                total_rows, L, S, H, gridtype, align_corners, grad_embeddings,
                                grid_partial, grid_parts, 1, stream);
+}
+
+extern "C" int dfhip_grid_field_backward_bf16(
+    const void *enc, const float *xyz, float bound, const float *w1, const float *b1,
+    const float *w2, const float *b2, const float *w3, const float *b3, const float *grad_sigma,
+    const void *grad_rgb, int grad_rgb_dtype, uint32_t cap, const int32_t *m_dev,
+    void *d_enc_lbc, float *mlp_partial, uint32_t mlp_parts, float *gw1, float *gb1, float *gw2,
+    float *gb2, float *gw3, float *gb3, int accumulate, dfhip_stream_t stream) {
+    return grid_field_backward("grid_field_backward_bf16", DFHIP_BF16, enc, xyz, bound, w1, b1,
+                               w2, b2, w3, b3, grad_sigma, grad_rgb, grad_rgb_dtype, cap, m_dev,
+                               d_enc_lbc, mlp_partial, mlp_parts, gw1, gb1, gw2, gb2, gw3, gb3,
+                               nullptr, 0, 16, 0.0f, 0, 0, 0, nullptr, nullptr, 0, accumulate,
+                               stream);
 }

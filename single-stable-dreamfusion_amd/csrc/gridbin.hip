@@ -645,8 +645,8 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
         set_error("%s: null pointer", name);
         return DFHIP_EINVAL;
     }
-    if (grad_dtype != DFHIP_F16 && grad_dtype != DFHIP_F32) {
-        set_error("%s: grad dtype must be f16 or f32", name);
+    if (grad_dtype != DFHIP_F16 && grad_dtype != DFHIP_F32 && grad_dtype != DFHIP_BF16) {
+        set_error("%s: grad dtype must be f16, bf16 or f32", name);
         return DFHIP_EDTYPE;
     }
     if (B > 0 && (!grad_lbc || !inputs)) {
@@ -683,6 +683,12 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
                             (const uint16_t *)entries, partial)
         if (grad_dtype == DFHIP_F16) {
             if (C == 1) DFHIP_WALK(half_t, 1); else if (C == 2) DFHIP_WALK(half_t, 2); else DFHIP_WALK(half_t, 4);
+        } else if (grad_dtype == DFHIP_BF16) {
+            if (C == 2) DFHIP_WALK(bf16_t, 2);
+            else {
+                set_error("%s: bf16 gradients are supported for C = 2", name);
+                return DFHIP_EINVAL;
+            }
         } else {
             if (C == 1) DFHIP_WALK(float, 1); else if (C == 2) DFHIP_WALK(float, 2); else DFHIP_WALK(float, 4);
         }

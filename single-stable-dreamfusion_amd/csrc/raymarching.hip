@@ -338,6 +338,10 @@ template <>
 __device__ __forceinline__ half_t grad_cast<float, half_t, float>(float v) {
     return (half_t)f32_rounded(v);
 }
+template <>
+__device__ __forceinline__ bf16_t grad_cast<float, bf16_t, float>(float v) {
+    return (bf16_t)f32_rounded(v);
+}
 
 // raymarching.cu:601-682.  DENSE: also zero rows the reference leaves untouched
 // (past each ray's break; with `tail`, also rows [total, M) after the last ray).
@@ -963,8 +967,11 @@ extern "C" int dfhip_composite_rays_train_forward_mixed(
     else if (rgb_dtype == DFHIP_F16)
         launch_comp_fwd<float, half_t>(s, sigmas, (const half_t *)rgbs, deltas, rays, M, N,
                                        T_thresh, weights_sum, depth, image);
+    else if (rgb_dtype == DFHIP_BF16)
+        launch_comp_fwd<float, bf16_t>(s, sigmas, (const bf16_t *)rgbs, deltas, rays, M, N,
+                                       T_thresh, weights_sum, depth, image);
     else {
-        set_error("%s: rgb dtype must be f32 or f16 (got %d)", name, rgb_dtype);
+        set_error("%s: rgb dtype must be f32, f16 or bf16 (got %d)", name, rgb_dtype);
         return DFHIP_EDTYPE;
     }
     return check_launch(name);
@@ -988,8 +995,13 @@ extern "C" int dfhip_composite_rays_train_backward_mixed(
                                              (const half_t *)rgbs, deltas, rays, weights_sum,
                                              image, M, N, T_thresh, grad_sigmas,
                                              (half_t *)grad_rgbs, zero_tail);
+    else if (rgb_dtype == DFHIP_BF16)
+        launch_comp_bwd<float, true, bf16_t>(s, grad_weights_sum, grad_image, sigmas,
+                                             (const bf16_t *)rgbs, deltas, rays, weights_sum,
+                                             image, M, N, T_thresh, grad_sigmas,
+                                             (bf16_t *)grad_rgbs, zero_tail);
     else {
-        set_error("%s: rgb dtype must be f32 or f16 (got %d)", name, rgb_dtype);
+        set_error("%s: rgb dtype must be f32, f16 or bf16 (got %d)", name, rgb_dtype);
         return DFHIP_EDTYPE;
     }
     return check_launch(name);

@@ -36,6 +36,10 @@ def get_parser():
     p.add_argument("--bg_radius", type=float, default=1.4)
     p.add_argument("--density_thresh", type=float, default=10)
     p.add_argument("--fp16", action="store_true")
+    # BASELINE configs[4] (C5): bf16 autocast (native bf16 field, no GradScaler)
+    # and SD-2.1-base guidance (text dim 1024); not in the reference
+    p.add_argument("--bf16", action="store_true")
+    p.add_argument("--sd_version", type=str, default="1.5", choices=["1.5", "2.1-base"])
     p.add_argument("--backbone", type=str, default="grid")
     p.add_argument("--w", type=int, default=64)
     p.add_argument("--h", type=int, default=64)
@@ -70,6 +74,8 @@ def parse_opt(argv=None):
         opt.fp16, opt.dir_text, opt.cuda_ray = True, True, True
     elif opt.O2:
         opt.fp16, opt.dir_text = True, True
+    if opt.bf16:
+        opt.fp16 = False  # -O --bf16: the C5 option replaces fp16 autocast
     return opt
 
 
@@ -87,7 +93,7 @@ def main(argv=None):
     device = torch.device("cuda")
     if opt.test:
         trainer = Trainer("df", opt, model, None, device=device, workspace=opt.workspace,
-                          fp16=opt.fp16, use_checkpoint=opt.ckpt)
+                          fp16=opt.fp16, bf16=opt.bf16, use_checkpoint=opt.ckpt)
         loader = NeRFDataset(opt, device=device, type="test", H=opt.H, W=opt.W, size=100).dataloader()
         for data in loader:
             trainer.test_step(data)
@@ -96,14 +102,16 @@ def main(argv=None):
                                size=100).dataloader()
     optimizer = lambda m: make_adam(m.get_params(opt.lr), betas=(0.9, 0.99), eps=1e-15)
     scheduler = lambda o: torch.optim.lr_scheduler.LambdaLR(o, lambda it: 0.1 ** min(it / opt.iters, 1))
+    text_dim = 1024 if opt.sd_version == "2.1-base" else 768
     if opt.guidance == "synthetic":
-        guidance = InjectedSDS(device)
+        guidance = InjectedSDS(device, text_dim=text_dim)
     elif opt.guidance == "mock":
-        guidance = SyntheticSDS(device)
+        guidance = SyntheticSDS(device, text_dim=text_dim)
     else:
-        guidance = StableDiffusion(device)
+        guidance = StableDiffusion(device, dtype=torch.bfloat16 if opt.bf16 else torch.float16)
     trainer = Trainer("df", opt, model, guidance, device=device, workspace=opt.workspace,
-                      optimizer=optimizer, ema_decay=None, fp16=opt.fp16, lr_scheduler=scheduler,
+                      optimizer=optimizer, ema_decay=None, fp16=opt.fp16, bf16=opt.bf16,
+                      lr_scheduler=scheduler,
                       use_checkpoint=opt.ckpt, eval_interval=opt.eval_interval,
                       scheduler_update_every_step=True)
     max_epoch = int(np.ceil(opt.iters / len(train_loader)))

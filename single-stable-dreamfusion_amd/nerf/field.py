@@ -10,8 +10,10 @@ feature gradient written straight into the [L, B, C] layout) then the sliced
 embedding backward.  With `m_dev` (the march's device-side sample count)
 only the live rows of capacity-sized buffers are processed, so the train
 step needs no host round trip.  Used under fp16 autocast for the reference's
-network shape (16 levels x 2 channels, 32 -> 64 -> 64 -> 4); anything else
-runs the unfused modules.
+network shape (16 levels x 2 channels, 32 -> 64 -> 64 -> 4), and under bf16
+autocast (the C5 option: the table, features and activations in bf16, the
+embedding gradient by the binned backward); anything else runs the unfused
+modules.
 """
 import os
 
@@ -55,8 +57,11 @@ class defer_embedding_backward:
 def eligible(encoder, layers, x):
     if not (x.is_cuda and torch.is_autocast_enabled("cuda")):
         return False
-    if torch.get_autocast_dtype("cuda") != torch.float16:
+    if torch.get_autocast_dtype("cuda") not in (torch.float16, torch.bfloat16):
         return False
+    if torch.get_autocast_dtype("cuda") == torch.bfloat16 and (
+            not _BINNED or getattr(encoder, "offsets_host", None) is None):
+        return False  # bf16 feature gradients: binned embedding backward only
     if encoder.num_levels != 16 or encoder.level_dim != 2 or encoder.input_dim != 3:
         return False
     if len(layers) != 3 or layers[0].bias is None:
@@ -73,11 +78,13 @@ class _GridField(Function):
         S, H, gridtype, align, offsets_host = meta
         x = x.contiguous().float()
         cap = x.shape[0]
-        table = embeddings.to(torch.half).contiguous()
+        elem = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") \
+            else torch.half  # f16 (fp16 autocast) or bf16 (bf16 autocast)
+        table = embeddings.to(elem).contiguous()
         L, C = offsets.shape[0] - 1, table.shape[1]
-        enc = torch.empty(cap, L * C, device=x.device, dtype=torch.half)
+        enc = torch.empty(cap, L * C, device=x.device, dtype=elem)
         sigma = torch.empty(cap, device=x.device, dtype=torch.float32)
-        albedo = torch.empty(cap, 3, device=x.device, dtype=torch.half)
+        albedo = torch.empty(cap, 3, device=x.device, dtype=elem)
         ws = [w.detach().float().contiguous() for w in weights]
         # algorithmic bytes per sample: xyz + features out + sigma/albedo out,
         # plus the f16 table once (the gathers hit L2 / MALL)
@@ -99,10 +106,10 @@ class _GridField(Function):
         if grad_sigma is None:
             grad_sigma = torch.zeros(cap, device=dev)
         if grad_albedo is None:
-            grad_albedo = torch.zeros(cap, 3, device=dev, dtype=torch.half)
+            grad_albedo = torch.zeros(cap, 3, device=dev, dtype=enc.dtype)
         grad_sigma = grad_sigma.float().contiguous()
-        grad_albedo = grad_albedo.contiguous()
-        d_enc = torch.empty(L, cap, C, device=dev, dtype=torch.half)
+        grad_albedo = grad_albedo.to(enc.dtype).contiguous()
+        d_enc = torch.empty(L, cap, C, device=dev, dtype=enc.dtype)
         mlp_partial = torch.empty((_fieldmlp.backward_parts(cap) if cap else 1)
                                   * _fieldmlp.params_count(), device=dev)
         grads = [torch.empty_like(w) for w in ws]
@@ -160,7 +167,7 @@ class _GridField(Function):
 
 
 def grid_field(x, bound, encoder, layers, m_dev=None):
-    """sigma [M] (f32), albedo [M, 3] (f16) of the grid field at x [M, 3].
+    """sigma [M] (f32), albedo [M, 3] (autocast dtype) of the grid field at x [M, 3].
     m_dev: optional int32 device tensor holding the live row count."""
     meta = (float(np.log2(encoder.per_level_scale)), int(encoder.base_resolution),
             encoder.gridtype_id, bool(encoder.align_corners),

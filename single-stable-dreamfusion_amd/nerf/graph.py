@@ -63,7 +63,7 @@ class GraphedTrainStep:
 
     def _body(self, static):
         t = self.trainer
-        with torch.autocast("cuda", enabled=t.fp16):
+        with torch.autocast("cuda", enabled=t.amp, dtype=t.amp_dtype):
             _, _, loss = t.train_step(static, shading=self.shading,
                                       ambient_ratio=self.ambient_ratio, text_z=self.text_z)
         t.backward_only(loss)

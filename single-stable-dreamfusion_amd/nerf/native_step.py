@@ -29,6 +29,11 @@ passes (SDS latents.backward, sd.py:115, then scaler.scale(loss).backward(),
 utils.py:708): the compositing / field backwards run once per pass and the
 second pass adds into the parameter gradients, as autograd accumulates them.
 
+Under bf16 autocast (trainer.bf16, BASELINE configs[4]) the table, features,
+activations, colours and their gradients are bf16 (csrc/fieldmlp.hip's bf16
+instantiations, v_mfma_f32_16x16x32_bf16), there is no GradScaler (the
+entropy term's upstream gradient is 1), and only the albedo shading is native.
+
 Applies to the albedo shading with the InjectedSDS guidance, the
 reference's grid network (16 x 2 tiled grid, 32 -> 64 -> 64 -> 4 MLP), a
 background MLP (bg_radius > 0) or a random background colour, and
@@ -57,8 +62,10 @@ def eligible(trainer, shading):
         return False
     if shading != "albedo" and not trainer.fused_backward:
         return False  # the two-pass form is built for the albedo step only
-    if not (trainer.fp16 and m.cuda_ray):
+    if not ((trainer.fp16 or getattr(trainer, "bf16", False)) and m.cuda_ray):
         return False
+    if getattr(trainer, "bf16", False) and shading != "albedo":
+        return False  # the shading kernels (csrc/shade.hip) take f16 albedo
     if opt.lambda_opacity > 0:
         return False
     enc = getattr(m, "encoder", None)
@@ -100,7 +107,9 @@ class NativeAlbedoStep:
         self.dt_gamma = float(opt.dt_gamma)
         self.lam = float(opt.lambda_entropy)
         f32 = dict(device=dev, dtype=torch.float32)
-        f16 = dict(device=dev, dtype=torch.float16)
+        # field element type: f16 (fp16 autocast, -O) or bf16 (bf16 autocast, C5)
+        self.elem = torch.bfloat16 if getattr(trainer, "bf16", False) else torch.float16
+        f16 = dict(device=dev, dtype=self.elem)
         i32 = dict(device=dev, dtype=torch.int32)
         # prologue outputs (graph inputs)
         self.rays_o = torch.empty(N, 3, **f32)

@@ -9,6 +9,11 @@ with three launches: the non-finite check, the Adam update of every tensor
 torch objects' own state (Adam's `step` / `exp_avg` / `exp_avg_sq` per
 parameter, GradScaler's `_scale` / `_growth_tracker`), so state_dict /
 load_state_dict and checkpoints are unchanged.
+
+Without a GradScaler (bf16 autocast, the C5 option: torch.amp.GradScaler is
+disabled) the same launches run against a private unit scale that never
+changes: the update is torch Adam's, except that a step whose gradients are
+not finite is skipped instead of writing non-finite parameters.
 """
 import ctypes
 
@@ -22,9 +27,9 @@ _MAX_TENSORS = 24
 def eligible(optimizer, scaler):
     if not isinstance(optimizer, torch.optim.Adam) or type(optimizer) is not torch.optim.Adam:
         return False
-    if scaler is None or not scaler.is_enabled():
+    if scaler is None:
         return False
-    if (scaler._growth_factor, scaler._backoff_factor) != (2.0, 0.5):
+    if scaler.is_enabled() and (scaler._growth_factor, scaler._backoff_factor) != (2.0, 0.5):
         return False
     n = 0
     for g in optimizer.param_groups:
@@ -44,6 +49,7 @@ class NativeAdamAmp:
         self.optimizer = optimizer
         self.scaler = scaler
         self.found_inf = None
+        self._unit = None  # (scale 1.0, growth tracker) when the scaler is disabled
         self._ptr_key = None
         self._arrays = None
 
@@ -61,10 +67,20 @@ class NativeAdamAmp:
         """One scaler.step(optimizer) + scaler.update() (parameters without a
         gradient are skipped, as torch does)."""
         sc = self.scaler
-        if sc._scale is None:
-            return  # scale() never called: nothing was back-propagated
+        if sc.is_enabled():
+            if sc._scale is None:
+                return  # scale() never called: nothing was back-propagated
+            scale, tracker = sc._scale, sc._growth_tracker
+            growth, backoff, interval = sc._growth_factor, sc._backoff_factor, sc._growth_interval
+        else:
+            if self._unit is None:
+                dev = next(p.device for g in self.optimizer.param_groups for p in g["params"])
+                self._unit = (torch.ones(1, dtype=torch.float32, device=dev),
+                              torch.zeros(1, dtype=torch.int32, device=dev))
+            scale, tracker = self._unit
+            growth, backoff, interval = 1.0, 1.0, 1 << 30
         if self.found_inf is None:
-            self.found_inf = torch.zeros(1, dtype=torch.float32, device=sc._scale.device)
+            self.found_inf = torch.zeros(1, dtype=torch.float32, device=scale.device)
         # fast path: same parameters / gradient buffers as last step (the graph-
         # replayed step keeps its gradients in place) -> only the lrs are new
         # (a reloaded optimizer state is a new dict: its identity is part of the key)
@@ -77,10 +93,9 @@ class NativeAdamAmp:
             return
         n, P, G, M, V, S, N, B1, B2, E, WD, groups = self._arrays
         lr = (ctypes.c_float * n)(*[float(self.optimizer.param_groups[i]["lr"]) for i in groups])
-        rc = self._fn(n, P, G, M, V, S, N, lr, B1, B2, E, WD, sc._scale.data_ptr(),
-                      sc._growth_tracker.data_ptr(), self.found_inf.data_ptr(),
-                      float(sc._growth_factor), float(sc._backoff_factor),
-                      int(sc._growth_interval), _dfhip.stream())
+        rc = self._fn(n, P, G, M, V, S, N, lr, B1, B2, E, WD, scale.data_ptr(),
+                      tracker.data_ptr(), self.found_inf.data_ptr(), float(growth),
+                      float(backoff), int(interval), _dfhip.stream())
         if rc != 0:
             raise RuntimeError(f"dfhip_adam_amp_step failed ({rc}): "
                                f"{_dfhip.load().dfhip_last_error().decode()}")

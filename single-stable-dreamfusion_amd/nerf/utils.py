@@ -236,7 +236,7 @@ class _EMA:
 class Trainer(object):
     def __init__(self, name, opt, model, guidance, criterion=None, optimizer=None, ema_decay=None,
                  lr_scheduler=None, metrics=[], local_rank=0, world_size=1, device=None,
-                 mute=False, fp16=False, eval_interval=1, max_keep_ckpt=2, workspace="workspace",
+                 mute=False, fp16=False, bf16=False, eval_interval=1, max_keep_ckpt=2, workspace="workspace",
                  best_mode="min", use_loss_as_metric=True, report_metric_at_train=False,
                  use_checkpoint="latest", use_tensorboardX=True, scheduler_update_every_step=False,
                  fused_backward=True, graph_step=False):
@@ -249,6 +249,11 @@ class Trainer(object):
         self.workspace = workspace
         self.ema_decay = ema_decay
         self.fp16 = fp16
+        # bf16 autocast (BASELINE configs[4], the C5 option; the reference has
+        # fp16 only): no GradScaler, the native step runs its bf16 field
+        self.bf16 = bool(bf16) and not fp16
+        self.amp = bool(fp16) or self.bf16
+        self.amp_dtype = torch.bfloat16 if self.bf16 else torch.float16
         self.best_mode = best_mode
         self.use_loss_as_metric = use_loss_as_metric
         self.report_metric_at_train = report_metric_at_train
@@ -323,7 +328,7 @@ class Trainer(object):
             self.best_path = f"{self.ckpt_path}/{self.name}.pth"
             os.makedirs(self.ckpt_path, exist_ok=True)
         self.log(f"[INFO] Trainer: {self.name} | {self.time_stamp} | {self.device} | "
-                 f"{'fp16' if self.fp16 else 'fp32'} | {self.workspace}")
+                 f"{'fp16' if self.fp16 else 'bf16' if self.bf16 else 'fp32'} | {self.workspace}")
         self.log(f"[INFO] #parameters: {sum(p.numel() for p in model.parameters() if p.requires_grad)}")
         if self.workspace is not None and self.use_checkpoint not in (None, "scratch"):
             if self.use_checkpoint == "latest":
@@ -460,7 +465,7 @@ class Trainer(object):
         """One optimisation step of the SDS loop (reference utils.py:693-715
         minus the per-step loss.item())."""
         if self.model.cuda_ray and self.global_step % self.opt.update_extra_interval == 0:
-            with torch.autocast("cuda", enabled=self.fp16):
+            with torch.autocast("cuda", enabled=self.amp, dtype=self.amp_dtype):
                 self.model.update_extra_state()
         self.local_step += 1
         self.global_step += 1
@@ -470,7 +475,7 @@ class Trainer(object):
                                               ("pose" in data and "intrinsics" in data)):
             return self._graph_iteration(data, shading, ambient_ratio)
         self.optimizer.zero_grad()
-        with torch.autocast("cuda", enabled=self.fp16):
+        with torch.autocast("cuda", enabled=self.amp, dtype=self.amp_dtype):
             pred_rgbs, pred_ws, loss = self.train_step(data, shading, ambient_ratio)
         self.backward_and_step(loss)
         # detached: a caller holding the loss must not keep this step's autograd
@@ -480,10 +485,10 @@ class Trainer(object):
 
     # ------------------------------------------------------------ graph step
     def _graph_eligible(self, shading):
-        if not (self.graph_step and self.fp16 and self.model.cuda_ray
+        if not (self.graph_step and self.amp and self.model.cuda_ray
                 and hasattr(self.guidance, "sds_grad") and self.device.type == "cuda"):
             return False
-        if not self.fused_backward or shading != "albedo":
+        if not self.fused_backward or shading != "albedo" or self.bf16:
             # the two-pass backward and the normal-shaded steps are graphed only
             # as the native step
             from . import native_step as _native

@@ -275,11 +275,12 @@ class _composite_rays_train(Function):
         ray-ordered samples are read (and their gradient written) as f16 by the
         mixed kernels: the f16 -> f32 cast is exact and the reference's
         autograd rounds the f32 colour gradient to f16 once, so the numbers are
-        the same without the two [M, 3] cast passes."""
+        the same without the two [M, 3] cast passes.  bf16 colours (bf16
+        autocast, the C5 option) take the same route."""
         ordered = bool(getattr(rays, _ORDERED_ATTR, False))
         if torch.is_autocast_enabled("cuda"):
             sigmas, deltas = sigmas.float(), deltas.float()
-            if not (ordered and rgbs.dtype == torch.float16):
+            if not (ordered and rgbs.dtype in (torch.float16, torch.bfloat16)):
                 rgbs = rgbs.float()
         sigmas = sigmas.contiguous()
         rgbs = rgbs.contiguous()
@@ -287,7 +288,7 @@ class _composite_rays_train(Function):
         m, n = sigmas.shape[0], rays.shape[0]
         # f32 sigmas with f16/f32 colours of ray-ordered samples: mixed kernels
         mixed = (ordered and sigmas.dtype == torch.float32 and deltas.dtype == torch.float32
-                 and rgbs.dtype in (torch.float16, torch.float32))
+                 and rgbs.dtype in (torch.float16, torch.bfloat16, torch.float32))
         opts = dict(dtype=sigmas.dtype, device=sigmas.device)
         weights_sum = torch.empty(n, **opts)
         depth = torch.empty(n, **opts)
