@@ -129,6 +129,22 @@ __device__ __forceinline__ typename Elem<E>::v8 b_from_tiles(const E (&v)[4][4],
                                 v[2 * s + 1][0], v[2 * s + 1][1], v[2 * s + 1][2],
                                 v[2 * s + 1][3]};
 }
+// bf16 tiles are kept as packed 4-vectors (two VGPRs each): element-wise
+// bf16 scalars cost a VGPR apiece and spilled the forward kernel.
+__device__ __forceinline__ bf8 b_from_tiles(const bf4 (&v)[4], int s) {
+    return __builtin_shufflevector(v[2 * s], v[2 * s + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// Four f32 accumulators -> ReLU -> packed bf16 (relu and round-to-nearest
+// commute, so this equals ReLU of the rounded value, autocast's order).
+__device__ __forceinline__ bf4 relu_bf4(f4 a) {
+    const f4 r = {fmaxf(a[0], 0.0f), fmaxf(a[1], 0.0f), fmaxf(a[2], 0.0f), fmaxf(a[3], 0.0f)};
+    return __builtin_convertvector(r, bf4);
+}
+
+// Per-tile activations of one layer: [tile][reg] as scalars (f16) or as
+// packed vectors (bf16); both index as t[tile][reg].
+template <typename E> struct Tiles { typedef E type[4][4]; };
+template <> struct Tiles<bf16_t> { typedef bf4 type[4]; };
 __device__ __forceinline__ f4 bias4(const float *b, int row0) {
     return f4{b[row0], b[row0 + 1], b[row0 + 2], b[row0 + 3]};
 }
@@ -138,22 +154,27 @@ __device__ __forceinline__ f4 bias4(const float *b, int row0) {
 // of both hidden layers and the f32 accumulators of the output layer.
 template <typename E>
 struct FwdG {
-    E a1[4][4], a2[4][4];  // [tile][reg]: neuron 16 t + 4 h + r of sample c
-    f4 o;                  // rows 4h + r (only h == 0 valid: outputs 0..3)
+    typename Tiles<E>::type a1, a2;  // [tile][reg]: neuron 16 t + 4 h + r of sample c
+    f4 o;                            // rows 4h + r (only h == 0 valid: outputs 0..3)
 };
 typedef FwdG<half_t> Fwd;
 
 template <typename E>
 __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem<E>::v8 xb, int c,
                                              int h, FwdG<E> &F) {
+    constexpr bool kBf = std::is_same<E, bf16_t>::value;
     f4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         acc[t] = mfma(a_nat(W.w1, kLd32, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
+        if constexpr (kBf) {
+            F.a1[t] = relu_bf4(acc[t]);
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const E v = (E)acc[t][r];
-            F.a1[t][r] = v > (E)0.0f ? v : (E)0.0f;
+            for (int r = 0; r < 4; ++r) {
+                const E v = (E)acc[t][r];
+                F.a1[t][r] = v > (E)0.0f ? v : (E)0.0f;
+            }
         }
     }
 #pragma unroll
@@ -161,10 +182,14 @@ __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem
         f4 a = bias4(W.b2, 16 * u + 4 * h);
 #pragma unroll
         for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kLd64, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
+        if constexpr (kBf) {
+            F.a2[u] = relu_bf4(a);
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const E v = (E)a[r];
-            F.a2[u][r] = v > (E)0.0f ? v : (E)0.0f;
+            for (int r = 0; r < 4; ++r) {
+                const E v = (E)a[r];
+                F.a2[u][r] = v > (E)0.0f ? v : (E)0.0f;
+            }
         }
     }
     f4 o = bias4(W.b3, 4 * h);
@@ -247,6 +272,8 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                                                               const LevelK *lk, bool align,
                                                               const float (&x)[3], int h) {
     typename Elem<E>::v8 out{};
+    typedef float f8 __attribute__((ext_vector_type(8)));
+    f8 outf{};  // bf16: the f32 features, converted to bf16 pairs at the end
     if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
         return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
     const uint32_t *tab = reinterpret_cast<const uint32_t *>(table);
@@ -313,10 +340,16 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                 }
             }
             const int q = 2 * half + qq;
-            out[2 * q] = (E)a0;
-            out[2 * q + 1] = (E)a1;
+            if constexpr (std::is_same<E, half_t>::value) {
+                out[2 * q] = a0;
+                out[2 * q + 1] = a1;
+            } else {
+                outf[2 * q] = a0;
+                outf[2 * q + 1] = a1;
+            }
         }
     }
+    if constexpr (!std::is_same<E, half_t>::value) out = __builtin_convertvector(outf, bf8);
     return out;
 }
 

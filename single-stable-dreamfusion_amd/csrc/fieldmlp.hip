@@ -58,6 +58,9 @@ __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
     const uint32_t tiles = ceil_div(M, 16u);
     for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles;
          tile += waves) {
+        // bf16: the weight operands are re-read from LDS every tile (a memory
+        // clobber keeps LICM from hoisting them; hoisted, they spilled)
+        if constexpr (!std::is_same<E, half_t>::value) asm volatile("" ::: "memory");
         const uint32_t sample = tile * 16 + c;
         const bool valid = sample < M;
         float x[3] = {0.0f, 0.0f, 0.0f}, x01[3] = {-1.0f, -1.0f, -1.0f};
@@ -270,26 +273,36 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             }
         }
         const v8 dob = v8{dO[0], dO[1], dO[2], dO[3], (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
+        // ReLU mask of an accumulator tile by the layer's activations
+        constexpr bool kBf = std::is_same<E, bf16_t>::value;
+        auto mask = [&](const auto &act, const f4 &d, auto &dst) {
+            if constexpr (kBf) {
+                const f4 m = {(float)act[0] > 0.0f ? d[0] : 0.0f,
+                              (float)act[1] > 0.0f ? d[1] : 0.0f,
+                              (float)act[2] > 0.0f ? d[2] : 0.0f,
+                              (float)act[3] > 0.0f ? d[3] : 0.0f};
+                dst = __builtin_convertvector(m, bf4);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dst[r] = act[r] > (E)0.0f ? (E)d[r] : (E)0.0f;
+            }
+        };
         // hidden layer 2: dA2^T = W3^T dO^T, ReLU mask
-        E dz2[4][4];
+        typename Tiles<E>::type dz2;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const f4 d = mfma(a_nat(T.w3t, kLd32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                dz2[u][r] = F.a2[u][r] > (E)0.0f ? (E)d[r] : (E)0.0f;
+            mask(F.a2[u], d, dz2[u]);
         }
         // hidden layer 1: dA1^T = W2^T dZ2^T, ReLU mask
-        E dz1[4][4];
+        typename Tiles<E>::type dz1;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             f4 d = f4{0, 0, 0, 0};
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
                 d = mfma(a_perm(T.w2t, kLd64, 16 * t + c, s2, h), b_from_tiles(dz2, s2), d);
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                dz1[t][r] = F.a1[t][r] > (E)0.0f ? (E)d[r] : (E)0.0f;
+            mask(F.a1[t], d, dz1[t]);
         }
         // encoder features: dX^T = W1^T dZ1^T -> [L, B, C] directly
 #pragma unroll
@@ -314,10 +327,17 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int col = 16 * t + 4 * h;
-            st_write4(S, c, kColA1 + col, F.a1[t][0], F.a1[t][1], F.a1[t][2], F.a1[t][3]);
-            st_write4(S, c, kColA2 + col, F.a2[t][0], F.a2[t][1], F.a2[t][2], F.a2[t][3]);
-            st_write4(S, c, kColD1 + col, dz1[t][0], dz1[t][1], dz1[t][2], dz1[t][3]);
-            st_write4(S, c, kColD2 + col, dz2[t][0], dz2[t][1], dz2[t][2], dz2[t][3]);
+            if constexpr (kBf) {
+                *reinterpret_cast<v4 *>(S.v + c * kStLd + kColA1 + col) = F.a1[t];
+                *reinterpret_cast<v4 *>(S.v + c * kStLd + kColA2 + col) = F.a2[t];
+                *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD1 + col) = dz1[t];
+                *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD2 + col) = dz2[t];
+            } else {
+                st_write4(S, c, kColA1 + col, F.a1[t][0], F.a1[t][1], F.a1[t][2], F.a1[t][3]);
+                st_write4(S, c, kColA2 + col, F.a2[t][0], F.a2[t][1], F.a2[t][2], F.a2[t][3]);
+                st_write4(S, c, kColD1 + col, dz1[t][0], dz1[t][1], dz1[t][2], dz1[t][3]);
+                st_write4(S, c, kColD2 + col, dz2[t][0], dz2[t][1], dz2[t][2], dz2[t][3]);
+            }
         }
         st_write4(S, c, kColDO + 4 * h, dO[0], dO[1], dO[2], dO[3]);  // h > 0: zeros
         __syncthreads();
