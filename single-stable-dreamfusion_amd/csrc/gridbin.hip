@@ -286,6 +286,26 @@ template <uint32_t D, uint32_t C, int MODE>
 __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
                                         const ge::LevelRows &lr, const uint32_t cell[D],
                                         const double (&cw)[1u << D][C]) {
+    if constexpr (MODE == 0 && D == 3) {
+        // mask form: corner k's row is base + ((i0 + o_k) & wmask) with the
+        // cell's tiled index i0 (two multiplies per flush, not per corner) and
+        // the uniform corner offsets o_k = {0, 1, m1, m1 + 1, m2, ...}; one
+        // unsigned compare against the slice's relative range
+        const uint32_t i0 = cell[0] + cell[1] * lr.m1 + cell[2] * lr.m2;
+        const uint32_t lo = r0 - c.base, n = r1 - r0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) {
+            if (k >> lr.lead) continue;
+            const uint32_t o = (k & 1u) + ((k & 2u) ? lr.m1 : 0u) + ((k & 4u) ? lr.m2 : 0u);
+            const uint32_t rel = ((i0 + o) & lr.wmask) - lo;
+            if (rel < n) {
+                double *dst = acc + (size_t)rel * C;
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch, cw[k][ch]);
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (uint32_t k = 0; k < (1u << D); ++k) {
         if (k >> lr.lead) continue;
@@ -486,6 +506,8 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         };
         if (Q <= 1)
             walk(std::integral_constant<uint32_t, 1>{});
+        else if (Q <= 4)  // most mid / fine-level segments: no 8-slot batch of duplicates
+            walk(std::integral_constant<uint32_t, 4>{});
         else
             walk(std::integral_constant<uint32_t, kRun>{});
         if (have) flush<D, C, MODE>(acc, r0, r1, c, lr, cur, cw);
