@@ -261,31 +261,34 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
 
 // ---------------------------------------------------------------- 2. walk
 // Flush one cell's merged corner contributions into the LDS slice [r0, r1).
-template <uint32_t D, uint32_t C, int MODE>
+template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD>
 __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
                                         const ge::LevelRows &lr, const uint32_t cell[D],
                                         const double (&cw)[1u << D][C]);
 
 constexpr int kModeAny = 3;  // MODE: the corner-row wrap fixed at compile time, or any
 
-template <uint32_t D, uint32_t C, int MODE>
+// LEAD: the level's corner count exponent (lr.lead) fixed at compile time
+// (the walk dispatches on it once per workgroup), or 0 to read lr.lead
+template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD = 0>
 __device__ __forceinline__ void flush(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
                                       const ge::LevelRows &lr, const uint32_t cell[D],
                                       const double (&cw)[1u << D][C]) {
     if constexpr (MODE != kModeAny) {
-        flush_m<D, C, MODE>(acc, r0, r1, c, lr, cell, cw);
+        flush_m<D, C, MODE, LEAD>(acc, r0, r1, c, lr, cell, cw);
     } else {
         const int mode = ge::row_mode(lr);  // uniform: one scalar branch per flush
-        if (mode == 0) flush_m<D, C, 0>(acc, r0, r1, c, lr, cell, cw);
-        else if (mode == 1) flush_m<D, C, 1>(acc, r0, r1, c, lr, cell, cw);
-        else flush_m<D, C, 2>(acc, r0, r1, c, lr, cell, cw);
+        if (mode == 0) flush_m<D, C, 0, LEAD>(acc, r0, r1, c, lr, cell, cw);
+        else if (mode == 1) flush_m<D, C, 1, LEAD>(acc, r0, r1, c, lr, cell, cw);
+        else flush_m<D, C, 2, LEAD>(acc, r0, r1, c, lr, cell, cw);
     }
 }
 
-template <uint32_t D, uint32_t C, int MODE>
+template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD>
 __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
                                         const ge::LevelRows &lr, const uint32_t cell[D],
                                         const double (&cw)[1u << D][C]) {
+    const uint32_t lead = LEAD ? LEAD : lr.lead;
     if constexpr (MODE == 0 && D == 3) {
         // mask form: corner k's row is base + ((i0 + o_k) & wmask) with the
         // cell's tiled index i0 (two multiplies per flush, not per corner) and
@@ -295,7 +298,7 @@ __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, c
         const uint32_t lo = r0 - c.base, n = r1 - r0;
 #pragma unroll
         for (uint32_t k = 0; k < 8u; ++k) {
-            if (k >> lr.lead) continue;
+            if (k >> lead) continue;
             const uint32_t o = (k & 1u) + ((k & 2u) ? lr.m1 : 0u) + ((k & 4u) ? lr.m2 : 0u);
             const uint32_t rel = ((i0 + o) & lr.wmask) - lo;
             if (rel < n) {
@@ -308,7 +311,7 @@ __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, c
     }
 #pragma unroll
     for (uint32_t k = 0; k < (1u << D); ++k) {
-        if (k >> lr.lead) continue;
+        if (k >> lead) continue;
         const uint32_t row = c.base + ge::corner_row_m<D, MODE>(lr, cell, k);
         if (row >= r0 && row < r1) {
             double *dst = acc + (size_t)(row - r0) * C;
@@ -426,11 +429,16 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     const bool align = align_corners != 0;
     const LevelCtx c = ge::level_ctx<D>(offsets, lv, l, gridtype, align);
     const ge::LevelRows lr = ge::level_rows<D>(c);
-    const uint32_t lead = lr.lead;
     const uint32_t M = ge::dyn_count(dyn, B);
     const uint32_t ntiles = ceil_div(M, kTile);
     const grad_t *gl = grad + (size_t)l * B * C;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
+    // the level's lead (corners 2^lead) is uniform over the workgroup: the
+    // walk is instantiated per lead, so the corner loops and the trailing-dim
+    // weights are resolved at compile time (as selects on a runtime lead they
+    // cost two v_cndmask per f64 accumulator per entry)
+    auto tiles = [&](auto lead_c) {
+    constexpr uint32_t lead = decltype(lead_c)::value;
     // part j of P: tiles j, j + P, ...; wave w takes every waves-th of those
     for (uint32_t t = part + P * wave; t < ntiles; t += P * waves) {
         const uint32_t cnt = counts[(size_t)t * nb + b];
@@ -476,7 +484,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                         for (uint32_t d = 0; d < D; ++d)
                             if (d < lead) same = same && (cell[d] == cur[d]);
                         if (!same) {
-                            if (have) flush<D, C, MODE>(acc, r0, r1, c, lr, cur, cw);
+                            if (have) flush<D, C, MODE, lead>(acc, r0, r1, c, lr, cur, cw);
 #pragma unroll
                             for (uint32_t kc = 0; kc < (1u << D); ++kc)
 #pragma unroll
@@ -510,8 +518,12 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
             walk(std::integral_constant<uint32_t, 4>{});
         else
             walk(std::integral_constant<uint32_t, kRun>{});
-        if (have) flush<D, C, MODE>(acc, r0, r1, c, lr, cur, cw);
+        if (have) flush<D, C, MODE, lead>(acc, r0, r1, c, lr, cur, cw);
     }
+    };
+    if (lr.lead >= 3 && D >= 3) tiles(std::integral_constant<uint32_t, (D >= 3 ? 3u : D)>{});
+    else if (lr.lead == 2 && D >= 2) tiles(std::integral_constant<uint32_t, (D >= 2 ? 2u : D)>{});
+    else tiles(std::integral_constant<uint32_t, 1u>{});
     __syncthreads();
     float *out = partial + (size_t)slot * ((size_t)srows * C);
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = (float)acc[i];
