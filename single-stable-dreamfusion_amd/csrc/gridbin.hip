@@ -262,32 +262,32 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
 // ---------------------------------------------------------------- 2. walk
 // Flush one cell's merged corner contributions into the LDS slice [r0, r1).
 template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD>
-__device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
-                                        const ge::LevelRows &lr, const uint32_t cell[D],
-                                        const double (&cw)[1u << D][C]);
+__device__ __forceinline__ void flush_m(double *acc, uint32_t cs, uint32_t r0, uint32_t r1,
+                                        const LevelCtx &c, const ge::LevelRows &lr,
+                                        const uint32_t cell[D], const double (&cw)[1u << D][C]);
 
 constexpr int kModeAny = 3;  // MODE: the corner-row wrap fixed at compile time, or any
 
 // LEAD: the level's corner count exponent (lr.lead) fixed at compile time
 // (the walk dispatches on it once per workgroup), or 0 to read lr.lead
 template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD = 0>
-__device__ __forceinline__ void flush(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
-                                      const ge::LevelRows &lr, const uint32_t cell[D],
-                                      const double (&cw)[1u << D][C]) {
+__device__ __forceinline__ void flush(double *acc, uint32_t cs, uint32_t r0, uint32_t r1,
+                                      const LevelCtx &c, const ge::LevelRows &lr,
+                                      const uint32_t cell[D], const double (&cw)[1u << D][C]) {
     if constexpr (MODE != kModeAny) {
-        flush_m<D, C, MODE, LEAD>(acc, r0, r1, c, lr, cell, cw);
+        flush_m<D, C, MODE, LEAD>(acc, cs, r0, r1, c, lr, cell, cw);
     } else {
         const int mode = ge::row_mode(lr);  // uniform: one scalar branch per flush
-        if (mode == 0) flush_m<D, C, 0, LEAD>(acc, r0, r1, c, lr, cell, cw);
-        else if (mode == 1) flush_m<D, C, 1, LEAD>(acc, r0, r1, c, lr, cell, cw);
-        else flush_m<D, C, 2, LEAD>(acc, r0, r1, c, lr, cell, cw);
+        if (mode == 0) flush_m<D, C, 0, LEAD>(acc, cs, r0, r1, c, lr, cell, cw);
+        else if (mode == 1) flush_m<D, C, 1, LEAD>(acc, cs, r0, r1, c, lr, cell, cw);
+        else flush_m<D, C, 2, LEAD>(acc, cs, r0, r1, c, lr, cell, cw);
     }
 }
 
 template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD>
-__device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, const LevelCtx &c,
-                                        const ge::LevelRows &lr, const uint32_t cell[D],
-                                        const double (&cw)[1u << D][C]) {
+__device__ __forceinline__ void flush_m(double *acc, uint32_t cs, uint32_t r0, uint32_t r1,
+                                        const LevelCtx &c, const ge::LevelRows &lr,
+                                        const uint32_t cell[D], const double (&cw)[1u << D][C]) {
     const uint32_t lead = LEAD ? LEAD : lr.lead;
     if constexpr (MODE == 0 && D == 3) {
         // mask form: corner k's row is base + ((i0 + o_k) & wmask) with the
@@ -302,9 +302,9 @@ __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, c
             const uint32_t o = (k & 1u) + ((k & 2u) ? lr.m1 : 0u) + ((k & 4u) ? lr.m2 : 0u);
             const uint32_t rel = ((i0 + o) & lr.wmask) - lo;
             if (rel < n) {
-                double *dst = acc + (size_t)rel * C;
+                double *dst = acc + rel;
 #pragma unroll
-                for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch, cw[k][ch]);
+                for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch * cs, cw[k][ch]);
             }
         }
         return;
@@ -314,9 +314,9 @@ __device__ __forceinline__ void flush_m(double *acc, uint32_t r0, uint32_t r1, c
         if (k >> lead) continue;
         const uint32_t row = c.base + ge::corner_row_m<D, MODE>(lr, cell, k);
         if (row >= r0 && row < r1) {
-            double *dst = acc + (size_t)(row - r0) * C;
+            double *dst = acc + (row - r0);
 #pragma unroll
-            for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch, cw[k][ch]);
+            for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch * cs, cw[k][ch]);
         }
     }
 }
@@ -424,7 +424,9 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     const uint32_t r0 = bi.base[l] + (k << bi.shift);
     const uint32_t r1 = min(r0 + srows, bi.base[l] + bi.rows[l]);
     const uint32_t n = (r1 - r0) * C;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.0;
+    // channel-major slice image (acc[ch * srows + row]): a wave's f64 adds to
+    // random rows then spread over 32 bank pairs instead of 16 row groups
+    for (uint32_t i = threadIdx.x; i < srows * C; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
     const bool align = align_corners != 0;
     const LevelCtx c = ge::level_ctx<D>(offsets, lv, l, gridtype, align);
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                         for (uint32_t d = 0; d < D; ++d)
                             if (d < lead) same = same && (cell[d] == cur[d]);
                         if (!same) {
-                            if (have) flush<D, C, MODE, lead>(acc, r0, r1, c, lr, cur, cw);
+                            if (have) flush<D, C, MODE, lead>(acc, srows, r0, r1, c, lr, cur, cw);
 #pragma unroll
                             for (uint32_t kc = 0; kc < (1u << D); ++kc)
 #pragma unroll
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
             walk(std::integral_constant<uint32_t, 4>{});
         else
             walk(std::integral_constant<uint32_t, kRun>{});
-        if (have) flush<D, C, MODE, lead>(acc, r0, r1, c, lr, cur, cw);
+        if (have) flush<D, C, MODE, lead>(acc, srows, r0, r1, c, lr, cur, cw);
     }
     };
     if (lr.lead >= 3 && D >= 3) tiles(std::integral_constant<uint32_t, (D >= 3 ? 3u : D)>{});
@@ -526,7 +528,8 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     else tiles(std::integral_constant<uint32_t, 1u>{});
     __syncthreads();
     float *out = partial + (size_t)slot * ((size_t)srows * C);
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = (float)acc[i];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+        out[i] = (float)acc[(i % C) * srows + i / C];
     if (bi.trace) {
         __syncthreads();
         if (threadIdx.x == 0) {
