@@ -327,6 +327,9 @@ REGION_KERNELS = {
 }
 
 
+MEASURE_TRAFFIC_DETAIL = {}  # region -> per-kernel bytes of the last measure_traffic
+
+
 def measure_traffic(region, timeout=180):
     """HBM bytes per launch of timed region `region`, measured now: two
     rocprofv3 passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE, kernel-trace
@@ -342,7 +345,11 @@ def measure_traffic(region, timeout=180):
     rp = shutil.which("rocprofv3")
     if rp is None:
         return None, "rocprofv3 not on PATH"
-    child = [sys.executable, str(Path(__file__).resolve()), "--steps", "3", "--warmup", "3",
+    # the child warms up as long as the timed run does (the occupancy grid, and
+    # with it M, settles over the first refreshes); only its last `keep`
+    # dispatches of each kernel are averaged
+    keep = 3
+    child = [sys.executable, str(Path(__file__).resolve()), "--steps", str(keep), "--warmup", "10",
              "--no-cpu-baseline", "--no-kernel-timing", "--no-alt-backward", "--no-shading",
              "--no-infer", "--no-traffic", "--no-c5"]
     env = {k: v for k, v in os.environ.items()
@@ -371,16 +378,23 @@ def measure_traffic(region, timeout=180):
                 for i, alts in enumerate(pats):
                     alts = (alts,) if isinstance(alts, str) else alts
                     if any(a in r["Kernel_Name"] for a in alts):
-                        sums.setdefault(i, []).append(float(r["Counter_Value"]))
+                        key = int(r.get("Dispatch_Id", len(sums.get(i, []))) or 0)
+                        sums.setdefault(i, []).append((key, float(r["Counter_Value"])))
+        sums = {i: [v for _, v in sorted(vs)[-keep:]] for i, vs in sums.items()}
         if len(sums) != len(pats):
             return None, f"{counter}: not every kernel of {region} was profiled"
         scale = 2.0 if counter == "FETCH_SIZE" else 1.0
-        per[counter] = sum(scale * 1024.0 * sum(v) / len(v) for v in sums.values())
+        per[counter] = {i: scale * 1024.0 * sum(v) / len(v) for i, v in sums.items()}
     shutil.rmtree(tmp, ignore_errors=True)
-    return int(per["FETCH_SIZE"] + per["WRITE_SIZE"]), (
+    total = sum(per["FETCH_SIZE"].values()) + sum(per["WRITE_SIZE"].values())
+    names = [a if isinstance(a, str) else a[0] for a in pats]
+    MEASURE_TRAFFIC_DETAIL[region] = {
+        names[i]: {"fetch_x2": int(per["FETCH_SIZE"][i]), "write": int(per["WRITE_SIZE"][i])}
+        for i in range(len(pats))}
+    return int(total), (
         "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs) of "
-        "a 3+3-step child bench; FETCH_SIZE x2 (gfx950), KiB -> bytes, summed over the region's "
-        "kernels, mean per launch")
+        "a 10 + 3-step child bench, the last 3 dispatches of each kernel; FETCH_SIZE x2 "
+        "(gfx950), KiB -> bytes, summed over the region's kernels, mean per launch")
 
 
 def _free_port():
@@ -519,7 +533,8 @@ def main():
         result["roofline"] = {
             "kernel": dom, "bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
-            "traffic": traffic, "traffic_source": note, "avg_us": kd["avg_us"],
+            "traffic": traffic, "traffic_source": note,
+            "traffic_by_kernel": MEASURE_TRAFFIC_DETAIL.get(dom), "avg_us": kd["avg_us"],
             "bytes_per_launch": kd["bytes_per_launch"]}
         if dom == "grid_encode_backward":
             # the binned backward's real ceiling: one f64 LDS add per (sample,
