@@ -1,0 +1,57 @@
+"""C4 fused inference renderer (csrc/render.hip k_render_infer) on the bench's
+800x800 scene (tools for timing studies / PMC passes):
+    python tools/infer_case.py [--reps 10] [--res 800]"""
+import argparse
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (str(ROOT), str(ROOT / "single-stable-dreamfusion_amd")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--res", type=int, default=800)
+    args = ap.parse_args()
+    import main as m
+    from nerf.network_grid import NeRFNetwork
+    from nerf.provider import NeRFDataset
+    dev = torch.device("cuda")
+    opt = m.parse_opt(["--text", "a hamburger", "-O", "--h", str(args.res), "--w", str(args.res)])
+    torch.manual_seed(1)
+    model = NeRFNetwork(opt).to(dev)
+    with torch.no_grad():
+        model.encoder.embeddings.uniform_(-0.5, 0.5)
+    with torch.autocast("cuda", dtype=torch.float16):
+        for _ in range(3):
+            model.update_extra_state()
+    model.eval()
+    model.native_infer = True
+    data = NeRFDataset(opt, device=dev, type="test", H=args.res, W=args.res, size=8).collate([1])
+
+    def frame():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            return model.render(data["rays_o"], data["rays_d"], staged=True, perturb=False,
+                                light_d=None, ambient_ratio=1.0, shading="albedo",
+                                force_all_rays=True, bg_color=None, **vars(opt))
+    for _ in range(3):
+        out = frame()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.reps):
+        frame()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.reps
+    img = out["image"].float()
+    print(f"res={args.res} ms_per_frame={ms:.3f} image_mean={float(img.mean()):.6f} "
+          f"ws_mean={float(out['weights_sum'].float().mean()):.6f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
