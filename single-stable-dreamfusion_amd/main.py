@@ -97,6 +97,8 @@ def main(argv=None):
         loader = NeRFDataset(opt, device=device, type="test", H=opt.H, W=opt.W, size=100).dataloader()
         for data in loader:
             trainer.test_step(data)
+        if opt.save_mesh:
+            trainer.save_mesh(resolution=256)  # main.py:121-122
         return
     train_loader = NeRFDataset(opt, device=device, type="train", H=opt.h, W=opt.w,
                                size=100).dataloader()
@@ -116,6 +118,8 @@ def main(argv=None):
                       scheduler_update_every_step=True)
     max_epoch = int(np.ceil(opt.iters / len(train_loader)))
     trainer.train(train_loader, None, max_epoch)
+    if opt.save_mesh:
+        trainer.save_mesh(resolution=256)  # main.py:161-162
 
 
 if __name__ == "__main__":

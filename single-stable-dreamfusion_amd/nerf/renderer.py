@@ -133,9 +133,12 @@ class NeRFRenderer(nn.Module):
 
     @torch.no_grad()
     def export_mesh(self, path, resolution=None, S=128):
-        # renderer.py:121-299 needs mcubes / xatlas / nvdiffrast, none of
-        # which exist on this platform.
-        raise NotImplementedError("export_mesh needs mcubes/xatlas/nvdiffrast (not available)")
+        """renderer.py:121-299: density on a resolution^3 lattice, isosurface at
+        min(mean_density, density_thresh), `mesh.obj` under `path`.  mcubes /
+        xatlas / nvdiffrast do not exist here: marching tetrahedra and vertex
+        colours instead (nerf/mesh.py)."""
+        from .mesh import export_mesh
+        return export_mesh(self, path, resolution=resolution, S=S)
 
     def _bg(self, rays_d, bg_color):
         if self.bg_radius > 0:

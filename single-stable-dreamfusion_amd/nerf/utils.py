@@ -565,6 +565,16 @@ class Trainer(object):
         return out["image"].reshape(B, H, W, 3), out["depth"].reshape(B, H, W)
 
     # ------------------------------------------------------------ checkpoints
+    def save_mesh(self, save_path=None, resolution=128):
+        """utils.py:459-470: export the density isosurface under
+        `workspace/mesh` (NeRFRenderer.export_mesh, nerf/mesh.py)."""
+        if save_path is None:
+            save_path = os.path.join(self.workspace, "mesh")
+        self.log(f"==> Saving mesh to {save_path}")
+        os.makedirs(save_path, exist_ok=True)
+        self.model.export_mesh(save_path, resolution=resolution)
+        self.log("==> Finished saving mesh.")
+
     def save_checkpoint(self, name=None, full=False, best=False):
         """Same checkpoint dict layout as the reference (utils.py:847-902)."""
         if name is None:
