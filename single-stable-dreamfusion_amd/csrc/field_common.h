@@ -28,6 +28,9 @@ constexpr int kOffW1 = 0, kOffB1 = kOffW1 + kHid * kIn, kOffW2 = kOffB1 + kHid,
 // Field element type T: f16 (the reference's fp16 autocast, C2) or bf16 (the
 // C5 option: bf16 autocast, new in this build).  Operand vectors of T and
 // the matching gfx950 MFMAs (v_mfma_f32_16x16x32_{f16,bf16}).
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 template <typename T> struct Elem;
 template <> struct Elem<half_t> { typedef half8 v8; typedef half4 v4; };
 template <> struct Elem<bf16_t> { typedef bf8 v8; typedef bf4 v4; };
@@ -324,6 +327,14 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
             typedef typename std::conditional<std::is_same<E, half_t>::value, half_t, float>::type
                 acc_t;
             acc_t a0 = (acc_t)0.0f, a1 = (acc_t)0.0f;
+            // f16: both channels at once, c10::Half's two roundings per corner:
+            // p = Half(w * float(g)) as v_pk_mul_f32 + v_cvt_pk_f16_f32 (the
+            // value barrier keeps them from fusing into one rounding), then
+            // r = Half(float(r) + float(p)) as v_pk_add_f16 — f32 holds
+            // 24 >= 2 x 11 + 2 bits, so rounding the f32 sum again to f16
+            // equals the correctly rounded f16 add (double rounding is
+            // innocuous at that precision)
+            half2v acc2 = half2v{(half_t)0.0f, (half_t)0.0f};
 #pragma unroll
             for (uint32_t c = 0; c < 8; ++c) {
                 float w = 1.0f;
@@ -332,12 +343,17 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                 E v[2];
                 __builtin_memcpy(v, &bits[qq][c], 4);
                 if constexpr (std::is_same<E, half_t>::value) {
-                    ge::acc_corner(a0, w, v[0]);
-                    ge::acc_corner(a1, w, v[1]);
+                    f2v prod = f2v{w, w} * f2v{(float)v[0], (float)v[1]};
+                    asm("" : "+v"(prod));
+                    acc2 += __builtin_convertvector(prod, half2v);
                 } else {
                     a0 = fmaf(w, (float)v[0], a0);
                     a1 = fmaf(w, (float)v[1], a1);
                 }
+            }
+            if constexpr (std::is_same<E, half_t>::value) {
+                a0 = acc2[0];
+                a1 = acc2[1];
             }
             const int q = 2 * half + qq;
             if constexpr (std::is_same<E, half_t>::value) {
