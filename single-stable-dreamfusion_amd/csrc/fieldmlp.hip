@@ -345,38 +345,44 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
         //   wave 0 / 1: W2 rows tn in {0,1} / {2,3} x 4 column tiles, b2 rows tn
         //   wave 2 / 3: W1 rows tn in {0,1} / {2,3} x 2 feature tiles, b1 rows tn,
         //               W3 columns tm in {0,1} / {2,3}; wave 2 also b3
+        // k = 32 samples per MFMA (v_mfma_f32_16x16x32, the full-rate form on
+        // gfx950): operand element jj of lane group g is sample row 4g + (jj & 3)
+        // of stage st + (jj >> 2) — two transposed reads, the same map for both
+        // operands
+        auto tr2 = [&](int st, int c0) {
+            const v4 lo = tr_operand(stage[st], c0, lane);
+            const v4 hi = tr_operand(stage[st + 1], c0, lane);
+            return (v8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        };
+        const v8 ones8 = __builtin_shufflevector(ones, ones, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
-        for (int st = 0; st < kBwdWaves; ++st) {
-            const StageT<E> &X = stage[st];
+        for (int st = 0; st < kBwdWaves; st += 2) {
             if (wave < 2) {
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int tn = 2 * wave + k;
-                    const v4 a = tr_operand(X, kColD2 + 16 * tn, lane);
+                    const v8 a = tr2(st, kColD2 + 16 * tn);
 #pragma unroll
                     for (int tm = 0; tm < 4; ++tm)
-                        acc[5 * k + tm] = mfma16(a, tr_operand(X, kColA1 + 16 * tm, lane),
-                                                 acc[5 * k + tm]);
-                    acc[5 * k + 4] = mfma16(a, ones, acc[5 * k + 4]);
+                        acc[5 * k + tm] = mfma(a, tr2(st, kColA1 + 16 * tm), acc[5 * k + tm]);
+                    acc[5 * k + 4] = mfma(a, ones8, acc[5 * k + 4]);
                 }
             } else {
                 const int w2i = wave - 2;
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int tn = 2 * w2i + k;
-                    const v4 a = tr_operand(X, kColD1 + 16 * tn, lane);
+                    const v8 a = tr2(st, kColD1 + 16 * tn);
 #pragma unroll
                     for (int tf = 0; tf < 2; ++tf)
-                        acc[3 * k + tf] = mfma16(a, tr_operand(X, kColX + 16 * tf, lane),
-                                                 acc[3 * k + tf]);
-                    acc[3 * k + 2] = mfma16(a, ones, acc[3 * k + 2]);
+                        acc[3 * k + tf] = mfma(a, tr2(st, kColX + 16 * tf), acc[3 * k + tf]);
+                    acc[3 * k + 2] = mfma(a, ones8, acc[3 * k + 2]);
                 }
-                const v4 ao = tr_operand(X, kColDO, lane);
+                const v8 ao = tr2(st, kColDO);
 #pragma unroll
                 for (int k = 0; k < 2; ++k)
-                    acc[6 + k] = mfma16(ao, tr_operand(X, kColA2 + 16 * (2 * w2i + k), lane),
-                                        acc[6 + k]);
-                if (wave == 2) acc[8] = mfma16(ao, ones, acc[8]);
+                    acc[6 + k] = mfma(ao, tr2(st, kColA2 + 16 * (2 * w2i + k)), acc[6 + k]);
+                if (wave == 2) acc[8] = mfma(ao, ones8, acc[8]);
             }
         }
         __syncthreads();  // the images are rewritten next round
