@@ -175,6 +175,24 @@ __device__ __forceinline__ void slice_mask(const ge::LevelRows &lr, const uint32
                                            uint32_t shift, uint64_t (&mask)[W]) {
 #pragma unroll
     for (uint32_t h = 0; h < W; ++h) mask[h] = 0;
+    if constexpr (MODE == 0 && D == 3) {
+        // mask form (as the walk's flush): the cell's tiled index once, the
+        // corner offsets {0, 1, m1, m1 + 1, m2, ...} uniform
+        const uint32_t i0 = cell[0] + cell[1] * lr.m1 + cell[2] * lr.m2;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) {
+            if (k >> lr.lead) continue;
+            const uint32_t o = (k & 1u) + ((k & 2u) ? lr.m1 : 0u) + ((k & 4u) ? lr.m2 : 0u);
+            const uint32_t v = ((i0 + o) & lr.wmask) >> shift;
+            if constexpr (W == 1) {
+                mask[0] |= 1ull << v;
+            } else {
+                if (v < 64) mask[0] |= 1ull << v;
+                else mask[1] |= 1ull << (v - 64);
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (uint32_t k = 0; k < (1u << D); ++k) {
         if (k >> lr.lead) continue;
