@@ -26,14 +26,23 @@ def embedding_window(d_enc, d_enc_win, x01, offsets, S, H):
 
 
 def check_field(xyz, emb, offsets, S, H, weights, sigma, albedo, grad_sigma=None,
-                grad_albedo16=None, grads=None, grad_emb=None, label=""):
+                grad_albedo16=None, grads=None, grad_emb=None, label="", bf16=False):
     """Compare one GPU field evaluation (and optionally its backward) with the
     oracle.  Arrays are numpy; weights = the six f32 MLP tensors; grads = the
-    six GPU gradients; grad_emb = the GPU embedding gradient.  Returns a dict
-    of statistics (printed by the callers)."""
+    six GPU gradients; grad_emb = the GPU embedding gradient.  bf16: the bf16
+    autocast restatement (oracle.field.precision("bf16"); albedo and
+    grad_albedo16 then hold bf16 values as f32).  Returns a dict of
+    statistics (printed by the callers)."""
+    with of.precision("bf16" if bf16 else "f16"):
+        return _check_field(xyz, emb, offsets, S, H, weights, sigma, albedo, grad_sigma,
+                            grad_albedo16, grads, grad_emb, label, bf16)
+
+
+def _check_field(xyz, emb, offsets, S, H, weights, sigma, albedo, grad_sigma, grad_albedo16,
+                 grads, grad_emb, label, bf16):
     M = xyz.shape[0]
     stats = {"M": M}
-    x16 = of.encode(xyz, 1.0, emb, offsets, S, H)
+    x16 = (of.encode_bf16 if bf16 else of.encode)(xyz, 1.0, emb, offsets, S, H)
     fo = of.field_forward(xyz, weights, x16)
     fb = of.forward_bounds(fo, weights, acc_ulps=MFMA_ULPS)
     dlog = np.abs(np.log(sigma.astype(np.float64)) - np.log(fo["sigma"].astype(np.float64)))
@@ -49,8 +58,10 @@ def check_field(xyz, emb, offsets, S, H, weights, sigma, albedo, grad_sigma=None
         return stats
     bo = of.field_backward(fo, weights, grad_sigma, grad_albedo16)
     bb = of.backward_bounds(fo, bo, weights, fb, acc_ulps=None)
-    sub = np.abs(bo["d_enc"].astype(np.float64)) < 2.0 ** -14
-    d_win = bb["d_enc"] + np.where(sub, 2.0 ** -24, 0.0)  # see test_gpu_field_oracle.py
+    d_win = bb["d_enc"]
+    if not bf16:  # f16 subnormal allowance, see test_gpu_field_oracle.py
+        sub = np.abs(bo["d_enc"].astype(np.float64)) < 2.0 ** -14
+        d_win = d_win + np.where(sub, 2.0 ** -24, 0.0)
     for i, (a, b, w) in enumerate(zip(grads, bo["grads"], bb["grads"])):
         a = np.asarray(a, np.float64).reshape(b.shape)
         err = np.abs(a - b)

@@ -22,8 +22,10 @@ def _field(gpu, seed=0, emb_scale=0.5):
     return enc, layers
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("M", [1, 31, 50_003])
-def test_fused_field_matches_oracle(gpu, M):
+def test_fused_field_matches_oracle(gpu, M, dtype):
+    """fp16 autocast (the reference's -O) and bf16 autocast (the C5 option)."""
     from nerf.field import eligible, grid_field
     from oracle_checks import check_field
     enc, layers = _field(gpu)
@@ -31,10 +33,12 @@ def test_fused_field_matches_oracle(gpu, M):
     x = (torch.rand(M, 3, generator=g) * 2 - 1).mul_(0.9).to(gpu)
     gs = (torch.randn(M, generator=g) * 1e-2).to(gpu)
     ga = (torch.randn(M, 3, generator=g) * 1e-2).to(gpu)
-    with torch.autocast("cuda", dtype=torch.float16):
+    with torch.autocast("cuda", dtype=dtype):
         assert eligible(enc, layers, x)
         s1, a1 = grid_field(x, 1.0, enc, layers)
-    assert s1.dtype == torch.float32 and a1.dtype == torch.float16
+    assert s1.dtype == torch.float32 and a1.dtype == dtype
+    bf16 = dtype == torch.bfloat16
+    ga_np = ga.to(dtype).float().cpu().numpy() if bf16 else ga.cpu().numpy().astype(np.float16)
     params = [enc.embeddings] + list(layers.parameters())
     g1 = torch.autograd.grad((s1 * gs).sum() + (a1.float() * ga).sum(), params)
     for t in g1:
@@ -42,9 +46,10 @@ def test_fused_field_matches_oracle(gpu, M):
     ws = [p.detach().float().cpu().numpy() for p in layers.parameters()]
     stats = check_field(x.cpu().numpy(), enc.embeddings.detach().cpu().numpy(),
                         enc.offsets.cpu().numpy(), float(np.log2(enc.per_level_scale)), 16, ws,
-                        s1.detach().cpu().numpy(), a1.detach().cpu().numpy(),
-                        gs.cpu().numpy(), ga.cpu().numpy().astype(np.float16),
-                        [t.cpu().numpy() for t in g1[1:]], g1[0].cpu().numpy(), label=f"M={M}")
+                        s1.detach().cpu().numpy(), a1.detach().float().cpu().numpy(),
+                        gs.cpu().numpy(), ga_np,
+                        [t.cpu().numpy() for t in g1[1:]], g1[0].cpu().numpy(),
+                        label=f"M={M} {dtype}", bf16=bf16)
     print(stats)
 
 
