@@ -630,6 +630,19 @@ int dfhip_shading_backward(const float *sigma7, const void *albedo7, const float
                            const int32_t *m_dev, uint32_t cap, const float *grad_sigma,
                            const void *grad_color, const float *grad_loss, float lambda_orient,
                            float *grad_sigma7, void *grad_albedo7, dfhip_stream_t stream);
+/* bf16 forms (bf16 autocast, the C5 option): albedo7 / color / grad_color /
+ * grad_albedo7 are bf16 and the autocast rounding points round to bf16. */
+int dfhip_shading_forward_bf16(const float *sigma7, const void *albedo7, const float *dirs,
+                               const float *light, float ratio, float eps, int shading,
+                               const int32_t *m_dev, uint32_t cap, float *sigma, void *color,
+                               float *normal, double *partial, float lambda_orient,
+                               float *orient, float *loss, dfhip_stream_t stream);
+int dfhip_shading_backward_bf16(const float *sigma7, const void *albedo7, const float *dirs,
+                                const float *light, float ratio, float eps, int shading,
+                                const int32_t *m_dev, uint32_t cap, const float *grad_sigma,
+                                const void *grad_color, const float *grad_loss,
+                                float lambda_orient, float *grad_sigma7, void *grad_albedo7,
+                                dfhip_stream_t stream);
 /* The step's light direction safe_normalize(rays_o[0] + randn(3))
  * (renderer.py:462-464), drawn from Philox keyed by (seed, step). */
 int dfhip_shading_light(const float *rays_o, uint64_t seed, uint64_t step, float *light,

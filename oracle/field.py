@@ -465,20 +465,20 @@ def shade_forward(sigma, sig_pm, albedo16, dirs, light, ratio, shading, eps=1e-2
     # normal @ l: f16 operands (products exact), f32 sum, f16 result
     p = r16(n).astype(F64) * l16[None, :]
     d16 = r16(((p[:, 0] + p[:, 1]) + p[:, 2]).astype(F32))
-    c16 = np.maximum(d16, F16(0)).astype(F32)
+    c16 = np.maximum(d16.astype(F32), F32(0))
     omr = F32(1.0 - float(ratio))
     lam16 = r16(F32(ratio) + r16(c16 * omr).astype(F32))
     if shading == "textureless":
         color = np.repeat(lam16[:, None], 3, 1)
     else:  # lambertian
-        color = r16(np.asarray(albedo16, F16).astype(F32) * lam16.astype(F32)[:, None])
+        color = r16(np.asarray(albedo16).astype(_vd()).astype(F32) * lam16.astype(F32)[:, None])
     w = (F32(1) - np.exp(-np.asarray(sigma, F32).astype(F64)).astype(F32)).astype(F32)
     d = np.asarray(dirs, F32)
     nd = ((n[:, 0] * d[:, 0] + n[:, 1] * d[:, 1]) + n[:, 2] * d[:, 2]).astype(F32)
     c = np.maximum(nd, F32(0))
     orient = (w * (c * c)).astype(F32)
     return {"v": v, "normal": n, "ss": ss, "r": r, "nan": nan, "d16": d16, "lam16": lam16,
-            "color": color.astype(F16), "w": w, "nd": nd, "orient": orient, "l16": l16}
+            "color": color.astype(_vd()), "w": w, "nd": nd, "orient": orient, "l16": l16}
 
 
 def padded_rows(m):
@@ -492,13 +492,13 @@ def shade_backward(fwd, albedo16, dirs, grad_color16, grad_loss, lam_orient, m_r
     [M, 3] and the loss-scale upstream grad_loss of lam_orient * mean(orient)
     over m_rows (= M').  Returns (grad_sig_pm [6, M] f32, grad_albedo16 [M, 3]
     f16 or None)."""
-    g = np.asarray(grad_color16, F16).astype(F32)
+    g = np.asarray(grad_color16).astype(_vd()).astype(F32)
     lam = fwd["lam16"].astype(F32)
     ga = None
     if shading == "textureless":
         glam = r16((g[:, 0] + g[:, 1]) + g[:, 2]).astype(F32)
     else:
-        a = np.asarray(albedo16, F16).astype(F32)
+        a = np.asarray(albedo16).astype(_vd()).astype(F32)
         ga = r16(g * lam[:, None])
         gl = r16(g * a).astype(F32)
         glam = r16((gl[:, 0] + gl[:, 1]) + gl[:, 2]).astype(F32)

@@ -93,6 +93,10 @@ _SIGS = {
                               _vp, _f32, _vp, _vp, _vp],
     "dfhip_shading_backward": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp, _vp,
                                _f32, _vp, _vp, _vp],
+    "dfhip_shading_forward_bf16": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp,
+                                   _vp, _vp, _f32, _vp, _vp, _vp],
+    "dfhip_shading_backward_bf16": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp,
+                                    _vp, _f32, _vp, _vp, _vp],
     "dfhip_shading_light": [_vp, _u64, _u64, _vp, _vp],
     "dfhip_grid_field_forward_bf16": [_vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,

@@ -25,8 +25,11 @@
 // to f16), the gradients of the f16 tensors rounded to f16 where autograd
 // would hold them in f16.  Loss-scale handling follows autograd: the
 // orientation term's gradient carries the GradScaler scale, as the entropy
-// term's does.
+// term's does.  Under bf16 autocast (the C5 option) the same rounding points
+// round to bf16 (the kernels are instantiated on the element type E).
 #include "common.h"
+
+#include <type_traits>
 
 #include <math.h>
 
@@ -36,7 +39,9 @@ namespace shd {
 constexpr int kStencil = 6;
 constexpr uint32_t kThreads = 256;
 
-__device__ __forceinline__ float r16(float x) { return (float)(half_t)f32_rounded(x); }
+// round to the autocast element type E (f16 or bf16), through an f32 value
+template <typename E>
+__device__ __forceinline__ float rnd(float x) { return (float)(E)f32_rounded(x); }
 
 __device__ __forceinline__ uint32_t live(const int32_t *m_dev, uint32_t cap) {
     const int32_t m = *m_dev;
@@ -103,51 +108,55 @@ __device__ __forceinline__ Normal fd_normal(const float *__restrict__ sigma7, ui
     return o;
 }
 
-// (normal @ l) under autocast: f16 operands, f32 accumulation, f16 result
+// (normal @ l) under autocast: E operands, f32 accumulation, E result
+template <typename E>
 __device__ __forceinline__ float dot16(const float n[3], const float l16[3]) {
-    const float p0 = r16(n[0]) * l16[0], p1 = r16(n[1]) * l16[1], p2 = r16(n[2]) * l16[2];
-    return r16((p0 + p1) + p2);
+    const float p0 = rnd<E>(n[0]) * l16[0], p1 = rnd<E>(n[1]) * l16[1],
+                p2 = rnd<E>(n[2]) * l16[2];
+    return rnd<E>((p0 + p1) + p2);
 }
 
 struct Shade {
     float d16, lam16;
 };
 
+template <typename E>
 __device__ __forceinline__ Shade lambert(const float n[3], const float l16[3], float ratio,
                                          float omr) {
     Shade s;
-    s.d16 = dot16(n, l16);
-    const float c16 = s.d16 > 0.0f ? s.d16 : 0.0f;  // clamp(min=0)
-    s.lam16 = r16(ratio + r16(c16 * omr));          // ratio + (1 - ratio) * c
+    s.d16 = dot16<E>(n, l16);
+    const float c16 = s.d16 > 0.0f ? s.d16 : 0.0f;     // clamp(min=0)
+    s.lam16 = rnd<E>(ratio + rnd<E>(c16 * omr));       // ratio + (1 - ratio) * c
     return s;
 }
 
 // Forward: the samples' density (f32) and colour (f16) for the compositing,
 // the normal (f32, kept for the backward) and per-block partial sums of the
 // orientation term (f64).  sigma7 / albedo7: the field on the 7 M rows.
+template <typename E>
 __global__ __launch_bounds__(kThreads) void k_shade_fwd(
-    const float *__restrict__ sigma7, const half_t *__restrict__ albedo7,
+    const float *__restrict__ sigma7, const E *__restrict__ albedo7,
     const float *__restrict__ dirs, const float *__restrict__ light, float ratio, float omr,
     float eps, int lambertian, const int32_t *__restrict__ m_dev, uint32_t cap,
-    float *__restrict__ sigma, half_t *__restrict__ color, float *__restrict__ normal,
+    float *__restrict__ sigma, E *__restrict__ color, float *__restrict__ normal,
     double *__restrict__ part) {
     __shared__ double red[kThreads / 64];
     const uint32_t M = live(m_dev, cap);
     float l16[3];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) l16[d] = r16(light[d]);
+    for (int d = 0; d < 3; ++d) l16[d] = rnd<E>(light[d]);
     double acc = 0.0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
         const Normal nm = fd_normal(sigma7, i, eps);
-        const Shade sh = lambert(nm.n, l16, ratio, omr);
+        const Shade sh = lambert<E>(nm.n, l16, ratio, omr);
         const float sg = sigma7[7 * (size_t)i];
         sigma[i] = sg;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             normal[3 * (size_t)i + d] = nm.n[d];
-            const float c = lambertian ? r16((float)albedo7[21 * (size_t)i + d] * sh.lam16)
+            const float c = lambertian ? rnd<E>((float)albedo7[21 * (size_t)i + d] * sh.lam16)
                                        : sh.lam16;
-            color[3 * (size_t)i + d] = (half_t)c;
+            color[3 * (size_t)i + d] = (E)c;
         }
         // orientation term: (1 - exp(-sigma)) * clamp(n . d, min=0)^2
         const float w = 1.0f - expf(-sg);
@@ -189,23 +198,24 @@ __global__ __launch_bounds__(64) void k_orient_finish(const double *__restrict__
 // gradients grad_sigma7 [7 M] (sample rows: the compositing's, stencil rows:
 // through the normal) and grad_albedo7 [7 M, 3] (sample rows: the lambertian
 // product's albedo gradient, else 0; stencil rows 0).
+template <typename E>
 __global__ __launch_bounds__(kThreads) void k_shade_bwd(
-    const float *__restrict__ sigma7, const half_t *__restrict__ albedo7,
+    const float *__restrict__ sigma7, const E *__restrict__ albedo7,
     const float *__restrict__ dirs, const float *__restrict__ light, float ratio, float omr,
     float eps, int lambertian, const int32_t *__restrict__ m_dev, uint32_t cap,
-    const float *__restrict__ grad_sigma, const half_t *__restrict__ grad_color,
+    const float *__restrict__ grad_sigma, const E *__restrict__ grad_color,
     const float *__restrict__ grad_loss, float lambda, float *__restrict__ grad_sigma7,
-    half_t *__restrict__ grad_albedo7) {
+    E *__restrict__ grad_albedo7) {
     const uint32_t M = live(m_dev, cap);
     float l16[3];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) l16[d] = r16(light[d]);
+    for (int d = 0; d < 3; ++d) l16[d] = rnd<E>(light[d]);
     // d loss / d orient_i: (scale * lambda) / M' (MulBackward, MeanBackward)
     const float go = (grad_loss[0] * lambda) / padded_rows(M);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
         const Normal nm = fd_normal(sigma7, i, eps);
-        const Shade sh = lambert(nm.n, l16, ratio, omr);
-        half_t *ga = grad_albedo7 + 21 * (size_t)i;
+        const Shade sh = lambert<E>(nm.n, l16, ratio, omr);
+        E *ga = grad_albedo7 + 21 * (size_t)i;
         float g[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) g[d] = (float)grad_color[3 * (size_t)i + d];
@@ -215,20 +225,20 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
                 const float a = (float)albedo7[21 * (size_t)i + d];
-                ga[d] = (half_t)r16(g[d] * sh.lam16);
-                gl[d] = r16(g[d] * a);
+                ga[d] = (E)rnd<E>(g[d] * sh.lam16);
+                gl[d] = rnd<E>(g[d] * a);
             }
-            glam = r16((gl[0] + gl[1]) + gl[2]);  // sum over the broadcast dim
+            glam = rnd<E>((gl[0] + gl[1]) + gl[2]);  // sum over the broadcast dim
         } else {
 #pragma unroll
-            for (int d = 0; d < 3; ++d) ga[d] = (half_t)0.0f;
-            glam = r16((g[0] + g[1]) + g[2]);  // RepeatBackward
+            for (int d = 0; d < 3; ++d) ga[d] = (E)0.0f;
+            glam = rnd<E>((g[0] + g[1]) + g[2]);  // RepeatBackward
         }
-        const float gc = r16(glam * omr);                 // (1 - ratio) * c
+        const float gc = rnd<E>(glam * omr);              // (1 - ratio) * c
         const float gd = sh.d16 >= 0.0f ? gc : 0.0f;      // clamp(min=0)
         float gn[3];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) gn[d] = r16(gd * l16[d]);  // mv backward (f16), cast back
+        for (int d = 0; d < 3; ++d) gn[d] = rnd<E>(gd * l16[d]);  // mv backward (E), cast back
         // orientation term: d/dn of go * w * clamp(n . d, 0)^2
         const float w = 1.0f - expf(-sigma7[7 * (size_t)i]);
         const float dx = dirs[3 * (size_t)i], dy = dirs[3 * (size_t)i + 1],
@@ -259,7 +269,7 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
         }
         // the stencil rows carry no albedo gradient
 #pragma unroll
-        for (int k = 3; k < 21; ++k) ga[k] = (half_t)0.0f;
+        for (int k = 3; k < 21; ++k) ga[k] = (E)0.0f;
     }
 }
 
@@ -339,13 +349,13 @@ static bool shading_mode(const char *name, int shading, int &lambertian) {
     return true;
 }
 
-extern "C" int dfhip_shading_forward(const float *sigma7, const void *albedo7, const float *dirs,
-                                     const float *light, float ratio, float eps, int shading,
-                                     const int32_t *m_dev, uint32_t cap, float *sigma,
-                                     void *color, float *normal, double *partial,
-                                     float lambda_orient, float *orient, float *loss,
-                                     dfhip_stream_t stream) {
-    const char *name = "shading_forward";
+// elem: DFHIP_F16 (fp16 autocast) or DFHIP_BF16 (bf16 autocast) for the
+// albedo / colour tensors and the rounding points
+static int shading_forward(const char *name, int elem, const float *sigma7, const void *albedo7,
+                           const float *dirs, const float *light, float ratio, float eps,
+                           int shading, const int32_t *m_dev, uint32_t cap, float *sigma,
+                           void *color, float *normal, double *partial, float lambda_orient,
+                           float *orient, float *loss, dfhip_stream_t stream) {
     int lam = 0;
     if (!shading_mode(name, shading, lam)) return DFHIP_EINVAL;
     if (!sigma7 || !albedo7 || !dirs || !light || !m_dev || !sigma || !color || !normal ||
@@ -356,12 +366,67 @@ extern "C" int dfhip_shading_forward(const float *sigma7, const void *albedo7, c
     hipStream_t s = as_stream(stream);
     const uint32_t blocks = shade_blocks(cap);
     const float omr = (float)(1.0 - (double)ratio);
-    shd::k_shade_fwd<<<blocks, shd::kThreads, 0, s>>>(sigma7, (const half_t *)albedo7, dirs,
-                                                      light, ratio, omr, eps, lam, m_dev, cap,
-                                                      sigma, (half_t *)color, normal, partial);
+    if (elem == DFHIP_BF16)
+        shd::k_shade_fwd<bf16_t><<<blocks, shd::kThreads, 0, s>>>(
+            sigma7, (const bf16_t *)albedo7, dirs, light, ratio, omr, eps, lam, m_dev, cap, sigma,
+            (bf16_t *)color, normal, partial);
+    else
+        shd::k_shade_fwd<half_t><<<blocks, shd::kThreads, 0, s>>>(
+            sigma7, (const half_t *)albedo7, dirs, light, ratio, omr, eps, lam, m_dev, cap, sigma,
+            (half_t *)color, normal, partial);
     shd::k_orient_finish<<<1, 64, 0, s>>>(partial, blocks, m_dev, cap, lambda_orient, orient,
                                           loss);
     return check_launch(name);
+}
+
+static int shading_backward(const char *name, int elem, const float *sigma7,
+                            const void *albedo7, const float *dirs, const float *light,
+                            float ratio, float eps, int shading, const int32_t *m_dev,
+                            uint32_t cap, const float *grad_sigma, const void *grad_color,
+                            const float *grad_loss, float lambda_orient, float *grad_sigma7,
+                            void *grad_albedo7, dfhip_stream_t stream) {
+    int lam = 0;
+    if (!shading_mode(name, shading, lam)) return DFHIP_EINVAL;
+    if (!sigma7 || !albedo7 || !dirs || !light || !m_dev || !grad_sigma || !grad_color ||
+        !grad_loss || !grad_sigma7 || !grad_albedo7) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    const float omr = (float)(1.0 - (double)ratio);
+    hipStream_t s = as_stream(stream);
+    if (elem == DFHIP_BF16)
+        shd::k_shade_bwd<bf16_t><<<shade_blocks(cap), shd::kThreads, 0, s>>>(
+            sigma7, (const bf16_t *)albedo7, dirs, light, ratio, omr, eps, lam, m_dev, cap,
+            grad_sigma, (const bf16_t *)grad_color, grad_loss, lambda_orient, grad_sigma7,
+            (bf16_t *)grad_albedo7);
+    else
+        shd::k_shade_bwd<half_t><<<shade_blocks(cap), shd::kThreads, 0, s>>>(
+            sigma7, (const half_t *)albedo7, dirs, light, ratio, omr, eps, lam, m_dev, cap,
+            grad_sigma, (const half_t *)grad_color, grad_loss, lambda_orient, grad_sigma7,
+            (half_t *)grad_albedo7);
+    return check_launch(name);
+}
+
+extern "C" int dfhip_shading_forward(const float *sigma7, const void *albedo7, const float *dirs,
+                                     const float *light, float ratio, float eps, int shading,
+                                     const int32_t *m_dev, uint32_t cap, float *sigma,
+                                     void *color, float *normal, double *partial,
+                                     float lambda_orient, float *orient, float *loss,
+                                     dfhip_stream_t stream) {
+    return shading_forward("shading_forward", DFHIP_F16, sigma7, albedo7, dirs, light, ratio,
+                           eps, shading, m_dev, cap, sigma, color, normal, partial,
+                           lambda_orient, orient, loss, stream);
+}
+
+extern "C" int dfhip_shading_forward_bf16(const float *sigma7, const void *albedo7,
+                                          const float *dirs, const float *light, float ratio,
+                                          float eps, int shading, const int32_t *m_dev,
+                                          uint32_t cap, float *sigma, void *color,
+                                          float *normal, double *partial, float lambda_orient,
+                                          float *orient, float *loss, dfhip_stream_t stream) {
+    return shading_forward("shading_forward_bf16", DFHIP_BF16, sigma7, albedo7, dirs, light,
+                           ratio, eps, shading, m_dev, cap, sigma, color, normal, partial,
+                           lambda_orient, orient, loss, stream);
 }
 
 extern "C" int dfhip_shading_backward(const float *sigma7, const void *albedo7,
@@ -371,20 +436,21 @@ extern "C" int dfhip_shading_backward(const float *sigma7, const void *albedo7,
                                       const float *grad_loss, float lambda_orient,
                                       float *grad_sigma7, void *grad_albedo7,
                                       dfhip_stream_t stream) {
-    const char *name = "shading_backward";
-    int lam = 0;
-    if (!shading_mode(name, shading, lam)) return DFHIP_EINVAL;
-    if (!sigma7 || !albedo7 || !dirs || !light || !m_dev || !grad_sigma || !grad_color ||
-        !grad_loss || !grad_sigma7 || !grad_albedo7) {
-        set_error("%s: null pointer", name);
-        return DFHIP_EINVAL;
-    }
-    const float omr = (float)(1.0 - (double)ratio);
-    shd::k_shade_bwd<<<shade_blocks(cap), shd::kThreads, 0, as_stream(stream)>>>(
-        sigma7, (const half_t *)albedo7, dirs, light, ratio, omr, eps, lam, m_dev, cap, grad_sigma,
-        (const half_t *)grad_color, grad_loss, lambda_orient, grad_sigma7,
-        (half_t *)grad_albedo7);
-    return check_launch(name);
+    return shading_backward("shading_backward", DFHIP_F16, sigma7, albedo7, dirs, light, ratio,
+                            eps, shading, m_dev, cap, grad_sigma, grad_color, grad_loss,
+                            lambda_orient, grad_sigma7, grad_albedo7, stream);
+}
+
+extern "C" int dfhip_shading_backward_bf16(const float *sigma7, const void *albedo7,
+                                           const float *dirs, const float *light, float ratio,
+                                           float eps, int shading, const int32_t *m_dev,
+                                           uint32_t cap, const float *grad_sigma,
+                                           const void *grad_color, const float *grad_loss,
+                                           float lambda_orient, float *grad_sigma7,
+                                           void *grad_albedo7, dfhip_stream_t stream) {
+    return shading_backward("shading_backward_bf16", DFHIP_BF16, sigma7, albedo7, dirs, light,
+                            ratio, eps, shading, m_dev, cap, grad_sigma, grad_color, grad_loss,
+                            lambda_orient, grad_sigma7, grad_albedo7, stream);
 }
 
 extern "C" int dfhip_shading_light(const float *rays_o, uint64_t seed, uint64_t step,

@@ -30,9 +30,9 @@ utils.py:708): the compositing / field backwards run once per pass and the
 second pass adds into the parameter gradients, as autograd accumulates them.
 
 Under bf16 autocast (trainer.bf16, BASELINE configs[4]) the table, features,
-activations, colours and their gradients are bf16 (csrc/fieldmlp.hip's bf16
-instantiations, v_mfma_f32_16x16x32_bf16), there is no GradScaler (the
-entropy term's upstream gradient is 1), and only the albedo shading is native.
+activations, colours and their gradients are bf16 (csrc/fieldmlp.hip's and
+csrc/shade.hip's bf16 instantiations, v_mfma_f32_16x16x32_bf16) and there is
+no GradScaler (the entropy and orientation terms' upstream gradient is 1).
 
 Applies to the albedo shading with the InjectedSDS guidance, the
 reference's grid network (16 x 2 tiled grid, 32 -> 64 -> 64 -> 4 MLP), a
@@ -64,8 +64,6 @@ def eligible(trainer, shading):
         return False  # the two-pass form is built for the albedo step only
     if not ((trainer.fp16 or getattr(trainer, "bf16", False)) and m.cuda_ray):
         return False
-    if getattr(trainer, "bf16", False) and shading != "albedo":
-        return False  # the shading kernels (csrc/shade.hip) take f16 albedo
     if opt.lambda_opacity > 0:
         return False
     enc = getattr(m, "encoder", None)
@@ -110,6 +108,9 @@ class NativeAlbedoStep:
         # field element type: f16 (fp16 autocast, -O) or bf16 (bf16 autocast, C5)
         self.elem = torch.bfloat16 if getattr(trainer, "bf16", False) else torch.float16
         f16 = dict(device=dev, dtype=self.elem)
+        bf = self.elem == torch.bfloat16
+        self._shade_fwd = "dfhip_shading_forward_bf16" if bf else "dfhip_shading_forward"
+        self._shade_bwd = "dfhip_shading_backward_bf16" if bf else "dfhip_shading_backward"
         i32 = dict(device=dev, dtype=torch.int32)
         # prologue outputs (graph inputs)
         self.rays_o = torch.empty(N, 3, **f32)
@@ -257,7 +258,7 @@ class NativeAlbedoStep:
         if self.shade_code:
             # normals, lambertian, colour, orientation loss (network_grid.py:116-144,
             # renderer.py:485-489)
-            call("dfhip_shading_forward", ptr(self.sigma_field), ptr(self.albedo),
+            call(self._shade_fwd, ptr(self.sigma_field), ptr(self.albedo),
                  ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
                  ptr(self.m_dev), cap, ptr(self.sigma), ptr(self.color), ptr(self.normal),
                  ptr(self.orient_partial), self.lam_orient, ptr(self.orient), None, stream())
@@ -295,7 +296,7 @@ class NativeAlbedoStep:
             self.grad_color if self.shade_code else self.grad_albedo, False)
         if self.shade_code:
             # density / colour / orientation gradients -> the field rows' gradients
-            call("dfhip_shading_backward", ptr(self.sigma_field), ptr(self.albedo),
+            call(self._shade_bwd, ptr(self.sigma_field), ptr(self.albedo),
                  ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
                  ptr(self.m_dev), cap, ptr(self.grad_sigma), ptr(self.grad_color), ptr(scale),
                  self.lam_orient, ptr(self.grad_sigma_field), ptr(self.grad_albedo), stream())
