@@ -267,9 +267,14 @@ __device__ __forceinline__ void stage_levels(LevelK *lk, const int32_t *__restri
 // corner order).  bf16 (no reference counterpart: its kernels dispatch f32 /
 // f16 / f64 only): f32 accumulators, fmaf per corner in corner order, ONE
 // rounding to bf16 — per-corner bf16 rounding would lose 3 more bits than the
-// f16 path's.  All 32 row loads of the four levels are issued before the
-// first accumulation (the corners of z-dropped tiled levels load the row of
-// their z = 0 twin, an L1 hit), so a lane has 32 gathers in flight.
+// f16 path's.  Tiled / dense levels load the corners as four x-neighbour
+// pairs (one 8-byte load each; two on z-dropped levels, whose corners 4-7
+// are the rows of 0-3): 50 gathers per sample over the 16 levels instead of
+// 128, which is what bounds this gather (one scattered lane request per CU
+// clock in the L1).  Two levels' loads are issued before their accumulation.
+// two table rows (f16 / bf16 pairs) at a 4-byte-aligned address
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+
 template <typename E>
 __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restrict__ table,
                                                               const LevelK *lk, bool align,
@@ -280,13 +285,13 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
     if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
         return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
     const uint32_t *tab = reinterpret_cast<const uint32_t *>(table);
-    // two batches of two levels: 16 row loads in flight per lane per batch
-    // (32 at once held 64 VGPRs of rows and bits and capped the kernel at 4
-    // waves per SIMD)
+    // two batches of two levels: up to 8 pair loads in flight per lane per
+    // batch (all four levels at once held 64 VGPRs of rows and bits and
+    // capped the kernel at 4 waves per SIMD)
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
         float frac[2][3];
-        uint32_t row[2][8];
+        uint32_t bits[2][8];
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) {
             const LevelK k = lk[4 * (2 * half + qq) + h];
@@ -298,12 +303,31 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                 frac[qq][d] = p - (float)cell[d];
             }
             if (k.flags == 0u) {
-                // tiled / dense: corner offsets {0, 1, m1, m1 + 1, m2, ...}
+                // tiled / dense: corner offsets {0, 1, m1, m1 + 1, m2, ...}.
+                // Corners 2p and 2p + 1 are neighbouring rows unless the
+                // wrap falls between them: one 8-byte load per pair.  On a
+                // z-dropped level (m2 = 0) corners 4-7 are the rows of 0-3.
                 const uint32_t i0 = cell[0] + cell[1] * k.m1 + cell[2] * k.m2;
-                const uint32_t o[8] = {0u, 1u, k.m1, k.m1 + 1u, k.m2, k.m2 + 1u, k.m2 + k.m1,
-                                       k.m2 + k.m1 + 1u};
+                const uint32_t ob[4] = {0u, k.m1, k.m2, k.m2 + k.m1};
+                const bool zdrop = k.m2 == 0u;
 #pragma unroll
-                for (int c = 0; c < 8; ++c) row[qq][c] = k.base + ((i0 + o[c]) & k.wmask);
+                for (int p = 0; p < 4; ++p) {
+                    if (p >= 2 && zdrop) {
+                        bits[qq][2 * p] = bits[qq][2 * p - 4];
+                        bits[qq][2 * p + 1] = bits[qq][2 * p - 3];
+                        continue;
+                    }
+                    const uint32_t r = (i0 + ob[p]) & k.wmask;
+                    const uint32_t *src = tab + k.base + r;
+                    if (r != k.wmask) {
+                        const u32x2a v = *reinterpret_cast<const u32x2a *>(src);
+                        bits[qq][2 * p] = v[0];
+                        bits[qq][2 * p + 1] = v[1];
+                    } else {
+                        bits[qq][2 * p] = src[0];
+                        bits[qq][2 * p + 1] = tab[k.base + ((r + 1u) & k.wmask)];
+                    }
+                }
             } else {
 #pragma unroll
                 for (uint32_t c = 0; c < 8; ++c) {
@@ -312,15 +336,10 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                     uint32_t idx = (k.flags & 2u) ? (px ^ (py * 2654435761u) ^ (pz * 805459861u))
                                                   : px + py * k.m1 + pz * k.m2;
                     idx = (k.flags & 1u) ? idx % k.hsize : (idx & k.wmask);
-                    row[qq][c] = k.base + idx;
+                    bits[qq][c] = tab[k.base + idx];
                 }
             }
         }
-        uint32_t bits[2][8];
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq)
-#pragma unroll
-            for (int c = 0; c < 8; ++c) bits[qq][c] = tab[row[qq][c]];
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) {
             // f16: half accumulators (the reference's scalar_t); bf16: f32
