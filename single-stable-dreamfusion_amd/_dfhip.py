@@ -98,6 +98,10 @@ _SIGS = {
     "dfhip_shading_backward_bf16": [_vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp, _u32, _vp, _vp,
                                     _vp, _f32, _vp, _vp, _vp],
     "dfhip_shading_light": [_vp, _u64, _u64, _vp, _vp],
+    "dfhip_grid_quads": [_i32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _u32, _vp, _vp, _vp],
+    "dfhip_grid_field_forward_quads": [_i32, _vp, _f32, _vp, _vp, _vp, _u32, _f32, _u32, _u32,
+                                       _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
+                                       _u32, _vp, _vp],
     "dfhip_grid_field_forward_bf16": [_vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,
                                       _vp],

@@ -67,8 +67,27 @@ def field_mlp_backward(enc, xyz, weights, grad_sigma, grad_rgb, d_enc_lbc, parti
 
 # ---- fused grid field (encoding + MLP in one kernel; device-side sample count)
 
+def grid_quads(embeddings, offsets, S, H, gridtype, align_corners, table, quads):
+    """The autocast cast of the f32 embeddings [rows, 2] into `table` (f16 or
+    bf16, [rows, 2]) and its corner quads into `quads` ([rows, 4] int32) for
+    grid_field_forward(..., quads=quads)."""
+    _f32(embeddings, "embeddings")
+    checked(table, "table")
+    checked(quads, "quads", "int")
+    rows = embeddings.shape[0]
+    if table.dtype not in (torch.float16, torch.bfloat16) or tuple(table.shape) != (rows, 2) \
+            or tuple(embeddings.shape) != (rows, 2):
+        raise RuntimeError("embeddings [rows, 2] f32 and table [rows, 2] f16 / bf16 expected")
+    if quads.dtype != torch.int32 or tuple(quads.shape) != (rows, 4):
+        raise RuntimeError("quads must be a [rows, 4] int32 tensor")
+    elem = _d.BF16 if table.dtype == torch.bfloat16 else _d.F16
+    call("dfhip_grid_quads", elem, ptr(embeddings), ptr(offsets), offsets.shape[0] - 1, float(S),
+         int(H), int(gridtype), int(bool(align_corners)), rows, ptr(table), ptr(quads), stream())
+
+
 def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners, weights, enc,
-                       sigma, rgb, m_dev=None):
+                       sigma, rgb, m_dev=None,
+                       quads=None):
     """xyz [cap, 3] f32 in [-bound, bound]; table [rows, 2] f16 (fp16 autocast,
     the reference's -O) or bf16 (the C5 bf16 option: features and activations
     bf16 too); offsets [17] int32.  Writes sigma [cap] f32, rgb [cap, 3] (the
@@ -90,6 +109,14 @@ def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners
         checked(enc, "enc")
     if m_dev is not None:
         checked(m_dev, "m_dev", "int")
+    if quads is not None:
+        checked(quads, "quads", "int")
+        elem = _d.BF16 if table.dtype == torch.bfloat16 else _d.F16
+        call("dfhip_grid_field_forward_quads", elem, ptr(xyz), float(bound), ptr(table),
+             ptr(quads), ptr(offsets), offsets.shape[0] - 1, float(S), int(H), int(gridtype),
+             int(bool(align_corners)), *_weights(weights), ptr(enc), ptr(sigma), ptr(rgb),
+             _d.dtype_code(rgb, "rgb"), cap, ptr(m_dev), stream())
+        return
     fn = "dfhip_grid_field_forward_bf16" if table.dtype == torch.bfloat16 else \
         "dfhip_grid_field_forward"
     call(fn, ptr(xyz), float(bound), ptr(table), ptr(offsets),

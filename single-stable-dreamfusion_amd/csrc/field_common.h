@@ -274,11 +274,18 @@ __device__ __forceinline__ void stage_levels(LevelK *lk, const int32_t *__restri
 // clock in the L1).  Two levels' loads are issued before their accumulation.
 // two table rows (f16 / bf16 pairs) at a 4-byte-aligned address
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <typename E>
+// QUAD: `quads` (dfhip_grid_quads) holds, for every row r of a tiled / dense
+// level, the rows r, r + 1, r + m1, r + m1 + 1 (wrapped like the corners), so
+// a level's corners 0-3 are ONE 16-byte load and corners 4-7 another (none on
+// a z-dropped level): 25 gathers per sample.  Same values, same order.
+template <typename E, bool QUAD = false>
 __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restrict__ table,
                                                               const LevelK *lk, bool align,
-                                                              const float (&x)[3], int h) {
+                                                              const float (&x)[3], int h,
+                                                              const u32x4 *__restrict__ quads =
+                                                                  nullptr) {
     typename Elem<E>::v8 out{};
     typedef float f8 __attribute__((ext_vector_type(8)));
     f8 outf{};  // bf16: the f32 features, converted to bf16 pairs at the end
@@ -310,6 +317,17 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                 const uint32_t i0 = cell[0] + cell[1] * k.m1 + cell[2] * k.m2;
                 const uint32_t ob[4] = {0u, k.m1, k.m2, k.m2 + k.m1};
                 const bool zdrop = k.m2 == 0u;
+                if constexpr (QUAD) {
+                    const u32x4 q0 = quads[k.base + (i0 & k.wmask)];
+                    u32x4 q1 = q0;
+                    if (!zdrop) q1 = quads[k.base + ((i0 + k.m2) & k.wmask)];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        bits[qq][j] = q0[j];
+                        bits[qq][4 + j] = q1[j];
+                    }
+                    continue;
+                }
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
                     if (p >= 2 && zdrop) {

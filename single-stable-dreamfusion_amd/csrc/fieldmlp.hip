@@ -38,10 +38,10 @@ namespace fm {
 // table loads in flight per lane), the features go straight into the MLP's
 // B operand, and are also written (permuted order, 16 B per lane) for the
 // backward.  xyz in [-bound, bound] is mapped to [0, 1] as grid.py:142 does.
-template <typename E, typename rgb_t>
+template <typename E, typename rgb_t, bool QUAD>
 __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
     const float *__restrict__ xyz, float bound, const E *__restrict__ table,
-    const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
+    const u32x4 *__restrict__ quads, const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, E *__restrict__ enc, float *__restrict__ sigma,
     rgb_t *__restrict__ rgb, uint32_t cap, const int32_t *__restrict__ m_dev) {
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
                 x[d] = xyz[(size_t)sample * 3 + d];
                 x01[d] = (x[d] + bound) / (2.0f * bound);
             }
-        const v8 xb = valid ? grid_features(table, LK, align, x01, h) : v8{};
+        const v8 xb = valid ? grid_features<E, QUAD>(table, LK, align, x01, h, quads) : v8{};
         if (enc && valid) *reinterpret_cast<v8 *>(enc + (size_t)sample * kIn + 8 * h) = xb;
         FwdG<E> F;
         forward_tile(W, xb, c, h, F);
@@ -590,9 +590,9 @@ static bool check_field_grid(const char *name, uint32_t L) {
     return true;
 }
 
-template <typename E, typename rgb_t>
+template <typename E, typename rgb_t, bool QUAD>
 static void launch_field_fwd(hipStream_t s, const float *xyz, float bound, const void *table,
-                             const int32_t *offsets, const ge::Levels &lv, uint32_t gridtype,
+                             const void *quads, const int32_t *offsets, const ge::Levels &lv, uint32_t gridtype,
                              int align_corners, const float *w1, const float *b1, const float *w2,
                              const float *b2, const float *w3, const float *b3, void *enc,
                              float *sigma, void *rgb, uint32_t cap, const int32_t *m_dev) {
@@ -600,17 +600,17 @@ static void launch_field_fwd(hipStream_t s, const float *xyz, float bound, const
     // walks ~M / (16 * waves) tiles); more blocks than fit leave a partial
     // last round of blocks (4096 blocks at 5 waves/SIMD were 3.2 rounds)
     const uint32_t tiles = ceil_div(cap, 16u);
-    const uint32_t fit = resident_blocks(k_field_fwd_fused<E, rgb_t>);
+    const uint32_t fit = resident_blocks(k_field_fwd_fused<E, rgb_t, QUAD>);
     const uint32_t blocks = ceil_div(tiles, 4u) < fit ? ceil_div(tiles, 4u) : fit;
-    k_field_fwd_fused<E, rgb_t><<<blocks, 256, 0, s>>>(
-        xyz, bound, (const E *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3,
+    k_field_fwd_fused<E, rgb_t, QUAD><<<blocks, 256, 0, s>>>(
+        xyz, bound, (const E *)table, (const u32x4 *)quads, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3,
         b3, (E *)enc, sigma, (rgb_t *)rgb, cap, m_dev);
 }
 
 // elem: DFHIP_F16 (table, features, activations in f16: the reference's fp16
 // autocast) or DFHIP_BF16 (all of them bf16: bf16 autocast, the C5 option).
 static int grid_field_forward(const char *name, int elem, const float *xyz, float bound,
-                              const void *table, const int32_t *offsets, uint32_t L, float S,
+                              const void *table, const void *quads, const int32_t *offsets, uint32_t L, float S,
                               uint32_t H, uint32_t gridtype, int align_corners, const float *w1,
                               const float *b1, const float *w2, const float *b2, const float *w3,
                               const float *b3, void *enc, float *sigma, void *rgb, int rgb_dtype,
@@ -628,8 +628,12 @@ static int grid_field_forward(const char *name, int elem, const float *xyz, floa
     hipStream_t s = as_stream(stream);
     const ge::Levels lv = ge::make_levels(L, S, H);
 #define DFHIP_FWD(E, R)                                                                       \
-    launch_field_fwd<E, R>(s, xyz, bound, table, offsets, lv, gridtype, align_corners, w1, b1, \
-                           w2, b2, w3, b3, enc, sigma, rgb, cap, m_dev)
+    (quads ? launch_field_fwd<E, R, true>(s, xyz, bound, table, quads, offsets, lv, gridtype,    \
+                                          align_corners, w1, b1, w2, b2, w3, b3, enc, sigma, rgb,  \
+                                          cap, m_dev)                                              \
+           : launch_field_fwd<E, R, false>(s, xyz, bound, table, nullptr, offsets, lv, gridtype,  \
+                                           align_corners, w1, b1, w2, b2, w3, b3, enc, sigma, rgb, \
+                                           cap, m_dev))
     if (elem == DFHIP_F16 && rgb_dtype == DFHIP_F32) DFHIP_FWD(half_t, float);
     else if (elem == DFHIP_F16 && rgb_dtype == DFHIP_F16) DFHIP_FWD(half_t, half_t);
     else if (elem == DFHIP_BF16 && rgb_dtype == DFHIP_F32) DFHIP_FWD(bf16_t, float);
@@ -649,7 +653,8 @@ extern "C" int dfhip_grid_field_forward(const float *xyz, float bound, const voi
                                         const float *w3, const float *b3, void *enc,
                                         float *sigma, void *rgb, int rgb_dtype, uint32_t cap,
                                         const int32_t *m_dev, dfhip_stream_t stream) {
-    return grid_field_forward("grid_field_forward", DFHIP_F16, xyz, bound, table, offsets, L, S,
+    return grid_field_forward("grid_field_forward", DFHIP_F16, xyz, bound, table, nullptr,
+                              offsets, L, S,
                               H, gridtype, align_corners, w1, b1, w2, b2, w3, b3, enc, sigma,
                               rgb, rgb_dtype, cap, m_dev, stream);
 }
@@ -662,9 +667,108 @@ extern "C" int dfhip_grid_field_forward_bf16(const float *xyz, float bound, cons
                                              void *enc, float *sigma, void *rgb, int rgb_dtype,
                                              uint32_t cap, const int32_t *m_dev,
                                              dfhip_stream_t stream) {
-    return grid_field_forward("grid_field_forward_bf16", DFHIP_BF16, xyz, bound, table, offsets,
+    return grid_field_forward("grid_field_forward_bf16", DFHIP_BF16, xyz, bound, table, nullptr,
+                              offsets,
                               L, S, H, gridtype, align_corners, w1, b1, w2, b2, w3, b3, enc,
                               sigma, rgb, rgb_dtype, cap, m_dev, stream);
+}
+
+// The autocast table (f32 embeddings rounded to the element type, as
+// grid.py:38-39's cast) and its corner quads for QUAD forwards: one thread per
+// row; quad entries of hashed / modulo levels and corners past a dense
+// level's end (never read: a reachable cell's corners are rows of its level)
+// are left zero.
+template <typename E>
+__global__ __launch_bounds__(256) void k_grid_quads(const float *__restrict__ emb,
+                                                    const int32_t *__restrict__ offsets,
+                                                    ge::Levels lv, uint32_t gridtype,
+                                                    int align_corners, uint32_t rows,
+                                                    uint32_t *__restrict__ table,
+                                                    u32x4 *__restrict__ quads) {
+    __shared__ LevelK LK[kLevels];
+    __shared__ uint32_t OFF[kLevels + 1];
+    stage_levels(LK, offsets, lv, gridtype, align_corners != 0);
+    for (int l = threadIdx.x; l <= kLevels; l += blockDim.x) OFF[l] = (uint32_t)offsets[l];
+    __syncthreads();
+    const float2 *e2 = reinterpret_cast<const float2 *>(emb);
+    auto pack = [&](uint32_t row) {
+        const float2 f = e2[row];
+        E v[2] = {(E)f.x, (E)f.y};
+        uint32_t u;
+        __builtin_memcpy(&u, v, 4);
+        return u;
+    };
+    for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < rows;
+         row += gridDim.x * blockDim.x) {
+        table[row] = pack(row);
+        int l = 0;
+        while (l < kLevels - 1 && row >= OFF[l + 1]) ++l;
+        const LevelK k = LK[l];
+        u32x4 q = {0u, 0u, 0u, 0u};
+        if (k.flags == 0u) {
+            const uint32_t r = row - k.base, n = OFF[l + 1] - OFF[l];
+            const uint32_t o[4] = {0u, 1u, k.m1, k.m1 + 1u};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t idx = (r + o[j]) & k.wmask;
+                if (idx < n) q[j] = pack(k.base + idx);
+            }
+        }
+        quads[row] = q;
+    }
+}
+
+extern "C" int dfhip_grid_quads(int elem, const float *embeddings, const int32_t *offsets,
+                                uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                int align_corners, uint32_t rows, void *table, void *quads,
+                                dfhip_stream_t stream) {
+    const char *name = "grid_quads";
+    if (!check_field_grid(name, L)) return DFHIP_EINVAL;
+    if (rows == 0) return DFHIP_OK;
+    if (!embeddings || !offsets || !table || !quads) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    if (((uintptr_t)quads & 15u) != 0) {
+        set_error("%s: quads must be 16-byte aligned", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const ge::Levels lv = ge::make_levels(L, S, H);
+    const uint32_t blocks = ceil_div(rows, 256u) < 4096u ? ceil_div(rows, 256u) : 4096u;
+    if (elem == DFHIP_F16)
+        k_grid_quads<half_t><<<blocks, 256, 0, s>>>(embeddings, offsets, lv, gridtype,
+                                                     align_corners, rows, (uint32_t *)table,
+                                                     (u32x4 *)quads);
+    else if (elem == DFHIP_BF16)
+        k_grid_quads<bf16_t><<<blocks, 256, 0, s>>>(embeddings, offsets, lv, gridtype,
+                                                     align_corners, rows, (uint32_t *)table,
+                                                     (u32x4 *)quads);
+    else {
+        set_error("%s: elem must be f16 or bf16", name);
+        return DFHIP_EDTYPE;
+    }
+    return check_launch(name);
+}
+
+// The fused forward reading the corner quads of dfhip_grid_quads (same
+// results as dfhip_grid_field_forward[_bf16] on the table made with them).
+extern "C" int dfhip_grid_field_forward_quads(int elem, const float *xyz, float bound,
+                                              const void *table, const void *quads,
+                                              const int32_t *offsets, uint32_t L, float S,
+                                              uint32_t H, uint32_t gridtype, int align_corners,
+                                              const float *w1, const float *b1, const float *w2,
+                                              const float *b2, const float *w3, const float *b3,
+                                              void *enc, float *sigma, void *rgb, int rgb_dtype,
+                                              uint32_t cap, const int32_t *m_dev,
+                                              dfhip_stream_t stream) {
+    if (!quads) {
+        set_error("grid_field_forward_quads: null quads");
+        return DFHIP_EINVAL;
+    }
+    return grid_field_forward("grid_field_forward_quads", elem, xyz, bound, table, quads,
+                              offsets, L, S, H, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
+                              enc, sigma, rgb, rgb_dtype, cap, m_dev, stream);
 }
 
 static int grid_field_backward(

@@ -144,6 +144,8 @@ class NativeAlbedoStep:
         self.meta = (float(np.log2(enc.per_level_scale)), int(enc.base_resolution),
                      enc.gridtype_id, bool(enc.align_corners), enc.offsets_host)
         self.table = torch.empty(self.rows, self.C, **f16)
+        # corner quads of the table (dfhip_grid_quads): the forward's gathers
+        self.quads = torch.empty(self.rows, 4, device=dev, dtype=torch.int32)
         self.mlp = []
         for lin in m.sigma_net.net:
             self.mlp += [lin.weight, lin.bias]
@@ -246,14 +248,16 @@ class NativeAlbedoStep:
         # field (grid.py:38-39 autocast table, network_grid.py:76-87); with a
         # shading, the six finite-difference stencil points of every sample are
         # field rows too (network_grid.py:90-114)
-        self.table.copy_(self.encoder.embeddings.detach())
         S, Hb, gridtype, align, _ = self.meta
+        _fieldmlp.grid_quads(self.encoder.embeddings.detach(), self.encoder.offsets, S, Hb,
+                             gridtype, align, self.table, self.quads)
         if self.shade_code:
             call("dfhip_shading_stencil", ptr(self.xyzs), ptr(self.m_dev), cap, FD_EPS,
                  float(m.bound), ptr(self.xyz_field), ptr(self.m7), stream())
         _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table, self.encoder.offsets,
                                      S, Hb, gridtype, align, self.mlp, self.enc,
-                                     self.sigma_field, self.albedo, self.m_field)
+                                     self.sigma_field, self.albedo, self.m_field,
+                                     quads=self.quads)
         rgb = self.albedo
         if self.shade_code:
             # normals, lambertian, colour, orientation loss (network_grid.py:116-144,
@@ -373,7 +377,8 @@ class NativeAlbedoStep:
         def fwd():
             _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table,
                                          self.encoder.offsets, S, Hb, gridtype, align, self.mlp,
-                                         self.enc, self.sigma_field, self.albedo, self.m_field)
+                                         self.enc, self.sigma_field, self.albedo, self.m_field,
+                                         quads=self.quads)
 
         def bwd():
             _fieldmlp.grid_field_backward(

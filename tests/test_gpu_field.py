@@ -103,3 +103,42 @@ def test_fused_field_device_count(gpu):
     g_m = torch.autograd.grad((s_m * gs[:M]).sum() + (a_m.float() * ga[:M]).sum(), params)
     for u, v in zip(g_cap, g_m):
         torch.testing.assert_close(u, v, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("align,lo,hi", [(False, -1.0, 1.0), (True, -1.0, 1.0),
+                                         (False, 0.999, 1.0)])
+def test_quad_forward_bit_identical(gpu, dtype, align, lo, hi):
+    """dfhip_grid_quads + dfhip_grid_field_forward_quads (the native step's
+    forward) against the table forward: the cast table equals torch's cast,
+    features / sigma / rgb are bit-identical (including the far corner of the
+    cube, where corners reach the last rows of dense levels)."""
+    import _fieldmlp
+    enc, layers = _field(gpu, seed=5)
+    enc.align_corners = align
+    S = float(np.log2(enc.per_level_scale))
+    Hb, gt = int(enc.base_resolution), enc.gridtype_id
+    ws = [p.detach().float().contiguous() for lin in layers for p in (lin.weight, lin.bias)]
+    g = torch.Generator(device=gpu).manual_seed(9)
+    M = 40_001
+    x = (torch.rand(M, 3, device=gpu, generator=g) * (hi - lo) + lo).contiguous()
+    x[:8] = torch.tensor([[1.0, 1.0, 1.0], [-1.0, -1.0, -1.0], [1.0, -1.0, 1.0],
+                          [0.0, 0.0, 0.0], [1.0, 0.5, -1.0], [-1.0, 1.0, 1.0],
+                          [0.99999, 0.99999, 0.99999], [-0.99999, 1.0, 0.3]], device=gpu)
+    emb = enc.embeddings.detach()
+    rows = emb.shape[0]
+    table = torch.empty(rows, 2, device=gpu, dtype=dtype)
+    quads = torch.empty(rows, 4, device=gpu, dtype=torch.int32)
+    _fieldmlp.grid_quads(emb, enc.offsets, S, Hb, gt, align, table, quads)
+    assert torch.equal(table, emb.to(dtype))
+    outs = []
+    for q in (None, quads):
+        e = torch.empty(M, 32, device=gpu, dtype=dtype)
+        s = torch.empty(M, device=gpu)
+        a = torch.empty(M, 3, device=gpu, dtype=dtype)
+        _fieldmlp.grid_field_forward(x, 1.0, table, enc.offsets, S, Hb, gt, align, ws, e, s, a,
+                                     None, quads=q)
+        outs.append((e, s, a))
+    for u, v in zip(*outs):
+        assert torch.equal(u.view(torch.int16) if u.dtype != torch.float32 else u,
+                           v.view(torch.int16) if v.dtype != torch.float32 else v)
