@@ -74,6 +74,7 @@ def grid_quads(embeddings, offsets, S, H, gridtype, align_corners, table, quads)
     _f32(embeddings, "embeddings")
     checked(table, "table")
     checked(quads, "quads", "int")
+    checked(offsets, "offsets", "int")
     rows = embeddings.shape[0]
     if table.dtype not in (torch.float16, torch.bfloat16) or tuple(table.shape) != (rows, 2) \
             or tuple(embeddings.shape) != (rows, 2):
