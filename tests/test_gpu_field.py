@@ -106,15 +106,24 @@ def test_fused_field_device_count(gpu):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("align,lo,hi", [(False, -1.0, 1.0), (True, -1.0, 1.0),
-                                         (False, 0.999, 1.0)])
-def test_quad_forward_bit_identical(gpu, dtype, align, lo, hi):
+@pytest.mark.parametrize("align,lo,hi,gridtype", [(False, -1.0, 1.0, "tiled"),
+                                                  (True, -1.0, 1.0, "tiled"),
+                                                  (False, 0.999, 1.0, "tiled"),
+                                                  (False, -1.0, 1.0, "hash")])
+def test_quad_forward_bit_identical(gpu, dtype, align, lo, hi, gridtype):
     """dfhip_grid_quads + dfhip_grid_field_forward_quads (the native step's
     forward) against the table forward: the cast table equals torch's cast,
     features / sigma / rgb are bit-identical (including the far corner of the
-    cube, where corners reach the last rows of dense levels)."""
+    cube, where corners reach the last rows of dense levels); on a hash grid
+    the hashed levels fall back to the table."""
     import _fieldmlp
+    from gridencoder import GridEncoder
     enc, layers = _field(gpu, seed=5)
+    if gridtype == "hash":
+        enc = GridEncoder(input_dim=3, num_levels=16, level_dim=2, base_resolution=16,
+                          log2_hashmap_size=16, desired_resolution=2048, gridtype="hash").to(gpu)
+        with torch.no_grad():
+            enc.embeddings.uniform_(-0.5, 0.5)
     enc.align_corners = align
     S = float(np.log2(enc.per_level_scale))
     Hb, gt = int(enc.base_resolution), enc.gridtype_id
