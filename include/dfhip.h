@@ -552,6 +552,17 @@ int dfhip_ray_head_backward_entropy(uint32_t N, const float *g_image, const floa
                                     float *partial, float *gw1, float *gb1, float *gw2,
                                     float *gb2, const float *grad_loss, float lambda,
                                     dfhip_stream_t stream);
+/* dfhip_ray_head_backward_entropy that also writes the entropy loss
+ * lambda * mean(entropy(clamp(ws))) (dfhip_entropy_forward's value, same
+ * reduction) to loss[0], computed inside the weight-gradient sum launch. */
+int dfhip_ray_head_backward_entropy_loss(uint32_t N, const float *g_image, const float *ws,
+                                         const float *rays_d, const float *w1, const float *b1,
+                                         const float *w2, const float *b2,
+                                         const float *bg_color, float *grad_image,
+                                         float *grad_ws, float *grad_bg, float *partial,
+                                         float *gw1, float *gb1, float *gw2, float *gb2,
+                                         const float *grad_loss, float lambda, float *loss,
+                                         dfhip_stream_t stream);
 
 /* nerf/utils.py:386-391 entropy regulariser: loss[0] = lambda * mean(-a log2 a
  * - (1 - a) log2(1 - a)), a = clamp(ws, 1e-5, 1 - 1e-5) (f64 sum); backward

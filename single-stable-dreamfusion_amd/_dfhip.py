@@ -120,6 +120,9 @@ _SIGS = {
                                 _vp, _vp, _vp, _vp, _vp],
     "dfhip_ray_head_backward_entropy": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp],
+    "dfhip_ray_head_backward_entropy_loss": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp,
+                                             _vp],
     "dfhip_entropy_forward": [_u32, _vp, _f32, _vp, _vp],
     "dfhip_entropy_backward": [_u32, _vp, _vp, _f32, _vp, _vp],
     "dfhip_entropy_backward_accumulate": [_u32, _vp, _vp, _f32, _vp, _vp],

@@ -266,9 +266,23 @@ __global__ __launch_bounds__(256) void k_head_bwd_net(
 
 // Fixed-order sum of the per-block partials: block = 64 outputs, its 16
 // waves take every 16th partial, then a fixed-order sum of the 16.
+// (declared ahead of k_head_wsum, which may run it as its last block)
+__device__ __forceinline__ void entropy_loss_block(uint32_t N, const float *__restrict__ ws,
+                                                   float lambda, float *__restrict__ loss);
+
+// With `loss`, one extra (last) block computes the entropy loss of ws — the
+// forward value k_entropy_fwd would give, by the same code — so the native
+// step needs no launch of its own for it.
 __global__ __launch_bounds__(1024) void k_head_wsum(const float *__restrict__ partial,
                                                     uint32_t blocks, float *gw1, float *gb1,
-                                                    float *gw2, float *gb2) {
+                                                    float *gw2, float *gb2,
+                                                    const float *__restrict__ ent_ws = nullptr,
+                                                    uint32_t ent_n = 0, float ent_lambda = 0.0f,
+                                                    float *__restrict__ loss = nullptr) {
+    if (loss && blockIdx.x == gridDim.x - 1) {
+        entropy_loss_block(ent_n, ent_ws, ent_lambda, loss);
+        return;
+    }
     __shared__ float red[16][64];
     const int o = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int p = blockIdx.x * 64 + o;
@@ -298,8 +312,9 @@ __global__ __launch_bounds__(1024) void k_head_wsum(const float *__restrict__ pa
 }
 
 // ---------------------------------------------------------------- entropy
-__global__ __launch_bounds__(1024) void k_entropy_fwd(uint32_t N, const float *__restrict__ ws,
-                                                      float lambda, float *__restrict__ loss) {
+// lambda * mean(entropy(clamp(ws))) by one 1024-thread block (fixed order).
+__device__ __forceinline__ void entropy_loss_block(uint32_t N, const float *__restrict__ ws,
+                                                   float lambda, float *__restrict__ loss) {
     __shared__ double part[16];
     double s = 0.0;
     // elements n, n + blockDim, ... added in that order; eight loads in flight
@@ -326,6 +341,11 @@ __global__ __launch_bounds__(1024) void k_entropy_fwd(uint32_t N, const float *_
         for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += part[i];
         loss[0] = lambda * (float)(t / (double)N);
     }
+}
+
+__global__ __launch_bounds__(1024) void k_entropy_fwd(uint32_t N, const float *__restrict__ ws,
+                                                      float lambda, float *__restrict__ loss) {
+    entropy_loss_block(N, ws, lambda, loss);
 }
 
 // d loss / d ws = g * lambda / N * log2((1 - a) / a), zero where the clamp is
@@ -383,7 +403,7 @@ static int ray_head_backward(uint32_t N, const float *g_image, const float *ws,
                              float *grad_image, float *grad_ws, float *grad_bg, float *partial,
                              float *gw1, float *gb1, float *gw2, float *gb2,
                              const float *ent_grad_loss, float ent_lambda,
-                             dfhip_stream_t stream) {
+                             dfhip_stream_t stream, float *ent_loss = nullptr) {
     const char *name = "ray_head_backward";
     if (N == 0) return DFHIP_OK;
     if (!g_image || !ws || !grad_image || !grad_ws) {
@@ -402,14 +422,16 @@ static int ray_head_backward(uint32_t N, const float *g_image, const float *ws,
         hd::k_head_bwd_net<<<blocks, 256, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
                                                   grad_image, grad_ws, partial, ent_grad_loss,
                                                   ent_lambda);
-        hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u), 1024, 0, s>>>(
-            partial, blocks, gw1, gb1, gw2, gb2);
+        hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u) + (ent_loss ? 1u : 0u), 1024, 0,
+                          s>>>(partial, blocks, gw1, gb1, gw2, gb2, ws, N, ent_lambda,
+                               ent_loss);
     } else {
         hd::k_head_bwd_plain<<<ceil_div(N, 256u), 256, 0, s>>>(N, g_image, ws, bg_color,
                                                                grad_image, grad_ws, grad_bg);
         if (ent_grad_loss)
             hd::k_entropy_bwd<true><<<ceil_div(N, 256u), 256, 0, s>>>(N, ws, ent_grad_loss,
                                                                      ent_lambda, grad_ws);
+        if (ent_loss) hd::k_entropy_fwd<<<1, 1024, 0, s>>>(N, ws, ent_lambda, ent_loss);
     }
     return check_launch(name);
 }
@@ -437,6 +459,27 @@ extern "C" int dfhip_ray_head_backward_entropy(
     return ray_head_backward(N, g_image, ws, rays_d, w1, b1, w2, b2, bg_color, grad_image,
                              grad_ws, grad_bg, partial, gw1, gb1, gw2, gb2, grad_loss, lambda,
                              stream);
+}
+
+// dfhip_ray_head_backward_entropy that also writes the entropy loss
+// (dfhip_entropy_forward's value) to `loss`, inside the weight-sum launch.
+extern "C" int dfhip_ray_head_backward_entropy_loss(
+    uint32_t N, const float *g_image, const float *ws, const float *rays_d, const float *w1,
+    const float *b1, const float *w2, const float *b2, const float *bg_color, float *grad_image,
+    float *grad_ws, float *grad_bg, float *partial, float *gw1, float *gb1, float *gw2,
+    float *gb2, const float *grad_loss, float lambda, float *loss, dfhip_stream_t stream) {
+    if (!loss) {
+        set_error("ray_head_backward_entropy_loss: null loss");
+        return DFHIP_EINVAL;
+    }
+    if (N == 0) return dfhip_entropy_forward(N, ws, lambda, loss, stream);
+    if (!grad_loss) {
+        set_error("ray_head_backward_entropy_loss: null grad_loss");
+        return DFHIP_EINVAL;
+    }
+    return ray_head_backward(N, g_image, ws, rays_d, w1, b1, w2, b2, bg_color, grad_image,
+                             grad_ws, grad_bg, partial, gw1, gb1, gw2, gb2, grad_loss, lambda,
+                             stream, loss);
 }
 
 extern "C" int dfhip_entropy_forward(uint32_t N, const float *ws, float lambda, float *loss,

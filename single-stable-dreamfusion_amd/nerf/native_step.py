@@ -277,12 +277,13 @@ class NativeAlbedoStep:
              ptr(self.rays_d), ptr(self.nears), ptr(self.fars), *[ptr(w) for w in bw],
              ptr(self.bg_color), ptr(self.out_image), ptr(self.out_depth), ptr(self.mask),
              stream())
-        if self.lam > 0:
-            call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss), stream())
-        if self.lam_orient > 0:
-            self.loss.add_(self.orient, alpha=self.lam_orient)  # utils.py:398-400
-        # backward: SDS gradient at pred_rgb (unscaled), entropy gradient x scale
         if self.two_pass:
+            if self.lam > 0:
+                call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss),
+                     stream())
+            if self.lam_orient > 0:
+                self.loss.add_(self.orient, alpha=self.lam_orient)  # utils.py:398-400
+            # backward: SDS gradient at pred_rgb (unscaled), entropy gradient x scale
             self._backward_two_pass(bw, scale)
             return self.loss
         gbw = self._bg_grads()
@@ -290,10 +291,15 @@ class NativeAlbedoStep:
                      ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws), None,
                      ptr(self.head_partial), *[ptr(g) for g in gbw])
         if self.lam > 0:
-            # head backward + the entropy term's gradient (upstream: the scale)
-            call("dfhip_ray_head_backward_entropy", *head_args, ptr(scale), self.lam, stream())
+            # head backward + the entropy term's gradient (upstream: the scale);
+            # the entropy loss itself (utils.py:386-391) comes out of the same
+            # launches (dfhip_entropy_forward's value)
+            call("dfhip_ray_head_backward_entropy_loss", *head_args, ptr(scale), self.lam,
+                 ptr(self.loss), stream())
         else:
             call("dfhip_ray_head_backward", *head_args, stream())
+        if self.lam_orient > 0:
+            self.loss.add_(self.orient, alpha=self.lam_orient)  # utils.py:398-400
         _raymarching.composite_rays_train_backward_mixed(
             self.grad_ws, self.grad_image, self.sigma, rgb, self.deltas, self.rays,
             self.ws, self.image, cap, N, 1e-4, self.grad_sigma,
