@@ -110,13 +110,18 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     bi.nbins = nb;
     if (nb == 0 || nb > kMaxBins) return false;
     if (bi.G < nb) bi.G = nb;  // every bin can get a workgroup
-    const uint64_t tot = (uint64_t)nb * bi.tcap;
-    if (tot + (kTotSplit + 2ull) * nb >= (1ull << 32)) return false;
+    // totals + plan start on a 16-byte boundary and span whole 16-byte words,
+    // so the per-call clear is ONE aligned fill (an unaligned one took two
+    // fill launches)
+    const uint64_t tot = ((uint64_t)nb * bi.tcap + 3ull) & ~3ull;
+    if (tot + (kTotSplit + 2ull) * nb + 4ull >= (1ull << 32)) return false;
     bi.o_totals = (uint32_t)tot;
     bi.o_plan = bi.o_totals + nb * kTotSplit;
     return true;
 }
-static uint64_t counts_words(const BinInfo &bi) { return (uint64_t)bi.o_plan + 2ull * bi.nbins; }
+static uint64_t counts_words(const BinInfo &bi) {
+    return ((uint64_t)bi.o_plan + 2ull * bi.nbins + 3ull) & ~3ull;
+}
 
 __device__ __forceinline__ uint32_t bin_total(const uint32_t *__restrict__ totals, uint32_t b) {
     const uint4 *p = reinterpret_cast<const uint4 *>(totals + (size_t)b * kTotSplit);
@@ -714,7 +719,7 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
     if (phase & 1) {
         // totals (k_bin adds) and the plan (k_walk sets; P = 0: no images)
         (void)hipMemsetAsync(counts + bi.o_totals, 0,
-                             (size_t)bi.nbins * (gb::kTotSplit + 2) * sizeof(uint32_t), s);
+                             (size_t)(gb::counts_words(bi) - bi.o_totals) * sizeof(uint32_t), s);
         if (B > 0) {
             const uint32_t gbin = bi.tcap < 4096u ? bi.tcap : 4096u;
             const bool pow2 = ge::dyn_pow2(dyn.bound);
