@@ -523,3 +523,89 @@ def shade_backward(fwd, albedo16, dirs, grad_color16, grad_loss, lam_orient, m_r
         out[2 * a] = gdiff[:, a]
         out[2 * a + 1] = -gdiff[:, a]
     return out, ga
+
+
+# ----------------------------------------------------------------- backward structures of the step
+#
+# The reference runs TWO backward passes per train step: nerf/sd.py:115
+# `latents.backward(gradient=grad, retain_graph=True)` carries the UNSCALED SDS
+# gradient down the render graph, then nerf/utils.py:708
+# `scaler.scale(loss).backward()` carries the loss-scaled regulariser
+# gradient; autograd's AccumulateGrad adds the second pass's parameter
+# gradients onto the first's in f32.  The fused structure (this package's
+# headline, Trainer.fused_backward) runs ONE backward with both upstream
+# gradients summed where they meet — at weights_sum, in f32 — so every f16
+# rounding point of the field backward (dO = r16(...), dz2, dz1, d_enc) rounds
+# the SUM once instead of each pass's part separately.  Both are restated
+# here on top of the compositing backward (oracle.c) and field_backward.
+
+def step_upstreams(structure, grad_ws_sds, grad_ws_loss, grad_image):
+    """Upstream gradients at the compositing outputs, one (grad_ws [N],
+    grad_image [N, 3]) pair per backward pass: "fused" -> one pass with the
+    weights-sum gradients added in f32; "two_pass" -> the SDS pass (image and
+    its weights-sum gradient) then the loss pass (weights-sum only)."""
+    gs, gl = np.asarray(grad_ws_sds, F32), np.asarray(grad_ws_loss, F32)
+    gi = np.asarray(grad_image, F32)
+    if structure == "fused":
+        return [((gs + gl).astype(F32), gi)]
+    if structure == "two_pass":
+        return [(gs, gi), (gl, np.zeros_like(gi))]
+    raise ValueError(structure)
+
+
+def composite_backward(grad_ws, grad_image, sigma, rgb16, deltas, rays, ws, image):
+    """One pass of the compositing backward (raymarching.cu:601-693 via
+    oracle.c, f32): (grad_sigma f32 [M], grad_albedo [M, 3] rounded to the
+    element type, as autocast's cast backward delivers it to the f16 / bf16
+    albedo)."""
+    from . import composite_rays_train_backward
+    gs, gc = composite_rays_train_backward(grad_ws, grad_image, sigma,
+                                           np.asarray(rgb16).astype(F32), deltas, rays, ws,
+                                           image)
+    return gs, r16(gc)
+
+
+def backward_passes(fwd, weights, passes):
+    """field_backward of every pass [(grad_sigma, grad_albedo16), ...]:
+    returns {"passes": [bo, ...], "d_enc": [d_enc of each pass], "grads": the
+    six parameter gradients summed over the passes (each pass exact in f64;
+    AccumulateGrad's f32 add is within the windows of backward_pass_bounds)}."""
+    bos = [field_backward(fwd, weights, gs, ga) for gs, ga in passes]
+    grads = [sum(bo["grads"][i] for bo in bos) for i in range(6)]
+    return {"passes": bos, "d_enc": [bo["d_enc"] for bo in bos], "grads": grads}
+
+
+def backward_pass_bounds(fwd, bp, weights, fwd_bounds, acc_ulps=None):
+    """Windows of backward_passes: per-pass d_enc windows, and the summed
+    parameter gradients' windows (the passes' windows added, plus one f32
+    rounding of the running sum per pass)."""
+    bbs = [backward_bounds(fwd, bo, weights, fwd_bounds, acc_ulps=acc_ulps)
+           for bo in bp["passes"]]
+    grads = []
+    for i in range(6):
+        w = sum(bb["grads"][i] for bb in bbs)
+        mag = sum(np.abs(bo["grads"][i]) for bo in bp["passes"])
+        grads.append(w + len(bbs) * U32 * (mag + w))
+    return {"passes": bbs, "d_enc": [bb["d_enc"] for bb in bbs], "grads": grads}
+
+
+def f16_underflow(fwd, bo):
+    """How much of a pass's f16 backward falls out of the element type's
+    normal range: for the first rounding point dO = r16(grad_sigma exp(y)),
+    r16(g (1 - a) a) and for the feature gradients d_enc = r16(dX), the
+    fraction of entries whose exact value is nonzero but below 2^-14 (f16
+    subnormal: fewer than 11 significant bits) and the fraction that round to
+    zero.  Returns a dict of those four fractions."""
+    yc = np.clip(fwd["y"].astype(F64), -15, 15)
+    e0 = bo["grad_sigma"].astype(F64) * np.exp(yc)
+    a = fwd["albedo"].astype(F64)
+    er = bo["g16"].astype(F64) * (1 - a) * a
+    exact_o = np.concatenate([e0[:, None], er], 1)
+    out = {}
+    for name, exact, rounded in (("dO", exact_o, bo["dO"]), ("d_enc", bo["dX"], bo["d_enc"])):
+        ex = np.abs(exact)
+        nz = ex > 0
+        n = max(int(nz.sum()), 1)
+        out[name + "_subnormal"] = float(((ex < 2.0 ** -14) & nz).sum() / n)
+        out[name + "_zero"] = float(((rounded == 0) & nz).sum() / n)
+    return out

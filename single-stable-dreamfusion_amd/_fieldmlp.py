@@ -112,6 +112,8 @@ def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners
         checked(m_dev, "m_dev", "int")
     if quads is not None:
         checked(quads, "quads", "int")
+        if quads.dtype != torch.int32 or tuple(quads.shape) != (table.shape[0], 4):
+            raise RuntimeError("quads must be a [rows, 4] int32 tensor (rows = table rows)")
         elem = _d.BF16 if table.dtype == torch.bfloat16 else _d.F16
         call("dfhip_grid_field_forward_quads", elem, ptr(xyz), float(bound), ptr(table),
              ptr(quads), ptr(offsets), offsets.shape[0] - 1, float(S), int(H), int(gridtype),

@@ -766,6 +766,10 @@ extern "C" int dfhip_grid_field_forward_quads(int elem, const float *xyz, float 
         set_error("grid_field_forward_quads: null quads");
         return DFHIP_EINVAL;
     }
+    if (reinterpret_cast<uintptr_t>(quads) & 15) {
+        set_error("grid_field_forward_quads: quads must be 16-byte aligned");
+        return DFHIP_EINVAL;
+    }
     return grid_field_forward("grid_field_forward_quads", elem, xyz, bound, table, quads,
                               offsets, L, S, H, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
                               enc, sigma, rgb, rgb_dtype, cap, m_dev, stream);

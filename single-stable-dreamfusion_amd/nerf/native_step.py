@@ -208,6 +208,10 @@ class NativeAlbedoStep:
             self.d_enc2 = torch.empty_like(self.d_enc)
             self.zero_image = torch.zeros(N, 3, **f32)
             self.grad_ws2 = torch.empty(N, **f32)
+            # pass 2's compositing gradients in buffers of their own, so both
+            # passes' intermediates stay readable after the step (tests)
+            self.grad_sigma2 = torch.empty(cap, **f32)
+            self.grad_albedo2 = torch.empty(cap, 3, **f16)
             self._emb_launch2 = None
         self.params = [p for p in m.parameters() if p.requires_grad]
         self.grads = [(p, p.grad) for p in self.params]
@@ -281,8 +285,7 @@ class NativeAlbedoStep:
             if self.lam > 0:
                 call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss),
                      stream())
-            if self.lam_orient > 0:
-                self.loss.add_(self.orient, alpha=self.lam_orient)  # utils.py:398-400
+            self._add_orient_loss()
             # backward: SDS gradient at pred_rgb (unscaled), entropy gradient x scale
             self._backward_two_pass(bw, scale)
             return self.loss
@@ -298,8 +301,7 @@ class NativeAlbedoStep:
                  ptr(self.loss), stream())
         else:
             call("dfhip_ray_head_backward", *head_args, stream())
-        if self.lam_orient > 0:
-            self.loss.add_(self.orient, alpha=self.lam_orient)  # utils.py:398-400
+        self._add_orient_loss()
         _raymarching.composite_rays_train_backward_mixed(
             self.grad_ws, self.grad_image, self.sigma, rgb, self.deltas, self.rays,
             self.ws, self.image, cap, N, 1e-4, self.grad_sigma,
@@ -330,18 +332,20 @@ class NativeAlbedoStep:
         call("dfhip_ray_head_backward", N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d),
              *[ptr(w) for w in bw], ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws),
              None, ptr(self.head_partial), *[ptr(g) for g in gbw], stream())
-        passes = [(self.grad_ws, self.grad_image, self.d_enc, False)]
+        passes = [(self.grad_ws, self.grad_image, self.grad_sigma, self.grad_albedo, self.d_enc,
+                   False)]
         if self.lam > 0:
-            passes.append((self.grad_ws2, self.zero_image, self.d_enc2, True))
-        for i, (g_ws, g_img, d_enc, acc) in enumerate(passes):
+            passes.append((self.grad_ws2, self.zero_image, self.grad_sigma2, self.grad_albedo2,
+                           self.d_enc2, True))
+        for i, (g_ws, g_img, g_sig, g_alb, d_enc, acc) in enumerate(passes):
             if i == 1:
                 call("dfhip_entropy_backward", N, ptr(self.ws), ptr(scale), self.lam,
                      ptr(self.grad_ws2), stream())
             _raymarching.composite_rays_train_backward_mixed(
                 g_ws, g_img, self.sigma, self.albedo, self.deltas, self.rays, self.ws,
-                self.image, cap, N, 1e-4, self.grad_sigma, self.grad_albedo, False)
+                self.image, cap, N, 1e-4, g_sig, g_alb, False)
             _fieldmlp.grid_field_backward(
-                self.enc, self.xyzs, m.bound, self.mlp, self.grad_sigma, self.grad_albedo, d_enc,
+                self.enc, self.xyzs, m.bound, self.mlp, g_sig, g_alb, d_enc,
                 self.mlp_partial, [p.grad for p in self.mlp], self.encoder.offsets, self.rows, S,
                 Hb, gridtype, align, None, None, _parts(self.rows, self.C), self.m_dev,
                 accumulate=acc)
@@ -410,6 +414,17 @@ class NativeAlbedoStep:
             p.grad = g
 
     # ------------------------------------------------------------ helpers
+    def _add_orient_loss(self):
+        """loss += lambda_orient * orient (utils.py:398-400).  The entropy
+        launch writes the loss fresh each step; without it (lambda_entropy ==
+        0) the orientation term overwrites it, so no step adds onto the last."""
+        if self.lam_orient <= 0:
+            return
+        if self.lam > 0:
+            self.loss.add_(self.orient, alpha=self.lam_orient)
+        else:
+            torch.mul(self.orient, self.lam_orient, out=self.loss)
+
     def _bg_weights(self):
         if self.bg_layers is None:
             return [None] * 4

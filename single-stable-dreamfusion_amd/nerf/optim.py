@@ -24,10 +24,15 @@ import _dfhip
 _MAX_TENSORS = 24
 
 
-def eligible(optimizer, scaler):
+def eligible(optimizer, scaler, unit_scale=False):
+    """True when NativeAdamAmp reproduces scaler.step(optimizer) +
+    scaler.update().  A disabled GradScaler is accepted only with
+    unit_scale=True (the bf16 trainer): the unit-scale form skips a step with
+    non-finite gradients where torch Adam would write them into the
+    parameters, so plain fp32 training keeps torch's optimizer."""
     if not isinstance(optimizer, torch.optim.Adam) or type(optimizer) is not torch.optim.Adam:
         return False
-    if scaler is None:
+    if scaler is None or (not scaler.is_enabled() and not unit_scale):
         return False
     if scaler.is_enabled() and (scaler._growth_factor, scaler._backoff_factor) != (2.0, 0.5):
         return False

@@ -172,7 +172,7 @@ def flat_allreduce_(params, world_size, group=None):
     When the grads are views of one bucket (flat_grad_bucket_, the native
     step) the all-reduce and the 1/world scaling run in place on it."""
     params = [p for p in params if p.requires_grad]
-    if world_size <= 1 or not params:
+    if not params or (world_size <= 1 and not (dist.is_available() and dist.is_initialized())):
         return
     bucket = _grad_bucket(params)
     if bucket is not None:
@@ -450,8 +450,8 @@ class Trainer(object):
         if self._native_opt is None:
             from . import optim as _optim
             self._native_opt = (_optim.NativeAdamAmp(self.optimizer, self.scaler)
-                                if self.native_optimizer and _optim.eligible(self.optimizer,
-                                                                            self.scaler)
+                                if self.native_optimizer and _optim.eligible(
+                                    self.optimizer, self.scaler, unit_scale=self.bf16)
                                 else False)
         if self._native_opt:
             self._native_opt.step()
@@ -491,8 +491,9 @@ class Trainer(object):
         if not self.fused_backward or shading != "albedo" or self.bf16:
             # the two-pass backward and the normal-shaded steps are graphed only
             # as the native step
+            from . import graph as _graph
             from . import native_step as _native
-            return _native.eligible(self, shading)
+            return _graph._NATIVE and _native.eligible(self, shading)
         return (self.graph_step and self.fp16 and self.model.cuda_ray and shading == "albedo"
                 and self.fused_backward and hasattr(self.guidance, "sds_grad")
                 and self.device.type == "cuda")

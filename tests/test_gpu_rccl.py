@@ -1,0 +1,70 @@
+"""The RCCL (torch.distributed "nccl") gradient exchange on the one GPU of the
+box: a 1-rank process group initialised the way bench.py does it
+(`init_process_group("nccl", device_id=...)`), a graph-replayed native train
+step whose gradients are views of one flat bucket, and `flat_allreduce_`
+(reference DDP all-reduce, nerf/utils.py:200-202) run in place on that bucket
+through RCCL.  Run in a spawned process so the process group never leaks into
+the rest of the session."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(port, out):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "single-stable-dreamfusion_amd")]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    res = {"backend": dist.get_backend()}
+    import bench
+    from nerf.utils import _grad_bucket, flat_allreduce_
+    trainer, data = bench.make_trainer(64, 3, 0, 1, True, graph=True)
+    for i in range(4):
+        trainer.train_iteration(data.collate([i]))
+    torch.cuda.synchronize()
+    params = [p for p in trainer.model.parameters() if p.requires_grad]
+    bucket = _grad_bucket(params)
+    res["bucket"] = bucket is not None
+    if bucket is not None:
+        before = bucket.clone()
+        ptr = bucket.data_ptr()
+        flat_allreduce_(params, 1)  # in place on the bucket, through RCCL
+        torch.cuda.synchronize()
+        res["in_place"] = _grad_bucket(params) is not None and bucket.data_ptr() == ptr
+        res["unchanged"] = bool(torch.equal(before, bucket))
+        res["numel"] = bucket.numel()
+    x = torch.arange(1024, dtype=torch.float32, device=dev)
+    dist.all_reduce(x)
+    res["sum_ok"] = bool(torch.equal(x, torch.arange(1024, dtype=torch.float32, device=dev)))
+    dist.destroy_process_group()
+    out.put(res)
+
+
+def test_rccl_flat_allreduce_in_place(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert res["backend"] == "nccl"
+    assert res["bucket"], "native step gradients are not views of one flat bucket"
+    assert res["in_place"] and res["unchanged"]
+    assert res["numel"] >= 903480 * 2  # grid table + MLPs, one bucket
+    assert res["sum_ok"]

@@ -178,3 +178,27 @@ def test_shaded_graph_training_runs(gpu, dtype):
     after = [p.detach() for p in model.parameters() if p.requires_grad]
     for a, b in zip(after, before):
         assert torch.isfinite(a).all() and not torch.equal(a, b)
+
+
+@pytest.mark.parametrize("two_pass", [False, True])
+def test_shaded_loss_is_fresh_each_step_without_entropy(gpu, two_pass):
+    """lambda_entropy = 0 with a shading: the loss is lambda_orient * orient of
+    this step (utils.py:385-402 builds it fresh), not a sum over steps; repeated
+    body() calls on the same draws give the same loss."""
+    trainer, data = _trainer(64, 5)
+    trainer.opt.lambda_entropy = 0.0
+    trainer.fused_backward = not two_pass
+    from nerf.native_step import NativeAlbedoStep
+    shading = "lambertian" if not two_pass else "albedo"
+    nat = NativeAlbedoStep(trainer, 64, 64, shading, 0.1)
+    batch = data.collate([0])
+    nat.prologue(batch["pose"], batch["intrinsics"], 3, 77)
+    losses = []
+    for _ in range(3):
+        losses.append(float(nat.body()))
+    torch.cuda.synchronize()
+    assert losses[0] == losses[1] == losses[2], losses
+    if shading != "albedo":
+        want = trainer.opt.lambda_orient * float(nat.orient)
+        np.testing.assert_allclose(losses[0], want, rtol=1e-6)
+        assert losses[0] > 0

@@ -202,3 +202,16 @@ def test_bench_launches_n_ranks_itself():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["replicas_identical"]
+
+
+def test_native_adam_unit_scale_only_for_bf16():
+    """A disabled GradScaler (fp32 or bf16 training) takes the native
+    unit-scale Adam only when the trainer asks for it (bf16); plain fp32 keeps
+    torch Adam, which writes non-finite gradients where the native form skips."""
+    import torch
+    from nerf.optim import eligible
+    p = torch.nn.Parameter(torch.zeros(4))
+    opt = torch.optim.Adam([p], lr=1e-3)
+    off = torch.amp.GradScaler("cuda", enabled=False)
+    assert not eligible(opt, off)
+    assert not eligible(opt, None, unit_scale=True)
