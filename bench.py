@@ -232,20 +232,16 @@ def bench_c5(args, rank, world):
     injected w(t) N(0,1) guidance of SD-2.1-base's text width (1024); the
     SD-2.1-base UNet / VAE cannot be loaded offline, so the full SDS step is
     not timed."""
-    import _dfhip
     tr, dat = make_trainer(args.c5_res, args.seed, rank, world, True, graph=not args.eager,
                            mock_sds=args.mock_sds, bf16=True)
     for _ in range(args.warmup):
         tr.train_iteration(dat.collate([0]))
-    timer = _dfhip.new_kernel_timer()
-    _dfhip.set_kernel_timer(timer)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.train_iteration(dat.collate([0]))
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
-    _dfhip.set_kernel_timer(None)
     last = min(16, args.steps)
     rows = [(tr.model.local_step - 1 - i) % 16 for i in range(last)]
     samples = float(tr.model.step_counter[rows, 0].float().mean().item())
@@ -258,8 +254,10 @@ def bench_c5(args, rank, world):
            "dtype": "bf16+f32", "rays_per_step": n, "steps": args.steps,
            "ms_per_step": round(dt * 1e3, 3), "steps_per_sec": round(1.0 / dt, 3),
            "rays_per_sec": round(n / dt, 1), "mean_samples_per_step": round(samples, 1),
-           "native_step": bool(g is not None and g.native is not None),
-           "kernels": summarize_kernels(timer.records)}
+           "native_step": bool(g is not None and g.native is not None)}
+    if not args.no_kernel_timing:
+        kern, info = kernel_timing_pass(tr, lambda: tr.train_iteration(dat.collate([0])), 5)
+        out["kernels"], out["kernel_timing"] = kern, info
     fm = field_mlp_report(tr)
     if fm:
         out["field_mlp"] = fm
@@ -291,6 +289,76 @@ def field_mlp_report(trainer):
                      "mfma": {"achieved": round(tf, 2), "peak": MFMA_PEAK_TFLOPS,
                               "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TFLOPS, 5)}}
     return out
+
+
+SPIN_CYCLES = 4_000_000  # > the eager step's host issue time (~1 ms)
+
+
+def kernel_timing_pass(trainer, step, k):
+    """Per-kernel HIP-event timings of the train step, measured right after the
+    timed region in the same process: k more steps in which every graphed
+    native step runs its eager twin (GraphedTrainStep.step_timed: the same
+    launches, arguments and buffers the replay runs) with a kernel timer
+    installed, so each launch is bracketed by events on its launch stream.
+    The timed region itself replays graphs with no events inside; the
+    rocprofv3 kernel trace of a bench run (profiles/) times the replayed
+    kernels for comparison.  Returns (summary per region, info)."""
+    import _dfhip
+    eager = not trainer.graph_step
+    trainer.step_hook = None if eager else (lambda g: g.step_timed())
+    timer = _dfhip.new_kernel_timer()
+    _dfhip.set_kernel_timer(timer)
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            # a spin kernel holds the stream while the host issues the whole
+            # eager step, so its launches then run back to back as in the graph
+            # and no region's events bracket host launch gaps
+            torch.cuda._sleep(SPIN_CYCLES)
+            step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / k
+    finally:
+        _dfhip.set_kernel_timer(None)
+        trainer.step_hook = None
+    info = {"steps": k, "ms_per_step_incl_spin": round(dt * 1e3, 3),
+            "note": (f"HIP events around each launch on its stream, {k} steps of the eager twin "
+                     "of the replayed native step run after the timed region"
+                     if not eager else f"HIP events around each launch, {k} eager steps")}
+    return summarize_kernels(timer.records), info
+
+
+# SURVEY §8(d) per-step algorithmic byte model of the reference's op sequence
+# (each logical operand once, backward once): 472 M + 492 N + 50.85 MB
+def survey_step_bytes(M, N):
+    return 472.0 * M + 492.0 * N + 28.0 * 1_816_247
+
+
+def step_roofline(kernels, steps, M, N, trainer):
+    """SURVEY §8(d) step-level roofline: sum of every timed region's
+    algorithmic bytes / sum of their kernel time, per step, against the HBM
+    peak; with each region's bytes per launch, time and share."""
+    tot_b = sum(v["bytes_per_launch"] * v["launches"] for v in kernels.values()) / steps
+    tot_us = sum(v["total_ms"] for v in kernels.values()) * 1e3 / steps
+    gbs = tot_b / (tot_us * 1e-6) / 1e9
+    per = {k: {"bytes_per_launch": v["bytes_per_launch"], "avg_us": v["avg_us"],
+               "launches_per_step": round(v["launches"] / steps, 3),
+               "achieved_GBs": v["achieved_GBs"],
+               "frac": round(v["achieved_GBs"] / HBM_PEAK_GBS, 4),
+               "share_of_kernel_time": round(v["total_ms"] * 1e3 / steps / tot_us, 4)}
+           for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_ms"])}
+    sb = survey_step_bytes(M, N)
+    return {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "bytes_per_step": int(tot_b), "kernel_us_per_step": round(tot_us, 2),
+            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "frac_of_measured_6290": round(gbs / 6290.0, 4),
+            "survey_model_bytes_per_step": int(sb),
+            "survey_model_GBs": round(sb / (tot_us * 1e-6) / 1e9, 1),
+            "note": "bytes: each region's compulsory operand bytes at this path's dtypes "
+                    "(nerf/native_step.py timed regions); survey_model: SURVEY 8(d) "
+                    "472 M + 492 N + 50.85 MB over the same kernel time",
+            "kernels": per}
 
 
 def summarize_kernels(records):
@@ -472,16 +540,13 @@ def main():
     for _ in range(args.warmup):
         step()
 
-    timer = None
-    if not args.no_kernel_timing:
-        timer = _dfhip.new_kernel_timer()
-        _dfhip.set_kernel_timer(timer)
-
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
+    # the timed region runs the product path: one graph replay per step (the
+    # native step's graph holds the whole backward and, on one GPU, Adam)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -489,7 +554,6 @@ def main():
     host_issue = time.perf_counter() - t0  # host done issuing (no sync inside the loop)
     barrier()
     elapsed = time.perf_counter() - t0
-    _dfhip.set_kernel_timer(None)
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -500,7 +564,9 @@ def main():
     last = min(16, args.steps)
     rows = [(trainer.model.local_step - 1 - i) % 16 for i in range(last)]
     samples = float(trainer.model.step_counter[rows, 0].float().mean().item())
-    kernels = summarize_kernels(timer.records) if timer else {}
+    kernels, timing = {}, None
+    if not args.no_kernel_timing:
+        kernels, timing = kernel_timing_pass(trainer, step, min(args.steps, 20))
 
     rays_per_step = args.res * args.res
     steps_per_sec = args.steps * world / elapsed  # whole-job aggregate (every rank steps)
@@ -524,6 +590,9 @@ def main():
         "steps_per_sec": round(steps_per_sec, 3),
         "host_issue_ms_per_step": round(host_issue / args.steps * 1e3, 3),
     }
+    g0 = next(iter(trainer._graphs.values()), None)
+    if g0 is not None:
+        result["config"]["optimizer_in_graph"] = bool(g0.optimizer_in_graph)
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         kd = kernels[dom]
@@ -535,7 +604,8 @@ def main():
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
             "traffic": traffic, "traffic_source": note,
             "traffic_by_kernel": MEASURE_TRAFFIC_DETAIL.get(dom), "avg_us": kd["avg_us"],
-            "bytes_per_launch": kd["bytes_per_launch"]}
+            "bytes_per_launch": kd["bytes_per_launch"],
+            "timing": timing["note"] if timing else None}
         if dom == "grid_encode_backward":
             # the binned backward's real ceiling: one f64 LDS add per (sample,
             # level, corner, channel) before the walk's in-register merging
@@ -546,9 +616,9 @@ def main():
                 "unit": "T f64 LDS adds/s", "frac": round(rate / LDS_F64_ATOMIC_PEAK, 4),
                 "ops_per_launch": int(ops)}
         result["kernels"] = kernels
-        step_ms = result["ms_per_step"]
-        result["kernel_share_of_step"] = {k: round(v["total_ms"] / args.steps / step_ms, 4)
-                                          for k, v in kernels.items()}
+        result["step_roofline"] = step_roofline(kernels, timing["steps"], samples,
+                                                rays_per_step, trainer)
+        result["kernel_timing"] = timing
     if world == 1 and not args.no_kernel_timing:
         result["field_mlp"] = field_mlp_report(trainer)
     if world == 1 and not args.no_alt_backward:
@@ -591,8 +661,12 @@ def main():
         shade["albedo_ms_per_step"] = base
         shade["schedule_ms_per_step"] = round(0.2 * base + 0.4 * shade["textureless_ms_per_step"]
                                               + 0.4 * shade["lambertian_ms_per_step"], 3)
+        # main.py -O: albedo_iters 1000 of iters 10000, then the schedule
+        shade["iters_weighted_ms_per_step"] = round(0.1 * base + 0.9 * shade["schedule_ms_per_step"],
+                                                    3)
         shade["note"] = ("steps >= albedo_iters: 0.2 albedo + 0.4 textureless + 0.4 lambertian "
-                         "(utils.py:346-359), native graph-replayed, fused backward")
+                         "(utils.py:346-359), native graph-replayed, fused backward; "
+                         "iters_weighted: 0.1 albedo (albedo_iters 1000 of 10000) + 0.9 schedule")
         result["shading"] = shade
     if world == 1 and not args.no_c5:
         result["c5"] = bench_c5(args, rank, world)

@@ -517,6 +517,19 @@ int dfhip_adam_amp_step(int count, float *const *params, const float *const *gra
                         float *scale, int32_t *growth_tracker, float *found_inf,
                         float growth_factor, float backoff_factor, int growth_interval,
                         dfhip_stream_t stream);
+/* The same update with the learning rates read on the device at run time:
+ * tensor k uses lr_dev[lr_slot[k]] (lr_slot: HOST int array, values 0..255;
+ * lr_dev: DEVICE f32 array), so the launches can be captured once in a HIP
+ * graph and replayed while LambdaLR changes the rates (main.py:131; the native
+ * train step writes lr_dev from its prologue, dfhip_train_step_prologue_lr). */
+int dfhip_adam_amp_step_lr_dev(int count, float *const *params, const float *const *grads,
+                               float *const *exp_avg, float *const *exp_avg_sq,
+                               float *const *steps, const uint64_t *numel,
+                               const int32_t *lr_slot, const float *lr_dev, const float *beta1,
+                               const float *beta2, const float *eps, const float *weight_decay,
+                               float *scale, int32_t *growth_tracker, float *found_inf,
+                               float growth_factor, float backoff_factor, int growth_interval,
+                               dfhip_stream_t stream);
 
 /* Per-ray tail of run_cuda (nerf/renderer.py:536-551, csrc/head.hip).
  * Forward: bg = sigmoid(W2 relu(W1 freq6(rays_d) + b1) + b2) with the
@@ -596,6 +609,18 @@ int dfhip_train_step_prologue(const float *pose, float fx, float fy, float cx, f
                               float *rays_d, float *nears, float *fars, float *noises,
                               float *bg_color, float *g_image, int32_t *counter,
                               dfhip_stream_t stream);
+/* The same launch also writing this step's learning rates lr_dev[0..n_lr) =
+ * lr_host[0..n_lr) (n_lr <= 8; lr_host a HOST array copied into the launch's
+ * arguments, lr_dev DEVICE memory), read later in the step by
+ * dfhip_adam_amp_step_lr_dev inside the replayed graph. */
+int dfhip_train_step_prologue_lr(const float *pose, float fx, float fy, float cx, float cy,
+                                 uint32_t H, uint32_t W, const float *aabb, float min_near,
+                                 uint64_t seed, uint64_t step, int perturb, const float *alphas,
+                                 uint32_t min_step, uint32_t max_step, float *rays_o,
+                                 float *rays_d, float *nears, float *fars, float *noises,
+                                 float *bg_color, float *g_image, int32_t *counter,
+                                 const float *lr_host, uint32_t n_lr, float *lr_dev,
+                                 dfhip_stream_t stream);
 
 /* nerf/renderer.py:496-532 — the inference branch of run_cuda (the host loop
  * of march_rays raymarching.cu:700-804 -> network_grid.common_forward

@@ -114,6 +114,8 @@ _SIGS = {
         _vp],
     "dfhip_adam_amp_step": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                             _vp, _vp, _f32, _f32, _i32, _vp],
+    "dfhip_adam_amp_step_lr_dev": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _f32, _f32, _i32, _vp],
     "dfhip_ray_head_forward": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                _vp, _vp, _vp],
     "dfhip_ray_head_backward": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -129,6 +131,10 @@ _SIGS = {
     "dfhip_train_step_prologue": [_vp, _f32, _f32, _f32, _f32, _u32, _u32, _vp, _f32,
                                   ctypes.c_uint64, ctypes.c_uint64, _i32, _vp, _u32, _u32, _vp,
                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_train_step_prologue_lr": [_vp, _f32, _f32, _f32, _f32, _u32, _u32, _vp, _f32,
+                                     ctypes.c_uint64, ctypes.c_uint64, _i32, _vp, _u32, _u32,
+                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp,
+                                     _vp],
     "dfhip_render_rays_infer": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _vp,
                                 _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp, _vp, _vp, _vp],

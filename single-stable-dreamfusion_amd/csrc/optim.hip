@@ -50,6 +50,10 @@ struct Batch {
     Tensor t[kMaxTensors];
     int count;
     uint32_t blocks;
+    // device learning rates (graph-replayed step): tensor k's lr is
+    // lr_dev[lr_slot[k]] read at run time; null: the by-value t.lr
+    const float *lr_dev;
+    uint8_t lr_slot[kMaxTensors];
 };
 
 // The tensor of this (wave-uniform) block: a scalar scan of the block table.
@@ -106,13 +110,15 @@ __device__ __forceinline__ float adam1(const Tensor &t, const AdamK &k, float g,
 __global__ __launch_bounds__(kThreads) void k_adam(Batch B, const float *scale,
                                                    const float *found_inf) {
     if (*found_inf != 0.0f) return;
-    const Tensor &t = B.t[block_tensor(B)];
+    const int ti = block_tensor(B);
+    const Tensor &t = B.t[ti];
     const uint64_t e0 = (uint64_t)(blockIdx.x - t.block0) * kPerBlock;
     // per-tensor constants (the same f32 expressions torch evaluates per element)
     const float step = *t.step + 1.0f;
     AdamK k;
     k.s = *scale;
-    k.step_size = t.lr / (1.0f - powf(t.b1, step));
+    const float lr = B.lr_dev ? B.lr_dev[B.lr_slot[ti]] : t.lr;
+    k.step_size = lr / (1.0f - powf(t.b1, step));
     k.bc2s = sqrtf(1.0f - powf(t.b2, step));
     for_chunk(
         t, e0,
@@ -171,6 +177,74 @@ __global__ __launch_bounds__(64) void k_finalize(Batch B, float *scale, int32_t 
 
 using namespace dfhip;
 
+namespace dfhip {
+namespace opt {
+
+static int adam_amp_step(int count, float *const *params, const float *const *grads,
+                         float *const *exp_avg, float *const *exp_avg_sq, float *const *steps,
+                         const uint64_t *numel, const float *lr, const int32_t *lr_slot,
+                         const float *lr_dev, const float *beta1, const float *beta2,
+                         const float *eps, const float *weight_decay, float *scale,
+                         int32_t *growth_tracker, float *found_inf, float growth_factor,
+                         float backoff_factor, int growth_interval, hipStream_t s) {
+    const char *name = "adam_amp_step";
+    if (count <= 0) return DFHIP_OK;
+    if (count > kMaxTensors) {
+        set_error("%s: at most %d tensors (got %d)", name, kMaxTensors, count);
+        return DFHIP_EINVAL;
+    }
+    if (!scale || !growth_tracker || !found_inf) {
+        set_error("%s: null scaler state", name);
+        return DFHIP_EINVAL;
+    }
+    Batch B;
+    B.count = count;
+    B.lr_dev = lr_dev;
+    uint32_t blocks = 0;
+    for (int k = 0; k < count; ++k) {
+        if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || !steps[k]) {
+            set_error("%s: null pointer in tensor %d", name, k);
+            return DFHIP_EINVAL;
+        }
+        Tensor &t = B.t[k];
+        t.p = params[k];
+        t.g = grads[k];
+        t.m = exp_avg[k];
+        t.v = exp_avg_sq[k];
+        t.step = steps[k];
+        t.n = numel[k];
+        t.block0 = blocks;
+        t.lr = lr ? lr[k] : 0.0f;
+        if (lr_dev) {
+            if (lr_slot[k] < 0 || lr_slot[k] > 255) {
+                set_error("%s: lr slot of tensor %d out of range", name, k);
+                return DFHIP_EINVAL;
+            }
+            B.lr_slot[k] = (uint8_t)lr_slot[k];
+        }
+        t.b1 = beta1[k];
+        t.b2 = beta2[k];
+        t.eps = eps[k];
+        t.wd = weight_decay[k];
+        const uint64_t nb = ceil_div<uint64_t>(numel[k], kPerBlock);
+        if (nb > 0x7FFFFFFFull - blocks) {
+            set_error("%s: tensor %d has an unsupported size", name, k);
+            return DFHIP_EINVAL;
+        }
+        blocks += (uint32_t)nb;
+    }
+    B.blocks = blocks;
+    if (blocks == 0) blocks = 1;  // all tensors empty: one block that finds no work
+    k_nonfinite<<<blocks, kThreads, 0, s>>>(B, found_inf);
+    k_adam<<<blocks, kThreads, 0, s>>>(B, scale, found_inf);
+    k_finalize<<<1, 64, 0, s>>>(B, scale, growth_tracker, found_inf, growth_factor,
+                                backoff_factor, growth_interval);
+    return check_launch(name);
+}
+
+}  // namespace opt
+}  // namespace dfhip
+
 extern "C" int dfhip_adam_amp_step(int count, float *const *params, const float *const *grads,
                                    float *const *exp_avg, float *const *exp_avg_sq,
                                    float *const *steps, const uint64_t *numel, const float *lr,
@@ -179,50 +253,32 @@ extern "C" int dfhip_adam_amp_step(int count, float *const *params, const float 
                                    int32_t *growth_tracker, float *found_inf,
                                    float growth_factor, float backoff_factor,
                                    int growth_interval, dfhip_stream_t stream) {
-    const char *name = "adam_amp_step";
-    if (count <= 0) return DFHIP_OK;
-    if (count > opt::kMaxTensors) {
-        set_error("%s: at most %d tensors (got %d)", name, opt::kMaxTensors, count);
+    if (count > 0 && !lr) {
+        set_error("adam_amp_step: null lr array");
         return DFHIP_EINVAL;
     }
-    if (!scale || !growth_tracker || !found_inf) {
-        set_error("%s: null scaler state", name);
+    return opt::adam_amp_step(count, params, grads, exp_avg, exp_avg_sq, steps, numel, lr,
+                              nullptr, nullptr, beta1, beta2, eps, weight_decay, scale,
+                              growth_tracker, found_inf, growth_factor, backoff_factor,
+                              growth_interval, as_stream(stream));
+}
+
+extern "C" int dfhip_adam_amp_step_lr_dev(int count, float *const *params,
+                                          const float *const *grads, float *const *exp_avg,
+                                          float *const *exp_avg_sq, float *const *steps,
+                                          const uint64_t *numel, const int32_t *lr_slot,
+                                          const float *lr_dev, const float *beta1,
+                                          const float *beta2, const float *eps,
+                                          const float *weight_decay, float *scale,
+                                          int32_t *growth_tracker, float *found_inf,
+                                          float growth_factor, float backoff_factor,
+                                          int growth_interval, dfhip_stream_t stream) {
+    if (count > 0 && (!lr_slot || !lr_dev)) {
+        set_error("adam_amp_step_lr_dev: null lr slot array or device lr");
         return DFHIP_EINVAL;
     }
-    opt::Batch B;
-    B.count = count;
-    uint32_t blocks = 0;
-    for (int k = 0; k < count; ++k) {
-        if (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k] || !steps[k]) {
-            set_error("%s: null pointer in tensor %d", name, k);
-            return DFHIP_EINVAL;
-        }
-        opt::Tensor &t = B.t[k];
-        t.p = params[k];
-        t.g = grads[k];
-        t.m = exp_avg[k];
-        t.v = exp_avg_sq[k];
-        t.step = steps[k];
-        t.n = numel[k];
-        t.block0 = blocks;
-        t.lr = lr[k];
-        t.b1 = beta1[k];
-        t.b2 = beta2[k];
-        t.eps = eps[k];
-        t.wd = weight_decay[k];
-        const uint64_t nb = ceil_div<uint64_t>(numel[k], opt::kPerBlock);
-        if (nb > 0x7FFFFFFFull - blocks) {
-            set_error("%s: tensor %d has an unsupported size", name, k);
-            return DFHIP_EINVAL;
-        }
-        blocks += (uint32_t)nb;
-    }
-    B.blocks = blocks;
-    hipStream_t s = as_stream(stream);
-    if (blocks == 0) blocks = 1;  // all tensors empty: one block that finds no work
-    opt::k_nonfinite<<<blocks, opt::kThreads, 0, s>>>(B, found_inf);
-    opt::k_adam<<<blocks, opt::kThreads, 0, s>>>(B, scale, found_inf);
-    opt::k_finalize<<<1, 64, 0, s>>>(B, scale, growth_tracker, found_inf, growth_factor,
-                                     backoff_factor, growth_interval);
-    return check_launch(name);
+    return opt::adam_amp_step(count, params, grads, exp_avg, exp_avg_sq, steps, numel, nullptr,
+                              lr_slot, lr_dev, beta1, beta2, eps, weight_decay, scale,
+                              growth_tracker, found_inf, growth_factor, backoff_factor,
+                              growth_interval, as_stream(stream));
 }

@@ -55,6 +55,8 @@ __device__ __forceinline__ void normal2(uint32_t a, uint32_t b, float &z0, float
     z1 = r * s;
 }
 
+constexpr uint32_t kMaxLr = 8;
+
 struct Args {
     cam::Pose pose;
     float fx, fy, cx, cy;
@@ -65,6 +67,11 @@ struct Args {
     int perturb;
     const float *alphas;  // alphas_cumprod [T]
     uint32_t min_step, max_step;
+    // per-step scalars for later launches of a replayed graph (the optimizer's
+    // learning rates): lr_dev[0..n_lr) = lr[0..n_lr)
+    float lr[kMaxLr];
+    uint32_t n_lr;
+    float *lr_dev;
 };
 
 __global__ __launch_bounds__(256) void k_step_prologue(Args a, float *__restrict__ rays_o,
@@ -81,6 +88,7 @@ __global__ __launch_bounds__(256) void k_step_prologue(Args a, float *__restrict
         counter[0] = 0;
         counter[1] = 0;
     }
+    if (n < a.n_lr) a.lr_dev[n] = a.lr[n];
     if (n >= N) return;
     float o[3], d[3];
     cam::pixel_ray(a.pose, a.fx, a.fy, a.cx, a.cy, a.W, n, o, d);
@@ -127,14 +135,12 @@ __global__ __launch_bounds__(256) void k_step_prologue(Args a, float *__restrict
 
 using namespace dfhip;
 
-extern "C" int dfhip_train_step_prologue(const float *pose, float fx, float fy, float cx,
-                                         float cy, uint32_t H, uint32_t W, const float *aabb,
-                                         float min_near, uint64_t seed, uint64_t step,
-                                         int perturb, const float *alphas, uint32_t min_step,
-                                         uint32_t max_step, float *rays_o, float *rays_d,
-                                         float *nears, float *fars, float *noises,
-                                         float *bg_color, float *g_image, int32_t *counter,
-                                         dfhip_stream_t stream) {
+extern "C" int dfhip_train_step_prologue_lr(
+    const float *pose, float fx, float fy, float cx, float cy, uint32_t H, uint32_t W,
+    const float *aabb, float min_near, uint64_t seed, uint64_t step, int perturb,
+    const float *alphas, uint32_t min_step, uint32_t max_step, float *rays_o, float *rays_d,
+    float *nears, float *fars, float *noises, float *bg_color, float *g_image, int32_t *counter,
+    const float *lr_host, uint32_t n_lr, float *lr_dev, dfhip_stream_t stream) {
     const char *name = "train_step_prologue";
     if (!pose || !aabb || !rays_o || !rays_d || !nears || !fars) {
         set_error("%s: null pointer", name);
@@ -146,6 +152,11 @@ extern "C" int dfhip_train_step_prologue(const float *pose, float fx, float fy, 
     }
     if (g_image && (!alphas || max_step < min_step)) {
         set_error("%s: the SDS draw needs alphas and min_step <= max_step", name);
+        return DFHIP_EINVAL;
+    }
+    if (n_lr > st::kMaxLr || (n_lr && (!lr_host || !lr_dev))) {
+        set_error("%s: at most %u learning rates, with host and device arrays", name,
+                  st::kMaxLr);
         return DFHIP_EINVAL;
     }
     const uint64_t n = (uint64_t)H * W;
@@ -165,9 +176,27 @@ extern "C" int dfhip_train_step_prologue(const float *pose, float fx, float fy, 
     a.alphas = alphas;
     a.min_step = min_step;
     a.max_step = max_step;
+    a.n_lr = n_lr;
+    a.lr_dev = lr_dev;
+    for (uint32_t i = 0; i < st::kMaxLr; ++i) a.lr[i] = i < n_lr ? lr_host[i] : 0.0f;
+    // at least one block: the counter reset and the lr pack run with no rays
     const uint32_t blocks = n ? ceil_div((uint32_t)n, 256u) : 1u;
     st::k_step_prologue<<<blocks, 256, 0, as_stream(stream)>>>(a, rays_o, rays_d, nears, fars,
                                                                 noises, bg_color, g_image,
                                                                 counter);
     return check_launch(name);
+}
+
+extern "C" int dfhip_train_step_prologue(const float *pose, float fx, float fy, float cx,
+                                         float cy, uint32_t H, uint32_t W, const float *aabb,
+                                         float min_near, uint64_t seed, uint64_t step,
+                                         int perturb, const float *alphas, uint32_t min_step,
+                                         uint32_t max_step, float *rays_o, float *rays_d,
+                                         float *nears, float *fars, float *noises,
+                                         float *bg_color, float *g_image, int32_t *counter,
+                                         dfhip_stream_t stream) {
+    return dfhip_train_step_prologue_lr(pose, fx, fy, cx, cy, H, W, aabb, min_near, seed, step,
+                                        perturb, alphas, min_step, max_step, rays_o, rays_d,
+                                        nears, fars, noises, bg_color, g_image, counter,
+                                        nullptr, 0, nullptr, stream);
 }

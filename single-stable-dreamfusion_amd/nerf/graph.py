@@ -12,12 +12,16 @@ replayed:
   capacity-sized sample buffers, the live count stays on the GPU, every
   per-sample consumer (fused grid field, mixed compositing, their backwards)
   stops at it;
-* the graph holds render -> SDS gradient -> regulariser -> backward down to
-  the feature gradients;
-* after each replay the embedding-gradient scatter (the step's largest
-  kernel) is launched eagerly (timed on its stream like any launch), then the
-  gradient all-reduce (multi-GPU), GradScaler + fused Adam and the LR
-  schedule run as in the eager step.
+* the native step's graph (nerf/native_step.py) holds render -> SDS
+  gradient -> regulariser -> the whole backward, the embedding-gradient
+  scatter included, and on one GPU GradScaler + Adam as well (device
+  learning rates written by the prologue launch); with data parallelism the
+  graph ends at the gradients, and the all-reduce and Adam follow eagerly;
+* the autograd form's graph ends at the feature gradients; the embedding
+  scatter is launched eagerly after each replay, then the optimizer step;
+* kernel timing (bench.py) never reaches into a graph: it runs the native
+  body eagerly under a kernel timer (step_timed()), the same launches the
+  graph replays.
 
 The albedo shading is captured in both forms; the textureless / lambertian
 steps (finite-difference normals, csrc/shade.hip) only as the native step.  RNG draws inside the graph (march noise, background colour, light
@@ -56,6 +60,7 @@ class GraphedTrainStep:
         self._text_src = text_z.data_ptr()  # prompt tensor currently in self.text_z
         self.stream = stream
         self.graph = torch.cuda.CUDAGraph()
+        self.optimizer_in_graph = False
         self.deferred = []
         self.grads = None
         self.counter = None
@@ -71,15 +76,29 @@ class GraphedTrainStep:
 
     def _capture_native(self, data):
         nat = self.native
-        model = self.trainer.model
+        t = self.trainer
+        model = t.model
         timer = _dfhip.set_kernel_timer(None)  # no event records inside the graph
         try:
+            # one GPU: the optimizer step joins the graph (no gradient exchange)
+            self.optimizer_in_graph = False
+            if t.world_size == 1:
+                adam = t.native_adam()
+                if adam:
+                    nat.attach_optimizer(adam)
+                    self.optimizer_in_graph = True
             self.load(data, self.text_z)
             self.stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.stream):
-                nat.body()  # dry run (first-use setup outside the capture)
+                # dry run (first-use setup outside the capture); the optimizer
+                # is not run, its launches are plain kernels
+                nat.body()
+                nat.embedding_backward()
             with torch.cuda.graph(self.graph, stream=self.stream):
                 self.loss = nat.body()
+                nat.embedding_backward()
+                if self.optimizer_in_graph:
+                    nat.optimizer_tail()
             torch.cuda.current_stream().wait_stream(self.stream)
         finally:
             _dfhip.set_kernel_timer(timer)
@@ -158,12 +177,26 @@ class GraphedTrainStep:
             self._text_src = text_z.data_ptr()
 
     def replay(self):
-        """Run the captured part, then the deferred embedding backward; leaves
-        every trainable parameter's .grad set for the optimizer step."""
+        """Run the captured part, then (autograd form) the deferred embedding
+        backward; leaves every trainable parameter's .grad set (and, with
+        optimizer_in_graph, the parameters already updated)."""
         self.graph.replay()
-        if self.native is not None:
-            self.native.embedding_backward()
         for launch, _ in self.deferred:
             launch()
+        for p, g in self.grads:
+            p.grad = g
+
+    def step_timed(self):
+        """The native step's launches run eagerly (no graph) under whatever
+        kernel timer is installed: the same kernels, arguments and buffers the
+        replay runs, each in its timed region (bench.py kernel-timing pass).
+        Call after load(); the optimizer runs when the graph holds it."""
+        nat = self.native
+        if nat is None:
+            raise RuntimeError("step_timed: only the native step has an eager twin")
+        nat.body()
+        nat.embedding_backward()
+        if self.optimizer_in_graph:
+            nat.optimizer_tail()
         for p, g in self.grads:
             p.grad = g

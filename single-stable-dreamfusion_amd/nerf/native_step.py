@@ -16,8 +16,16 @@ the step is, with the same kernels and the same arithmetic:
   graph: march count / emit -> f16 table copy -> fused grid field ->
       compositing -> ray head (background MLP, mix, depth, mask) -> entropy
       loss -> ray head backward with the entropy gradient fused into the
-      weights-sum gradient -> compositing backward -> field MLP backward
-  eager (timed): binned embedding backward -> GradScaler + Adam
+      weights-sum gradient -> compositing backward -> field MLP backward ->
+      binned embedding backward -> GradScaler + Adam (single GPU: the
+      learning rates are device values the prologue writes each step;
+      data-parallel: the graph ends at the embedding gradient, and the
+      all-reduce and Adam follow eagerly)
+
+Every launch sits in a _dfhip.timed region with its algorithmic bytes (the
+regions are no-ops unless a kernel timer is installed, and the graph is
+captured without one): bench.py's kernel-timing pass runs the same body
+eagerly under a timer for the per-kernel and step-level roofline.
 
 Gradients are bit-identical to the autograd step given the same draws
 (tests/test_gpu_native_step.py): the loss scale enters exactly where
@@ -39,6 +47,8 @@ reference's grid network (16 x 2 tiled grid, 32 -> 64 -> 64 -> 4 MLP), a
 background MLP (bg_radius > 0) or a random background colour, and
 lambda_opacity == 0 (the -O defaults); anything else keeps the autograd step.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -216,6 +226,23 @@ class NativeAlbedoStep:
         self.params = [p for p in m.parameters() if p.requires_grad]
         self.grads = [(p, p.grad) for p in self.params]
         self._emb_launch = None
+        # optimizer inside the graph (attach_optimizer): the learning rates
+        # live on the device, written by the prologue launch every step
+        self.lr_dev = torch.zeros(8, **f32)
+        self.adam = None
+        self._lr_source = None
+        self.n_params = sum(p.numel() for p in self.params)
+
+    def attach_optimizer(self, native_adam):
+        """Run GradScaler + Adam (nerf/optim.py NativeAdamAmp) as the step's
+        last launches, with device learning rates (captured in the graph)."""
+        self.adam = native_adam.device_lr_launch(self.lr_dev)
+        self._lr_source = native_adam.group_lrs
+
+    def optimizer_tail(self):
+        """The attached optimizer step (a timed region: 28 B per parameter)."""
+        with _dfhip.timed("adam", 28 * self.n_params):
+            self.adam()
 
     # ------------------------------------------------------------ per step
     def prologue(self, pose, intrinsics, seed, step):
@@ -224,11 +251,17 @@ class NativeAlbedoStep:
         host = np.ascontiguousarray(np.asarray(pose, dtype=np.float32).reshape(-1, 4, 4)[0, :3, :4])
         fx, fy, cx, cy = (float(v) for v in intrinsics)
         lo, hi = self.t_range
-        call("dfhip_train_step_prologue", host.ctypes.data, fx, fy, cx, cy, self.H, self.W,
-             self.aabb.ctypes.data, 0.2, int(seed) & 0xFFFFFFFFFFFFFFFF,
-             int(step) & 0xFFFFFFFFFFFFFFFF, 1, ptr(self.alphas), lo, hi, ptr(self.rays_o),
-             ptr(self.rays_d), ptr(self.nears), ptr(self.fars), ptr(self.noises),
-             ptr(self.bg_color), ptr(self.g_image), ptr(self.counter), stream())
+        lrs = self._lr_source() if self._lr_source is not None else []
+        lr_host = (ctypes.c_float * max(1, len(lrs)))(*lrs)
+        N = self.N
+        with _dfhip.timed("step_prologue", N * (24 + 8 + 4 + 12) +
+                          (12 * N if self.bg_color is not None else 0)):
+            call("dfhip_train_step_prologue_lr", host.ctypes.data, fx, fy, cx, cy, self.H,
+                 self.W, self.aabb.ctypes.data, 0.2, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                 int(step) & 0xFFFFFFFFFFFFFFFF, 1, ptr(self.alphas), lo, hi, ptr(self.rays_o),
+                 ptr(self.rays_d), ptr(self.nears), ptr(self.fars), ptr(self.noises),
+                 ptr(self.bg_color), ptr(self.g_image), ptr(self.counter), lr_host, len(lrs),
+                 ptr(self.lr_dev), stream())
         if self.shade_code:
             # the light direction (renderer.py:462-464), same (seed, step) key
             call("dfhip_shading_light", ptr(self.rays_o), int(seed) & 0xFFFFFFFFFFFFFFFF,
@@ -236,51 +269,65 @@ class NativeAlbedoStep:
 
     def body(self):
         """Forward and backward down to the feature / network gradients (the
-        graph-captured part).  Returns the loss tensor."""
+        graph-captured part).  Returns the loss tensor.  Each launch is a
+        timed region with its algorithmic bytes (fixed + per live row)."""
         m = self.trainer.model
         N, cap = self.N, self.cap
         sc = self.trainer.scaler
         scale = sc._scale if sc.is_enabled() else self._ones
-        # march (raymarching.py:161-235, device count)
-        _raymarching.march_rays_train_count_staged(
-            self.rays_o, self.rays_d, m.density_bitfield, m.bound, self.dt_gamma, self.max_steps,
-            N, m.cascade, m.grid_size, self.nears, self.fars, self.rays, self.counter,
-            self.noises, self.block_sums, self.stage)
-        _raymarching.march_rays_train_emit_staged(
-            self.rays_d, self.max_steps, N, cap, self.xyzs, self.dirs, self.deltas, self.rays,
-            self.block_sums, 0, self.stage)
+        T, md, mf = _dfhip.timed, self.m_dev, self.m_field
+        hb = 2 if self.elem in (torch.float16, torch.bfloat16) else 4  # colour element bytes
+        # march (raymarching.py:161-235, device count): rays + near/far +
+        # noise + bitfield in, (ray, offset, count) + one 20-B stage row per
+        # sample out; the emit copies the stage into xyz / dir / delta rows
+        with T("march_rays_train_count", 48 * N + (m.density_bitfield.numel()), md, 20):
+            _raymarching.march_rays_train_count_staged(
+                self.rays_o, self.rays_d, m.density_bitfield, m.bound, self.dt_gamma,
+                self.max_steps, N, m.cascade, m.grid_size, self.nears, self.fars, self.rays,
+                self.counter, self.noises, self.block_sums, self.stage)
+        with T("march_rays_train_emit", 24 * N, md, 52):
+            _raymarching.march_rays_train_emit_staged(
+                self.rays_d, self.max_steps, N, cap, self.xyzs, self.dirs, self.deltas,
+                self.rays, self.block_sums, 0, self.stage)
         # field (grid.py:38-39 autocast table, network_grid.py:76-87); with a
         # shading, the six finite-difference stencil points of every sample are
         # field rows too (network_grid.py:90-114)
         S, Hb, gridtype, align, _ = self.meta
-        _fieldmlp.grid_quads(self.encoder.embeddings.detach(), self.encoder.offsets, S, Hb,
-                             gridtype, align, self.table, self.quads)
+        rc = self.rows * self.C
+        with T("grid_quads", rc * (4 + hb) + 16 * self.rows):
+            _fieldmlp.grid_quads(self.encoder.embeddings.detach(), self.encoder.offsets, S, Hb,
+                                 gridtype, align, self.table, self.quads)
         if self.shade_code:
-            call("dfhip_shading_stencil", ptr(self.xyzs), ptr(self.m_dev), cap, FD_EPS,
-                 float(m.bound), ptr(self.xyz_field), ptr(self.m7), stream())
-        _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table, self.encoder.offsets,
-                                     S, Hb, gridtype, align, self.mlp, self.enc,
-                                     self.sigma_field, self.albedo, self.m_field,
-                                     quads=self.quads)
+            with T("shading_stencil", 0, md, 12 + 84):
+                call("dfhip_shading_stencil", ptr(self.xyzs), ptr(self.m_dev), cap, FD_EPS,
+                     float(m.bound), ptr(self.xyz_field), ptr(self.m7), stream())
+        with T("grid_field_forward", rc * hb, mf, 12 + self.L * self.C * hb + 4 + 3 * hb):
+            _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table,
+                                         self.encoder.offsets, S, Hb, gridtype, align, self.mlp,
+                                         self.enc, self.sigma_field, self.albedo, self.m_field,
+                                         quads=self.quads)
         rgb = self.albedo
         if self.shade_code:
             # normals, lambertian, colour, orientation loss (network_grid.py:116-144,
             # renderer.py:485-489)
-            call(self._shade_fwd, ptr(self.sigma_field), ptr(self.albedo),
-                 ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
-                 ptr(self.m_dev), cap, ptr(self.sigma), ptr(self.color), ptr(self.normal),
-                 ptr(self.orient_partial), self.lam_orient, ptr(self.orient), None, stream())
+            with T("shading_forward", 0, md, 28 + 3 * hb + 12 + 4 + 3 * hb + 12):
+                call(self._shade_fwd, ptr(self.sigma_field), ptr(self.albedo),
+                     ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
+                     ptr(self.m_dev), cap, ptr(self.sigma), ptr(self.color), ptr(self.normal),
+                     ptr(self.orient_partial), self.lam_orient, ptr(self.orient), None, stream())
             rgb = self.color
         # compositing (raymarching.py:238-269)
-        _raymarching.composite_rays_train_forward_mixed(
-            self.sigma, rgb, self.deltas, self.rays, cap, N, 1e-4, self.ws, self.depth,
-            self.image)
+        with T("composite_rays_train_forward", 32 * N, md, 4 + 3 * hb + 8):
+            _raymarching.composite_rays_train_forward_mixed(
+                self.sigma, rgb, self.deltas, self.rays, cap, N, 1e-4, self.ws, self.depth,
+                self.image)
         # ray head (renderer.py:536-551) and the entropy regulariser (utils.py:386-391)
         bw = self._bg_weights()
-        call("dfhip_ray_head_forward", N, ptr(self.ws), ptr(self.depth), ptr(self.image),
-             ptr(self.rays_d), ptr(self.nears), ptr(self.fars), *[ptr(w) for w in bw],
-             ptr(self.bg_color), ptr(self.out_image), ptr(self.out_depth), ptr(self.mask),
-             stream())
+        with T("ray_head_forward", 60 * N):
+            call("dfhip_ray_head_forward", N, ptr(self.ws), ptr(self.depth), ptr(self.image),
+                 ptr(self.rays_d), ptr(self.nears), ptr(self.fars), *[ptr(w) for w in bw],
+                 ptr(self.bg_color), ptr(self.out_image), ptr(self.out_depth), ptr(self.mask),
+                 stream())
         if self.two_pass:
             if self.lam > 0:
                 call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss),
@@ -293,31 +340,39 @@ class NativeAlbedoStep:
         head_args = (N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d), *[ptr(w) for w in bw],
                      ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws), None,
                      ptr(self.head_partial), *[ptr(g) for g in gbw])
-        if self.lam > 0:
-            # head backward + the entropy term's gradient (upstream: the scale);
-            # the entropy loss itself (utils.py:386-391) comes out of the same
-            # launches (dfhip_entropy_forward's value)
-            call("dfhip_ray_head_backward_entropy_loss", *head_args, ptr(scale), self.lam,
-                 ptr(self.loss), stream())
-        else:
-            call("dfhip_ray_head_backward", *head_args, stream())
+        with T("ray_head_backward", 60 * N):
+            if self.lam > 0:
+                # head backward + the entropy term's gradient (upstream: the
+                # scale); the entropy loss itself (utils.py:386-391) comes out
+                # of the same launches (dfhip_entropy_forward's value)
+                call("dfhip_ray_head_backward_entropy_loss", *head_args, ptr(scale), self.lam,
+                     ptr(self.loss), stream())
+            else:
+                call("dfhip_ray_head_backward", *head_args, stream())
         self._add_orient_loss()
-        _raymarching.composite_rays_train_backward_mixed(
-            self.grad_ws, self.grad_image, self.sigma, rgb, self.deltas, self.rays,
-            self.ws, self.image, cap, N, 1e-4, self.grad_sigma,
-            self.grad_color if self.shade_code else self.grad_albedo, False)
+        with T("composite_rays_train_backward", 44 * N, md, 4 + 3 * hb + 8 + 4 + 3 * hb):
+            _raymarching.composite_rays_train_backward_mixed(
+                self.grad_ws, self.grad_image, self.sigma, rgb, self.deltas, self.rays,
+                self.ws, self.image, cap, N, 1e-4, self.grad_sigma,
+                self.grad_color if self.shade_code else self.grad_albedo, False)
         if self.shade_code:
             # density / colour / orientation gradients -> the field rows' gradients
-            call(self._shade_bwd, ptr(self.sigma_field), ptr(self.albedo),
-                 ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
-                 ptr(self.m_dev), cap, ptr(self.grad_sigma), ptr(self.grad_color), ptr(scale),
-                 self.lam_orient, ptr(self.grad_sigma_field), ptr(self.grad_albedo), stream())
+            with T("shading_backward", 0, md, 28 + 3 * hb + 12 + 4 + 3 * hb + 28 + 21 * hb):
+                call(self._shade_bwd, ptr(self.sigma_field), ptr(self.albedo),
+                     ptr(self.dirs), ptr(self.light), self.ratio, FD_EPS, self.shade_code,
+                     ptr(self.m_dev), cap, ptr(self.grad_sigma), ptr(self.grad_color),
+                     ptr(scale), self.lam_orient, ptr(self.grad_sigma_field),
+                     ptr(self.grad_albedo), stream())
         from gridencoder.grid import _parts
-        _fieldmlp.grid_field_backward(
-            self.enc, self.xyz_field, m.bound, self.mlp, self.grad_sigma_field, self.grad_albedo,
-            self.d_enc, self.mlp_partial, [p.grad for p in self.mlp], self.encoder.offsets,
-            self.rows, S, Hb, gridtype, align, None, None, _parts(self.rows, self.C),
-            self.m_field)
+        # features + density / albedo gradients + positions in, feature
+        # gradients out (the weight gradients are per-workgroup partials)
+        per_bwd = 2 * self.L * self.C * hb + 4 + 3 * hb + 12
+        with T("field_mlp_backward", 4 * _fieldmlp.params_count(), mf, per_bwd):
+            _fieldmlp.grid_field_backward(
+                self.enc, self.xyz_field, m.bound, self.mlp, self.grad_sigma_field,
+                self.grad_albedo, self.d_enc, self.mlp_partial, [p.grad for p in self.mlp],
+                self.encoder.offsets, self.rows, S, Hb, gridtype, align, None, None,
+                _parts(self.rows, self.C), self.m_field)
         return self.loss
 
     def _backward_two_pass(self, bw, scale):

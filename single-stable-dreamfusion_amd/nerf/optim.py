@@ -106,6 +106,56 @@ class NativeAdamAmp:
                                f"{_dfhip.load().dfhip_last_error().decode()}")
         self.optimizer._opt_called = True  # what LRScheduler checks for "stepped"
 
+    def group_lrs(self):
+        """Current learning rate of every param group (host floats)."""
+        return [float(g["lr"]) for g in self.optimizer.param_groups]
+
+    def device_lr_launch(self, lr_dev):
+        """The step as a closure over device-resident learning rates (tensor k
+        reads lr_dev[its group]): captured once in the native train step's
+        HIP graph (nerf/graph.py), while the prologue launch writes lr_dev
+        every step from group_lrs().  Built against the current gradient
+        buffers and optimizer state, like step()'s fast path."""
+        sc = self.scaler
+        if sc.is_enabled():
+            if sc._scale is None:
+                raise RuntimeError("device_lr_launch: the GradScaler has no scale yet")
+            scale, tracker = sc._scale, sc._growth_tracker
+            growth, backoff, interval = sc._growth_factor, sc._backoff_factor, sc._growth_interval
+        else:
+            if self._unit is None:
+                dev = next(p.device for g in self.optimizer.param_groups for p in g["params"])
+                self._unit = (torch.ones(1, dtype=torch.float32, device=dev),
+                              torch.zeros(1, dtype=torch.int32, device=dev))
+            scale, tracker = self._unit
+            growth, backoff, interval = 1.0, 1.0, 1 << 30
+        if self.found_inf is None:
+            self.found_inf = torch.zeros(1, dtype=torch.float32, device=scale.device)
+        key = (id(self.optimizer.state), len(self.optimizer.state),
+               *(p.grad.data_ptr() if p.grad is not None else 0
+                 for g in self.optimizer.param_groups for p in g["params"]))
+        self._rebuild(key)
+        if self._arrays is None:
+            raise RuntimeError("device_lr_launch: no parameter has a gradient")
+        if len(self.optimizer.param_groups) > 8:
+            raise RuntimeError("device_lr_launch: at most 8 param groups")
+        n, P, G, M, V, S, N, B1, B2, E, WD, groups = self._arrays
+        slots = (ctypes.c_int32 * n)(*groups)
+        fn = _dfhip.load().dfhip_adam_amp_step_lr_dev
+        found_inf, opt = self.found_inf, self.optimizer
+        keep = (slots, self._arrays, lr_dev, scale, tracker, found_inf)
+
+        def launch():
+            rc = fn(n, P, G, M, V, S, N, slots, lr_dev.data_ptr(), B1, B2, E, WD,
+                    scale.data_ptr(), tracker.data_ptr(), found_inf.data_ptr(), float(growth),
+                    float(backoff), int(interval), _dfhip.stream())
+            if rc != 0:
+                raise RuntimeError(f"dfhip_adam_amp_step_lr_dev failed ({rc}): "
+                                   f"{_dfhip.load().dfhip_last_error().decode()}")
+            opt._opt_called = True
+        launch.keep = keep  # the host arrays the launch reads stay alive with it
+        return launch
+
     def _rebuild(self, key):
         ts = []
         for gi, g in enumerate(self.optimizer.param_groups):

@@ -273,6 +273,9 @@ class Trainer(object):
         self.native_losses = True
         self._native_opt = None
         self._capture_stream = None
+        # bench.py kernel timing: called with the GraphedTrainStep in place of
+        # its replay (runs the eager twin of the captured launches)
+        self.step_hook = None
         self.device = device if device is not None else torch.device(
             f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu")
 
@@ -443,21 +446,29 @@ class Trainer(object):
         elif scaled is not None:
             scaled.backward()
 
-    def optimizer_step(self):
-        """Gradient exchange, GradScaler + optimizer step, LR schedule."""
-        if self.world_size > 1:
-            flat_allreduce_(self.model.parameters(), self.world_size)
+    def native_adam(self):
+        """The native GradScaler + Adam (nerf/optim.py) when it reproduces
+        this trainer's optimizer step, else False."""
         if self._native_opt is None:
             from . import optim as _optim
             self._native_opt = (_optim.NativeAdamAmp(self.optimizer, self.scaler)
                                 if self.native_optimizer and _optim.eligible(
                                     self.optimizer, self.scaler, unit_scale=self.bf16)
                                 else False)
-        if self._native_opt:
-            self._native_opt.step()
-        else:
-            self.scaler.step(self.optimizer)
-            self.scaler.update()
+        return self._native_opt
+
+    def optimizer_step(self, stepped=False):
+        """Gradient exchange, GradScaler + optimizer step, LR schedule.
+        stepped: the optimizer already ran inside the replayed step graph
+        (single GPU native step), only the schedule advances."""
+        if not stepped:
+            if self.world_size > 1:
+                flat_allreduce_(self.model.parameters(), self.world_size)
+            if self.native_adam():
+                self._native_opt.step()
+            else:
+                self.scaler.step(self.optimizer)
+                self.scaler.update()
         if self.scheduler_update_every_step:
             self.lr_scheduler.step()
 
@@ -521,9 +532,12 @@ class Trainer(object):
         else:
             model.local_step += 1
         g.load(data, text_z)
-        g.replay()
+        if self.step_hook is not None:
+            self.step_hook(g)  # bench.py kernel timing: the eager twin of the replay
+        else:
+            g.replay()
         model.step_counter[row].copy_(g.counter)
-        self.optimizer_step()
+        self.optimizer_step(stepped=g.optimizer_in_graph)
         return g.loss
 
     def train_one_epoch(self, loader):
@@ -636,3 +650,6 @@ class Trainer(object):
                     self.log(f"[WARN] failed to load {key}.")
         if self.ema is not None and "ema" in ckpt:
             self.ema.load_state_dict(ckpt["ema"])
+        # captured step graphs hold the old optimizer-state pointers
+        self._graphs = {}
+        self._native_opt = None

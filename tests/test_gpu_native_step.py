@@ -168,3 +168,45 @@ def test_checkpoint_round_trip_resumes(gpu, tmp_path):
     losses = [float(fresh.train_iteration(data.collate([i % 4]))) for i in range(5)]
     assert all(np.isfinite(losses))
     assert fresh.global_step == 25
+
+
+def test_optimizer_in_graph_matches_host_lr_adam(gpu):
+    """Single GPU: the native step's graph ends with GradScaler + Adam reading
+    device learning rates the prologue writes (dfhip_adam_amp_step_lr_dev).
+    Over 20 steps of LambdaLR-decayed rates (main.py:131), crossing a density
+    refresh, the parameters, Adam moments, step counts and the loss scale equal
+    a twin trainer whose steps run the same launches eagerly and the optimizer
+    as the host-lr NativeAdamAmp.step() (nerf/optim.py), bit for bit."""
+    # one trainer after the other: make_trainer reseeds the global RNGs the
+    # camera sampler and the density refresh draw from, so both see the same
+    # poses and jitter
+    def run(hook):
+        tr, dt = _trainer(64, 5, graph=True)
+        tr.opt.iters = 50  # decay fast enough that every step's lr differs in f32
+        tr.step_hook = hook
+        for i in range(20):
+            tr.train_iteration(dt.collate([i % 4]))
+        torch.cuda.synchronize()
+        return tr
+
+    def host_optimizer(g):
+        g.optimizer_in_graph = False  # optimizer_step() then runs the host-lr Adam
+        g.native.body()
+        g.native.embedding_backward()
+        for p, gr in g.grads:
+            p.grad = gr
+    a = run(None)
+    b = run(host_optimizer)
+    torch.cuda.synchronize()
+    ga = next(iter(a._graphs.values()))
+    assert ga.native is not None and ga.optimizer_in_graph
+    lrs = [g["lr"] for g in a.optimizer.param_groups]
+    assert lrs == [g["lr"] for g in b.optimizer.param_groups]
+    assert lrs[0] < a.optimizer.param_groups[0]["initial_lr"]  # the schedule moved
+    for pa, pb in zip(a.model.parameters(), b.model.parameters()):
+        assert torch.equal(pa, pb)
+    sa, sb = a.optimizer.state_dict()["state"], b.optimizer.state_dict()["state"]
+    for i in sa:
+        for name in ("step", "exp_avg", "exp_avg_sq"):
+            assert torch.equal(sa[i][name], sb[i][name]), (i, name)
+    assert float(a.scaler.get_scale()) == float(b.scaler.get_scale())

@@ -186,17 +186,21 @@ def test_shaded_loss_is_fresh_each_step_without_entropy(gpu, two_pass):
     this step (utils.py:385-402 builds it fresh), not a sum over steps; repeated
     body() calls on the same draws give the same loss."""
     trainer, data = _trainer(64, 5)
+    for _ in range(3):  # occupancy refresh: the march emits samples
+        trainer.train_iteration(data.collate([0]))
     trainer.opt.lambda_entropy = 0.0
     trainer.fused_backward = not two_pass
     from nerf.native_step import NativeAlbedoStep
     shading = "lambertian" if not two_pass else "albedo"
     nat = NativeAlbedoStep(trainer, 64, 64, shading, 0.1)
     batch = data.collate([0])
-    nat.prologue(batch["pose"], batch["intrinsics"], 3, 77)
     losses = []
     for _ in range(3):
+        # the prologue resets the march counter: every body() sees the same draws
+        nat.prologue(batch["pose"], batch["intrinsics"], 3, 77)
         losses.append(float(nat.body()))
     torch.cuda.synchronize()
+    assert int(nat.counter[0]) > 1000
     assert losses[0] == losses[1] == losses[2], losses
     if shading != "albedo":
         want = trainer.opt.lambda_orient * float(nat.orient)

@@ -70,7 +70,7 @@ def _run(structure, emb_scale, seed=3):
     c = lambda t: t.detach().cpu().numpy()  # noqa: E731
     L, C = nat.L, nat.C
     out = {
-        "M": M, "scale": float(trainer.scaler._scale), "lam": nat.lam,
+        "M": M, "emb_scale": emb_scale, "scale": float(trainer.scaler._scale), "lam": nat.lam,
         "rays_o": c(nat.rays_o), "rays_d": c(nat.rays_d), "nears": c(nat.nears),
         "fars": c(nat.fars), "noises": c(nat.noises), "bitfield": c(m.density_bitfield),
         "xyz": c(nat.xyzs[:M]), "deltas": c(nat.deltas[:M]), "rays": c(nat.rays),
@@ -94,11 +94,18 @@ def _run(structure, emb_scale, seed=3):
     return out
 
 
+_FWD = {}
+
+
 def _forward_oracle(r):
-    x16 = of.encode(r["xyz"], 1.0, r["emb"], r["offsets"], r["S"], r["H"])
-    fo = of.field_forward(r["xyz"], r["mlp"], x16)
-    fb = of.forward_bounds(fo, r["mlp"], acc_ulps=MFMA_ULPS)
-    return fo, fb
+    """The oracle forward and its windows (identical for both structures: the
+    forward is shared, so it is computed once per embedding scale)."""
+    key = r["emb_scale"]
+    if key not in _FWD:
+        x16 = of.encode(r["xyz"], 1.0, r["emb"], r["offsets"], r["S"], r["H"])
+        fo = of.field_forward(r["xyz"], r["mlp"], x16)
+        _FWD[key] = (fo, of.forward_bounds(fo, r["mlp"], acc_ulps=MFMA_ULPS))
+    return _FWD[key]
 
 
 def _sds_part_window(r):
@@ -155,7 +162,10 @@ def test_step_structure_matches_its_oracle(gpu, structure, emb_scale):
     for gws, gimg, gs, ga in passes:
         ogs, oga = of.composite_backward(gws, gimg, r["sigma"], r["albedo"], r["deltas"],
                                          r["rays"], r["ws"], r["image"])
-        np.testing.assert_allclose(gs, ogs, rtol=1e-4, atol=1e-6 * np.abs(ogs).max())
+        # grad_sigma_i = dt_i (sum_c g_c (T_i+1 rgb_ic - (C_c - C_ic)) + ...): the
+        # (C - C_i) difference cancels, so near-zero entries carry an absolute
+        # error of a few f32 ulps of the ray's colour sums (2e-6 of the largest)
+        np.testing.assert_allclose(gs, ogs, rtol=1e-4, atol=2e-6 * np.abs(ogs).max())
         dga = np.abs(ga.astype(np.float64) - oga.astype(np.float64))
         assert np.all(dga <= of.ulp16(oga)), "colour gradient beyond one f16 ulp"
         assert (dga > 0).mean() < 1e-2
