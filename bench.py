@@ -148,13 +148,27 @@ def cpu_baseline(res, steps, c1_steps=10, c1_warmup=3):
     return out
 
 
-def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1):
+def sphere_occupancy_(model, radius=0.5):
+    """SURVEY §8d preset R1: the analytic sphere |x| < radius written straight
+    into the occupancy state (density grid 1 inside, 0 outside; bitfield by
+    packbits at 0.5), for a sample count that does not depend on the field."""
+    import raymarching
+    xyzs, indices = model._grid_points()
+    inside = (xyzs.norm(dim=-1) < radius).float()
+    with torch.no_grad():
+        model.density_grid[0, indices.long()] = inside
+        raymarching.packbits(model.density_grid, 0.5, model.density_bitfield)
+
+
+def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1,
+                    occupancy="grid"):
     """C4 (BASELINE configs[3]): res x res inference render of run_cuda's eval
     branch (albedo, fp16 autocast, max_steps 512, T_thresh 1e-4) from the
-    reference's test-view camera, on a grid whose occupancy comes from
+    reference's test-view camera.  occupancy "grid": the occupancy comes from
     update_extra_state of a seeded network with U(-0.5, 0.5) embeddings
-    (SURVEY §8d preset R0; no trained checkpoint exists offline).  Times the
-    fused persistent renderer (the product path) and, for comparison, the
+    (SURVEY §8d preset R0; no trained checkpoint exists offline); "sphere":
+    the analytic radius-0.5 sphere (preset R1) with the same field.  Times
+    the fused persistent renderer (the product path) and, for comparison, the
     reference-structured host loop (march_rays -> field -> composite_rays with
     one sync per iteration, renderer.py:496-532) on the same kernels."""
     import main
@@ -169,6 +183,8 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1)
     with torch.autocast("cuda", dtype=torch.float16):
         for _ in range(3):
             model.update_extra_state()
+    if occupancy == "sphere":
+        sphere_occupancy_(model)
     model.eval()
     data = NeRFDataset(opt, device=device, type="test", H=res, W=res, size=8).collate([1])
     rays_o, rays_d = data["rays_o"], data["rays_d"]
@@ -198,9 +214,10 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1)
     kern = summarize_kernels(timer.records).get("render_rays_infer", {})
     work = model.last_infer_work.cpu().numpy().view(np.uint32)
     samples = int(work[1]) + (int(work[2]) << 32)
+    occ = ("occupancy from update_extra_state of a seeded U(-0.5,0.5) grid network (R0)"
+           if occupancy == "grid" else "analytic radius-0.5 sphere occupancy (R1), same field")
     out = {"workload": f"C4: {res}x{res} run_cuda eval render (albedo, fp16, max_steps 512, "
-                       "T_thresh 1e-4), test-view camera, occupancy from update_extra_state "
-                       "of a seeded U(-0.5,0.5) grid network",
+                       f"T_thresh 1e-4), test-view camera, {occ}",
            "rays_per_frame": n, "ms_per_frame": round(fused_s * 1e3, 3),
            "rays_per_sec": round(n / fused_s, 1), "samples_per_frame": samples,
            "launch": "one persistent kernel (render_rays_infer)"}
@@ -672,6 +689,7 @@ def main():
         result["c5"] = bench_c5(args, rank, world)
     if rank == 0 and world == 1 and not args.no_infer:
         result["inference"] = bench_inference(device, args.infer_res)
+        result["inference_sphere"] = bench_inference(device, args.infer_res, occupancy="sphere")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.res, args.cpu_steps, args.c1_steps)
         result["gpu_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)

@@ -227,10 +227,10 @@ __device__ __forceinline__ uint32_t march(const MarchConsts &k, const Ray &r,
 // On success returns true with the sample position, dt and t - last_t
 // (deltas[0], deltas[1] of raymarching.cu:778-779) and t, last_t advanced as
 // the reference's loop leaves them; else t >= far.
-__device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
-                                           const uint8_t *__restrict__ grid, float &t,
-                                           float &last_t, float far, float (&xyz)[3],
-                                           float &dt_out, float &dl_out) {
+template <typename Occ>
+__device__ __forceinline__ bool march_next_f(const MarchConsts &k, const Ray &r, Occ occupied,
+                                             float &t, float &last_t, float far,
+                                             float (&xyz)[3], float &dt_out, float &dl_out) {
     while (t < far) {
         const float x = clampf(fmaf(t, r.dx, r.ox), -k.bound, k.bound);
         const float y = clampf(fmaf(t, r.dy, r.oy), -k.bound, k.bound);
@@ -245,7 +245,7 @@ __device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
         const int nz = cell_of(k, z, rbound);
         const uint32_t idx =
             (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
-        if ((grid[idx >> 3] >> (idx & 7)) & 1) {
+        if (occupied(idx)) {
             xyz[0] = x;
             xyz[1] = y;
             xyz[2] = z;
@@ -264,6 +264,26 @@ __device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
         } while (t < tt);
     }
     return false;
+}
+
+__device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
+                                           const uint8_t *__restrict__ grid, float &t,
+                                           float &last_t, float far, float (&xyz)[3],
+                                           float &dt_out, float &dl_out) {
+    return march_next_f(
+        k, r, [&](uint32_t idx) { return ((grid[idx >> 3] >> (idx & 7)) & 1) != 0; }, t, last_t,
+        far, xyz, dt_out, dl_out);
+}
+
+// Coarse occupancy of a Morton-ordered bitfield: morton3 interleaves x, y, z
+// from the low bits, so the 64 cells 64 b .. 64 b + 63 (bitfield bytes
+// 8 b .. 8 b + 7) are one 4x4x4 block and "those bytes are not all zero" is a
+// 32^3 (at H = 128) block map, one bit per block.  march_next with this map in
+// LDS reads the bitfield only inside occupied blocks; the visited t-sequence
+// is unchanged (an empty block's cells are skipped by the same per-cell
+// arithmetic, without their loads).
+__device__ __forceinline__ bool coarse_occupied(const uint32_t *coarse, uint32_t block) {
+    return ((coarse[block >> 5] >> (block & 31)) & 1u) != 0;
 }
 
 // ---------------------------------------------------------------- wave march

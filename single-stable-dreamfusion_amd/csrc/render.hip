@@ -48,6 +48,7 @@ namespace dfhip {
 namespace rd {
 
 constexpr int kWaves = 4;
+constexpr uint32_t kCoarseWords = 1024;  // 32^3 block map (H = 128, one cascade) in LDS
 constexpr int kK = 4;              // samples marched ahead per ray per round
 constexpr int kSlots = 64 * kK;    // per-wave staged samples
 
@@ -87,14 +88,24 @@ __global__ __launch_bounds__(256) void k_render_infer(
     const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *__restrict__ weights_sum, float *__restrict__ depth,
-    float *__restrict__ image, uint32_t *__restrict__ work) {
+    float *__restrict__ image, uint32_t *__restrict__ work,
+    const uint32_t *__restrict__ coarse, uint32_t coarse_words, uint64_t *prof) {
     __shared__ fm::Weights W;
     __shared__ fm::LevelK LK[fm::kLevels];
     __shared__ Stage stages[kWaves];
+    __shared__ uint32_t s_coarse[kCoarseWords];  // coarse_words used (0: no block map)
     const bool align = align_corners != 0;
     fm::load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
     fm::stage_levels(LK, offsets, lv, gridtype, align);
+    for (uint32_t i = threadIdx.x; i < coarse_words; i += blockDim.x) s_coarse[i] = coarse[i];
     __syncthreads();
+    const bool use_coarse = coarse_words != 0;
+    // occupancy of cell idx: the LDS block map first, the bitfield byte only
+    // inside occupied blocks
+    auto occupied = [&](uint32_t idx) {
+        if (use_coarse && !rm::coarse_occupied(s_coarse, idx >> 6)) return false;
+        return ((grid[idx >> 3] >> (idx & 7)) & 1) != 0;
+    };
     Stage &S = stages[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const float inv_extent = 1.0f / (2.0f * k.bound);
@@ -106,6 +117,10 @@ __global__ __launch_bounds__(256) void k_render_infer(
     float ws = 0.0f, dp = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
     uint32_t taken = 0;
     uint32_t samples = 0;  // per-lane count of evaluated samples (stats)
+    // debug phase profile (dfhip_debug_render_profile): cycles of refill,
+    // march, field and compositing, rounds and field tiles, per wave
+    uint64_t pc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t c0 = prof ? clock64() : 0;
 
     while (true) {
         // ---- refill lanes whose ray finished from the global queue
@@ -139,6 +154,12 @@ __global__ __launch_bounds__(256) void k_render_infer(
             }
         }
         if (__ballot(ray >= 0) == 0) break;
+        if (prof) {
+            const uint64_t c1 = clock64();
+            pc[0] += c1 - c0;
+            c0 = c1;
+            pc[4] += 1;
+        }
 
         // ---- march: up to kK samples per ray.  After each sample the march
         // restarts from the composited t (rays_t, raymarching.cu:739-748):
@@ -152,7 +173,7 @@ __global__ __launch_bounds__(256) void k_render_infer(
             for (int q = 0; q < kK; ++q) {
                 if (n == (uint32_t)q && !at_far && (uint32_t)q < budget) {
                     float dl;
-                    if (rm::march_next(k, r, grid, t, last_t, far, px[q], pdt[q], dl)) {
+                    if (rm::march_next_f(k, r, occupied, t, last_t, far, px[q], pdt[q], dl)) {
                         tc += dl;
                         t = tc;
                         last_t = tc;
@@ -178,9 +199,15 @@ __global__ __launch_bounds__(256) void k_render_infer(
                 S.tc[slot] = ptc[q];
             }
         fm::wave_lds_sync();
+        if (prof) {
+            const uint64_t c1 = clock64();
+            pc[1] += c1 - c0;
+            c0 = c1;
+        }
 
         // ---- field over the compacted samples, 16 per MFMA tile
         const uint32_t tiles = ceil_div(total, 16u);
+        if (prof) pc[5] += tiles;
         for (uint32_t tile = 0; tile < tiles; ++tile) {
             const uint32_t s = tile * 16 + c;
             const bool valid = s < total;
@@ -209,6 +236,11 @@ __global__ __launch_bounds__(256) void k_render_infer(
             }
         }
         fm::wave_lds_sync();
+        if (prof) {
+            const uint64_t c1 = clock64();
+            pc[2] += c1 - c0;
+            c0 = c1;
+        }
 
         // ---- composite each ray's samples in order (k_composite_infer,
         // raymarching.cu:848-873); retire on T < T_thresh, max_samples, or
@@ -245,7 +277,15 @@ __global__ __launch_bounds__(256) void k_render_infer(
             }
         }
         fm::wave_lds_sync();
+        if (prof) {
+            const uint64_t c1 = clock64();
+            pc[3] += c1 - c0;
+            c0 = c1;
+        }
     }
+    if (prof && lane == 0)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) atomicAdd((unsigned long long *)&prof[i], pc[i]);
     // stats: composited samples (64-bit, low / high words)
     uint32_t tot = samples;
 #pragma unroll
@@ -256,10 +296,35 @@ __global__ __launch_bounds__(256) void k_render_infer(
     }
 }
 
+// The 32^3 block map of a Morton bitfield (rm::coarse_occupied on idx >> 6):
+// 64 consecutive Morton cells (8 bytes) are one 4x4x4 block, so word w bit j
+// = (the 8 bytes at 8 (32 w + j) are not all zero); one lane per block, the
+// word assembled with a ballot.
+__global__ __launch_bounds__(256) void k_coarse_map(const uint8_t *__restrict__ bitfield,
+                                                    uint32_t words, uint32_t *__restrict__ out) {
+    const uint32_t blk = blockIdx.x * blockDim.x + threadIdx.x;  // one 8-byte block
+    const bool any = blk < 32 * words &&
+                     reinterpret_cast<const unsigned long long *>(bitfield)[blk] != 0ull;
+    const uint64_t m = __ballot(any);
+    const uint32_t lane = threadIdx.x & 63;
+    if (lane == 0 && blk / 32 < words) out[blk / 32] = (uint32_t)m;
+    if (lane == 32 && blk / 32 < words) out[blk / 32] = (uint32_t)(m >> 32);
+}
+
 }  // namespace rd
 }  // namespace dfhip
 
 using namespace dfhip;
+
+static uint64_t *g_render_prof = nullptr;  // set by dfhip_debug_render_profile (tools only)
+
+// Debug: per-wave phase cycles of k_render_infer summed into prof[0..5] =
+// {refill, march, field, composite cycles, rounds, field tiles} (u64, caller
+// zeroed); null turns it off.  Used by tools/infer_case.py only.
+extern "C" int dfhip_debug_render_profile(uint64_t *prof) {
+    g_render_prof = prof;
+    return DFHIP_OK;
+}
 
 extern "C" int dfhip_render_rays_infer(
     uint32_t N, const float *rays_o, const float *rays_d, const float *nears, const float *fars,
@@ -268,7 +333,7 @@ extern "C" int dfhip_render_rays_infer(
     uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
-    dfhip_stream_t stream) {
+    uint32_t *coarse, dfhip_stream_t stream) {
     const char *name = "render_rays_infer";
     if (L != 16) {
         set_error("%s: the fused renderer supports the reference's 16-level x 2-channel 3-D "
@@ -290,6 +355,15 @@ extern "C" int dfhip_render_rays_infer(
     if (N == 0) return DFHIP_OK;
     const rm::MarchConsts k = rm::make_consts(bound, dt_gamma, max_steps, C, H);
     const ge::Levels lv = ge::make_levels(L, S, base_res);
+    // the block map of the bitfield, staged in LDS by every workgroup (only
+    // when it fits: C * H^3 / 2048 words <= kCoarseWords, 8-B aligned grid)
+    const uint64_t grid_bytes = (uint64_t)C * H * H * H / 8;
+    uint32_t cw = 0;
+    if (coarse && grid_bytes % 256 == 0 && grid_bytes / 256 <= rd::kCoarseWords &&
+        ((uintptr_t)grid & 7) == 0) {
+        cw = (uint32_t)(grid_bytes / 256);
+        rd::k_coarse_map<<<ceil_div(32u * cw, 256u), 256, 0, s>>>(grid, cw, coarse);
+    }
     // persistent waves: as many workgroups as are co-resident on the chip
     // (occupancy query, once); the queue balances the rays among them
     static uint32_t resident = 0;
@@ -307,6 +381,6 @@ extern "C" int dfhip_render_rays_infer(
     rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
         N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
         (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
-        weights_sum, depth, image, work);
+        weights_sum, depth, image, work, coarse, cw, g_render_prof);
     return check_launch(name);
 }

@@ -16,6 +16,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--profile", action="store_true",
+                    help="per-wave phase cycles of k_render_infer (dfhip_debug_render_profile)")
+    ap.add_argument("--sphere", action="store_true", help="analytic sphere occupancy (R1)")
     args = ap.parse_args()
     import main as m
     from nerf.network_grid import NeRFNetwork
@@ -29,6 +32,9 @@ def main():
     with torch.autocast("cuda", dtype=torch.float16):
         for _ in range(3):
             model.update_extra_state()
+    if args.sphere:
+        import bench
+        bench.sphere_occupancy_(model)
     model.eval()
     model.native_infer = True
     data = NeRFDataset(opt, device=dev, type="test", H=args.res, W=args.res, size=8).collate([1])
@@ -51,6 +57,22 @@ def main():
     img = out["image"].float()
     print(f"res={args.res} ms_per_frame={ms:.3f} image_mean={float(img.mean()):.6f} "
           f"ws_mean={float(out['weights_sum'].float().mean()):.6f}", flush=True)
+    if args.profile:
+        import ctypes
+        import _dfhip
+        lib = _dfhip.load()
+        lib.dfhip_debug_render_profile.argtypes = [ctypes.c_void_p]
+        prof = torch.zeros(6, dtype=torch.int64, device=dev)
+        lib.dfhip_debug_render_profile(prof.data_ptr())
+        frame()
+        torch.cuda.synchronize()
+        lib.dfhip_debug_render_profile(None)
+        p = prof.cpu().tolist()
+        tot = sum(p[:4])
+        print("phase cycles (summed over waves): " + ", ".join(
+            f"{n} {v / tot:.3f}" for n, v in zip(("refill", "march", "field", "composite"), p[:4]))
+            + f"; rounds {p[4]}, tiles {p[5]}, cycles/round {tot / max(1, p[4]):.0f}, "
+            f"field cycles/tile {p[2] / max(1, p[5]):.0f}", flush=True)
 
 
 if __name__ == "__main__":
