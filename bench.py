@@ -584,6 +584,16 @@ def main():
     kernels, timing = {}, None
     if not args.no_kernel_timing:
         kernels, timing = kernel_timing_pass(trainer, step, min(args.steps, 20))
+    # host work per step with no queue back-pressure: one step issued on an
+    # idle GPU (median of 16; the refresh step every 16 is the outlier)
+    issue = []
+    for _ in range(16):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        issue.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    host_cost = float(np.median(issue))
 
     rays_per_step = args.res * args.res
     steps_per_sec = args.steps * world / elapsed  # whole-job aggregate (every rank steps)
@@ -606,6 +616,7 @@ def main():
                    "mean_samples_per_step": round(samples, 1)},
         "steps_per_sec": round(steps_per_sec, 3),
         "host_issue_ms_per_step": round(host_issue / args.steps * 1e3, 3),
+        "host_cost_ms_per_step": round(host_cost * 1e3, 3),
     }
     g0 = next(iter(trainer._graphs.values()), None)
     if g0 is not None:

@@ -639,13 +639,7 @@ int dfhip_train_step_prologue_lr(const float *pose, float fx, float fy, float cx
  *      near plane's rays_t, as composite_rays leaves it), image [N,3] f32 —
  *      every ray written once (no zero-fill needed).
  * work: [4] u32 caller scratch, zeroed here; after the launch work[1] +
- *      2^32 work[2] = number of samples evaluated.
- * coarse: u32 caller scratch of C*H^3/2048 words (1024 at the reference's
- *      C = 1, H = 128) or NULL: the launch writes the bitfield's 32^3 block
- *      map there (bit b = any of the 64 Morton cells 64 b .. 64 b + 63, a
- *      4x4x4 block, occupied) and every workgroup stages it in LDS, so the
- *      march reads the bitfield only inside occupied blocks (same visited
- *      samples); ignored when the map would exceed 1024 words. */
+ *      2^32 work[2] = number of samples evaluated. */
 int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d,
                             const float *nears, const float *fars, const float *noises,
                             float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
@@ -654,7 +648,7 @@ int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d
                             uint32_t gridtype, int align_corners, const float *w1,
                             const float *b1, const float *w2, const float *b2, const float *w3,
                             const float *b3, float *weights_sum, float *depth, float *image,
-                            uint32_t *work, uint32_t *coarse, dfhip_stream_t stream);
+                            uint32_t *work, dfhip_stream_t stream);
 
 /* ---- non-albedo shading of the train step (csrc/shade.hip) ------------------
  * Replaces, for the `textureless` / `lambertian` steps, network_grid.py:90-144

@@ -171,14 +171,12 @@ def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lb
 
 def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                       bitfield, T_thresh, table, offsets, S, base_res, gridtype, align_corners,
-                      weights, weights_sum, depth, image, work, coarse=None):
+                      weights, weights_sum, depth, image, work):
     """Inference render of N rays in one launch (csrc/render.hip; reference
     nerf/renderer.py:496-532).  rays_o/rays_d [N, 3] f32, nears/fars [N] f32,
     noises [N] f32 or None, bitfield u8, table [rows, 2] f16, offsets int32.
     Writes weights_sum [N], depth [N], image [N, 3] f32; work: [4] int32
-    scratch whose words 1, 2 hold the evaluated sample count afterwards;
-    coarse: int32 scratch of coarse_map_words(C, H) for the LDS block map of
-    the bitfield (None: every march step reads the bitfield)."""
+    scratch whose words 1, 2 hold the evaluated sample count afterwards."""
     n = rays_o.shape[0]
     for t, what in ((rays_o, "rays_o"), (rays_d, "rays_d"), (nears, "nears"), (fars, "fars"),
                     (weights_sum, "weights_sum"), (depth, "depth"), (image, "image")):
@@ -204,18 +202,8 @@ def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_
     checked(work, "work", "int")
     if work.numel() < 4:
         raise RuntimeError("work must hold 4 int32")
-    if coarse is not None:
-        checked(coarse, "coarse", "int")
-        if coarse.numel() < coarse_map_words(C, H):
-            raise RuntimeError("coarse must hold coarse_map_words(C, H) int32")
     call("dfhip_render_rays_infer", n, ptr(rays_o), ptr(rays_d), ptr(nears), ptr(fars),
          ptr(noises), float(bound), float(dt_gamma), int(max_steps), int(C), int(H), ptr(bitfield),
          float(T_thresh), ptr(table), ptr(offsets), offsets.shape[0] - 1, float(S),
          int(base_res), int(gridtype), int(bool(align_corners)), *_weights(weights),
-         ptr(weights_sum), ptr(depth), ptr(image), ptr(work), ptr(coarse), stream())
-
-
-def coarse_map_words(C, H):
-    """u32 words of the renderer's bitfield block map (one bit per 4x4x4 cell
-    block): C * H^3 / 2048."""
-    return max(1, (int(C) * int(H) ** 3 + 2047) // 2048)
+         ptr(weights_sum), ptr(depth), ptr(image), ptr(work), stream())

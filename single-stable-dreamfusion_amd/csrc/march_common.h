@@ -227,43 +227,54 @@ __device__ __forceinline__ uint32_t march(const MarchConsts &k, const Ray &r,
 // On success returns true with the sample position, dt and t - last_t
 // (deltas[0], deltas[1] of raymarching.cu:778-779) and t, last_t advanced as
 // the reference's loop leaves them; else t >= far.
+// One iteration of that loop: returns 2 if t >= far (nothing done), 1 with
+// the sample (position, dt, t - last_t; t and last_t advanced) when the cell
+// at t is occupied, else 0 after the skip to the cell's far face.
+template <typename Occ>
+__device__ __forceinline__ int march_step(const MarchConsts &k, const Ray &r, Occ occupied,
+                                          float &t, float &last_t, float far, float (&xyz)[3],
+                                          float &dt_out, float &dl_out) {
+    if (!(t < far)) return 2;
+    const float x = clampf(fmaf(t, r.dx, r.ox), -k.bound, k.bound);
+    const float y = clampf(fmaf(t, r.dy, r.oy), -k.bound, k.bound);
+    const float z = clampf(fmaf(t, r.dz, r.oz), -k.bound, k.bound);
+    const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
+    const Mip mp = mip_of(k, x, y, z, dt);
+    const int level = mp.level;
+    const float mip_bound = mp.bound;
+    const float rbound = mp.rbound;
+    const int nx = cell_of(k, x, rbound);
+    const int ny = cell_of(k, y, rbound);
+    const int nz = cell_of(k, z, rbound);
+    const uint32_t idx = (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
+    if (occupied(idx)) {
+        xyz[0] = x;
+        xyz[1] = y;
+        xyz[2] = z;
+        t += dt;
+        dt_out = dt;
+        dl_out = t - last_t;
+        last_t = t;
+        return 1;
+    }
+    const float tx = face_dist(k, nx, r.dx, r.rdx, x, mip_bound);
+    const float ty = face_dist(k, ny, r.dy, r.rdy, y, mip_bound);
+    const float tz = face_dist(k, nz, r.dz, r.rdz, z, mip_bound);
+    const float tt = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    do {
+        t += clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
+    } while (t < tt);
+    return 0;
+}
+
 template <typename Occ>
 __device__ __forceinline__ bool march_next_f(const MarchConsts &k, const Ray &r, Occ occupied,
                                              float &t, float &last_t, float far,
                                              float (&xyz)[3], float &dt_out, float &dl_out) {
-    while (t < far) {
-        const float x = clampf(fmaf(t, r.dx, r.ox), -k.bound, k.bound);
-        const float y = clampf(fmaf(t, r.dy, r.oy), -k.bound, k.bound);
-        const float z = clampf(fmaf(t, r.dz, r.oz), -k.bound, k.bound);
-        const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
-        const Mip mp = mip_of(k, x, y, z, dt);
-        const int level = mp.level;
-        const float mip_bound = mp.bound;
-        const float rbound = mp.rbound;
-        const int nx = cell_of(k, x, rbound);
-        const int ny = cell_of(k, y, rbound);
-        const int nz = cell_of(k, z, rbound);
-        const uint32_t idx =
-            (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
-        if (occupied(idx)) {
-            xyz[0] = x;
-            xyz[1] = y;
-            xyz[2] = z;
-            t += dt;
-            dt_out = dt;
-            dl_out = t - last_t;
-            last_t = t;
-            return true;
-        }
-        const float tx = face_dist(k, nx, r.dx, r.rdx, x, mip_bound);
-        const float ty = face_dist(k, ny, r.dy, r.rdy, y, mip_bound);
-        const float tz = face_dist(k, nz, r.dz, r.rdz, z, mip_bound);
-        const float tt = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
-        do {
-            t += clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
-        } while (t < tt);
+    for (;;) {
+        const int st = march_step(k, r, occupied, t, last_t, far, xyz, dt_out, dl_out);
+        if (st != 0) return st == 1;
     }
-    return false;
 }
 
 __device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
@@ -273,17 +284,6 @@ __device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
     return march_next_f(
         k, r, [&](uint32_t idx) { return ((grid[idx >> 3] >> (idx & 7)) & 1) != 0; }, t, last_t,
         far, xyz, dt_out, dl_out);
-}
-
-// Coarse occupancy of a Morton-ordered bitfield: morton3 interleaves x, y, z
-// from the low bits, so the 64 cells 64 b .. 64 b + 63 (bitfield bytes
-// 8 b .. 8 b + 7) are one 4x4x4 block and "those bytes are not all zero" is a
-// 32^3 (at H = 128) block map, one bit per block.  march_next with this map in
-// LDS reads the bitfield only inside occupied blocks; the visited t-sequence
-// is unchanged (an empty block's cells are skipped by the same per-cell
-// arithmetic, without their loads).
-__device__ __forceinline__ bool coarse_occupied(const uint32_t *coarse, uint32_t block) {
-    return ((coarse[block >> 5] >> (block & 31)) & 1u) != 0;
 }
 
 // ---------------------------------------------------------------- wave march

@@ -10,16 +10,12 @@ against the reference (e.g. its nerf/network_grid.py) subclasses it unchanged.
 The ray-marching ops it calls are the gfx950 kernels behind `raymarching`.
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
 
 import raymarching
 from .utils import custom_meshgrid, safe_normalize
-
-# the fused inference renderer stages the bitfield's 64^3 block map in LDS
-_COARSE_MAP = os.environ.get("DFHIP_COARSE", "1") != "0"
 
 
 def sample_pdf(bins, weights, n_samples, det=False):
@@ -341,9 +337,6 @@ class NeRFRenderer(nn.Module):
         depth = torch.empty(N, dtype=torch.float32, device=dev)
         image = torch.empty(N, 3, dtype=torch.float32, device=dev)
         work = torch.empty(4, dtype=torch.int32, device=dev)
-        # the bitfield's block map, staged in LDS by the renderer (DFHIP_COARSE=0: off)
-        coarse = (torch.empty(_fieldmlp.coarse_map_words(self.cascade, self.grid_size),
-                              dtype=torch.int32, device=dev) if _COARSE_MAP else None)
         noises = torch.rand(N, device=dev) if perturb else None
         weights = []
         for lin in layers:
@@ -361,7 +354,7 @@ class NeRFRenderer(nn.Module):
                 dt_gamma, max_steps, self.cascade, self.grid_size, self.density_bitfield,
                 T_thresh, table, encoder.offsets, float(np.log2(encoder.per_level_scale)),
                 int(encoder.base_resolution), encoder.gridtype_id, bool(encoder.align_corners),
-                weights, weights_sum, depth, image, work, coarse)
+                weights, weights_sum, depth, image, work)
         self.last_infer_work = work  # work[1] (+ 2^32 work[2]) = samples evaluated
         return weights_sum, depth, image
 
