@@ -62,6 +62,7 @@ struct BinInfo {
 };
 
 static uint64_t *g_walk_trace = nullptr;  // set by dfhip_debug_walk_trace (tools only)
+static bool g_fast_bin = true;            // dfhip_debug_fast_bin(0): the generic k_bin (A/B, tests)
 
 static uint32_t slice_shift(uint32_t C) {
     uint32_t shift = 0;
@@ -280,6 +281,108 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
         }
         __syncthreads();
     }
+}
+
+// Binning, mask-form fast path: every level wraps rows by a mask (or never
+// wraps), has at most 64 slices and L <= kFastLevels (the reference's grid:
+// three dense levels + thirteen 2^16-row tiled levels).  The per-level
+// constants are host-evaluated kernel arguments (scalar loads) instead of
+// level_ctx / level_rows per sample and level, and the slices of the 2^lead
+// corners come from the 2^(lead-1) x-neighbour pairs: corner rows r and
+// r + 1 share a slice unless r is the slice's last row (then r + 1 wraps by
+// the mask or starts the next slice).  Same entries as k_bin.
+constexpr uint32_t kFastLevels = 16;
+
+struct FastLevels {
+    float scale[kFastLevels];
+    uint32_t m1[kFastLevels], m2[kFastLevels], wmask[kFastLevels];
+    uint32_t lead[kFastLevels], bin0[kFastLevels];
+};
+
+template <bool POW2>
+__global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inputs,
+                                                  FastLevels fl, BinInfo bi, int align_corners,
+                                                  SliceDyn dyn, float inv, uint32_t B,
+                                                  uint32_t *__restrict__ counts,
+                                                  uint16_t *__restrict__ entries) {
+    __shared__ uint32_t cnt[kMaxBins];
+    const float half = align_corners ? 0.0f : 0.5f;
+    const uint32_t M = ge::dyn_count(dyn, B);
+    const uint32_t ntiles = ceil_div(M, kTile);
+    const uint32_t nb = bi.nbins, shift = bi.shift, smask = (1u << bi.shift) - 1u;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
+        __syncthreads();
+        uint16_t *seg = entries + (size_t)tile * nb * kTile;
+        const uint32_t s_end = min(M, (tile + 1) * kTile);
+        for (uint32_t s = tile * kTile + threadIdx.x; s < s_end; s += blockDim.x) {
+            float x[3];
+            if (!load_pos<3, POW2>(inputs, dyn, inv, s, x)) continue;
+            const uint16_t id = (uint16_t)(s - tile * kTile);
+            for (uint32_t l = 0; l < bi.L; ++l) {
+                const float sc = fl.scale[l];
+                const uint32_t c0 = (uint32_t)floorf(fmaf(x[0], sc, half));
+                const uint32_t c1 = (uint32_t)floorf(fmaf(x[1], sc, half));
+                const uint32_t c2 = (uint32_t)floorf(fmaf(x[2], sc, half));
+                const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
+                const uint32_t i0 = c0 + c1 * m1 + c2 * m2;
+                uint64_t mask = 0;
+#pragma unroll
+                for (uint32_t p = 0; p < 4; ++p) {  // x-neighbour pairs {0,1} + {0, m1, m2, m1+m2}
+                    if (p >= (1u << (lead - 1u))) break;  // uniform
+                    const uint32_t o = ((p & 1u) ? m1 : 0u) + ((p & 2u) ? m2 : 0u);
+                    const uint32_t r = (i0 + o) & wm;
+                    mask |= 1ull << (r >> shift);
+                    if ((r & smask) == smask) mask |= 1ull << (((r + 1u) & wm) >> shift);
+                }
+                const uint32_t b0 = fl.bin0[l];
+                while (mask) {
+                    const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mask);
+                    mask &= mask - 1;
+                    const uint32_t slot = atomicAdd(&cnt[b], 1u);
+                    seg[(size_t)b * kTile + slot] = id;
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+            const uint32_t v = cnt[b];
+            counts[(size_t)tile * nb + b] = v;
+            if (v) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], v);
+        }
+        __syncthreads();
+    }
+}
+
+// Host: the FastLevels of a layout, or false when the fast path does not
+// apply (the host restatement of ge::level_ctx / level_rows, D = 3).
+static bool make_fast_levels(const int32_t *offsets_host, const Levels &lv, const BinInfo &bi,
+                             uint32_t gridtype, bool align, FastLevels &fl) {
+    if (bi.L > kFastLevels) return false;
+    for (uint32_t l = 0; l < bi.L; ++l) {
+        // u32 stride as the device (and gridencoder.cu:56-63) evaluate it
+        const uint32_t hsize = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
+        const uint32_t smul = align ? lv.res[l] : lv.res[l] + 1u;
+        uint32_t stride = 1, used = 0;
+        uint64_t span = 1;
+        for (uint32_t d = 0; d < 3; ++d)
+            if (stride <= hsize) {
+                stride *= smul;
+                ++used;
+            }
+        for (uint32_t d = 0; d < used; ++d) span *= smul;
+        const bool hashed = gridtype == 0 && stride > hsize;
+        const bool pow2 = (hsize & (hsize - 1)) == 0;
+        if (hashed || (!pow2 && span > hsize)) return false;  // not the mask form
+        if (bi.bin0[l + 1] - bi.bin0[l] > 64 || used == 0) return false;
+        fl.scale[l] = lv.scale[l];
+        fl.lead[l] = used;
+        fl.m1[l] = used > 1 ? smul : 0u;
+        fl.m2[l] = used > 2 ? smul * smul : 0u;
+        fl.wmask[l] = pow2 ? hsize - 1u : 0xFFFFFFFFu;
+        fl.bin0[l] = bi.bin0[l];
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------- 2. walk
@@ -661,6 +764,13 @@ using namespace dfhip;
 // Debug: per-workgroup walk timeline {first bin, end bin, 0, entries, t0,
 // t_planned, range start, t_end} (wall clock ticks) into `trace` (8 u64 per
 // walk workgroup); null turns it off.  Used by tools/walk_trace.py only.
+// Debug: choose the generic binning kernel (0) or the mask-form fast path
+// where it applies (1, default).  Used by tests / A-B tools only.
+extern "C" int dfhip_debug_fast_bin(int on) {
+    gb::g_fast_bin = on != 0;
+    return DFHIP_OK;
+}
+
 extern "C" int dfhip_debug_walk_trace(uint64_t *trace) {
     gb::g_walk_trace = trace;
     return DFHIP_OK;
@@ -724,7 +834,18 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
             const uint32_t gbin = bi.tcap < 4096u ? bi.tcap : 4096u;
             const bool pow2 = ge::dyn_pow2(dyn.bound);
             const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-            if (pow2)
+            gb::FastLevels fl;
+            if (gb::g_fast_bin && gb::make_fast_levels(offsets_host, lv, bi, gridtype,
+                                                       align_corners != 0, fl)) {
+                if (pow2)
+                    gb::k_bin_fast<true><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
+                                                                dyn, inv, B, counts,
+                                                                (uint16_t *)entries);
+                else
+                    gb::k_bin_fast<false><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
+                                                                 dyn, inv, B, counts,
+                                                                 (uint16_t *)entries);
+            } else if (pow2)
                 gb::k_bin<3, true><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype,
                                                          align_corners, dyn, inv, B, counts,
                                                          (uint16_t *)entries);

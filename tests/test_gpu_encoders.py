@@ -384,3 +384,53 @@ def test_grid_backward_binned_phases(gpu):
     assert torch.equal(out["split"], out["whole"])
     with pytest.raises(RuntimeError):
         _gridencoder.binned_launcher(*args, phase=4)
+
+
+@pytest.mark.parametrize("gt", [1, 0])
+def test_grid_backward_fast_bins_equal_generic(gpu, gt):
+    """The mask-form binning fast path (gridbin.hip k_bin_fast: host-evaluated
+    level constants, corner slices from x-neighbour pairs) files exactly the
+    generic k_bin's entries: same per-(tile, slice) counts, same id set in
+    every segment; tiled grid (fast path) and hashed grid (falls back)."""
+    import ctypes
+    import _dfhip
+    import _gridencoder
+    lib = _dfhip.load()
+    lib.dfhip_debug_fast_bin.argtypes = [ctypes.c_int]
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    # include points on slice and level edges: lattice-aligned and clamped ones
+    x = _samples(40000, 41)
+    x[:64] = np.float32(1.0)
+    x[64:128] = np.float32(0.0)
+    B = x.shape[0]
+    g = (np.random.default_rng(42).normal(size=(B, 32)) * 0.1).astype(np.float16)
+    glbc = T(g, gpu).view(B, 16, 2).transpose(0, 1).contiguous()
+    xt = T(x, gpu)
+    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, 16, 2)
+    got = {}
+    try:
+        for fast in (0, 1):
+            lib.dfhip_debug_fast_bin(fast)
+            ent = torch.zeros(ne, dtype=torch.int32, device=gpu)
+            cnt = torch.zeros(nc, dtype=torch.int32, device=gpu)
+            part = torch.empty(npf, device=gpu)
+            gemb = torch.empty(rows, 2, device=gpu)
+            _gridencoder.binned_launcher(glbc, xt, 0.0, T(offs, gpu), offs, gemb, B, None, 3, 2,
+                                         16, S, 16, gt, False, ent, cnt, part)()
+            torch.cuda.synchronize()
+            got[fast] = (ent.cpu().numpy().view(np.uint16), cnt.cpu().numpy(), gemb.cpu().numpy())
+    finally:
+        lib.dfhip_debug_fast_bin(1)
+    tiles = -(-B // 1024)
+    (e0, c0, g0), (e1, c1, g1) = got[0], got[1]
+    # counts region [tiles][bins]; bins = slices of 8,192 rows per level (C = 2)
+    nb = int(sum(-(-int(offs[l + 1] - offs[l]) // 8192) for l in range(16)))
+    assert np.array_equal(c0[:tiles * nb], c1[:tiles * nb])
+    assert c0[:tiles * nb].sum() > 16 * (B - 128)  # every in-range sample, every level
+    for t in range(tiles):
+        for b in range(nb):
+            n = int(c0[t * nb + b])
+            base = (t * nb + b) * 1024
+            assert np.array_equal(np.sort(e0[base:base + n]), np.sort(e1[base:base + n])), (t, b)
+    np.testing.assert_allclose(g1, g0, rtol=1e-6, atol=1e-9)
