@@ -501,6 +501,27 @@ int dfhip_grid_encode_backward_binned_phase(int phase, int grad_dtype, const voi
                                             int align_corners, uint32_t *entries,
                                             uint32_t *counts, float *partial, int accumulate,
                                             dfhip_stream_t stream);
+/* The same over finite-difference stencil groups (the textureless /
+ * lambertian train step, network_grid.py:90-114): with group = 7, field row
+ * 7 g + a of grad_lbc [L, 7 B, C] belongs to point a of sample g (inputs [B,
+ * 3] the samples' raw positions): a = 0 the sample, a = 1 + s the point
+ * clamp(x + (s odd ? -eps : eps) e_(s >> 1), -bound, bound) — the rows
+ * dfhip_shading_stencil lays out.  Binned and walked per group (one entry per
+ * (group, slice)), rows [0, *m_dev) of groups; the result equals the row-wise
+ * call on the 7 B rows up to the f64 summation order.  Needs C = 2, f16 / bf16
+ * gradients, bound > 0 and a mask-form level layout (the reference's grid);
+ * group = 1 is dfhip_grid_encode_backward_binned_phase.  Scratch as
+ * dfhip_grid_backward_binned_scratch for capacity B (groups). */
+int dfhip_grid_encode_backward_binned_stencil(int phase, int grad_dtype, const void *grad_lbc,
+                                              const float *inputs, float bound,
+                                              const int32_t *offsets, const int32_t *offsets_host,
+                                              float *grad_embeddings, uint32_t B,
+                                              const int32_t *m_dev, uint32_t D, uint32_t C,
+                                              uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                              int align_corners, uint32_t group, float eps,
+                                              uint32_t *entries, uint32_t *counts,
+                                              float *partial, int accumulate,
+                                              dfhip_stream_t stream);
 
 /* nerf/utils.py:708-713 scaler.step(optimizer); scaler.update() for
  * torch.optim.Adam (csrc/optim.hip): non-finite check of every grad, then (if

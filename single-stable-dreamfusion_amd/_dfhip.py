@@ -79,6 +79,9 @@ _SIGS = {
     "dfhip_grid_encode_backward_binned_phase": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _u32,
                                                 _vp, _u32, _u32, _u32, _f32, _u32, _u32, _i32,
                                                 _vp, _vp, _vp, _i32, _vp],
+    "dfhip_grid_encode_backward_binned_stencil": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp,
+                                                  _u32, _vp, _u32, _u32, _u32, _f32, _u32, _u32,
+                                                  _i32, _u32, _f32, _vp, _vp, _vp, _i32, _vp],
     "dfhip_grid_grad_blc_to_lbc": [_i32, _vp, _vp, _u32, _u32, _u32, _vp],
     "dfhip_field_mlp_forward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp],
     "dfhip_field_mlp_backward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,

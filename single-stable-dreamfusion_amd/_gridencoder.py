@@ -124,11 +124,14 @@ def grid_encode_backward_binned(*args, **kw):
 
 def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddings,
                     B, m_dev, D, C, L, S, H, gridtype, align_corners, entries, counts,
-                    partial, accumulate=False, phase=3):
+                    partial, accumulate=False, phase=3, stencil_eps=None):
     """grad_lbc [L, B, C] (B = capacity), inputs [B, D] raw positions in
     [-bound, bound] (bound > 0) or [0, 1] (bound = 0); rows [0, m_dev[0]) walked
     when m_dev is given.  grad_embeddings [rows, C] f32 is overwritten (or
-    added into with accumulate)."""
+    added into with accumulate).  stencil_eps: finite-difference stencil
+    groups of 7 (dfhip_grid_encode_backward_binned_stencil): grad_lbc is
+    [L, 7 B, C], inputs / B / m_dev count samples, row 7 g + a is point a of
+    sample g's stencil."""
     import numpy as np
     checked(grad_lbc, "grad")
     checked(inputs, "inputs")
@@ -144,14 +147,22 @@ def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddi
     off = np.ascontiguousarray(offsets_host, dtype=np.int32)
     if phase not in (1, 2, 3):
         raise RuntimeError("phase must be 1 (bin), 2 (walk + sum) or 3 (both)")
-    args = (int(phase), _d.dtype_code(grad_lbc, "grad"), ptr(grad_lbc), ptr(inputs), float(bound),
+    head = (int(phase), _d.dtype_code(grad_lbc, "grad"), ptr(grad_lbc), ptr(inputs), float(bound),
             ptr(offsets), off.ctypes.data, ptr(grad_embeddings), int(B), ptr(m_dev), int(D),
-            int(C), int(L), float(S), int(H), int(gridtype), int(bool(align_corners)),
-            ptr(entries), ptr(counts), ptr(partial), int(bool(accumulate)))
+            int(C), int(L), float(S), int(H), int(gridtype), int(bool(align_corners)))
+    tail = (ptr(entries), ptr(counts), ptr(partial), int(bool(accumulate)))
     keep = (grad_lbc, inputs, offsets, off, grad_embeddings, m_dev, entries, counts, partial)
+    if stencil_eps is None:
+        name, args = "dfhip_grid_encode_backward_binned_phase", head + tail
+    else:
+        if grad_lbc.shape[1] < 7 * int(B) or inputs.shape[0] < int(B):
+            raise RuntimeError("stencil groups: grad_lbc must hold 7 B rows per level and "
+                               "inputs B samples")
+        name, args = ("dfhip_grid_encode_backward_binned_stencil",
+                      head + (7, float(stencil_eps)) + tail)
 
     def launch(_keep=keep):
         """Launch on the current stream with the validated, pre-marshalled
         arguments (the graph-replayed step calls this every step)."""
-        call("dfhip_grid_encode_backward_binned_phase", *args, stream())
+        call(name, *args, stream())
     return launch

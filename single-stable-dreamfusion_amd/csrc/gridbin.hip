@@ -299,12 +299,41 @@ struct FastLevels {
     uint32_t lead[kFastLevels], bin0[kFastLevels];
 };
 
-template <bool POW2>
+// Finite-difference stencil groups (the shaded train step, csrc/shade.hip):
+// field row GROUP g + a (GROUP = 7) is point a of sample g, a = 0 the sample
+// itself, a = 1 + s the clamped x + (s odd ? -eps : eps) e_(s >> 1)
+// (k_stencil's arithmetic, network_grid.py:90-104).  Binned per group, one
+// entry per (group, slice) instead of one per (row, slice); the walk derives
+// the seven points from the sample's position and reads the group's seven
+// gradient rows (adjacent in the [L, 7 M, C] planes).
+struct Stencil {
+    float eps, bound;
+};
+
+template <uint32_t GROUP>
+__device__ __forceinline__ void group_point(const float (&xr)[3], uint32_t a, const Stencil &st,
+                                            float (&p)[3]) {
+    if (GROUP == 1 || a == 0) {
+#pragma unroll
+        for (uint32_t d = 0; d < 3; ++d) p[d] = xr[d];
+        return;
+    }
+    const uint32_t s = a - 1u, axis = s >> 1;
+    const float off = (s & 1u) ? -st.eps : st.eps;
+#pragma unroll
+    for (uint32_t d = 0; d < 3; ++d) {
+        const float v = xr[d] + (d == axis ? off : 0.0f);
+        p[d] = fminf(fmaxf(v, -st.bound), st.bound);
+    }
+}
+
+template <bool POW2, uint32_t GROUP = 1>
 __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inputs,
                                                   FastLevels fl, BinInfo bi, int align_corners,
                                                   SliceDyn dyn, float inv, uint32_t B,
                                                   uint32_t *__restrict__ counts,
-                                                  uint16_t *__restrict__ entries) {
+                                                  uint16_t *__restrict__ entries,
+                                                  Stencil st = Stencil{0.0f, 0.0f}) {
     __shared__ uint32_t cnt[kMaxBins];
     const float half = align_corners ? 0.0f : 0.5f;
     const uint32_t M = ge::dyn_count(dyn, B);
@@ -316,24 +345,50 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
         uint16_t *seg = entries + (size_t)tile * nb * kTile;
         const uint32_t s_end = min(M, (tile + 1) * kTile);
         for (uint32_t s = tile * kTile + threadIdx.x; s < s_end; s += blockDim.x) {
-            float x[3];
-            if (!load_pos<3, POW2>(inputs, dyn, inv, s, x)) continue;
+            // the group's points, mapped to [0, 1]; out-of-range points skip
+            float xg[GROUP][3];
+            uint32_t in = 0;
+            if constexpr (GROUP == 1) {
+                if (!load_pos<3, POW2>(inputs, dyn, inv, s, xg[0])) continue;
+                in = 1;
+            } else {
+                float xr[3];
+#pragma unroll
+                for (uint32_t d = 0; d < 3; ++d) xr[d] = inputs[(size_t)s * 3 + d];
+#pragma unroll
+                for (uint32_t a = 0; a < GROUP; ++a) {
+                    float p[3];
+                    group_point<GROUP>(xr, a, st, p);
+                    bool ok = true;
+#pragma unroll
+                    for (uint32_t d = 0; d < 3; ++d) {
+                        xg[a][d] = ge::dyn_map_t<POW2>(dyn, inv, p[d]);
+                        ok = ok && !(xg[a][d] < 0.0f) && !(xg[a][d] > 1.0f);
+                    }
+                    in |= (ok ? 1u : 0u) << a;
+                }
+                if (!in) continue;
+            }
             const uint16_t id = (uint16_t)(s - tile * kTile);
             for (uint32_t l = 0; l < bi.L; ++l) {
                 const float sc = fl.scale[l];
-                const uint32_t c0 = (uint32_t)floorf(fmaf(x[0], sc, half));
-                const uint32_t c1 = (uint32_t)floorf(fmaf(x[1], sc, half));
-                const uint32_t c2 = (uint32_t)floorf(fmaf(x[2], sc, half));
                 const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
-                const uint32_t i0 = c0 + c1 * m1 + c2 * m2;
                 uint64_t mask = 0;
 #pragma unroll
-                for (uint32_t p = 0; p < 4; ++p) {  // x-neighbour pairs {0,1} + {0, m1, m2, m1+m2}
-                    if (p >= (1u << (lead - 1u))) break;  // uniform
-                    const uint32_t o = ((p & 1u) ? m1 : 0u) + ((p & 2u) ? m2 : 0u);
-                    const uint32_t r = (i0 + o) & wm;
-                    mask |= 1ull << (r >> shift);
-                    if ((r & smask) == smask) mask |= 1ull << (((r + 1u) & wm) >> shift);
+                for (uint32_t a = 0; a < GROUP; ++a) {
+                    if (!((in >> a) & 1u)) continue;
+                    const uint32_t c0 = (uint32_t)floorf(fmaf(xg[a][0], sc, half));
+                    const uint32_t c1 = (uint32_t)floorf(fmaf(xg[a][1], sc, half));
+                    const uint32_t c2 = (uint32_t)floorf(fmaf(xg[a][2], sc, half));
+                    const uint32_t i0 = c0 + c1 * m1 + c2 * m2;
+#pragma unroll
+                    for (uint32_t p = 0; p < 4; ++p) {  // x-neighbour pairs {0,1} + {0, m1, m2, m1+m2}
+                        if (p >= (1u << (lead - 1u))) break;  // uniform
+                        const uint32_t o = ((p & 1u) ? m1 : 0u) + ((p & 2u) ? m2 : 0u);
+                        const uint32_t r = (i0 + o) & wm;
+                        mask |= 1ull << (r >> shift);
+                        if ((r & smask) == smask) mask |= 1ull << (((r + 1u) & wm) >> shift);
+                    }
                 }
                 const uint32_t b0 = fl.bin0[l];
                 while (mask) {
@@ -490,15 +545,20 @@ __device__ __forceinline__ void load_grad(const grad_t *__restrict__ p, float (&
 // LDS atomic instruction rarely has two lanes on a row, and along its run a
 // lane merges consecutive contributions to the same cell in registers (at the
 // coarse levels a cell spans tens of samples of a ray).
-template <typename grad_t, uint32_t D, uint32_t C, bool POW2, int MODE>
-__global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad,  // [L, B, C]
+//
+// GROUP > 1 (stencil groups, see Stencil): an entry is a group; the lane
+// takes the group's points one after another through the same cell merge
+// (at the coarse levels a sample and its stencil points share a cell).
+template <typename grad_t, uint32_t D, uint32_t C, bool POW2, int MODE, uint32_t GROUP = 1>
+__global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad,  // [L, GROUP B, C]
                                                const float *__restrict__ inputs,
                                                const int32_t *__restrict__ offsets, Levels lv,
                                                BinInfo bi, uint32_t gridtype, int align_corners,
                                                SliceDyn dyn, float inv, uint32_t B,
                                                uint32_t *counts,
                                                const uint16_t *__restrict__ entries,
-                                               float *__restrict__ partial) {
+                                               float *__restrict__ partial,
+                                               Stencil st = Stencil{0.0f, 0.0f}) {
     extern __shared__ double acc[];
     __shared__ uint32_t sh_b, sh_j, sh_p;
     __shared__ uint32_t n_seen;
@@ -559,7 +619,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     const ge::LevelRows lr = ge::level_rows<D>(c);
     const uint32_t M = ge::dyn_count(dyn, B);
     const uint32_t ntiles = ceil_div(M, kTile);
-    const grad_t *gl = grad + (size_t)l * B * C;
+    const grad_t *gl = grad + (size_t)l * GROUP * B * C;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
     // the level's lead (corners 2^lead) is uniform over the workgroup: the
     // walk is instantiated per lead, so the corner loops and the trailing-dim
@@ -578,6 +638,42 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         double cw[1u << D][C];
         uint32_t cur[D];
         bool have = false;
+        // one contribution: the point x (in [0, 1]) with gradient g, merged
+        // into the lane's current cell or flushing it
+        auto take = [&](const float (&x)[D], const float (&g)[C]) {
+            uint32_t cell[D];
+            float frac[D];
+            locate<D>(c, align, x, cell, frac);
+            bool same = have;
+#pragma unroll
+            for (uint32_t d = 0; d < D; ++d)
+                if (d < lead) same = same && (cell[d] == cur[d]);
+            if (!same) {
+                if (have) flush<D, C, MODE, lead>(acc, srows, r0, r1, c, lr, cur, cw);
+#pragma unroll
+                for (uint32_t kc = 0; kc < (1u << D); ++kc)
+#pragma unroll
+                    for (uint32_t ch = 0; ch < C; ++ch) cw[kc][ch] = 0.0;
+#pragma unroll
+                for (uint32_t d = 0; d < D; ++d) cur[d] = cell[d];
+                have = true;
+            }
+            float tw = 1.0f;  // trailing dims dropped from the index: corners coincide
+#pragma unroll
+            for (uint32_t d = 0; d < D; ++d)
+                if (d >= lead) tw *= (1.0f - frac[d]) + frac[d];
+#pragma unroll
+            for (uint32_t kc = 0; kc < (1u << D); ++kc) {
+                if (kc >> lead) continue;
+                float w = tw;
+#pragma unroll
+                for (uint32_t d = 0; d < D; ++d)
+                    if (d < lead) w *= (kc & (1u << d)) ? frac[d] : 1.0f - frac[d];
+#pragma unroll
+                for (uint32_t ch = 0; ch < C; ++ch)
+                    cw[kc][ch] = fma((double)w, (double)g[ch], cw[kc][ch]);
+            }
+        };
         // a lane walks a run of Q entries in batches of RUN loads; segments
         // with Q == 1 (the fine levels) take single-entry batches instead of
         // eight clamped duplicate loads per entry
@@ -590,57 +686,44 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                 // with its own wait)
                 uint32_t sid[RUN];
                 float xs[RUN][D];
-                float gs[RUN][C];
+                float gs[RUN][GROUP][C];
 #pragma unroll
                 for (uint32_t i = 0; i < RUN; ++i) sid[i] = tbase + seg[min(e + i, e1 - 1)];
 #pragma unroll
                 for (uint32_t i = 0; i < RUN; ++i) {
                     load_pos3<D>(inputs, sid[i], xs[i]);
-                    load_grad<grad_t, C>(gl + (size_t)sid[i] * C, gs[i]);
+#pragma unroll
+                    for (uint32_t a = 0; a < GROUP; ++a)
+                        load_grad<grad_t, C>(gl + ((size_t)sid[i] * GROUP + a) * C, gs[i][a]);
                 }
 #pragma unroll
                 for (uint32_t i = 0; i < RUN; ++i) {
                     if (i < m) {  // guard, not break: keeps the run in registers
-                        float x[D];
-#pragma unroll
-                        for (uint32_t d = 0; d < D; ++d) x[d] = ge::dyn_map_t<POW2>(dyn, inv, xs[i][d]);
-                        uint32_t cell[D];
-                        float frac[D];
-                        locate<D>(c, align, x, cell, frac);
-                        bool same = have;
-#pragma unroll
-                        for (uint32_t d = 0; d < D; ++d)
-                            if (d < lead) same = same && (cell[d] == cur[d]);
-                        if (!same) {
-                            if (have) flush<D, C, MODE, lead>(acc, srows, r0, r1, c, lr, cur, cw);
-#pragma unroll
-                            for (uint32_t kc = 0; kc < (1u << D); ++kc)
-#pragma unroll
-                                for (uint32_t ch = 0; ch < C; ++ch) cw[kc][ch] = 0.0;
-#pragma unroll
-                            for (uint32_t d = 0; d < D; ++d) cur[d] = cell[d];
-                            have = true;
-                        }
-                        float tw = 1.0f;  // trailing dims dropped from the index: corners coincide
-#pragma unroll
-                        for (uint32_t d = 0; d < D; ++d)
-                            if (d >= lead) tw *= (1.0f - frac[d]) + frac[d];
-#pragma unroll
-                        for (uint32_t kc = 0; kc < (1u << D); ++kc) {
-                            if (kc >> lead) continue;
-                            float w = tw;
+                        if constexpr (GROUP == 1) {
+                            float x[D];
 #pragma unroll
                             for (uint32_t d = 0; d < D; ++d)
-                                if (d < lead) w *= (kc & (1u << d)) ? frac[d] : 1.0f - frac[d];
+                                x[d] = ge::dyn_map_t<POW2>(dyn, inv, xs[i][d]);
+                            take(x, gs[i][0]);
+                        } else {
 #pragma unroll
-                            for (uint32_t ch = 0; ch < C; ++ch)
-                                cw[kc][ch] = fma((double)w, (double)gs[i][ch], cw[kc][ch]);
+                            for (uint32_t a = 0; a < GROUP; ++a) {
+                                float p[3], x[D];
+                                group_point<GROUP>(xs[i], a, st, p);
+                                bool ok = true;
+#pragma unroll
+                                for (uint32_t d = 0; d < D; ++d) {
+                                    x[d] = ge::dyn_map_t<POW2>(dyn, inv, p[d]);
+                                    ok = ok && !(x[d] < 0.0f) && !(x[d] > 1.0f);
+                                }
+                                if (ok) take(x, gs[i][a]);
+                            }
                         }
                     }
                 }
             }
         };
-        if (Q <= 1)
+        if (GROUP > 1 || Q <= 1)
             walk(std::integral_constant<uint32_t, 1>{});
         else if (Q <= 4)  // most mid / fine-level segments: no 8-slot batch of duplicates
             walk(std::integral_constant<uint32_t, 4>{});
@@ -732,20 +815,28 @@ static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t 
     return mode == 0 ? 0 : kModeAny;  // only the mask form is specialised
 }
 
-template <typename grad_t, uint32_t C>
+template <typename grad_t, uint32_t C, uint32_t GROUP = 1>
 static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const float *inputs,
                         const int32_t *offsets, const int32_t *offsets_host, const Levels &lv,
                         const BinInfo &bi, uint32_t gridtype, int align, SliceDyn dyn,
-                        uint32_t B, uint32_t *counts, const uint16_t *entries, float *partial) {
+                        uint32_t B, uint32_t *counts, const uint16_t *entries, float *partial,
+                        Stencil st = Stencil{0.0f, 0.0f}) {
     const bool pow2 = ge::dyn_pow2(dyn.bound);
     const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-    const bool m0 = uniform_mode(offsets_host, lv, bi.L, 3, gridtype, align != 0) == 0;
+    // stencil groups are binned by the mask-form fast path only
+    const bool m0 = GROUP > 1 || uniform_mode(offsets_host, lv, bi.L, 3, gridtype, align != 0) == 0;
     typedef void (*walk_fn)(const grad_t *, const float *, const int32_t *, Levels, BinInfo,
                             uint32_t, int, SliceDyn, float, uint32_t, uint32_t *,
-                            const uint16_t *, float *);
+                            const uint16_t *, float *, Stencil);
     walk_fn kern;
-    if (pow2) kern = m0 ? k_walk<grad_t, 3, C, true, 0> : k_walk<grad_t, 3, C, true, kModeAny>;
-    else kern = m0 ? k_walk<grad_t, 3, C, false, 0> : k_walk<grad_t, 3, C, false, kModeAny>;
+    if constexpr (GROUP > 1) {
+        kern = pow2 ? k_walk<grad_t, 3, C, true, 0, GROUP> : k_walk<grad_t, 3, C, false, 0, GROUP>;
+    } else {
+        if (pow2)
+            kern = m0 ? k_walk<grad_t, 3, C, true, 0> : k_walk<grad_t, 3, C, true, kModeAny>;
+        else
+            kern = m0 ? k_walk<grad_t, 3, C, false, 0> : k_walk<grad_t, 3, C, false, kModeAny>;
+    }
     static bool attr[2][2] = {{false, false}, {false, false}};
     if (!attr[pow2][m0]) {
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -753,7 +844,7 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
         attr[pow2][m0] = true;
     }
     kern<<<bi.G, 1024, lds, s>>>(grad, inputs, offsets, lv, bi, gridtype, align, dyn, inv, B,
-                                 counts, entries, partial);
+                                 counts, entries, partial, st);
 }
 
 }  // namespace gb
@@ -791,13 +882,13 @@ extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *o
     return DFHIP_OK;
 }
 
-extern "C" int dfhip_grid_encode_backward_binned_phase(
-    int phase, int grad_dtype, const void *grad_lbc, const float *inputs, float bound,
-    const int32_t *offsets, const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
-    const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
-    uint32_t gridtype, int align_corners, uint32_t *entries, uint32_t *counts, float *partial,
-    int accumulate, dfhip_stream_t stream) {
-    const char *name = "grid_encode_backward_binned";
+static int binned_backward(const char *name, int phase, int grad_dtype, const void *grad_lbc,
+                           const float *inputs, float bound, const int32_t *offsets,
+                           const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
+                           const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S,
+                           uint32_t H, uint32_t gridtype, int align_corners, uint32_t group,
+                           float eps, uint32_t *entries, uint32_t *counts, float *partial,
+                           int accumulate, hipStream_t s) {
     if (phase < 1 || phase > 3) {
         set_error("%s: phase must be 1 (bin), 2 (walk + sum) or 3 (both), got %d", name, phase);
         return DFHIP_EINVAL;
@@ -823,9 +914,19 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
         set_error("%s: null pointer", name);
         return DFHIP_EINVAL;
     }
-    hipStream_t s = as_stream(stream);
     const ge::Levels lv = ge::make_levels(L, S, H);
     const ge::SliceDyn dyn{m_dev, bound};
+    gb::FastLevels fl;
+    const bool fast = gb::make_fast_levels(offsets_host, lv, bi, gridtype, align_corners != 0, fl);
+    if (group != 1) {
+        if (group != 7 || C != 2 || grad_dtype == DFHIP_F32 || !fast || !(bound > 0.0f) ||
+            !(eps >= 0.0f)) {
+            set_error("%s: stencil groups need group 7, C = 2, f16 / bf16 gradients, bound > 0, "
+                      "eps >= 0 and a mask-form level layout", name);
+            return DFHIP_EINVAL;
+        }
+    }
+    const gb::Stencil st{eps, bound};
     if (phase & 1) {
         // totals (k_bin adds) and the plan (k_walk sets; P = 0: no images)
         (void)hipMemsetAsync(counts + bi.o_totals, 0,
@@ -834,9 +935,16 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
             const uint32_t gbin = bi.tcap < 4096u ? bi.tcap : 4096u;
             const bool pow2 = ge::dyn_pow2(dyn.bound);
             const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-            gb::FastLevels fl;
-            if (gb::g_fast_bin && gb::make_fast_levels(offsets_host, lv, bi, gridtype,
-                                                       align_corners != 0, fl)) {
+            if (group == 7) {
+                if (pow2)
+                    gb::k_bin_fast<true, 7><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
+                                                                   dyn, inv, B, counts,
+                                                                   (uint16_t *)entries, st);
+                else
+                    gb::k_bin_fast<false, 7><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
+                                                                    dyn, inv, B, counts,
+                                                                    (uint16_t *)entries, st);
+            } else if (gb::g_fast_bin && fast) {
                 if (pow2)
                     gb::k_bin_fast<true><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
                                                                 dyn, inv, B, counts,
@@ -845,14 +953,15 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
                     gb::k_bin_fast<false><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
                                                                  dyn, inv, B, counts,
                                                                  (uint16_t *)entries);
-            } else if (pow2)
+            } else if (pow2) {
                 gb::k_bin<3, true><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype,
                                                          align_corners, dyn, inv, B, counts,
                                                          (uint16_t *)entries);
-            else
+            } else {
                 gb::k_bin<3, false><<<gbin, 1024, 0, s>>>(inputs, offsets, lv, bi, gridtype,
                                                           align_corners, dyn, inv, B, counts,
                                                           (uint16_t *)entries);
+            }
         }
     }
     if (!(phase & 2)) return check_launch(name);
@@ -862,7 +971,14 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
     gb::launch_walk<GT, CC>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
                             bi, gridtype, align_corners, dyn, B, counts,                     \
                             (const uint16_t *)entries, partial)
-        if (grad_dtype == DFHIP_F16) {
+#define DFHIP_WALK7(GT)                                                                       \
+    gb::launch_walk<GT, 2, 7>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
+                              bi, gridtype, align_corners, dyn, B, counts,                   \
+                              (const uint16_t *)entries, partial, st)
+        if (group == 7) {
+            if (grad_dtype == DFHIP_F16) DFHIP_WALK7(half_t);
+            else DFHIP_WALK7(bf16_t);
+        } else if (grad_dtype == DFHIP_F16) {
             if (C == 1) DFHIP_WALK(half_t, 1); else if (C == 2) DFHIP_WALK(half_t, 2); else DFHIP_WALK(half_t, 4);
         } else if (grad_dtype == DFHIP_BF16) {
             if (C == 2) DFHIP_WALK(bf16_t, 2);
@@ -874,6 +990,7 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
             if (C == 1) DFHIP_WALK(float, 1); else if (C == 2) DFHIP_WALK(float, 2); else DFHIP_WALK(float, 4);
         }
 #undef DFHIP_WALK
+#undef DFHIP_WALK7
     }
     // every row is written: rows of bins no walk touched get zero (or keep
     // their value when accumulating)
@@ -882,6 +999,30 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
     gb::k_sum<float><<<(uint32_t)(want < 4096 ? want : 4096), 256, 0, s>>>(
         partial, bi, C, total_rows, counts, grad_embeddings, accumulate);
     return check_launch(name);
+}
+
+extern "C" int dfhip_grid_encode_backward_binned_phase(
+    int phase, int grad_dtype, const void *grad_lbc, const float *inputs, float bound,
+    const int32_t *offsets, const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
+    const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+    uint32_t gridtype, int align_corners, uint32_t *entries, uint32_t *counts, float *partial,
+    int accumulate, dfhip_stream_t stream) {
+    return binned_backward("grid_encode_backward_binned", phase, grad_dtype, grad_lbc, inputs,
+                           bound, offsets, offsets_host, grad_embeddings, B, m_dev, D, C, L, S,
+                           H, gridtype, align_corners, 1, 0.0f, entries, counts, partial,
+                           accumulate, as_stream(stream));
+}
+
+extern "C" int dfhip_grid_encode_backward_binned_stencil(
+    int phase, int grad_dtype, const void *grad_lbc, const float *inputs, float bound,
+    const int32_t *offsets, const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
+    const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+    uint32_t gridtype, int align_corners, uint32_t group, float eps, uint32_t *entries,
+    uint32_t *counts, float *partial, int accumulate, dfhip_stream_t stream) {
+    return binned_backward("grid_encode_backward_binned_stencil", phase, grad_dtype, grad_lbc,
+                           inputs, bound, offsets, offsets_host, grad_embeddings, B, m_dev, D, C,
+                           L, S, H, gridtype, align_corners, group, eps, entries, counts,
+                           partial, accumulate, as_stream(stream));
 }
 
 extern "C" int dfhip_grid_encode_backward_binned(

@@ -59,6 +59,10 @@ import _raymarching
 from _dfhip import call, ptr, stream
 
 
+import os
+
+_STENCIL_BIN = os.environ.get("DFHIP_STENCIL_BIN", "1") != "0"
+
 # shading -> dfhip_shading code (csrc/shade.hip); albedo needs no shading kernel
 SHADINGS = {"albedo": 0, "textureless": 1, "lambertian": 2}
 FD_EPS = 1e-2  # network_grid.py:90 finite_difference_normal epsilon
@@ -199,8 +203,11 @@ class NativeAlbedoStep:
         self.d_enc = torch.empty(self.L, fcap, self.C, **f16)
         self.mlp_partial = torch.empty(_fieldmlp.backward_parts(fcap) * _fieldmlp.params_count(),
                                        **f32)
-        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(fcap, enc.offsets_host, self.L,
-                                                                self.C)
+        # shaded steps: the embedding backward bins and walks each sample's
+        # 7-point stencil as one group (DFHIP_STENCIL_BIN=0: the 7 M rows one by one)
+        self.stencil_bin = bool(self.shade_code) and _STENCIL_BIN
+        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
+            cap if self.stencil_bin else fcap, enc.offsets_host, self.L, self.C)
         self.bin_scratch = (torch.empty(ne, **i32), torch.empty(nc, **i32),
                             torch.empty(npf, **f32))
         sc = trainer.scaler
@@ -411,12 +418,21 @@ class NativeAlbedoStep:
         if self._emb_launch is None:
             m = self.trainer.model
             S, Hb, gridtype, align, offsets_host = self.meta
-            self._emb_launch = _gridencoder.binned_launcher(
-                self.d_enc, self.xyz_field, m.bound, self.encoder.offsets, offsets_host,
-                self.encoder.embeddings.grad, self.fcap, self.m_field, 3, self.C, self.L, S, Hb,
-                gridtype, align, *self.bin_scratch)
-        per = 12 + self.L * self.C * 2
-        with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_field, per):
+            if self.stencil_bin:
+                self._emb_launch = _gridencoder.binned_launcher(
+                    self.d_enc, self.xyzs, m.bound, self.encoder.offsets, offsets_host,
+                    self.encoder.embeddings.grad, self.cap, self.m_dev, 3, self.C, self.L, S, Hb,
+                    gridtype, align, *self.bin_scratch, stencil_eps=FD_EPS)
+            else:
+                self._emb_launch = _gridencoder.binned_launcher(
+                    self.d_enc, self.xyz_field, m.bound, self.encoder.offsets, offsets_host,
+                    self.encoder.embeddings.grad, self.fcap, self.m_field, 3, self.C, self.L, S,
+                    Hb, gridtype, align, *self.bin_scratch)
+        if self.stencil_bin:  # per sample: its position + 7 rows of feature gradients
+            live, per = self.m_dev, 12 + 7 * self.L * self.C * 2
+        else:
+            live, per = self.m_field, 12 + self.L * self.C * 2
+        with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, live, per):
             self._emb_launch()
         if self.two_pass and self.lam > 0:
             if self._emb_launch2 is None:

@@ -434,3 +434,53 @@ def test_grid_backward_fast_bins_equal_generic(gpu, gt):
             base = (t * nb + b) * 1024
             assert np.array_equal(np.sort(e0[base:base + n]), np.sort(e1[base:base + n])), (t, b)
     np.testing.assert_allclose(g1, g0, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_grid_backward_stencil_groups_equal_rows(gpu, dtype):
+    """dfhip_grid_encode_backward_binned_stencil (7-point finite-difference
+    groups binned and walked per sample, the shaded train step) equals the
+    row-wise binned backward over the 7 M stencil rows laid out by
+    dfhip_shading_stencil, and the exact f64 oracle over those rows; device
+    count, raw [-1, 1] positions, samples on the box faces (clamped
+    stencil points)."""
+    import _dfhip
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    cap, m, eps = 6000, 5321, 1e-2
+    x = (_samples(cap, 51, edge=False) * 2 - 1).astype(np.float32)
+    x[:50, 0] = np.float32(1.0)   # on the +x face: the +x stencil point clamps
+    x[50:100, 2] = np.float32(-1.0)
+    xt = T(x, gpu)
+    m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+    x7 = torch.empty(7 * cap, 3, device=gpu)
+    m7 = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _dfhip.call("dfhip_shading_stencil", xt.data_ptr(), m_dev.data_ptr(), cap, eps, 1.0,
+                x7.data_ptr(), m7.data_ptr(), _dfhip.stream())
+    g = (torch.randn(16, 7 * cap, 2, generator=torch.Generator().manual_seed(52)) * 0.1)
+    g = g.to(dtype).to(gpu)
+    out = {}
+    for mode in ("rows", "groups"):
+        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
+            7 * cap if mode == "rows" else cap, offs, 16, 2)
+        ent = torch.empty(ne, dtype=torch.int32, device=gpu)
+        cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
+        part = torch.empty(npf, device=gpu)
+        gemb = torch.full((rows, 2), float("nan"), device=gpu)
+        if mode == "rows":
+            _gridencoder.binned_launcher(g, x7, 1.0, T(offs, gpu), offs, gemb, 7 * cap, m7, 3, 2,
+                                         16, S, 16, 1, False, ent, cnt, part)()
+        else:
+            _gridencoder.binned_launcher(g, xt, 1.0, T(offs, gpu), offs, gemb, cap, m_dev, 3, 2,
+                                         16, S, 16, 1, False, ent, cnt, part, stencil_eps=eps)()
+        torch.cuda.synchronize()
+        out[mode] = gemb.double().cpu().numpy()
+    x01 = ((x7[:7 * m].cpu().numpy() + np.float32(1)) / np.float32(2)).astype(np.float32)
+    gl = g[:, :7 * m].float().cpu().numpy()  # [L, 7m, C]
+    want = oracle.grid_encode_backward(gl, x01, offs, 2, S, 16, gridtype=1, blc=False)
+    scale = np.abs(want).max()
+    # the walk's part images are f32: a different split of a slice's entries
+    # into parts rounds differently (a few f32 ulps of the parts' magnitude)
+    np.testing.assert_allclose(out["groups"], out["rows"], rtol=1e-5, atol=1e-7 * scale)
+    np.testing.assert_allclose(out["groups"], want, rtol=1e-5, atol=1e-7 * scale)
