@@ -413,6 +413,7 @@ REGION_KERNELS = {
 
 
 MEASURE_TRAFFIC_DETAIL = {}  # region -> per-kernel bytes of the last measure_traffic
+MEASURE_TRAFFIC_CHILD_M = {}  # region -> the profiled child's mean samples per step
 
 
 def measure_traffic(region, timeout=180):
@@ -443,43 +444,63 @@ def measure_traffic(region, timeout=180):
     tmp = tempfile.mkdtemp(prefix="dfhip_pmc_", dir="/tmp")
     pats = REGION_KERNELS.get(region, (region,))
     per = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(tmp, counter)
-        cmd = [rp, "--kernel-trace", "--pmc", counter, "--output-format", "csv", "-d", d, "-o",
-               "run", "--"] + child
-        proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                                env=env, start_new_session=True)
-        try:
-            rc = proc.wait(timeout=timeout)
-        except subprocess.TimeoutExpired:
-            os.killpg(proc.pid, signal.SIGKILL)
-            proc.wait()
-            return None, f"{counter} pass timed out"
+    # FETCH_SIZE and WRITE_SIZE each in a run of its own; then the L2 hit /
+    # miss split (TCC_HIT / TCC_MISS, 2 TCC counters), which says how much of
+    # the fetch the region's requests caused versus re-read from L2
+    child_m = []
+    for counters in (("FETCH_SIZE",), ("WRITE_SIZE",), ("TCC_HIT_sum", "TCC_MISS_sum")):
+        tag = counters[0]
+        d = os.path.join(tmp, tag)
+        cmd = [rp, "--kernel-trace", "--pmc", *counters, "--output-format", "csv", "-d", d,
+               "-o", "run", "--"] + child
+        with open(os.path.join(tmp, tag + ".out"), "w") as out:
+            proc = subprocess.Popen(cmd, stdout=out, stderr=subprocess.DEVNULL, env=env,
+                                    start_new_session=True)
+            try:
+                rc = proc.wait(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+                proc.wait()
+                return None, f"{tag} pass timed out"
         if rc != 0:
-            return None, f"{counter} pass exited {rc}"
+            return None, f"{tag} pass exited {rc}"
+        try:  # the child's samples per step (the traffic scales with it)
+            line = [l for l in open(os.path.join(tmp, tag + ".out")) if l.startswith("{")][-1]
+            child_m.append(json.loads(line)["config"]["mean_samples_per_step"])
+        except (IndexError, ValueError, KeyError):
+            pass
         sums = {}
         for f in Path(d).rglob("*counter_collection.csv"):
             for r in csv.DictReader(open(f)):
+                name = r.get("Counter_Name", tag)
                 for i, alts in enumerate(pats):
                     alts = (alts,) if isinstance(alts, str) else alts
                     if any(a in r["Kernel_Name"] for a in alts):
-                        key = int(r.get("Dispatch_Id", len(sums.get(i, []))) or 0)
-                        sums.setdefault(i, []).append((key, float(r["Counter_Value"])))
-        sums = {i: [v for _, v in sorted(vs)[-keep:]] for i, vs in sums.items()}
-        if len(sums) != len(pats):
-            return None, f"{counter}: not every kernel of {region} was profiled"
-        scale = 2.0 if counter == "FETCH_SIZE" else 1.0
-        per[counter] = {i: scale * 1024.0 * sum(v) / len(v) for i, v in sums.items()}
+                        key = int(r.get("Dispatch_Id", 0) or 0)
+                        sums.setdefault((i, name), []).append((key, float(r["Counter_Value"])))
+        for cname in counters:
+            got = {i: [v for _, v in sorted(vs)[-keep:]] for (i, n), vs in sums.items()
+                   if n == cname}
+            if len(got) != len(pats):
+                return None, f"{cname}: not every kernel of {region} was profiled"
+            scale = {"FETCH_SIZE": 2.0 * 1024.0, "WRITE_SIZE": 1024.0}.get(cname, 1.0)
+            per[cname] = {i: scale * sum(v) / len(v) for i, v in got.items()}
     shutil.rmtree(tmp, ignore_errors=True)
     total = sum(per["FETCH_SIZE"].values()) + sum(per["WRITE_SIZE"].values())
     names = [a if isinstance(a, str) else a[0] for a in pats]
+    MEASURE_TRAFFIC_CHILD_M[region] = (sum(child_m) / len(child_m)) if child_m else None
     MEASURE_TRAFFIC_DETAIL[region] = {
-        names[i]: {"fetch_x2": int(per["FETCH_SIZE"][i]), "write": int(per["WRITE_SIZE"][i])}
+        names[i]: {"fetch_x2": int(per["FETCH_SIZE"][i]), "write": int(per["WRITE_SIZE"][i]),
+                   "l2_hit_rate": round(per["TCC_HIT_sum"][i] /
+                                        max(1.0, per["TCC_HIT_sum"][i] + per["TCC_MISS_sum"][i]),
+                                        4)}
         for i in range(len(pats))}
     return int(total), (
-        "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs) of "
-        "a 10 + 3-step child bench, the last 3 dispatches of each kernel; FETCH_SIZE x2 "
-        "(gfx950), KiB -> bytes, summed over the region's kernels, mean per launch")
+        "measured in this run: rocprofv3 --pmc passes (separate runs: FETCH_SIZE, WRITE_SIZE, "
+        "TCC_HIT_sum + TCC_MISS_sum) of a 10 + 3-step child bench, the last 3 dispatches of each "
+        "kernel; FETCH_SIZE x2 (the gfx950 correction, calibrated for 16-B streaming loads "
+        "only: an upper bound for gathers; it also counts Infinity-Cache hits), KiB -> bytes, "
+        "summed over the region's kernels, mean per launch; l2_hit_rate per kernel")
 
 
 def _free_port():
@@ -631,7 +652,9 @@ def main():
             "kernel": dom, "bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
             "traffic": traffic, "traffic_source": note,
-            "traffic_by_kernel": MEASURE_TRAFFIC_DETAIL.get(dom), "avg_us": kd["avg_us"],
+            "traffic_by_kernel": MEASURE_TRAFFIC_DETAIL.get(dom),
+            "traffic_child_mean_samples": MEASURE_TRAFFIC_CHILD_M.get(dom),
+            "avg_us": kd["avg_us"],
             "bytes_per_launch": kd["bytes_per_launch"],
             "timing": timing["note"] if timing else None}
         if dom == "grid_encode_backward":
