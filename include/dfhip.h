@@ -660,7 +660,10 @@ int dfhip_train_step_prologue_lr(const float *pose, float fx, float fy, float cx
  *      near plane's rays_t, as composite_rays leaves it), image [N,3] f32 —
  *      every ray written once (no zero-fill needed).
  * work: [4] u32 caller scratch, zeroed here; after the launch work[1] +
- *      2^32 work[2] = number of samples evaluated. */
+ *      2^32 work[2] = number of samples evaluated.
+ * quads: the table's corner quads [rows, 4] u32 (dfhip_grid_quads of the
+ *      same table) or NULL: with them the field gathers each level's corners
+ *      0-3 / 4-7 as two 16-byte loads (bit-identical features). */
 int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d,
                             const float *nears, const float *fars, const float *noises,
                             float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
@@ -669,7 +672,7 @@ int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d
                             uint32_t gridtype, int align_corners, const float *w1,
                             const float *b1, const float *w2, const float *b2, const float *w3,
                             const float *b3, float *weights_sum, float *depth, float *image,
-                            uint32_t *work, dfhip_stream_t stream);
+                            uint32_t *work, const void *quads, dfhip_stream_t stream);
 
 /* ---- non-albedo shading of the train step (csrc/shade.hip) ------------------
  * Replaces, for the `textureless` / `lambertian` steps, network_grid.py:90-144

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void k_render_infer(
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *__restrict__ weights_sum, float *__restrict__ depth,
     float *__restrict__ image, uint32_t *__restrict__ work,
-    uint64_t *prof) {
+    const fm::u32x4 *__restrict__ quads, uint64_t *prof) {
     __shared__ fm::Weights W;
     __shared__ fm::LevelK LK[fm::kLevels];
     __shared__ Stage stages[kWaves];
@@ -244,7 +244,9 @@ __global__ __launch_bounds__(256) void k_render_infer(
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) xb[u] = fm::grid_features(table, LK, align, x01[u], h);
+            for (int u = 0; u < 2; ++u)
+                xb[u] = quads ? fm::grid_features<half_t, true>(table, LK, align, x01[u], h, quads)
+                              : fm::grid_features(table, LK, align, x01[u], h);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 if (u == 1 && tile + 1 >= tiles) break;  // uniform
@@ -345,7 +347,7 @@ extern "C" int dfhip_render_rays_infer(
     uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
-    dfhip_stream_t stream) {
+    const void *quads, dfhip_stream_t stream) {
     const char *name = "render_rays_infer";
     if (L != 16) {
         set_error("%s: the fused renderer supports the reference's 16-level x 2-channel 3-D "
@@ -384,6 +386,6 @@ extern "C" int dfhip_render_rays_infer(
     rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
         N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
         (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
-        weights_sum, depth, image, work, g_render_prof);
+        weights_sum, depth, image, work, (const fm::u32x4 *)quads, g_render_prof);
     return check_launch(name);
 }
