@@ -23,7 +23,7 @@
 //   3. k_sum: every table row sums its bin's P_b images in a fixed order.
 //
 // Slices are 2^shift rows of one level (8192 rows x 2 channels x f64 =
-// 128 KiB of LDS, one walk workgroup per CU at a time; G = 4 per CU).
+// 128 KiB of LDS, one walk workgroup per CU at a time; G = 3 per CU).
 // Measured on gfx950 (tools/walk_trace.py): the walk is bound by per-entry
 // issue and gather latency, not by the LDS atomics (removing all of them
 // gained 6 %); an XCD-local tile split bought nothing (the same per-entry
@@ -34,6 +34,8 @@
 // rounded to f32 once and the images are added in a fixed order (the
 // reference: f16 / f32 global atomics in arbitrary order).
 #include "grid_common.h"
+
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -84,6 +86,18 @@ static uint32_t device_cus() {
     return (uint32_t)cus;
 }
 
+// Walk workgroups per CU (DFHIP_WALK_G, 1..16, for A/B runs; default 3:
+// walk + sum 216.5 -> 208.4 us per C2 step against 4; 2 and 5-6 slower).
+static uint32_t walk_groups_per_cu() {
+    static uint32_t g = 0;
+    if (g == 0) {
+        const char *e = getenv("DFHIP_WALK_G");
+        const int v = e ? atoi(e) : 0;
+        g = (v >= 1 && v <= 16) ? (uint32_t)v : 3u;
+    }
+    return g;
+}
+
 // scratch layout (u32 words of `counts`):
 //   [tcap][nbins]  per-(tile, bin) counts          (k_bin)
 //   [nbins][16]    totals, as 16 partial sums      (k_bin; zeroed before it)
@@ -96,7 +110,7 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     bi.trace = g_walk_trace;
     bi.shift = slice_shift(C);
     bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, kTile);
-    bi.G = 4 * device_cus();
+    bi.G = walk_groups_per_cu() * device_cus();
     uint32_t nb = 0;
     for (uint32_t l = 0; l < L; ++l) {
         const uint32_t rows = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
