@@ -56,6 +56,7 @@ constexpr uint32_t kTotSplit = 16;            // bin totals as 16 partial sums (
 struct BinInfo {
     uint32_t L, nbins, shift, tcap;      // tcap: tiles of the capacity (counts row stride)
     uint32_t G;                          // walk workgroups
+    uint32_t lane_perm;                  // walk: bit-reversed lane -> run map (1) or identity
     uint32_t o_totals, o_plan;           // word offsets into `counts` (layout below)
     uint32_t bin0[ge::kMaxLevels + 1];   // first bin of level l (bin0[L] = nbins)
     uint32_t base[ge::kMaxLevels];       // first row of level l
@@ -111,6 +112,14 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     bi.shift = slice_shift(C);
     bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, kTile);
     bi.G = walk_groups_per_cu() * device_cus();
+    {
+        static int perm = -1;
+        if (perm < 0) {
+            const char *e = getenv("DFHIP_WALK_PERM");
+            perm = e ? (atoi(e) != 0) : 1;
+        }
+        bi.lane_perm = (uint32_t)perm;
+    }
     uint32_t nb = 0;
     for (uint32_t l = 0; l < L; ++l) {
         const uint32_t rows = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
@@ -648,7 +657,12 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile;
         const uint32_t tbase = t * kTile;
         const uint32_t Q = (cnt + 63) >> 6;
-        const uint32_t e0 = min(lane * Q, cnt), e1 = min(e0 + Q, cnt);
+        // lane -> run: bit-reversed lane index (lanes next to each other in a
+        // wave instruction take runs far apart in the segment, i.e. different
+        // rays: their flushes then rarely hit the same LDS rows at the coarse
+        // levels, where a cell holds many consecutive samples)
+        const uint32_t rl = bi.lane_perm ? (__builtin_bitreverse32(lane) >> 26) : lane;
+        const uint32_t e0 = min(rl * Q, cnt), e1 = min(e0 + Q, cnt);
         double cw[1u << D][C];
         uint32_t cur[D];
         bool have = false;
