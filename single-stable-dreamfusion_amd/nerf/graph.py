@@ -89,6 +89,9 @@ class GraphedTrainStep:
                     self.optimizer_in_graph = True
             self.load(data, self.text_z)
             self.stream.wait_stream(torch.cuda.current_stream())
+            # the capture (and its dry run) forks the quad build and the
+            # binning onto a side stream: graph branches
+            nat.fork = True
             with torch.cuda.stream(self.stream):
                 # dry run (first-use setup outside the capture); the optimizer
                 # is not run, its launches are plain kernels
@@ -101,6 +104,7 @@ class GraphedTrainStep:
                     nat.optimizer_tail()
             torch.cuda.current_stream().wait_stream(self.stream)
         finally:
+            nat.fork = False
             _dfhip.set_kernel_timer(timer)
         model.local_step += 1  # as run_cuda's step in the autograd capture
         model.last_counter = nat.counter
