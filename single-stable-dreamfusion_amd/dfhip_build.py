@@ -28,6 +28,7 @@ CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
     "-fno-gpu-rdc", "-mcode-object-version=5", "-Wall", "-Wno-unused-function",
     "-fhip-fp32-correctly-rounded-divide-sqrt", f"-I{ROOT / 'include'}",
+    *os.environ.get("DFHIP_EXTRA_CFLAGS", "").split(),  # A/B probe builds (tools only)
 ]
 
 
