@@ -32,6 +32,22 @@ __host__ __device__ __forceinline__ uint32_t spread3(uint32_t v) {
 __host__ __device__ __forceinline__ uint32_t morton3(uint32_t x, uint32_t y, uint32_t z) {
     return spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
 }
+// The same for coordinates < 256 (the marchers' cells, clamped to H - 1 with
+// H <= 256): the first spread step is the identity there.  The barriers keep
+// the compiler from folding "(v + (v << 2)) << 1" into a quarter-rate
+// v_mul_lo_u32 by 10 / 20.
+__device__ __forceinline__ uint32_t spread3_8(uint32_t v) {
+    v = (v + (v << 8)) & 0x0F00F00Fu;
+    v = (v + (v << 4)) & 0xC30C30C3u;
+    v = (v + (v << 2)) & 0x49249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t morton3_8(uint32_t x, uint32_t y, uint32_t z) {
+    uint32_t sy = spread3_8(y), sz = spread3_8(z);
+    asm("" : "+v"(sy), "+v"(sz));
+    return spread3_8(x) | (sy << 1) | (sz << 2);
+}
+
 // raymarching.cu:73-81
 __host__ __device__ __forceinline__ uint32_t compact3(uint32_t v) {
     v &= 0x49249249u;
@@ -117,6 +133,32 @@ __device__ __forceinline__ int cell_of(const MarchConsts &k, float c, float rbou
     return (int)clampf(v, 0.0f, k.Hm1);
 }
 
+// Bitfield index of a cell (raymarching.cu:377-378: the f32 fma of the level
+// offset and the Morton code).  With one cascade the level is 0 and, for
+// H <= 256, the code is < 2^24, so the fma returns the code itself; both
+// branches are uniform.
+__device__ __forceinline__ uint32_t grid_index(const MarchConsts &k, int level, int nx, int ny,
+                                               int nz) {
+    if (k.H <= 256u) {
+        const uint32_t m = morton3_8((uint32_t)nx, (uint32_t)ny, (uint32_t)nz);
+        if (k.Cf == 1.0f) return m;
+        return (uint32_t)fmaf((float)level, k.H3, (float)m);
+    }
+    return (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
+}
+
+// floor(n / d) for a quotient below ~2^16 (n < 2^30, 1 <= d < 2^24): the f32
+// estimate with an approximate reciprocal rd ~ 1/d is within one of the
+// quotient, and one 24-bit multiply fixes it (no quarter-rate integer
+// division sequence).
+__device__ __forceinline__ uint32_t small_udiv(uint32_t n, uint32_t d, float rd) {
+    uint32_t q = (uint32_t)((float)n * rd);
+    const uint32_t p = __umul24(q, d);
+    if (p > n) q -= 1u;
+    else if (n - p >= d) q += 1u;
+    return q;
+}
+
 // Distance (in t) to the far face of the current cell along one axis
 // (raymarching.cu:390-392, nvcc contraction model).
 __device__ __forceinline__ float face_dist(const MarchConsts &k, int n, float d, float rd,
@@ -186,8 +228,7 @@ __device__ __forceinline__ uint32_t march(const MarchConsts &k, const Ray &r,
         const int nx = cell_of(k, x, rbound);
         const int ny = cell_of(k, y, rbound);
         const int nz = cell_of(k, z, rbound);
-        const uint32_t idx =
-            (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
+        const uint32_t idx = grid_index(k, level, nx, ny, nz);
         const bool occ = (grid[idx >> 3] >> (idx & 7)) & 1;
         if (occ) {
             if (WRITE) {
@@ -246,7 +287,7 @@ __device__ __forceinline__ int march_step(const MarchConsts &k, const Ray &r, Oc
     const int nx = cell_of(k, x, rbound);
     const int ny = cell_of(k, y, rbound);
     const int nz = cell_of(k, z, rbound);
-    const uint32_t idx = (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
+    const uint32_t idx = grid_index(k, level, nx, ny, nz);
     if (occupied(idx)) {
         xyz[0] = x;
         xyz[1] = y;
@@ -304,7 +345,7 @@ __device__ __forceinline__ bool march_next(const MarchConsts &k, const Ray &r,
 // inc = rint(dt/ulp) unless dt/ulp is a tie; the window stops before the
 // binade ends.  Otherwise lane j repeats the reference's f32 additions.
 __device__ __forceinline__ int wave_window_t(const MarchConsts &k, float t_base, int lane,
-                                             float &tj, uint32_t &inc) {
+                                             float &tj, uint32_t &inc, float &rinc) {
     if (k.dt_gamma == 0.0f) {
         const uint32_t b0 = __float_as_uint(t_base);
         const uint32_t ex = b0 >> 23;
@@ -314,13 +355,17 @@ __device__ __forceinline__ int wave_window_t(const MarchConsts &k, float t_base,
             const float Dr = rintf(D);
             if (D >= 0.5f && D < 8388608.0f && fabsf(D - Dr) != 0.5f) {
                 inc = (uint32_t)Dr;
-                const uint32_t room = (0x7FFFFFu - (b0 & 0x7FFFFFu)) / inc + 1u;
+                rinc = __builtin_amdgcn_rcpf(Dr);
+                // room = rem / inc + 1 candidates before the binade ends
+                const uint32_t rem = 0x7FFFFFu - (b0 & 0x7FFFFFu);
                 tj = __uint_as_float(b0 + (uint32_t)lane * inc);
-                return room < 64u ? (int)room : 64;
+                if (rem >= 63u * inc) return 64;
+                return (int)small_udiv(rem, inc, rinc) + 1;
             }
         }
     }
     inc = 0;
+    rinc = 0.0f;
     float t = t_base;
     for (int i = 0; i < lane; ++i) t += clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
     tj = t;
@@ -358,9 +403,9 @@ __device__ __forceinline__ uint32_t march_wave(const MarchConsts &k, const Ray &
     float pend = -INFINITY;     // a skip in flight: resume at the first t >= pend
     if (limit == 0 || !(t0 < far)) return 0;
     for (;;) {
-        float tj;
+        float tj, rinc;
         uint32_t inc;
-        const int L = wave_window_t(k, t_base, lane, tj, inc);
+        const int L = wave_window_t(k, t_base, lane, tj, inc, rinc);
         const bool valid = lane < L && tj < far;
         const uint64_t vmask = __ballot(valid);
         const int Lf = __popcll(vmask);   // t is increasing: a lane prefix
@@ -378,8 +423,7 @@ __device__ __forceinline__ uint32_t march_wave(const MarchConsts &k, const Ray &
         const int nz = cell_of(k, z, rbound);
         bool occ = false;
         if (valid) {
-            const uint32_t idx =
-                (uint32_t)fmaf((float)level, k.H3, (float)morton3(nx, ny, nz));
+            const uint32_t idx = grid_index(k, level, nx, ny, nz);
             occ = (grid[idx >> 3] >> (idx & 7)) & 1;
         }
         const uint64_t omask = __ballot(occ);
@@ -394,8 +438,10 @@ __device__ __forceinline__ uint32_t march_wave(const MarchConsts &k, const Ray &
             nxt = lane + 1;
         } else if (inc != 0) {
             // t_i >= tt  <=>  bits(t_i) >= bits(tt) for positive floats
+            // need = ceil((bt - b0) / inc), only below 65 matters
             const uint32_t b0 = __float_as_uint(t_base), bt = __float_as_uint(tt);
-            const uint32_t need = bt > b0 ? (bt - b0 + inc - 1u) / inc : 0u;
+            const uint32_t n = bt > b0 ? bt - b0 : 0u;
+            const uint32_t need = n > 64u * inc ? 65u : small_udiv(n + inc - 1u, inc, rinc);
             nxt = (int)min(max(need, (uint32_t)lane + 1u), 64u);
         } else {
             int lo = lane + 1, hi = 64;   // first lane in [lo, hi) with t >= tt
@@ -425,6 +471,7 @@ __device__ __forceinline__ uint32_t march_wave(const MarchConsts &k, const Ray &
         uint64_t V = 0;   // visited lanes
         if (s0 < 64) {
             // P[b] = successor^(2^b); lane m follows the chain m steps from s0
+            // (raw ds_bpermute on byte addresses measured 2 % slower)
             int P[6];
             P[0] = nxt;
 #pragma unroll
