@@ -33,8 +33,9 @@
 //  * one lane owns one ray; a wave runs 64 rays.  The march runs AHEAD of the
 //    field: every iteration each lane takes one march step (one grid cell,
 //    rm::march_step) and stages the sample it finds in a per-wave LDS batch
-//    (slot = ballot / mbcnt, no atomics), up to kK pending samples per ray,
-//    until the batch holds kBatch (64) samples or no lane may march.  Lanes
+//    (slot = ballot / mbcnt, no atomics), up to kK (8) pending samples per
+//    ray, until the batch holds kBatch (64) samples or no lane may march
+//    (kK 4 -> 8: 2.86 -> 2.73 ms per frame; batches of 48-128 the same).  Lanes
 //    do not wait for the wave's slowest ray between samples (the previous
 //    form marched up to 4 samples per lane per round, so every round lasted
 //    as long as the lane with the longest empty-space run: the march was
@@ -52,15 +53,23 @@
 //    taken is finished before its wave exits, so each output is written
 //    exactly once (no zero-fill).
 #include "march_common.h"
+#include <type_traits>
 #include "field_common.h"
 
 namespace dfhip {
 namespace rd {
 
 constexpr int kWaves = 4;
-constexpr int kK = 4;              // samples a ray may have pending per batch
-constexpr int kBatch = 64;         // a batch closes at >= 64 staged samples
-constexpr int kSlots = 2 * kBatch; // per-wave staged samples (< 64 added after the last check)
+#ifndef DFHIP_RENDER_K
+#define DFHIP_RENDER_K 8
+#endif
+#ifndef DFHIP_RENDER_BATCH
+#define DFHIP_RENDER_BATCH 64
+#endif
+constexpr int kK = DFHIP_RENDER_K;          // samples a ray may have pending per batch
+constexpr int kBatch = DFHIP_RENDER_BATCH;  // a batch closes at >= kBatch staged samples
+typedef std::conditional<(kK > 4), uint64_t, uint32_t>::type slots_t;  // 8-bit slots
+constexpr int kSlots = kBatch + 64; // per-wave staged samples (< 64 added after the last check)
 
 // Per-wave LDS staging of one batch of samples, in the order the lanes found
 // them.  pos holds the sample position until the field has read it, then
@@ -183,7 +192,8 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
         // loop's (after each sample the march restarts from rays_t, as
         // raymarching.cu:739-748 at n_step = 1), so marching past a ray's
         // termination only adds samples that the compositing drops.
-        uint32_t count = 0, npend = 0, pslots = 0;  // pslots: 8-bit slots of the pending samples
+        uint32_t count = 0, npend = 0;
+        slots_t pslots = 0;  // 8-bit slots of the pending samples
         while (true) {
             const bool can = ray >= 0 && !at_far && !finished && npend < (uint32_t)kK &&
                              marched < max_samples;
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 S.pos[3 * slot + 2] = px[2];
                 S.dt[slot] = pdt;
                 S.tc[slot] = tc;
-                pslots |= slot << (8 * npend);
+                pslots |= (slots_t)slot << (8 * npend);
                 ++npend;
             }
             count += (uint32_t)__popcll(em);
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
         // max_samples, or when its march reached far with nothing pending
         if (ray >= 0) {
             for (uint32_t q = 0; q < npend && !finished; ++q) {
-                const uint32_t slot = (pslots >> (8 * q)) & 0xFFu;
+                const uint32_t slot = (uint32_t)(pslots >> (8 * q)) & 0xFFu;
                 const float sigma = S.pos[3 * slot];
                 const uint32_t rg = __float_as_uint(S.pos[3 * slot + 1]);
                 const uint32_t bz = __float_as_uint(S.pos[3 * slot + 2]);
