@@ -68,7 +68,19 @@ constexpr int kWaves = 4;
 #endif
 constexpr int kK = DFHIP_RENDER_K;          // samples a ray may have pending per batch
 constexpr int kBatch = DFHIP_RENDER_BATCH;  // a batch closes at >= kBatch staged samples
-typedef std::conditional<(kK > 4), uint64_t, uint32_t>::type slots_t;  // 8-bit slots
+// pending slots, 8 bits each: one u64 holds 8, a second one up to 16
+static_assert(kK >= 1 && kK <= 16, "kK: 1..16 pending samples");
+struct PendSlots {
+    uint64_t lo = 0, hi = 0;
+    __device__ __forceinline__ void put(uint32_t i, uint32_t slot) {
+        if (kK <= 8 || i < 8) lo |= (uint64_t)slot << (8 * (i & 7));
+        else hi |= (uint64_t)slot << (8 * (i & 7));
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t i) const {
+        const uint64_t w = (kK <= 8 || i < 8) ? lo : hi;
+        return (uint32_t)(w >> (8 * (i & 7))) & 0xFFu;
+    }
+};
 constexpr int kSlots = kBatch + 64; // per-wave staged samples (< 64 added after the last check)
 
 // Per-wave LDS staging of one batch of samples, in the order the lanes found
@@ -193,7 +205,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
         // raymarching.cu:739-748 at n_step = 1), so marching past a ray's
         // termination only adds samples that the compositing drops.
         uint32_t count = 0, npend = 0;
-        slots_t pslots = 0;  // 8-bit slots of the pending samples
+        PendSlots pslots;  // slots of the pending samples
         while (true) {
             const bool can = ray >= 0 && !at_far && !finished && npend < (uint32_t)kK &&
                              marched < max_samples;
@@ -222,7 +234,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 S.pos[3 * slot + 2] = px[2];
                 S.dt[slot] = pdt;
                 S.tc[slot] = tc;
-                pslots |= (slots_t)slot << (8 * npend);
+                pslots.put(npend, slot);
                 ++npend;
             }
             count += (uint32_t)__popcll(em);
@@ -292,7 +304,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
         // max_samples, or when its march reached far with nothing pending
         if (ray >= 0) {
             for (uint32_t q = 0; q < npend && !finished; ++q) {
-                const uint32_t slot = (uint32_t)(pslots >> (8 * q)) & 0xFFu;
+                const uint32_t slot = pslots.get(q);
                 const float sigma = S.pos[3 * slot];
                 const uint32_t rg = __float_as_uint(S.pos[3 * slot + 1]);
                 const uint32_t bz = __float_as_uint(S.pos[3 * slot + 2]);
