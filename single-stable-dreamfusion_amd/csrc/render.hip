@@ -68,6 +68,10 @@ constexpr int kWaves = 4;
 #endif
 constexpr int kK = DFHIP_RENDER_K;          // samples a ray may have pending per batch
 constexpr int kBatch = DFHIP_RENDER_BATCH;  // a batch closes at >= kBatch staged samples
+#ifndef DFHIP_RENDER_TPP
+#define DFHIP_RENDER_TPP 2
+#endif
+constexpr int kTPP = DFHIP_RENDER_TPP;  // field tiles per pass
 // pending slots, 8 bits each: one u64 holds 8, a second one up to 16
 static_assert(kK >= 1 && kK <= 16, "kK: 1..16 pending samples");
 struct PendSlots {
@@ -251,14 +255,14 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
         const uint32_t total = count;
         const uint32_t tiles = ceil_div(total, 16u);
         if (prof) pc[5] += tiles;
-        // two tiles per pass: both tiles' table gathers are issued before
-        // either MLP waits on them (twice the loads in flight per lane)
-        for (uint32_t tile = 0; tile < tiles; tile += 2) {
-            float x[2][3], x01[2][3];
-            bool valid[2];
-            fm::half8 xb[2];
+        // kTPP tiles per pass: their table gathers are issued before any MLP
+        // waits on them (more loads in flight per lane)
+        for (uint32_t tile = 0; tile < tiles; tile += kTPP) {
+            float x[kTPP][3], x01[kTPP][3];
+            bool valid[kTPP];
+            fm::half8 xb[kTPP];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < kTPP; ++u) {
                 const uint32_t s = (tile + u) * 16 + c;
                 valid[u] = s < total;
 #pragma unroll
@@ -268,12 +272,12 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < kTPP; ++u)
                 xb[u] = quads ? fm::grid_features<half_t, true>(table, LK, align, x01[u], h, quads)
                               : fm::grid_features(table, LK, align, x01[u], h);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if (u == 1 && tile + 1 >= tiles) break;  // uniform
+            for (int u = 0; u < kTPP; ++u) {
+                if (u > 0 && tile + u >= tiles) break;  // uniform
                 const uint32_t s = (tile + u) * 16 + c;
                 fm::Fwd F;
                 fm::forward_tile(W, xb[u], c, h, F);
