@@ -128,10 +128,14 @@ __global__ __launch_bounds__(256) void k_packbits_f32v(const float *__restrict__
 
 // ------------------------------------------------------------------ training march
 
-// Rays per workgroup of the train marcher: one wave per ray, 8 waves.  The
+// Rays per workgroup of the train marcher: one wave per ray, 16 waves (8:
+// count 61.7 -> 57.0 us per C2 step, emit 14.2 -> 14.8; tools/ab_march.sh).  The
 // count pass leaves one total per workgroup in block_sums; the emit pass
 // derives a ray's offset from the preceding totals plus the block's counts.
-constexpr uint32_t kMarchRaysPerBlock = 8;
+#ifndef DFHIP_MARCH_RPB
+#define DFHIP_MARCH_RPB 16
+#endif
+constexpr uint32_t kMarchRaysPerBlock = DFHIP_MARCH_RPB;  // <= 16 (march_wave's flag rows)
 constexpr uint32_t kStageFloats = 5;  // x, y, z, dt, dl of a staged sample
 
 // Pass 1 (raymarching.cu:341-400): count occupied samples per ray.
