@@ -55,7 +55,7 @@ def test_errors_are_reported_without_a_gpu():
     assert rc == 2  # f16 accumulation with odd C (the reference silently drops it)
     # empty batches are no-ops that touch no device state
     assert lib.dfhip_morton3D(None, 0, None, None) == 0
-    assert lib.dfhip_march_rays_train_scratch_ints(16384) == 2048  # one total per 8 rays
+    assert lib.dfhip_march_rays_train_scratch_ints(16384) == 1024  # one total per 16 rays
 
 
 def test_shims_raise_on_cpu_tensors():
