@@ -642,6 +642,14 @@ def main():
     g0 = next(iter(trainer._graphs.values()), None)
     if g0 is not None:
         result["config"]["optimizer_in_graph"] = bool(g0.optimizer_in_graph)
+        nat0 = getattr(g0, "native", None)
+        if world > 1:
+            # one replay per step: RCCL all-reduce of the flat gradient bucket,
+            # 1/world and GradScaler + Adam captured in the step graph
+            result["config"]["grad_exchange"] = (
+                "rccl all-reduce inside the replayed step graph"
+                if nat0 is not None and nat0.dp_world is not None
+                else "eager all-reduce after the replay")
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         kd = kernels[dom]

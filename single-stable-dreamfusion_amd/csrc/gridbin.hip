@@ -783,6 +783,343 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     }
 }
 
+// ---------------------------------------------------------------- 2b. flat walk
+// k_walk_flat: the same slice ownership, plan and arithmetic as k_walk for the
+// mask-form layouts (FastLevels), with the work of a part laid out as ONE
+// sequence instead of one wave per tile segment:
+//
+//   * the part's tiles (part, part + P, ...) are taken in chunks of up to 1024;
+//     each thread loads one tile's count and a workgroup scan lays the chunk's
+//     segments end to end (E entries);
+//   * the E entries are cut into 1024 equal runs, one per thread (lanes of a
+//     wave take runs 16 apart, so one LDS instruction's lanes flush different
+//     rays); a run may cross tile segments (the cursor moves to the next
+//     segment in LDS, no global round trip);
+//   * a lane's next batch of ids is loaded before the current batch's
+//     positions / gradients are used.
+//
+// k_walk gave each wave whole segments: a part of ~30 tiles left half its
+// 16 waves one segment behind the others, each segment paid a dependent
+// count -> ids -> data round trip, and short segments left lanes idle.
+// Cells are compared by their tiled index (one compare), a new cell's
+// accumulators start at the products (f64, exact) instead of zero + fma, and
+// the level's corner count is a template parameter.
+constexpr uint32_t kChunkTiles = 1024;
+#ifndef DFHIP_WALK_RUN
+#define DFHIP_WALK_RUN 6
+#endif
+
+template <uint32_t C>
+struct FlatCell {
+    double cw[8][C];
+    uint32_t i0;
+    bool have;
+};
+
+// One point (x in [0, 1]^3) with gradient g into the lane's current cell.
+template <uint32_t C, uint32_t LEAD>
+__device__ __forceinline__ void flat_take(FlatCell<C> &st, double *acc, uint32_t srows,
+                                          uint32_t lo, uint32_t n, float sc, float half,
+                                          uint32_t m1, uint32_t m2, uint32_t wm,
+                                          const float (&x)[3], const float (&g)[C]) {
+    float fr[3];
+    uint32_t ci[3];
+#pragma unroll
+    for (uint32_t d = 0; d < 3; ++d) {
+        const float p = fmaf(x[d], sc, half);
+        const float fl = floorf(p);
+        fr[d] = p - fl;
+        ci[d] = (uint32_t)fl;
+    }
+    uint32_t i0 = ci[0];
+    if (LEAD > 1) i0 += ci[1] * m1;
+    if (LEAD > 2) i0 += ci[2] * m2;
+    float tw = 1.0f;  // trailing dims dropped from the index: their corners coincide
+#pragma unroll
+    for (uint32_t d = LEAD; d < 3; ++d) tw *= (1.0f - fr[d]) + fr[d];
+    double gd[C];
+#pragma unroll
+    for (uint32_t ch = 0; ch < C; ++ch) gd[ch] = (double)g[ch];
+    const bool same = st.have && i0 == st.i0;
+    if (!same) {
+        if (st.have) {
+#pragma unroll
+            for (uint32_t k = 0; k < (1u << LEAD); ++k) {
+                const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
+                const uint32_t rel = ((st.i0 + o) & wm) - lo;
+                if (rel < n) {
+#pragma unroll
+                    for (uint32_t ch = 0; ch < C; ++ch)
+                        atomicAdd(acc + ch * srows + rel, st.cw[k][ch]);
+                }
+            }
+        }
+        st.i0 = i0;
+        st.have = true;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < (1u << LEAD); ++k) {
+        float w = tw;
+#pragma unroll
+        for (uint32_t d = 0; d < LEAD; ++d) w *= (k & (1u << d)) ? fr[d] : 1.0f - fr[d];
+        const double wd = (double)w;
+#pragma unroll
+        for (uint32_t ch = 0; ch < C; ++ch)
+            st.cw[k][ch] = same ? fma(wd, gd[ch], st.cw[k][ch]) : wd * gd[ch];
+    }
+}
+
+template <uint32_t C, uint32_t LEAD>
+__device__ __forceinline__ void flat_flush(FlatCell<C> &st, double *acc, uint32_t srows,
+                                           uint32_t lo, uint32_t n, uint32_t m1, uint32_t m2,
+                                           uint32_t wm) {
+    if (!st.have) return;
+#pragma unroll
+    for (uint32_t k = 0; k < (1u << LEAD); ++k) {
+        const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
+        const uint32_t rel = ((st.i0 + o) & wm) - lo;
+        if (rel < n) {
+#pragma unroll
+            for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(acc + ch * srows + rel, st.cw[k][ch]);
+        }
+    }
+    st.have = false;
+}
+
+// A sample's GROUP gradient rows (adjacent in the [L, GROUP B, C] planes) as
+// wide loads where the rows are dwords (C = 2 of f16 / bf16): 7 rows = one
+// 16-byte + one 12-byte load instead of seven.
+typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u3a __attribute__((ext_vector_type(3), aligned(4)));
+template <typename grad_t, uint32_t C, uint32_t GROUP>
+__device__ __forceinline__ void load_group_grads(const grad_t *__restrict__ p,
+                                                 float (&g)[GROUP][C]) {
+    if constexpr (sizeof(grad_t) == 2 && C == 2 && GROUP == 7) {
+        const u4a a = *reinterpret_cast<const u4a *>(p);
+        const u3a b = *reinterpret_cast<const u3a *>(p + 8);
+        const uint32_t w[7] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z};
+#pragma unroll
+        for (uint32_t i = 0; i < 7; ++i) {
+            grad_t lo, hi;
+            const uint16_t l16 = (uint16_t)(w[i] & 0xFFFFu), h16 = (uint16_t)(w[i] >> 16);
+            __builtin_memcpy(&lo, &l16, 2);
+            __builtin_memcpy(&hi, &h16, 2);
+            g[i][0] = (float)lo;
+            g[i][1] = (float)hi;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t a = 0; a < GROUP; ++a) load_grad<grad_t, C>(p + a * C, g[a]);
+    }
+}
+
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RUN>
+__device__ __forceinline__ void flat_walk_level(
+    const grad_t *__restrict__ gl, const float *__restrict__ inputs, const uint32_t *counts,
+    const uint16_t *__restrict__ entries, double *acc, uint32_t *pre, uint32_t *wsum,
+    uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t ntiles, uint32_t srows,
+    uint32_t lo, uint32_t n, float sc, float half, uint32_t m1, uint32_t m2, uint32_t wm,
+    const SliceDyn &dyn, float inv, const Stencil &st) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t waves = blockDim.x >> 6, nthr = blockDim.x;
+    const uint32_t nt = ntiles > part ? ceil_div(ntiles - part, P) : 0u;
+    FlatCell<C> cell;
+    cell.have = false;
+    cell.i0 = 0;
+    for (uint32_t cb = 0; cb < nt; cb += kChunkTiles) {
+        const uint32_t nc = min(nt - cb, kChunkTiles);
+        // the chunk's segments end to end: exclusive scan of the counts
+        const uint32_t v = tid < nc ? counts[(size_t)(part + (cb + tid) * P) * nb + b] : 0u;
+        uint32_t inc = v;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t wofs = 0;
+        for (uint32_t w = 0; w < wave; ++w) wofs += wsum[w];
+        if (tid < nc) pre[tid] = wofs + inc - v;
+        if (tid == 0) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < waves; ++w) tot += wsum[w];
+            pre[nc] = tot;
+        }
+        __syncthreads();
+        const uint32_t E = pre[nc];
+        const uint32_t Q = ceil_div(E, nthr);
+        const uint32_t r = lane * waves + wave;  // lanes of a wave: runs `waves` apart
+        uint32_t e = min(r * Q, E);
+        const uint32_t e1 = min(e + Q, E);
+        if (e < e1) {
+            // segment of entry e: the last ti with pre[ti] <= e
+            uint32_t a = 0, z = nc;  // pre[a] <= e < pre[z]
+            while (z - a > 1) {
+                const uint32_t mid = (a + z) >> 1;
+                if (pre[mid] <= e) a = mid;
+                else z = mid;
+            }
+            uint32_t ti = a, tend = pre[ti + 1], slot = e - pre[ti];
+            uint32_t t = part + (cb + ti) * P;
+            // batch descriptor: (segment, first slot, size, tile base)
+            auto batch_size = [&](uint32_t ee, uint32_t te) { return min(RUN, min(e1, te) - ee); };
+            uint32_t m = batch_size(e, tend);
+            const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile;
+            uint32_t ids[RUN];
+#pragma unroll
+            for (uint32_t i = 0; i < RUN; ++i) ids[i] = seg[slot + min(i, m - 1)];
+            while (true) {
+                const uint32_t tbase = t * kTile;
+                // next batch: cursor and its ids, loaded ahead of this batch's data
+                uint32_t ne = e + m, nslot = slot + m, nti = ti, ntend = tend, nt2 = t;
+                const uint16_t *nseg = seg;
+                if (ne == ntend && ne < e1) {
+                    ++nti;
+                    nslot = 0;
+                    ntend = pre[nti + 1];
+                    nt2 = part + (cb + nti) * P;
+                    nseg = entries + ((size_t)nt2 * nb + b) * kTile;
+                }
+                const bool more = ne < e1;
+                const uint32_t nm = more ? batch_size(ne, ntend) : 1u;
+                uint32_t nids[RUN];
+                if (more) {
+#pragma unroll
+                    for (uint32_t i = 0; i < RUN; ++i) nids[i] = nseg[nslot + min(i, nm - 1)];
+                }
+                float xs[RUN][3];
+                float gs[RUN][GROUP][C];
+#pragma unroll
+                for (uint32_t i = 0; i < RUN; ++i) {
+                    const uint32_t s = tbase + ids[i];
+                    load_pos3<3>(inputs, s, xs[i]);
+                    load_group_grads<grad_t, C, GROUP>(gl + (size_t)s * GROUP * C, gs[i]);
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < RUN; ++i) {
+                    if (i < m) {
+                        if constexpr (GROUP == 1) {
+                            float x[3];
+#pragma unroll
+                            for (uint32_t d = 0; d < 3; ++d)
+                                x[d] = ge::dyn_map_t<POW2>(dyn, inv, xs[i][d]);
+                            flat_take<C, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2, wm, x,
+                                               gs[i][0]);
+                        } else {
+#pragma unroll
+                            for (uint32_t a2 = 0; a2 < GROUP; ++a2) {
+                                float p[3], x[3];
+                                group_point<GROUP>(xs[i], a2, st, p);
+                                bool ok = true;
+#pragma unroll
+                                for (uint32_t d = 0; d < 3; ++d) {
+                                    x[d] = ge::dyn_map_t<POW2>(dyn, inv, p[d]);
+                                    ok = ok && !(x[d] < 0.0f) && !(x[d] > 1.0f);
+                                }
+                                if (ok)
+                                    flat_take<C, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2,
+                                                       wm, x, gs[i][a2]);
+                            }
+                        }
+                    }
+                }
+                if (!more) break;
+                e = ne;
+                slot = nslot;
+                ti = nti;
+                tend = ntend;
+                t = nt2;
+                seg = nseg;
+                m = nm;
+#pragma unroll
+                for (uint32_t i = 0; i < RUN; ++i) ids[i] = nids[i];
+            }
+        }
+        __syncthreads();  // pre / wsum are rewritten by the next chunk
+    }
+    flat_flush<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm);
+}
+
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP>
+__global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ grad,  // [L, GROUP B, C]
+                                                    const float *__restrict__ inputs,
+                                                    FastLevels fl, BinInfo bi, int align_corners,
+                                                    SliceDyn dyn, float inv, uint32_t B,
+                                                    uint32_t *counts,
+                                                    const uint16_t *__restrict__ entries,
+                                                    float *__restrict__ partial, Stencil st) {
+    extern __shared__ double acc[];
+    __shared__ uint32_t pre[kChunkTiles + 1];
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t sh_b, sh_j, sh_p;
+    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
+    const uint32_t *totals = counts + bi.o_totals;
+    if (threadIdx.x < 64) {  // plan (wave 0), as k_walk
+        const uint32_t ln = threadIdx.x;
+        u64 T = 0, nz = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t e = b0 + ln < nb ? bin_total(totals, b0 + ln) : 0u;
+            u64 t, z;
+            (void)wave_excl_scan(e, ln, &t);
+            (void)wave_excl_scan(e ? 1u : 0u, ln, &z);
+            T += t;
+            nz += z;
+        }
+        const u64 extra = G > nz ? G - nz : 0;
+        uint32_t carry = 0;
+        if (ln == 0) sh_p = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t b = b0 + ln;
+            const uint32_t e = b < nb ? bin_total(totals, b) : 0u;
+            const uint32_t p = e ? 1u + (uint32_t)((u64)e * extra / (T ? T : 1)) : 0u;
+            u64 tot;
+            const uint32_t s = carry + (uint32_t)wave_excl_scan(p, ln, &tot);
+            if (b < nb && p && slot >= s && slot < s + p) {
+                sh_b = b;
+                sh_j = slot - s;
+                sh_p = p;
+            }
+            if (b < nb && p && slot == s) {
+                counts[bi.o_plan + 2 * b] = s;
+                counts[bi.o_plan + 2 * b + 1] = p;
+            }
+            carry += (uint32_t)tot;
+        }
+    }
+    __syncthreads();
+    const uint32_t P = sh_p;
+    if (P == 0) return;  // uniform
+    const uint32_t b = sh_b, part = sh_j;
+    uint32_t l = 0;
+    while (l + 1 < bi.L && bi.bin0[l + 1] <= b) ++l;
+    const uint32_t srows = 1u << bi.shift;
+    const uint32_t lo = (b - bi.bin0[l]) << bi.shift;  // slice start, relative to the level
+    const uint32_t n = min(srows, bi.rows[l] - lo);
+    for (uint32_t i = threadIdx.x; i < srows * C; i += blockDim.x) acc[i] = 0.0;
+    __syncthreads();
+    const uint32_t M = ge::dyn_count(dyn, B);
+    const uint32_t ntiles = ceil_div(M, kTile);
+    const grad_t *gl = grad + (size_t)l * GROUP * B * C;
+    const float sc = fl.scale[l], half = align_corners ? 0.0f : 0.5f;
+    const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
+    // entries whose loads are in flight together per lane (and the next
+    // batch's ids): 6 keeps the f16 walk within 128 VGPRs (8 spilled)
+    constexpr uint32_t RUN = GROUP > 1 ? 2u : (uint32_t)DFHIP_WALK_RUN;
+#define DFHIP_FLAT(LD)                                                                         \
+    flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN>(gl, inputs, counts, entries, acc, pre,    \
+                                                     wsum, nb, b, part, P, ntiles, srows, lo, \
+                                                     n, sc, half, m1, m2, wm, dyn, inv, st)
+    if (lead >= 3) DFHIP_FLAT(3);
+    else if (lead == 2) DFHIP_FLAT(2);
+    else DFHIP_FLAT(1);
+#undef DFHIP_FLAT
+    __syncthreads();
+    float *out = partial + (size_t)slot * ((size_t)srows * C);
+    for (uint32_t i = threadIdx.x; i < n * C; i += blockDim.x)
+        out[i] = (float)acc[(i % C) * srows + i / C];
+}
+
 // ---------------------------------------------------------------- 3. sum
 // Every (row, channel) of the table sums its bin's P_b images (slots
 // S_b .. S_b + P_b - 1, recorded by k_walk) in order.
@@ -843,14 +1180,42 @@ static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t 
     return mode == 0 ? 0 : kModeAny;  // only the mask form is specialised
 }
 
+// The flat walk (k_walk_flat) for mask-form layouts; DFHIP_WALK_FLAT=0 keeps
+// the per-segment k_walk (A/B runs, tests).
+static bool flat_walk_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("DFHIP_WALK_FLAT");
+        on = e ? (atoi(e) != 0) : 0;
+    }
+    return on != 0;
+}
+
 template <typename grad_t, uint32_t C, uint32_t GROUP = 1>
 static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const float *inputs,
                         const int32_t *offsets, const int32_t *offsets_host, const Levels &lv,
                         const BinInfo &bi, uint32_t gridtype, int align, SliceDyn dyn,
                         uint32_t B, uint32_t *counts, const uint16_t *entries, float *partial,
-                        Stencil st = Stencil{0.0f, 0.0f}) {
+                        const FastLevels *fl, Stencil st = Stencil{0.0f, 0.0f}) {
     const bool pow2 = ge::dyn_pow2(dyn.bound);
     const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
+    if constexpr (C == 2) if (fl && flat_walk_enabled()) {
+        typedef void (*flat_fn)(const grad_t *, const float *, FastLevels, BinInfo, int,
+                                SliceDyn, float, uint32_t, uint32_t *, const uint16_t *,
+                                float *, Stencil);
+        const flat_fn kf = pow2 ? k_walk_flat<grad_t, C, true, GROUP>
+                                : k_walk_flat<grad_t, C, false, GROUP>;
+        static bool fattr[2] = {false, false};
+        if (!fattr[pow2]) {
+            (void)hipFuncSetAttribute((const void *)kf,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kSliceBytes);
+            fattr[pow2] = true;
+        }
+        kf<<<bi.G, 1024, lds, s>>>(grad, inputs, *fl, bi, align, dyn, inv, B, counts, entries,
+                                   partial, st);
+        return;
+    }
     // stencil groups are binned by the mask-form fast path only
     const bool m0 = GROUP > 1 || uniform_mode(offsets_host, lv, bi.L, 3, gridtype, align != 0) == 0;
     typedef void (*walk_fn)(const grad_t *, const float *, const int32_t *, Levels, BinInfo,
@@ -995,14 +1360,15 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
     if (!(phase & 2)) return check_launch(name);
     if (B > 0) {
         const size_t lds = ((size_t)1 << bi.shift) * C * sizeof(double);
+        const gb::FastLevels *flp = fast ? &fl : nullptr;
 #define DFHIP_WALK(GT, CC)                                                                    \
     gb::launch_walk<GT, CC>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
                             bi, gridtype, align_corners, dyn, B, counts,                     \
-                            (const uint16_t *)entries, partial)
+                            (const uint16_t *)entries, partial, flp)
 #define DFHIP_WALK7(GT)                                                                       \
     gb::launch_walk<GT, 2, 7>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
                               bi, gridtype, align_corners, dyn, B, counts,                   \
-                              (const uint16_t *)entries, partial, st)
+                              (const uint16_t *)entries, partial, flp, st)
         if (group == 7) {
             if (grad_dtype == DFHIP_F16) DFHIP_WALK7(half_t);
             else DFHIP_WALK7(bf16_t);

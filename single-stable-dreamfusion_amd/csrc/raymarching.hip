@@ -135,7 +135,11 @@ __global__ __launch_bounds__(256) void k_packbits_f32v(const float *__restrict__
 #ifndef DFHIP_MARCH_RPB
 #define DFHIP_MARCH_RPB 16
 #endif
-constexpr uint32_t kMarchRaysPerBlock = DFHIP_MARCH_RPB;  // <= 16 (march_wave's flag rows)
+constexpr uint32_t kMarchRaysPerBlock = DFHIP_MARCH_RPB;
+// march_wave's s_vis[1024] holds one 64-byte flag row per wave, and a
+// workgroup is at most 1024 threads
+static_assert(kMarchRaysPerBlock >= 1 && kMarchRaysPerBlock <= 16,
+              "DFHIP_MARCH_RPB: 1..16 rays per workgroup");
 constexpr uint32_t kStageFloats = 5;  // x, y, z, dt, dl of a staged sample
 
 // Pass 1 (raymarching.cu:341-400): count occupied samples per ray.

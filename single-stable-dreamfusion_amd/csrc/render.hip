@@ -86,6 +86,7 @@ struct PendSlots {
     }
 };
 constexpr int kSlots = kBatch + 64; // per-wave staged samples (< 64 added after the last check)
+static_assert(kSlots <= 256, "PendSlots keeps LDS slot numbers in 8 bits: DFHIP_RENDER_BATCH <= 192");
 
 // Per-wave LDS staging of one batch of samples, in the order the lanes found
 // them.  pos holds the sample position until the field has read it, then

@@ -14,9 +14,12 @@ replayed:
   stops at it;
 * the native step's graph (nerf/native_step.py) holds render -> SDS
   gradient -> regulariser -> the whole backward, the embedding-gradient
-  scatter included, and on one GPU GradScaler + Adam as well (device
-  learning rates written by the prologue launch); with data parallelism the
-  graph ends at the gradients, and the all-reduce and Adam follow eagerly;
+  scatter included, and GradScaler + Adam as well (device learning rates
+  written by the prologue launch); with data parallelism over RCCL the flat
+  in-place all-reduce of the gradient bucket and the 1/world scaling sit
+  in the graph before Adam, so each rank replays ONE graph per step (a gloo
+  group, not capturable, ends the graph at the gradients and the exchange
+  and Adam follow eagerly);
 * the autograd form's graph ends at the feature gradients; the embedding
   scatter is launched eagerly after each replay, then the optimizer step;
 * kernel timing (bench.py) never reaches into a graph: it runs the native
@@ -80,12 +83,17 @@ class GraphedTrainStep:
         model = t.model
         timer = _dfhip.set_kernel_timer(None)  # no event records inside the graph
         try:
-            # one GPU: the optimizer step joins the graph (no gradient exchange)
+            # the optimizer step joins the graph: on one GPU directly, with data
+            # parallelism behind the flat RCCL all-reduce of the gradient
+            # bucket (captured too: one replay per step on every rank)
             self.optimizer_in_graph = False
-            if t.world_size == 1:
+            collective = t.graph_collective()
+            if t.world_size == 1 or collective:
                 adam = t.native_adam()
                 if adam:
                     nat.attach_optimizer(adam)
+                    if collective:
+                        nat.attach_allreduce(t.world_size)
                     self.optimizer_in_graph = True
             self.load(data, self.text_z)
             self.stream.wait_stream(torch.cuda.current_stream())
@@ -93,14 +101,19 @@ class GraphedTrainStep:
             # binning onto a side stream: graph branches
             nat.fork = True
             with torch.cuda.stream(self.stream):
-                # dry run (first-use setup outside the capture); the optimizer
-                # is not run, its launches are plain kernels
+                # dry run (first-use setup outside the capture, including the
+                # communicator's first collective); the optimizer is not run,
+                # its launches are plain kernels
                 nat.body()
                 nat.embedding_backward()
+                if nat.dp_world is not None:
+                    nat.allreduce_tail()
             with torch.cuda.graph(self.graph, stream=self.stream):
                 self.loss = nat.body()
                 nat.embedding_backward()
                 if self.optimizer_in_graph:
+                    if nat.dp_world is not None:
+                        nat.allreduce_tail()
                     nat.optimizer_tail()
             torch.cuda.current_stream().wait_stream(self.stream)
         finally:
@@ -201,6 +214,8 @@ class GraphedTrainStep:
         nat.body()
         nat.embedding_backward()
         if self.optimizer_in_graph:
+            if nat.dp_world is not None:
+                nat.allreduce_tail()
             nat.optimizer_tail()
         for p, g in self.grads:
             p.grad = g

@@ -248,6 +248,8 @@ class NativeAlbedoStep:
         # optimizer inside the graph (attach_optimizer): the learning rates
         # live on the device, written by the prologue launch every step
         self.lr_dev = torch.zeros(8, **f32)
+        self.dp_world = None  # attach_allreduce: the exchange joins the step
+        self.dp_group = None
         self.adam = None
         self._lr_source = None
         self.n_params = sum(p.numel() for p in self.params)
@@ -257,6 +259,21 @@ class NativeAlbedoStep:
         last launches, with device learning rates (captured in the graph)."""
         self.adam = native_adam.device_lr_launch(self.lr_dev)
         self._lr_source = native_adam.group_lrs
+
+    def attach_allreduce(self, world_size, group=None):
+        """Make the step's tail the data-parallel exchange: ONE in-place
+        all-reduce of the flat gradient bucket (flat_allreduce_'s bucket form,
+        the reference's DDP averaging, utils.py:200-202) then the 1/world
+        scaling, before the attached optimizer (captured in the graph)."""
+        self.dp_world = int(world_size)
+        self.dp_group = group
+
+    def allreduce_tail(self):
+        """The attached exchange (a timed region: the bucket read and written)."""
+        import torch.distributed as dist
+        with _dfhip.timed("grad_allreduce", 8 * self.n_params):
+            dist.all_reduce(self.grad_bucket, op=dist.ReduceOp.SUM, group=self.dp_group)
+            self.grad_bucket.div_(self.dp_world)
 
     def optimizer_tail(self):
         """The attached optimizer step (a timed region: 28 B per parameter)."""

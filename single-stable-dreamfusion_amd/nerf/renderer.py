@@ -328,6 +328,13 @@ class NeRFRenderer(nn.Module):
         this field for `shading`, else None (subclass hook)."""
         return None
 
+    def invalidate_infer_operands(self):
+        """The parameters changed behind torch's back (native Adam, a graph
+        replay, a checkpoint load): the next eval frame rebuilds its cached
+        launch operands."""
+        self.__dict__["_param_generation"] = self.__dict__.get("_param_generation", 0) + 1
+        self.__dict__.pop("_infer_operands", None)
+
     def _infer_fused(self, rays_o, rays_d, nears, fars, field, perturb, dt_gamma, max_steps,
                      T_thresh):
         """The inference loop below as ONE persistent launch (csrc/render.hip):
@@ -344,10 +351,14 @@ class NeRFRenderer(nn.Module):
         work = torch.empty(4, dtype=torch.int32, device=dev)
         noises = torch.rand(N, device=dev) if perturb else None
         # the field's launch operands (f32 weights, the f16 table and its corner
-        # quads) are rebuilt only when a parameter changed (tensor versions):
-        # consecutive eval frames reuse them
+        # quads) are rebuilt only when a parameter changed: consecutive eval
+        # frames reuse them.  Tensor versions miss the native optimizer (a
+        # kernel writing through data_ptr, also inside a replayed graph), so
+        # the trainer bumps param_generation after every optimizer step and
+        # checkpoint load (invalidate_infer_operands)
         params = [encoder.embeddings] + [p for lin in layers for p in (lin.weight, lin.bias)]
-        key = tuple((p.data_ptr(), p._version) for p in params)
+        key = (self.__dict__.get("_param_generation", 0),
+               *((p.data_ptr(), p._version) for p in params))
         cached = self.__dict__.get("_infer_operands")
         if cached is None or cached[0] != key:
             weights = []

@@ -266,6 +266,12 @@ class Trainer(object):
         self.fused_backward = fused_backward
         # HIP-graph replay of albedo steps (nerf/graph.py)
         self.graph_step = graph_step
+        # data parallelism inside the replayed native step (nerf/graph.py): the
+        # flat RCCL all-reduce, the 1/world scaling and GradScaler + Adam are
+        # captured with the step.  None: whenever a process group with the
+        # nccl (RCCL) backend is up; False: all-reduce + Adam eagerly after
+        # the replay; True: capture with any backend that supports it
+        self.dp_in_graph = None
         self._graphs = {}
         # GradScaler + Adam as one native call (nerf/optim.py) when eligible
         self.native_optimizer = os.environ.get("DFHIP_NATIVE_ADAM", "1") != "0"
@@ -457,10 +463,20 @@ class Trainer(object):
                                 else False)
         return self._native_opt
 
+    def graph_collective(self):
+        """True when the step graph should hold the gradient all-reduce (a
+        capturable RCCL process group is up).  With world_size 1 this is the
+        in-graph data-parallel form reduced over one rank (tests)."""
+        if self.dp_in_graph is False or not (dist.is_available() and dist.is_initialized()):
+            return False
+        if self.dp_in_graph is None and dist.get_backend() != "nccl":
+            return False  # gloo collectives run on the host: not capturable
+        return True
+
     def optimizer_step(self, stepped=False):
         """Gradient exchange, GradScaler + optimizer step, LR schedule.
-        stepped: the optimizer already ran inside the replayed step graph
-        (single GPU native step), only the schedule advances."""
+        stepped: the exchange (if any) and the optimizer already ran inside
+        the replayed step graph (native step), only the schedule advances."""
         if not stepped:
             if self.world_size > 1:
                 flat_allreduce_(self.model.parameters(), self.world_size)
@@ -469,6 +485,9 @@ class Trainer(object):
             else:
                 self.scaler.step(self.optimizer)
                 self.scaler.update()
+        inv = getattr(self.model, "invalidate_infer_operands", None)
+        if inv is not None:
+            inv()  # the parameters moved in place (eval-frame operand cache)
         if self.scheduler_update_every_step:
             self.lr_scheduler.step()
 
@@ -636,6 +655,8 @@ class Trainer(object):
         if self.model.cuda_ray:
             self.model.mean_count = ckpt.get("mean_count", self.model.mean_count)
             self.model.mean_density = ckpt.get("mean_density", self.model.mean_density)
+        if hasattr(self.model, "invalidate_infer_operands"):
+            self.model.invalidate_infer_operands()
         if model_only:
             return
         self.stats = ckpt.get("stats", self.stats)

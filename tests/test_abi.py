@@ -55,7 +55,13 @@ def test_errors_are_reported_without_a_gpu():
     assert rc == 2  # f16 accumulation with odd C (the reference silently drops it)
     # empty batches are no-ops that touch no device state
     assert lib.dfhip_morton3D(None, 0, None, None) == 0
-    assert lib.dfhip_march_rays_train_scratch_ints(16384) == 1024  # one total per 16 rays
+    # one total per workgroup of R rays (R = DFHIP_MARCH_RPB of the build, 1..16)
+    totals = lib.dfhip_march_rays_train_scratch_ints(16384)
+    rpb = 16384 // totals
+    assert 1 <= rpb <= 16 and rpb * totals == 16384
+    assert lib.dfhip_march_rays_train_scratch_ints(rpb) == 1
+    assert lib.dfhip_march_rays_train_scratch_ints(rpb + 1) == 2
+    assert lib.dfhip_march_rays_train_scratch_ints(0) == 1
 
 
 def test_shims_raise_on_cpu_tensors():

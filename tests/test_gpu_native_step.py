@@ -210,3 +210,44 @@ def test_optimizer_in_graph_matches_host_lr_adam(gpu):
         for name in ("step", "exp_avg", "exp_avg_sq"):
             assert torch.equal(sa[i][name], sb[i][name]), (i, name)
     assert float(a.scaler.get_scale()) == float(b.scaler.get_scale())
+
+
+def test_eval_frame_operands_follow_graph_training(gpu):
+    """The fused eval renderer caches its launch operands (f32 weights, f16
+    table, corner quads) between frames.  The graph-replayed step updates the
+    parameters in place with the native Adam (no torch version bump), so a
+    render -> train -> render sequence (the reference's periodic eval,
+    utils.py train() -> evaluate_one_epoch) must see the new parameters: the
+    second frame equals a frame rendered with the cache dropped."""
+    from scenes import camera_rays
+    trainer, data = _trainer(64, 13, graph=True)
+    m = trainer.model
+    for i in range(3):
+        trainer.train_iteration(data.collate([i % 4]))
+    o, d = camera_rays(32, 32, 13, radius=1.6)
+    rays_o = torch.from_numpy(o).to(gpu)[None]
+    rays_d = torch.from_numpy(d).to(gpu)[None]
+
+    def frame():
+        m.eval()
+        try:
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+                out = m.render(rays_o, rays_d, staged=True, perturb=False, light_d=None,
+                               ambient_ratio=1.0, shading="albedo", force_all_rays=True,
+                               bg_color=None, **vars(trainer.opt))
+        finally:
+            m.train()
+        torch.cuda.synchronize()
+        return out["image"].float().clone()
+
+    a = frame()
+    assert m.__dict__.get("_infer_operands") is not None  # the fused path ran and cached
+    for i in range(3):
+        trainer.train_iteration(data.collate([(i + 3) % 4]))
+    g = next(iter(trainer._graphs.values()))
+    assert g.native is not None and g.optimizer_in_graph
+    b = frame()
+    m.__dict__.pop("_infer_operands", None)
+    c = frame()
+    assert torch.equal(b, c)
+    assert not torch.equal(a, b)  # training moved the field

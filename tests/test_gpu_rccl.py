@@ -60,11 +60,78 @@ def test_rccl_flat_allreduce_in_place(gpu):
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_port(), q))
     p.start()
-    res = q.get(timeout=240)
-    p.join(timeout=60)
+    try:
+        res = q.get(timeout=240)
+        p.join(timeout=60)
+    finally:
+        if p.is_alive():  # hung or dead before reporting: never leave it on the GPU
+            p.kill()
+            p.join(timeout=30)
     assert p.exitcode == 0
     assert res["backend"] == "nccl"
     assert res["bucket"], "native step gradients are not views of one flat bucket"
     assert res["in_place"] and res["unchanged"]
     assert res["numel"] >= 903480 * 2  # grid table + MLPs, one bucket
     assert res["sum_ok"]
+
+
+def _worker_in_graph(port, out):
+    """The in-graph data-parallel step (RCCL all-reduce + 1/world + Adam
+    captured in the native step graph) over a 1-rank nccl group against the
+    plain one-GPU graph (no collective): same draws, so bit-identical."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "single-stable-dreamfusion_amd")]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import bench
+
+    def run(in_graph):
+        tr, dt = bench.make_trainer(64, 5, 0, 1, True, graph=True)
+        tr.dp_in_graph = in_graph
+        tr.opt.iters = 50  # a moving LR schedule (device learning rates)
+        for i in range(20):
+            tr.train_iteration(dt.collate([i % 4]))
+        torch.cuda.synchronize()
+        g = next(iter(tr._graphs.values()))
+        return tr, g
+
+    a, ga = run(None)  # auto: the nccl group is up -> collective in the graph
+    b, gb = run(False)
+    res = {"a_collective": ga.native is not None and ga.native.dp_world == 1,
+           "a_opt": bool(ga.optimizer_in_graph),
+           "b_plain": gb.native is not None and gb.native.dp_world is None
+           and bool(gb.optimizer_in_graph),
+           "params_equal": all(bool(torch.equal(pa, pb)) for pa, pb in
+                               zip(a.model.parameters(), b.model.parameters())),
+           "scale_equal": float(a.scaler.get_scale()) == float(b.scaler.get_scale()),
+           "moved": not all(bool(torch.equal(p, q)) for p, q in
+                            zip(a.model.parameters(), bench.make_trainer(
+                                64, 5, 0, 1, True)[0].model.parameters()))}
+    sa, sb = a.optimizer.state_dict()["state"], b.optimizer.state_dict()["state"]
+    res["state_equal"] = all(bool(torch.equal(sa[i][k], sb[i][k])) for i in sa
+                             for k in ("step", "exp_avg", "exp_avg_sq"))
+    dist.destroy_process_group()
+    out.put(res)
+
+
+def test_rccl_all_reduce_captured_in_step_graph(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_in_graph, args=(_port(), q))
+    p.start()
+    try:
+        res = q.get(timeout=300)
+        p.join(timeout=60)
+    finally:
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=30)
+    assert p.exitcode == 0
+    assert res["a_collective"] and res["a_opt"], res
+    assert res["b_plain"], res
+    assert res["moved"], res
+    assert res["params_equal"] and res["state_equal"] and res["scale_equal"], res

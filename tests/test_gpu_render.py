@@ -187,3 +187,40 @@ def test_fused_infer_matches_oracle(gpu, occupancy, scale, seed):
           f"{np.abs(fi - oi)[opened].max() if opened.any() else 0.0:.2e}")
     # measured: <= 5e-6 on those rays (a one-ulp h change moves one sample's alpha)
     assert np.abs(fi - oi).max() <= 1e-3 and np.abs(fw - ow).max() <= 1e-3
+
+
+@pytest.mark.parametrize("occupancy", ["grid", "sphere"])
+def test_fused_infer_bit_exact_at_c4_size(gpu, occupancy):
+    """C4 itself (BASELINE configs[3]): the 800 x 800 test-view frame of the
+    bench (640,000 rays; R0 = update_extra_state occupancy of a seeded
+    U(-0.5, 0.5) network, R1 = the analytic radius-0.5 sphere), where the
+    persistent kernel's ray queue, refills and retirements run under full
+    contention.  Every ray must equal the n_step = 1 loop bit for bit (the
+    loop's kernels are pinned to the CPU oracle in test_gpu_raymarching)."""
+    import bench
+    import main
+    from nerf.network_grid import NeRFNetwork
+    from nerf.provider import NeRFDataset
+    res = 800
+    opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res)])
+    torch.manual_seed(1)
+    m = NeRFNetwork(opt).to(gpu)
+    with torch.no_grad():
+        m.encoder.embeddings.uniform_(-0.5, 0.5)
+    with torch.autocast("cuda", dtype=torch.float16):
+        for _ in range(3):
+            m.update_extra_state()
+    if occupancy == "sphere":
+        bench.sphere_occupancy_(m)
+    m.eval()
+    data = NeRFDataset(opt, device=gpu, type="test", H=res, W=res, size=8).collate([1])
+    rays_o = data["rays_o"][0].contiguous()
+    rays_d = data["rays_d"][0].contiguous()
+    assert rays_o.shape[0] == 640000
+    (fw, fd, fi), (lw, ld, li) = _both(m, rays_o, rays_d, n_step_max=1)
+    samples = int(m.last_infer_work.cpu().numpy().view(np.uint32)[1])
+    assert samples > 5_000_000  # a C4-sized workload (bench: 11.6 M / 13.5 M samples)
+    assert (lw > 0).sum() > 100_000
+    np.testing.assert_array_equal(fw, lw)
+    np.testing.assert_array_equal(fd, ld)
+    np.testing.assert_array_equal(fi, li)
