@@ -30,10 +30,6 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "SDS train steps/sec + rays/sec at 128×128, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# ds_add_f64 issue rate measured on gfx950 (tools/micro/lds_atomic.hip):
-# 2.53 lane-ops per CU per clock x 256 CUs x 2.4 GHz
-LDS_F64_ATOMIC_PEAK = 2.53 * 256 * 2.4e9
-ATOMIC_PEAK_GBS = 1300.0     # MI355X_MICROARCH.md: global float atomics ~1.3 TB/s
 
 
 def parse():
@@ -339,7 +335,7 @@ def kernel_timing_pass(trainer, step, k):
     finally:
         _dfhip.set_kernel_timer(None)
         trainer.step_hook = None
-    info = {"steps": k, "ms_per_step_incl_spin": round(dt * 1e3, 3),
+    info = {"steps": k, "ms_per_step_incl_spin": round(dt * 1e3, 3), "models": dict(timer.models),
             "note": (f"HIP events around each launch on its stream, {k} steps of the eager twin "
                      "of the replayed native step run after the timed region"
                      if not eager else f"HIP events around each launch, {k} eager steps")}
@@ -414,15 +410,20 @@ REGION_KERNELS = {
 
 MEASURE_TRAFFIC_DETAIL = {}  # region -> per-kernel bytes of the last measure_traffic
 MEASURE_TRAFFIC_CHILD_M = {}  # region -> the profiled child's mean samples per step
+MEASURE_TRAFFIC_TRACE_US = {}  # region -> its kernels' replayed duration per step (child trace)
+MEASURE_STEP_TRACE_US = {}  # "step" -> every kernel's replayed duration per step (child trace)
 
 
 def measure_traffic(region, timeout=180):
-    """HBM bytes per launch of timed region `region`, measured now: two
-    rocprofv3 passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE, kernel-trace
-    only, each its own run, as MI355X_MICROARCH.md prescribes) over a short
-    child run of this same bench (3 + 3 steps, no extras).  FETCH_SIZE is
-    doubled (the gfx950 correction for wide reads; the guide leaves gathers
-    uncalibrated), both are KiB.  Returns (bytes or None, note)."""
+    """HBM bytes per launch of timed region `region`, measured now: rocprofv3
+    passes over a short child run of this same bench (graph-replayed steps, no
+    extras), each its own run as MI355X_MICROARCH.md prescribes: a plain
+    kernel trace (the replayed kernels' durations: MEASURE_TRAFFIC_TRACE_US),
+    --pmc FETCH_SIZE, --pmc WRITE_SIZE, --pmc TCC_HIT_sum + TCC_MISS_sum.
+    FETCH_SIZE is doubled (the gfx950 correction for wide reads; the guide
+    leaves gathers uncalibrated), both are KiB.  The child's samples per step
+    are recorded so bytes, time and traffic are compared at ONE workload.
+    Returns (bytes or None, note)."""
     import shutil
     import signal
     import subprocess
@@ -448,11 +449,16 @@ def measure_traffic(region, timeout=180):
     # miss split (TCC_HIT / TCC_MISS, 2 TCC counters), which says how much of
     # the fetch the region's requests caused versus re-read from L2
     child_m = []
-    for counters in (("FETCH_SIZE",), ("WRITE_SIZE",), ("TCC_HIT_sum", "TCC_MISS_sum")):
-        tag = counters[0]
+    trace_us = None
+    for counters in ((), ("FETCH_SIZE",), ("WRITE_SIZE",), ("TCC_HIT_sum", "TCC_MISS_sum")):
+        tag = counters[0] if counters else "TRACE"
         d = os.path.join(tmp, tag)
-        cmd = [rp, "--kernel-trace", "--pmc", *counters, "--output-format", "csv", "-d", d,
-               "-o", "run", "--"] + child
+        if counters:
+            cmd = [rp, "--kernel-trace", "--pmc", *counters, "--output-format", "csv", "-d", d,
+                   "-o", "run", "--"] + child
+        else:  # the replayed graph's kernel durations (no counters)
+            cmd = [rp, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d,
+                   "-o", "run", "--"] + child
         with open(os.path.join(tmp, tag + ".out"), "w") as out:
             proc = subprocess.Popen(cmd, stdout=out, stderr=subprocess.DEVNULL, env=env,
                                     start_new_session=True)
@@ -469,6 +475,34 @@ def measure_traffic(region, timeout=180):
             child_m.append(json.loads(line)["config"]["mean_samples_per_step"])
         except (IndexError, ValueError, KeyError):
             pass
+        if not counters:
+            durs = {}
+            for f in Path(d).rglob("*kernel_trace.csv"):
+                for r in csv.DictReader(open(f)):
+                    for i, alts in enumerate(pats):
+                        alts = (alts,) if isinstance(alts, str) else alts
+                        if any(a in r["Kernel_Name"] for a in alts):
+                            durs.setdefault(i, []).append(
+                                (int(r["Start_Timestamp"]),
+                                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+            if len(durs) != len(pats):
+                return None, "kernel trace: not every kernel of the region was traced"
+            # the last `keep` dispatches of each kernel (one per step)
+            trace_us = {i: sum(v for _, v in sorted(x)[-keep:]) / keep / 1e3
+                        for i, x in durs.items()}
+            # every kernel of the last `keep` steps (from the keep-th last step
+            # prologue on): the replayed step's kernel time
+            allk = []
+            for f in Path(d).rglob("*kernel_trace.csv"):
+                for r in csv.DictReader(open(f)):
+                    allk.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                                 r["Kernel_Name"]))
+            starts = sorted(t0 for t0, _, n in allk if "k_step_prologue" in n)
+            if len(starts) >= keep:
+                b0 = starts[-keep]
+                MEASURE_STEP_TRACE_US["step"] = sum(
+                    t1 - t0 for t0, t1, _ in allk if t0 >= b0) / keep / 1e3
+            continue
         sums = {}
         for f in Path(d).rglob("*counter_collection.csv"):
             for r in csv.DictReader(open(f)):
@@ -493,8 +527,10 @@ def measure_traffic(region, timeout=180):
         names[i]: {"fetch_x2": int(per["FETCH_SIZE"][i]), "write": int(per["WRITE_SIZE"][i]),
                    "l2_hit_rate": round(per["TCC_HIT_sum"][i] /
                                         max(1.0, per["TCC_HIT_sum"][i] + per["TCC_MISS_sum"][i]),
-                                        4)}
+                                        4),
+                   "replayed_us": round(trace_us[i], 2)}
         for i in range(len(pats))}
+    MEASURE_TRAFFIC_TRACE_US[region] = sum(trace_us.values())
     return int(total), (
         "measured in this run: rocprofv3 --pmc passes (separate runs: FETCH_SIZE, WRITE_SIZE, "
         "TCC_HIT_sum + TCC_MISS_sum) of a 10 + 3-step child bench, the last 3 dispatches of each "
@@ -656,27 +692,60 @@ def main():
         traffic, note = (None, "skipped (--no-traffic or N > 1)")
         if world == 1 and not args.no_traffic:
             traffic, note = measure_traffic(dom)
-        result["roofline"] = {
+        roof = {
             "kernel": dom, "bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
             "traffic": traffic, "traffic_source": note,
             "traffic_by_kernel": MEASURE_TRAFFIC_DETAIL.get(dom),
-            "traffic_child_mean_samples": MEASURE_TRAFFIC_CHILD_M.get(dom),
             "avg_us": kd["avg_us"],
             "bytes_per_launch": kd["bytes_per_launch"],
             "timing": timing["note"] if timing else None}
-        if dom == "grid_encode_backward":
-            # the binned backward's real ceiling: one f64 LDS add per (sample,
-            # level, corner, channel) before the walk's in-register merging
-            ops = samples * 16 * 8 * 2
-            rate = ops / (kd["avg_us"] * 1e-6)
-            result["lds_atomic_roofline"] = {
-                "achieved": round(rate / 1e12, 4), "peak": round(LDS_F64_ATOMIC_PEAK / 1e12, 4),
-                "unit": "T f64 LDS adds/s", "frac": round(rate / LDS_F64_ATOMIC_PEAK, 4),
-                "ops_per_launch": int(ops)}
+        cm, tus = MEASURE_TRAFFIC_CHILD_M.get(dom), MEASURE_TRAFFIC_TRACE_US.get(dom)
+        model = (timing or {}).get("models", {}).get(dom)
+        if cm and tus and model:
+            # ONE workload for bytes, time and traffic: the profiled child's
+            # graph-replayed steps (its samples per step cm), its kernels'
+            # rocprofv3 durations, its PMC bytes; the eager-twin event figures
+            # of this process stay beside them
+            base, per_row, live = model
+            cb = base + (per_row * cm if live else 0)
+            gbs = cb / (tus * 1e-6) / 1e9
+            roof.update({
+                "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                "avg_us": round(tus, 2), "bytes_per_launch": int(cb),
+                "samples_per_step": round(cm, 1),
+                "algorithmic_bytes_per_sample": round(cb / cm, 2),
+                "traffic_per_sample": round(traffic / cm, 2) if traffic else None,
+                "traffic_over_algorithmic": round(traffic / cb, 3) if traffic else None,
+                "timing": ("rocprofv3 kernel trace of the child's graph-replayed steps "
+                           "(last 3 dispatches of each region kernel), bytes from the "
+                           "region's model at the child's samples per step"),
+                "eager_twin": {"avg_us": kd["avg_us"], "bytes_per_launch": kd["bytes_per_launch"],
+                               "achieved": kd["achieved_GBs"],
+                               "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
+                               "samples_per_step": round(samples, 1),
+                               "timing": timing["note"] if timing else None}})
+        result["roofline"] = roof
+
         result["kernels"] = kernels
         result["step_roofline"] = step_roofline(kernels, timing["steps"], samples,
                                                 rays_per_step, trainer)
+        st_us = MEASURE_STEP_TRACE_US.get("step")
+        if cm and st_us:
+            # the same figure for the profiled child's replayed steps: every
+            # region's byte model at the child's samples per step over the
+            # rocprofv3 time of all kernels of a step
+            models = timing.get("models", {})
+            per_step = {k: v["launches"] / timing["steps"] for k, v in kernels.items()}
+            sb = sum(per_step.get(k, 1.0) * (b + (pr * cm if lv else 0))
+                     for k, (b, pr, lv) in models.items() if k in kernels)
+            g = sb / (st_us * 1e-6) / 1e9
+            result["step_roofline"]["replayed"] = {
+                "samples_per_step": round(cm, 1), "bytes_per_step": int(sb),
+                "kernel_us_per_step": round(st_us, 2), "achieved": round(g, 1),
+                "frac": round(g / HBM_PEAK_GBS, 4),
+                "note": "rocprofv3 kernel trace of the child's last 3 graph-replayed steps "
+                        "(every kernel from the step prologue on; no density refresh among them)"}
         result["kernel_timing"] = timing
     if world == 1 and not args.no_kernel_timing:
         result["field_mlp"] = field_mlp_report(trainer)

@@ -202,8 +202,13 @@ def exported_symbols() -> list[str]:
 class _KernelTimer:
     def __init__(self):
         self.records = []  # (name, start_event, end_event, bytes or callable -> bytes)
+        # name -> (fixed bytes, bytes per live row, live-row based?): the
+        # region's byte model, to evaluate it at another run's row count
+        self.models = {}
 
     def region(self, name, nbytes, live=None, per_row=0):
+        if not callable(nbytes):
+            self.models[name] = (nbytes, per_row, live is not None)
         return _Region(self, name, nbytes, live, per_row)
 
 

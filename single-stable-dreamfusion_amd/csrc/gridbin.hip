@@ -393,17 +393,29 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                 if (!in) continue;
             }
             const uint16_t id = (uint16_t)(s - tile * kTile);
+            // stencil groups: point 1 + 2 axis + k moves only along `axis`, so
+            // when its other two mapped coordinates equal the sample's (the
+            // sample inside the bound: the clamp is the identity) its cell
+            // differs from the sample's along that axis only, and its tiled
+            // index is the sample's plus (c' - c) times the axis stride (one
+            // floor per point instead of three; a z move is invisible at the
+            // z-dropped levels)
+            bool incr = false;
+            if constexpr (GROUP == 7) {
+                incr = in == 0x7Fu;
+#pragma unroll
+                for (uint32_t a = 1; a < 7; ++a) {
+                    const uint32_t ax = (a - 1u) >> 1;
+#pragma unroll
+                    for (uint32_t d = 0; d < 3; ++d)
+                        if (d != ax) incr = incr && xg[a][d] == xg[0][d];
+                }
+            }
             for (uint32_t l = 0; l < bi.L; ++l) {
                 const float sc = fl.scale[l];
                 const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
                 uint64_t mask = 0;
-#pragma unroll
-                for (uint32_t a = 0; a < GROUP; ++a) {
-                    if (!((in >> a) & 1u)) continue;
-                    const uint32_t c0 = (uint32_t)floorf(fmaf(xg[a][0], sc, half));
-                    const uint32_t c1 = (uint32_t)floorf(fmaf(xg[a][1], sc, half));
-                    const uint32_t c2 = (uint32_t)floorf(fmaf(xg[a][2], sc, half));
-                    const uint32_t i0 = c0 + c1 * m1 + c2 * m2;
+                auto pairs = [&](uint32_t i0) {
 #pragma unroll
                     for (uint32_t p = 0; p < 4; ++p) {  // x-neighbour pairs {0,1} + {0, m1, m2, m1+m2}
                         if (p >= (1u << (lead - 1u))) break;  // uniform
@@ -412,6 +424,30 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                         mask |= 1ull << (r >> shift);
                         if ((r & smask) == smask) mask |= 1ull << (((r + 1u) & wm) >> shift);
                     }
+                };
+                if (GROUP == 7 && incr) {
+                    uint32_t c[3];
+#pragma unroll
+                    for (uint32_t d = 0; d < 3; ++d) c[d] = (uint32_t)floorf(fmaf(xg[0][d], sc, half));
+                    const uint32_t i0 = c[0] + c[1] * m1 + c[2] * m2;
+                    pairs(i0);
+#pragma unroll
+                    for (uint32_t a = 1; a < 7; ++a) {
+                        const uint32_t ax = (a - 1u) >> 1;
+                        const uint32_t stride = ax == 0 ? 1u : (ax == 1 ? m1 : m2);
+                        if (stride == 0) continue;  // uniform: a dim the index drops
+                        const uint32_t ca = (uint32_t)floorf(fmaf(xg[a][ax], sc, half));
+                        if (ca != c[ax]) pairs(i0 + (ca - c[ax]) * stride);
+                    }
+                } else {
+#pragma unroll
+                for (uint32_t a = 0; a < GROUP; ++a) {
+                    if (!((in >> a) & 1u)) continue;
+                    const uint32_t c0 = (uint32_t)floorf(fmaf(xg[a][0], sc, half));
+                    const uint32_t c1 = (uint32_t)floorf(fmaf(xg[a][1], sc, half));
+                    const uint32_t c2 = (uint32_t)floorf(fmaf(xg[a][2], sc, half));
+                    pairs(c0 + c1 * m1 + c2 * m2);
+                }
                 }
                 const uint32_t b0 = fl.bin0[l];
                 while (mask) {
@@ -791,10 +827,12 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
 //   * the part's tiles (part, part + P, ...) are taken in chunks of up to 1024;
 //     each thread loads one tile's count and a workgroup scan lays the chunk's
 //     segments end to end (E entries);
-//   * the E entries are cut into 1024 equal runs, one per thread (lanes of a
-//     wave take runs 16 apart, so one LDS instruction's lanes flush different
-//     rays); a run may cross tile segments (the cursor moves to the next
-//     segment in LDS, no global round trip);
+//   * the E entries are cut into 1024 equal runs, one per thread: wave w
+//     takes the w-th sixteenth (its lanes stay on neighbouring samples, which
+//     hit in L1: equal runs spread over the whole part cost 1.7x per entry),
+//     lanes take its runs bit-reversed (one LDS instruction's lanes flush
+//     different rays); a run may cross tile segments (the cursor moves to the
+//     next non-empty segment in LDS, no global round trip);
 //   * a lane's next batch of ids is loaded before the current batch's
 //     positions / gradients are used.
 //
@@ -816,6 +854,21 @@ struct FlatCell {
     bool have;
 };
 
+// Cell and fractional position of a point's coordinate (gridencoder.cu:146-154).
+__device__ __forceinline__ void flat_locate1(float x, float sc, float half, float &fr,
+                                             uint32_t &ci) {
+    const float p = fmaf(x, sc, half);
+    const float fl = floorf(p);
+    fr = p - fl;
+    ci = (uint32_t)fl;
+}
+
+template <uint32_t C, uint32_t LEAD>
+__device__ __forceinline__ void flat_take_at(FlatCell<C> &st, double *acc, uint32_t srows,
+                                             uint32_t lo, uint32_t n, uint32_t m1, uint32_t m2,
+                                             uint32_t wm, const float (&fr)[3],
+                                             const uint32_t (&ci)[3], const float (&g)[C]);
+
 // One point (x in [0, 1]^3) with gradient g into the lane's current cell.
 template <uint32_t C, uint32_t LEAD>
 __device__ __forceinline__ void flat_take(FlatCell<C> &st, double *acc, uint32_t srows,
@@ -825,12 +878,16 @@ __device__ __forceinline__ void flat_take(FlatCell<C> &st, double *acc, uint32_t
     float fr[3];
     uint32_t ci[3];
 #pragma unroll
-    for (uint32_t d = 0; d < 3; ++d) {
-        const float p = fmaf(x[d], sc, half);
-        const float fl = floorf(p);
-        fr[d] = p - fl;
-        ci[d] = (uint32_t)fl;
-    }
+    for (uint32_t d = 0; d < 3; ++d) flat_locate1(x[d], sc, half, fr[d], ci[d]);
+    flat_take_at<C, LEAD>(st, acc, srows, lo, n, m1, m2, wm, fr, ci, g);
+}
+
+// The point located at (fr, ci) with gradient g into the lane's current cell.
+template <uint32_t C, uint32_t LEAD>
+__device__ __forceinline__ void flat_take_at(FlatCell<C> &st, double *acc, uint32_t srows,
+                                             uint32_t lo, uint32_t n, uint32_t m1, uint32_t m2,
+                                             uint32_t wm, const float (&fr)[3],
+                                             const uint32_t (&ci)[3], const float (&g)[C]) {
     uint32_t i0 = ci[0];
     if (LEAD > 1) i0 += ci[1] * m1;
     if (LEAD > 2) i0 += ci[2] * m2;
@@ -913,7 +970,109 @@ __device__ __forceinline__ void load_group_grads(const grad_t *__restrict__ p,
     }
 }
 
-template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RUN>
+// One entry: sample position xr (raw) and its GROUP gradient rows g, taken
+// into the lane's cell state (GROUP 7: the finite-difference stencil).
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD>
+__device__ __forceinline__ void flat_entry(FlatCell<C> &cell, double *acc, uint32_t srows,
+                                           uint32_t lo, uint32_t n, float sc, float half,
+                                           uint32_t m1, uint32_t m2, uint32_t wm,
+                                           const SliceDyn &dyn, float inv, const Stencil &st,
+                                           const float (&xr)[3], const float (&g)[GROUP][C]) {
+    if constexpr (GROUP == 1) {
+        float x[3];
+#pragma unroll
+        for (uint32_t d = 0; d < 3; ++d)
+            x[d] = ge::dyn_map_t<POW2>(dyn, inv, xr[d]);
+        flat_take<C, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2, wm, x,
+                           g[0]);
+    } else {
+        // the sample inside the bound (the clamp of the
+        // unmoved coordinates is the identity): point
+        // 1 + 2 ax + k differs from the sample along ax
+        // only, so only that coordinate is located again
+        bool inb = true;
+#pragma unroll
+        for (uint32_t d = 0; d < 3; ++d)
+            inb = inb && xr[d] >= -st.bound && xr[d] <= st.bound;
+        float x0[3];
+#pragma unroll
+        for (uint32_t d = 0; d < 3; ++d) {
+            x0[d] = ge::dyn_map_t<POW2>(dyn, inv, xr[d]);
+            inb = inb && !(x0[d] < 0.0f) && !(x0[d] > 1.0f);
+        }
+        if (inb) {
+            float fr0[3];
+            uint32_t ci0[3];
+#pragma unroll
+            for (uint32_t d = 0; d < 3; ++d)
+                flat_locate1(x0[d], sc, half, fr0[d], ci0[d]);
+            flat_take_at<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm, fr0,
+                                  ci0, g[0]);
+#pragma unroll
+            for (uint32_t a2 = 1; a2 < GROUP; ++a2) {
+                const uint32_t ax = (a2 - 1u) >> 1;
+                const float off = ((a2 - 1u) & 1u) ? -st.eps : st.eps;
+                const float v = fminf(fmaxf(xr[ax] + off, -st.bound),
+                                      st.bound);
+                float fr[3] = {fr0[0], fr0[1], fr0[2]};
+                uint32_t ci[3] = {ci0[0], ci0[1], ci0[2]};
+                flat_locate1(ge::dyn_map_t<POW2>(dyn, inv, v), sc, half,
+                             fr[ax], ci[ax]);
+                flat_take_at<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm,
+                                      fr, ci, g[a2]);
+            }
+        } else {  // rare (a sample on the bound): the general form
+#pragma unroll
+            for (uint32_t a2 = 0; a2 < GROUP; ++a2) {
+                float p[3], x[3];
+                group_point<GROUP>(xr, a2, st, p);
+                bool ok = true;
+#pragma unroll
+                for (uint32_t d = 0; d < 3; ++d) {
+                    x[d] = ge::dyn_map_t<POW2>(dyn, inv, p[d]);
+                    ok = ok && !(x[d] < 0.0f) && !(x[d] > 1.0f);
+                }
+                if (ok)
+                    flat_take<C, LEAD>(cell, acc, srows, lo, n, sc, half, m1,
+                                       m2, wm, x, g[a2]);
+            }
+        }
+    }
+}
+
+// A lane's entries [ea, eb) of one piece of a tile segment (ids at seg),
+// RB loads in flight per batch (clamped ids: every load is issued before the
+// first use).
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RB>
+__device__ __forceinline__ void flat_piece(FlatCell<C> &cell, const grad_t *__restrict__ gl,
+                                           const float *__restrict__ inputs,
+                                           const uint16_t *__restrict__ seg, uint32_t tbase,
+                                           uint32_t ea, uint32_t eb, double *acc, uint32_t srows,
+                                           uint32_t lo, uint32_t n, float sc, float half,
+                                           uint32_t m1, uint32_t m2, uint32_t wm,
+                                           const SliceDyn &dyn, float inv, const Stencil &st) {
+    for (uint32_t x = ea; x < eb; x += RB) {
+        const uint32_t m = min(eb - x, RB);
+        uint32_t sid[RB];
+#pragma unroll
+        for (uint32_t i = 0; i < RB; ++i) sid[i] = tbase + seg[x + min(i, m - 1)];
+        float xs[RB][3];
+        float gs[RB][GROUP][C];
+#pragma unroll
+        for (uint32_t i = 0; i < RB; ++i) {
+            load_pos3<3>(inputs, sid[i], xs[i]);
+            load_group_grads<grad_t, C, GROUP>(gl + (size_t)sid[i] * GROUP * C, gs[i]);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < RB; ++i)
+            if (i < m)
+                flat_entry<grad_t, C, POW2, GROUP, LEAD>(cell, acc, srows, lo, n, sc, half, m1,
+                                                         m2, wm, dyn, inv, st, xs[i], gs[i]);
+    }
+}
+
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RUN,
+          uint32_t WMODE>
 __device__ __forceinline__ void flat_walk_level(
     const grad_t *__restrict__ gl, const float *__restrict__ inputs, const uint32_t *counts,
     const uint16_t *__restrict__ entries, double *acc, uint32_t *pre, uint32_t *wsum,
@@ -948,8 +1107,55 @@ __device__ __forceinline__ void flat_walk_level(
         }
         __syncthreads();
         const uint32_t E = pre[nc];
+        if constexpr (WMODE == 2) {
+            // per-wave pieces: wave w takes entries [E w / waves, E (w+1) / waves)
+            // and walks them segment piece by segment piece, the 64 lanes of
+            // the wave on one piece at a time (runs of ceil(piece / 64),
+            // bit-reversed), as k_walk does per whole segment
+            const uint32_t w0 = (uint32_t)((uint64_t)E * wave / waves);
+            const uint32_t w1 = (uint32_t)((uint64_t)E * (wave + 1) / waves);
+            if (w0 < w1) {
+                uint32_t a = 0, z = nc;  // pre[a] <= w0 < pre[z]
+                while (z - a > 1) {
+                    const uint32_t mid = (a + z) >> 1;
+                    if (pre[mid] <= w0) a = mid;
+                    else z = mid;
+                }
+                const uint32_t rl = __builtin_bitreverse32(lane) >> 26;
+                uint32_t ti = a, e = w0;
+                while (e < w1) {
+                    const uint32_t pe = min(pre[ti + 1], w1);
+                    const uint32_t cnt = pe - e;
+                    const uint32_t t = part + (cb + ti) * P;
+                    const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile + (e - pre[ti]);
+                    const uint32_t Qp = (cnt + 63u) >> 6;
+                    const uint32_t ea = min(rl * Qp, cnt), eb = min(ea + Qp, cnt);
+                    if (GROUP > 1 || Qp <= 1)
+                        flat_piece<grad_t, C, POW2, GROUP, LEAD, 1>(
+                            cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                            half, m1, m2, wm, dyn, inv, st);
+                    else if (Qp <= 4)
+                        flat_piece<grad_t, C, POW2, GROUP, LEAD, 4>(
+                            cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                            half, m1, m2, wm, dyn, inv, st);
+                    else
+                        flat_piece<grad_t, C, POW2, GROUP, LEAD, 8>(
+                            cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                            half, m1, m2, wm, dyn, inv, st);
+                    e = pe;
+                    ++ti;
+                    while (e < w1 && pre[ti + 1] == e) ++ti;  // empty segments
+                }
+            }
+            __syncthreads();  // pre / wsum are rewritten by the next chunk
+            continue;
+        }
         const uint32_t Q = ceil_div(E, nthr);
-        const uint32_t r = lane * waves + wave;  // lanes of a wave: runs `waves` apart
+        // wave w takes the w-th 1/waves of the chunk, so its lanes stay on
+        // neighbouring samples (one or two tile segments: positions and
+        // gradients hit in L1); inside it lane -> run is bit-reversed, so the
+        // lanes of one LDS instruction flush different rays
+        const uint32_t r = wave * 64u + (__builtin_bitreverse32(lane) >> 26);
         uint32_t e = min(r * Q, E);
         const uint32_t e1 = min(e + Q, E);
         if (e < e1) {
@@ -975,9 +1181,14 @@ __device__ __forceinline__ void flat_walk_level(
                 uint32_t ne = e + m, nslot = slot + m, nti = ti, ntend = tend, nt2 = t;
                 const uint16_t *nseg = seg;
                 if (ne == ntend && ne < e1) {
-                    ++nti;
+                    // the next non-empty segment (ne < e1 <= E: one exists); an
+                    // empty one would make a batch of zero entries whose clamped
+                    // id loads read slots never written
+                    do {
+                        ++nti;
+                        ntend = pre[nti + 1];
+                    } while (ntend == ne);
                     nslot = 0;
-                    ntend = pre[nti + 1];
                     nt2 = part + (cb + nti) * P;
                     nseg = entries + ((size_t)nt2 * nb + b) * kTile;
                 }
@@ -999,29 +1210,9 @@ __device__ __forceinline__ void flat_walk_level(
 #pragma unroll
                 for (uint32_t i = 0; i < RUN; ++i) {
                     if (i < m) {
-                        if constexpr (GROUP == 1) {
-                            float x[3];
-#pragma unroll
-                            for (uint32_t d = 0; d < 3; ++d)
-                                x[d] = ge::dyn_map_t<POW2>(dyn, inv, xs[i][d]);
-                            flat_take<C, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2, wm, x,
-                                               gs[i][0]);
-                        } else {
-#pragma unroll
-                            for (uint32_t a2 = 0; a2 < GROUP; ++a2) {
-                                float p[3], x[3];
-                                group_point<GROUP>(xs[i], a2, st, p);
-                                bool ok = true;
-#pragma unroll
-                                for (uint32_t d = 0; d < 3; ++d) {
-                                    x[d] = ge::dyn_map_t<POW2>(dyn, inv, p[d]);
-                                    ok = ok && !(x[d] < 0.0f) && !(x[d] > 1.0f);
-                                }
-                                if (ok)
-                                    flat_take<C, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2,
-                                                       wm, x, gs[i][a2]);
-                            }
-                        }
+                        flat_entry<grad_t, C, POW2, GROUP, LEAD>(cell, acc, srows, lo, n, sc,
+                                                                 half, m1, m2, wm, dyn, inv,
+                                                                 st, xs[i], gs[i]);
                     }
                 }
                 if (!more) break;
@@ -1041,7 +1232,7 @@ __device__ __forceinline__ void flat_walk_level(
     flat_flush<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm);
 }
 
-template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP>
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t WMODE>
 __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ grad,  // [L, GROUP B, C]
                                                     const float *__restrict__ inputs,
                                                     FastLevels fl, BinInfo bi, int align_corners,
@@ -1107,7 +1298,7 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     // batch's ids): 6 keeps the f16 walk within 128 VGPRs (8 spilled)
     constexpr uint32_t RUN = GROUP > 1 ? 2u : (uint32_t)DFHIP_WALK_RUN;
 #define DFHIP_FLAT(LD)                                                                         \
-    flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN>(gl, inputs, counts, entries, acc, pre,    \
+    flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN, WMODE>(gl, inputs, counts, entries, acc, pre,    \
                                                      wsum, nb, b, part, P, ntiles, srows, lo, \
                                                      n, sc, half, m1, m2, wm, dyn, inv, st)
     if (lead >= 3) DFHIP_FLAT(3);
@@ -1182,13 +1373,14 @@ static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t 
 
 // The flat walk (k_walk_flat) for mask-form layouts; DFHIP_WALK_FLAT=0 keeps
 // the per-segment k_walk (A/B runs, tests).
-static bool flat_walk_enabled() {
+static int flat_walk_mode() {
     static int on = -1;
     if (on < 0) {
         const char *e = getenv("DFHIP_WALK_FLAT");
-        on = e ? (atoi(e) != 0) : 0;
+        on = e ? atoi(e) : 0;
+        if (on < 0 || on > 2) on = 0;
     }
-    return on != 0;
+    return on;
 }
 
 template <typename grad_t, uint32_t C, uint32_t GROUP = 1>
@@ -1199,12 +1391,15 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
                         const FastLevels *fl, Stencil st = Stencil{0.0f, 0.0f}) {
     const bool pow2 = ge::dyn_pow2(dyn.bound);
     const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-    if constexpr (C == 2) if (fl && flat_walk_enabled()) {
+    if constexpr (C == 2) if (fl && flat_walk_mode()) {
         typedef void (*flat_fn)(const grad_t *, const float *, FastLevels, BinInfo, int,
                                 SliceDyn, float, uint32_t, uint32_t *, const uint16_t *,
                                 float *, Stencil);
-        const flat_fn kf = pow2 ? k_walk_flat<grad_t, C, true, GROUP>
-                                : k_walk_flat<grad_t, C, false, GROUP>;
+        const int wmode = flat_walk_mode();
+        const flat_fn kf = wmode == 2 ? (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 2>
+                                              : k_walk_flat<grad_t, C, false, GROUP, 2>)
+                                      : (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 1>
+                                              : k_walk_flat<grad_t, C, false, GROUP, 1>);
         static bool fattr[2] = {false, false};
         if (!fattr[pow2]) {
             (void)hipFuncSetAttribute((const void *)kf,
