@@ -414,7 +414,7 @@ MEASURE_TRAFFIC_TRACE_US = {}  # region -> its kernels' replayed duration per st
 MEASURE_STEP_TRACE_US = {}  # "step" -> every kernel's replayed duration per step (child trace)
 
 
-def measure_traffic(region, timeout=180):
+def measure_traffic(region, timeout=180, warmup=10):
     """HBM bytes per launch of timed region `region`, measured now: rocprofv3
     passes over a short child run of this same bench (graph-replayed steps, no
     extras), each its own run as MI355X_MICROARCH.md prescribes: a plain
@@ -432,11 +432,13 @@ def measure_traffic(region, timeout=180):
     rp = shutil.which("rocprofv3")
     if rp is None:
         return None, "rocprofv3 not on PATH"
-    # the child warms up as long as the timed run does (the occupancy grid, and
-    # with it M, settles over the first refreshes); only its last `keep`
-    # dispatches of each kernel are averaged
+    # the child runs as many steps as this process's warm-up + timed region
+    # (the occupancy grid, and with it M, grows over the first hundred
+    # steps): its last `keep` steps, the ones profiled, sit where the timed
+    # region ends
     keep = 3
-    child = [sys.executable, str(Path(__file__).resolve()), "--steps", str(keep), "--warmup", "10",
+    child = [sys.executable, str(Path(__file__).resolve()), "--steps", str(keep), "--warmup",
+             str(max(1, warmup)),
              "--no-cpu-baseline", "--no-kernel-timing", "--no-alt-backward", "--no-shading",
              "--no-infer", "--no-traffic", "--no-c5"]
     env = {k: v for k, v in os.environ.items()
@@ -691,7 +693,7 @@ def main():
         kd = kernels[dom]
         traffic, note = (None, "skipped (--no-traffic or N > 1)")
         if world == 1 and not args.no_traffic:
-            traffic, note = measure_traffic(dom)
+            traffic, note = measure_traffic(dom, warmup=args.warmup + args.steps - 3)
         roof = {
             "kernel": dom, "bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),

@@ -145,9 +145,15 @@ __device__ __forceinline__ bf4 relu_bf4(f4 a) {
 }
 
 // Per-tile activations of one layer: [tile][reg] as scalars (f16) or as
-// packed vectors (bf16); both index as t[tile][reg].
-template <typename E> struct Tiles { typedef E type[4][4]; };
-template <> struct Tiles<bf16_t> { typedef bf4 type[4]; };
+// packed vectors (bf16; and f16 with P, the backward: one VGPR per two
+// values instead of one per value); all index as t[tile][reg].
+template <typename E, bool P = false> struct TilesT { typedef E type[4][4]; };
+template <typename E> struct TilesT<E, true> { typedef typename Elem<E>::v4 type[4]; };
+template <> struct TilesT<bf16_t, false> { typedef bf4 type[4]; };
+template <typename E> struct Tiles : TilesT<E, false> {};
+__device__ __forceinline__ half8 b_from_tiles(const half4 (&v)[4], int s) {
+    return __builtin_shufflevector(v[2 * s], v[2 * s + 1], 0, 1, 2, 3, 4, 5, 6, 7);
+}
 __device__ __forceinline__ f4 bias4(const float *b, int row0) {
     return f4{b[row0], b[row0 + 1], b[row0 + 2], b[row0 + 3]};
 }
@@ -155,16 +161,16 @@ __device__ __forceinline__ f4 bias4(const float *b, int row0) {
 // One 16-sample tile through the MLP.  xb: B operand of the encoder features
 // (lane: sample c, features 8h..8h+7).  Outputs the post-ReLU activations (T)
 // of both hidden layers and the f32 accumulators of the output layer.
-template <typename E>
+template <typename E, bool P = false>
 struct FwdG {
-    typename Tiles<E>::type a1, a2;  // [tile][reg]: neuron 16 t + 4 h + r of sample c
-    f4 o;                            // rows 4h + r (only h == 0 valid: outputs 0..3)
+    typename TilesT<E, P>::type a1, a2;  // [tile][reg]: neuron 16 t + 4 h + r of sample c
+    f4 o;                                // rows 4h + r (only h == 0 valid: outputs 0..3)
 };
 typedef FwdG<half_t> Fwd;
 
-template <typename E>
+template <typename E, bool P>
 __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem<E>::v8 xb, int c,
-                                             int h, FwdG<E> &F) {
+                                             int h, FwdG<E, P> &F) {
     constexpr bool kBf = std::is_same<E, bf16_t>::value;
     f4 acc[4];
 #pragma unroll

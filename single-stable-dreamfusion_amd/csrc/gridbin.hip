@@ -57,6 +57,7 @@ struct BinInfo {
     uint32_t L, nbins, shift, tcap;      // tcap: tiles of the capacity (counts row stride)
     uint32_t G;                          // walk workgroups
     uint32_t lane_perm;                  // walk: bit-reversed lane -> run map (1) or identity
+    uint32_t xcd_map;                    // walk: XCD-grouped logical slots (xcd_slot) or identity
     uint32_t o_totals, o_plan;           // word offsets into `counts` (layout below)
     uint32_t bin0[ge::kMaxLevels + 1];   // first bin of level l (bin0[L] = nbins)
     uint32_t base[ge::kMaxLevels];       // first row of level l
@@ -119,6 +120,12 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
             perm = e ? (atoi(e) != 0) : 1;
         }
         bi.lane_perm = (uint32_t)perm;
+        static int xmap = -1;  // DFHIP_WALK_XCD=0: identity slots (A/B)
+        if (xmap < 0) {
+            const char *e = getenv("DFHIP_WALK_XCD");
+            xmap = e ? (atoi(e) != 0) : 1;
+        }
+        bi.xcd_map = (uint32_t)xmap;
     }
     uint32_t nb = 0;
     for (uint32_t l = 0; l < L; ++l) {
@@ -145,6 +152,18 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
 }
 static uint64_t counts_words(const BinInfo &bi) {
     return ((uint64_t)bi.o_plan + 2ull * bi.nbins + 3ull) & ~3ull;
+}
+
+// Logical walk slot of workgroup b: the G workgroups are dealt round-robin
+// over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch: blocks b and b + 8
+// share one; speed only, never correctness), so consecutive logical slots —
+// the parts of one bin, and the bins of one level — are given to blocks of
+// one XCD: that XCD's L2 then holds its levels' feature gradients instead of
+// all eight L2s pulling every level's.  A bijection on [0, G).
+__device__ __forceinline__ uint32_t xcd_slot(uint32_t b, uint32_t G) {
+    const uint32_t x = b & 7u, i = b >> 3;
+    const uint32_t q = G >> 3, r = G & 7u;  // XCD x holds q + (x < r) blocks
+    return x * q + min(x, r) + i;
 }
 
 __device__ __forceinline__ uint32_t bin_total(const uint32_t *__restrict__ totals, uint32_t b) {
@@ -623,7 +642,8 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     __shared__ uint32_t n_seen;
     uint64_t tr0 = 0;
     if (bi.trace) tr0 = wall_clock64();
-    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
+    const uint32_t nb = bi.nbins, G = bi.G;
+    const uint32_t slot = bi.xcd_map ? xcd_slot(blockIdx.x, G) : blockIdx.x;
     const uint32_t *totals = counts + bi.o_totals;
     if (threadIdx.x < 64) {  // plan (wave 0): this workgroup's bin b and part j of P_b
         const uint32_t ln = threadIdx.x;
@@ -913,6 +933,12 @@ __device__ __forceinline__ void flat_take_at(FlatCell<C> &st, double *acc, uint3
         }
         st.i0 = i0;
         st.have = true;
+        // zeroed on the (divergent) new-cell path, then one fma per value for
+        // every lane (a select between fma and mul costs two more per value)
+#pragma unroll
+        for (uint32_t k = 0; k < (1u << LEAD); ++k)
+#pragma unroll
+            for (uint32_t ch = 0; ch < C; ++ch) st.cw[k][ch] = 0.0;
     }
 #pragma unroll
     for (uint32_t k = 0; k < (1u << LEAD); ++k) {
@@ -921,8 +947,7 @@ __device__ __forceinline__ void flat_take_at(FlatCell<C> &st, double *acc, uint3
         for (uint32_t d = 0; d < LEAD; ++d) w *= (k & (1u << d)) ? fr[d] : 1.0f - fr[d];
         const double wd = (double)w;
 #pragma unroll
-        for (uint32_t ch = 0; ch < C; ++ch)
-            st.cw[k][ch] = same ? fma(wd, gd[ch], st.cw[k][ch]) : wd * gd[ch];
+        for (uint32_t ch = 0; ch < C; ++ch) st.cw[k][ch] = fma(wd, gd[ch], st.cw[k][ch]);
     }
 }
 
@@ -1244,7 +1269,8 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     __shared__ uint32_t pre[kChunkTiles + 1];
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t sh_b, sh_j, sh_p;
-    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
+    const uint32_t nb = bi.nbins, G = bi.G;
+    const uint32_t slot = bi.xcd_map ? xcd_slot(blockIdx.x, G) : blockIdx.x;
     const uint32_t *totals = counts + bi.o_totals;
     if (threadIdx.x < 64) {  // plan (wave 0), as k_walk
         const uint32_t ln = threadIdx.x;
@@ -1371,16 +1397,21 @@ static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t 
     return mode == 0 ? 0 : kModeAny;  // only the mask form is specialised
 }
 
-// The flat walk (k_walk_flat) for mask-form layouts; DFHIP_WALK_FLAT=0 keeps
-// the per-segment k_walk (A/B runs, tests).
-static int flat_walk_mode() {
-    static int on = -1;
-    if (on < 0) {
+// Walk form for mask-form layouts (DFHIP_WALK_FLAT: 0 the per-segment
+// k_walk, 1 the flat k_walk_flat, 2 its per-wave pieces; A/B runs, tests).
+// Default: flat for stencil groups (textureless step, rocprof: walk 1307 ->
+// 1051 us), per-segment for single samples (albedo step: 189 us against 197
+// per-wave pieces and 269 flat — one entry's work is too short to pay for
+// lanes spread over a part's tiles).
+static int g_walk_mode = -2;  // -1: default per group; set by dfhip_debug_walk_mode (tests)
+static int flat_walk_mode(uint32_t group) {
+    if (g_walk_mode == -2) {
         const char *e = getenv("DFHIP_WALK_FLAT");
-        on = e ? atoi(e) : 0;
-        if (on < 0 || on > 2) on = 0;
+        g_walk_mode = e ? atoi(e) : -1;
+        if (g_walk_mode < -1 || g_walk_mode > 2) g_walk_mode = -1;
     }
-    return on;
+    if (g_walk_mode >= 0) return g_walk_mode;
+    return group > 1 ? 1 : 0;
 }
 
 template <typename grad_t, uint32_t C, uint32_t GROUP = 1>
@@ -1391,21 +1422,21 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
                         const FastLevels *fl, Stencil st = Stencil{0.0f, 0.0f}) {
     const bool pow2 = ge::dyn_pow2(dyn.bound);
     const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-    if constexpr (C == 2) if (fl && flat_walk_mode()) {
+    if constexpr (C == 2) if (fl && flat_walk_mode(GROUP)) {
         typedef void (*flat_fn)(const grad_t *, const float *, FastLevels, BinInfo, int,
                                 SliceDyn, float, uint32_t, uint32_t *, const uint16_t *,
                                 float *, Stencil);
-        const int wmode = flat_walk_mode();
+        const int wmode = flat_walk_mode(GROUP);
         const flat_fn kf = wmode == 2 ? (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 2>
                                               : k_walk_flat<grad_t, C, false, GROUP, 2>)
                                       : (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 1>
                                               : k_walk_flat<grad_t, C, false, GROUP, 1>);
-        static bool fattr[2] = {false, false};
-        if (!fattr[pow2]) {
+        static bool fattr[3][2] = {{false, false}, {false, false}, {false, false}};
+        if (!fattr[wmode][pow2]) {
             (void)hipFuncSetAttribute((const void *)kf,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kSliceBytes);
-            fattr[pow2] = true;
+            fattr[wmode][pow2] = true;
         }
         kf<<<bi.G, 1024, lds, s>>>(grad, inputs, *fl, bi, align, dyn, inv, B, counts, entries,
                                    partial, st);
@@ -1447,6 +1478,17 @@ using namespace dfhip;
 // where it applies (1, default).  Used by tests / A-B tools only.
 extern "C" int dfhip_debug_fast_bin(int on) {
     gb::g_fast_bin = on != 0;
+    return DFHIP_OK;
+}
+
+// Debug: the walk form for mask-form layouts (0 per segment, 1 flat, 2 flat
+// per-wave pieces; -1 the default per group).  Used by tests / A-B tools only.
+extern "C" int dfhip_debug_walk_mode(int mode) {
+    if (mode < -1 || mode > 2) {
+        set_error("debug_walk_mode: mode must be -1, 0, 1 or 2 (got %d)", mode);
+        return DFHIP_EINVAL;
+    }
+    gb::g_walk_mode = mode;
     return DFHIP_OK;
 }
 

@@ -484,3 +484,61 @@ def test_grid_backward_stencil_groups_equal_rows(gpu, dtype):
     # into parts rounds differently (a few f32 ulps of the parts' magnitude)
     np.testing.assert_allclose(out["groups"], out["rows"], rtol=1e-5, atol=1e-7 * scale)
     np.testing.assert_allclose(out["groups"], want, rtol=1e-5, atol=1e-7 * scale)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_grid_backward_walk_forms(gpu, mode):
+    """Every walk form of the binned backward (gridbin.hip: 0 = one wave per
+    tile segment, 1 = the part's segments end to end in equal runs, 2 = equal
+    per-wave ranges walked piece by piece) against the exact f64 oracle, for
+    single samples (the albedo step, with a device count and raw positions)
+    and for 7-point stencil groups (the shaded steps, samples on the box
+    faces)."""
+    import ctypes
+    import _dfhip
+    import _gridencoder
+    lib = _dfhip.load()
+    lib.dfhip_debug_walk_mode.argtypes = [ctypes.c_int]
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    try:
+        assert lib.dfhip_debug_walk_mode(mode) == 0
+        # single samples: capacity planes, live count on the device
+        cap, m = 40000, 33333
+        x01 = _samples(cap, 61, edge=False)
+        g = (np.random.default_rng(62).normal(size=(cap, 32)) * 0.1).astype(np.float16)
+        want = oracle.grid_encode_backward(g[:m], x01[:m], offs, 2, S, 16)
+        glbc = T(g, gpu).view(cap, 16, 2).transpose(0, 1).contiguous()
+        m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+        gemb = _binned(glbc, T(x01 * 2 - 1, gpu), 1.0, offs, rows, cap, m_dev, 3, 2, 16, S, 16,
+                       1, gpu)
+        scale = np.abs(want).max()
+        np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
+                                   atol=1e-7 * scale)
+        # stencil groups
+        cap, m, eps = 5000, 4321, 1e-2
+        x = (_samples(cap, 63, edge=False) * 2 - 1).astype(np.float32)
+        x[:40, 1] = np.float32(1.0)
+        xt = T(x, gpu)
+        m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+        x7 = torch.empty(7 * cap, 3, device=gpu)
+        m7 = torch.zeros(1, dtype=torch.int32, device=gpu)
+        _dfhip.call("dfhip_shading_stencil", xt.data_ptr(), m_dev.data_ptr(), cap, eps, 1.0,
+                    x7.data_ptr(), m7.data_ptr(), _dfhip.stream())
+        g7 = (torch.randn(16, 7 * cap, 2, generator=torch.Generator().manual_seed(64)) * 0.1)
+        g7 = g7.half().to(gpu)
+        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offs, 16, 2)
+        ent = torch.empty(ne, dtype=torch.int32, device=gpu)
+        cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
+        part = torch.empty(npf, device=gpu)
+        gemb = torch.full((rows, 2), float("nan"), device=gpu)
+        _gridencoder.binned_launcher(g7, xt, 1.0, T(offs, gpu), offs, gemb, cap, m_dev, 3, 2, 16,
+                                     S, 16, 1, False, ent, cnt, part, stencil_eps=eps)()
+        torch.cuda.synchronize()
+        x01 = ((x7[:7 * m].cpu().numpy() + np.float32(1)) / np.float32(2)).astype(np.float32)
+        gl = g7[:, :7 * m].float().cpu().numpy()
+        want = oracle.grid_encode_backward(gl, x01, offs, 2, S, 16, gridtype=1, blc=False)
+        np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
+                                   atol=1e-7 * np.abs(want).max())
+    finally:
+        lib.dfhip_debug_walk_mode(-1)

@@ -17,8 +17,12 @@ timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 \
     || { echo "bench failed"; tail -30 $OUT/bench.log; exit 3; }
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 python -c "import json; d=json.load(open('$OUT/bench.json')); print('ms/step', d['ms_per_step'], 'value', d['value'], 'roof', d.get('roofline',{}).get('frac'), 'infer', d.get('inference',{}).get('ms_per_frame'))"
+# the same child command bench.py's roofline passes profile: its kernel trace
+# reproduces the line's roofline.frac (tools/roofline_check.py)
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
-    -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing --no-alt-backward --no-shading \
+    -- python bench.py --steps 3 --warmup ${CHILD_WARMUP:-47} --no-cpu-baseline --no-kernel-timing --no-alt-backward \
+       --no-shading --no-infer --no-traffic --no-c5 \
     > $OUT/bench_prof.log 2>&1 || { echo "prof failed"; tail -20 $OUT/bench_prof.log; exit 4; }
 python tools/prof_top.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/rocprof_top.txt
 cat $OUT/rocprof_top.txt
+python tools/roofline_check.py $OUT/bench.json $OUT/prof/run_kernel_trace.csv | tee $OUT/roofline_check.json

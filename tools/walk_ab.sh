@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-for v in ${VALS:-1 0}; do
+for v in ${VALS:-2 1 0}; do
   DFHIP_WALK_FLAT=$v TAG=flat$v TOPN=12 bash tools/prof_c2.sh || exit 4
   OUT=gpurun_out/prof_shade_flat$v
   mkdir -p $OUT
