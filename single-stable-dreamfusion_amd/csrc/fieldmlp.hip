@@ -29,8 +29,6 @@
 // make the weight gradients deterministic.
 #include "field_common.h"
 
-#include <stdlib.h>
-
 namespace dfhip {
 namespace fm {
 
@@ -220,11 +218,8 @@ __device__ __forceinline__ void load_tile(TileIn<E> &g, uint32_t tile, const E *
 // PERM: enc holds the fused forward's permuted feature order (k_field_fwd_fused);
 // otherwise the natural [M, 32] encoder output.  M = *m_dev (clamped to cap)
 // when m_dev is given; d_enc is [16, cap, 2].
-// NW waves per workgroup: 4 (two workgroups per CU, 2 waves / SIMD) or 12
-// (one workgroup per CU sharing one copy of the weights: 3 waves / SIMD, and
-// each wave owns only 3-4 of the 37 weight-gradient tiles)
-template <typename E, typename rgb_t, bool PERM, int NW = kBwdWaves>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_field_bwd(
+template <typename E, typename rgb_t, bool PERM>
+__global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
     const E *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
     const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
     const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t cap,
@@ -235,7 +230,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_field_bwd(
     typedef typename Elem<E>::v4 v4;
     __shared__ WeightsG<E> W;
     __shared__ WeightsTG<E> T;
-    __shared__ StageT<E> stage[NW];
+    __shared__ StageT<E> stage[kBwdWaves];
     load_weights<PERM>(W, &T, w1, b1, w2, b2, w3, b3);
     const uint32_t M = active_count(m_dev, cap);
     const int wave = threadIdx.x >> 6;
@@ -243,18 +238,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_field_bwd(
     StageT<E> &S = stage[wave];
     __syncthreads();
 
-    // this wave's accumulator tiles (see the ownership tables below)
-    constexpr int kAcc = NW == 4 ? 10 : 4;
-    f4 acc[kAcc];
+    // this wave's accumulator tiles (see the ownership table below)
+    f4 acc[10];
 #pragma unroll
-    for (int i = 0; i < kAcc; ++i) acc[i] = f4{0, 0, 0, 0};
+    for (int i = 0; i < 10; ++i) acc[i] = f4{0, 0, 0, 0};
     const v4 ones = v4{(E)1.0f, (E)1.0f, (E)1.0f, (E)1.0f};
 
     const uint32_t tiles = ceil_div(M, 16u);
-    const uint32_t per_round = gridDim.x * NW;
+    const uint32_t per_round = gridDim.x * kBwdWaves;
     const uint32_t rounds = ceil_div(tiles, per_round);
     TileIn<E> cur;
-    uint32_t tile = blockIdx.x * NW + wave;
+    uint32_t tile = blockIdx.x * kBwdWaves + wave;
     load_tile<E, rgb_t>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
     for (uint32_t round = 0; round < rounds; ++round, tile += per_round) {
         // the next round's inputs are loaded while this one is processed
@@ -354,36 +348,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_field_bwd(
             return (v8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         };
         const v8 ones8 = __builtin_shufflevector(ones, ones, 0, 1, 2, 3, 4, 5, 6, 7);
-        if constexpr (NW == 12) {
-            // 37 tiles over 12 waves, grouped by their A operand:
-            //   waves 0-3  (tn = w):     W2 row tn x A1 tiles 0, 1, 2
-            //   waves 4-7  (tn = w - 4): W2 row tn x A1 tile 3, b2 row tn, W1 row tn x X tile 0
-            //   waves 8-11 (tn = w - 8): W1 row tn x X tile 1, b1 row tn, W3 x A2 tile tn;
-            //                            wave 8 also b3
-#pragma unroll
-            for (int st = 0; st < NW; st += 2) {
-                if (wave < 4) {
-                    const v8 a = tr2(st, kColD2 + 16 * wave);
-#pragma unroll
-                    for (int tm = 0; tm < 3; ++tm)
-                        acc[tm] = mfma(a, tr2(st, kColA1 + 16 * tm), acc[tm]);
-                } else if (wave < 8) {
-                    const int tn = wave - 4;
-                    const v8 a = tr2(st, kColD2 + 16 * tn);
-                    acc[0] = mfma(a, tr2(st, kColA1 + 48), acc[0]);
-                    acc[1] = mfma(a, ones8, acc[1]);
-                    acc[2] = mfma(tr2(st, kColD1 + 16 * tn), tr2(st, kColX), acc[2]);
-                } else {
-                    const int tn = wave - 8;
-                    const v8 a = tr2(st, kColD1 + 16 * tn);
-                    acc[0] = mfma(a, tr2(st, kColX + 16), acc[0]);
-                    acc[1] = mfma(a, ones8, acc[1]);
-                    const v8 ao = tr2(st, kColDO);
-                    acc[2] = mfma(ao, tr2(st, kColA2 + 16 * tn), acc[2]);
-                    if (wave == 8) acc[3] = mfma(ao, ones8, acc[3]);
-                }
-            }
-        } else {
 #pragma unroll
         for (int st = 0; st < kBwdWaves; st += 2) {
             if (wave < 2) {
@@ -414,7 +378,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_field_bwd(
                 if (wave == 2) acc[8] = mfma(ao, ones8, acc[8]);
             }
         }
-        }
         __syncthreads();  // the images are rewritten next round
         cur = nxt;
     }
@@ -422,28 +385,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_field_bwd(
     // ---- this workgroup's partial: every entry written by exactly one lane.
     // Accumulator element r of lane (c, h): row 4h + r, column c of the tile.
     float *out = partial + (size_t)blockIdx.x * kParams;
-    if constexpr (NW == 12) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (wave < 4) {
-                const int n = 16 * wave + 4 * h + r;
-#pragma unroll
-                for (int tm = 0; tm < 3; ++tm) out[kOffW2 + n * kHid + 16 * tm + c] = acc[tm][r];
-            } else if (wave < 8) {
-                const int n = 16 * (wave - 4) + 4 * h + r;
-                out[kOffW2 + n * kHid + 48 + c] = acc[0][r];
-                if (c == 0) out[kOffB2 + n] = acc[1][r];
-                out[kOffW1 + n * kIn + (PERM ? perm_feature(c) : c)] = acc[2][r];
-            } else {
-                const int tn = wave - 8, n = 16 * tn + 4 * h + r;
-                out[kOffW1 + n * kIn + (PERM ? perm_feature(16 + c) : 16 + c)] = acc[0][r];
-                if (c == 0) out[kOffB1 + n] = acc[1][r];
-                if (h == 0) out[kOffW3 + r * kHid + 16 * tn + c] = acc[2][r];
-                if (wave == 8 && lane == 0) out[kOffB3 + r] = acc[3][r];
-            }
-        }
-        return;
-    }
     if (wave < 2) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -540,24 +481,12 @@ static uint32_t resident_blocks(K kern) {
     return cached;
 }
 
-// Waves per workgroup of the fused field backward (DFHIP_FIELD_BWD_WAVES: 4
-// or 12, A/B runs).
-static int bwd_waves() {
-    static int w = 0;
-    if (w == 0) {
-        const char *e = getenv("DFHIP_FIELD_BWD_WAVES");
-        w = (e && atoi(e) == 12) ? 12 : 4;
-    }
-    return w;
-}
-
 static uint32_t bwd_blocks(uint32_t M) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t nw = (uint32_t)bwd_waves();
-    const uint32_t want = ceil_div(ceil_div(M, 16u), nw);
-    const uint32_t cap = (nw == 4 ? 2u : 1u) * (uint32_t)cus;  // resident workgroups
+    const uint32_t want = ceil_div(ceil_div(M, 16u), (uint32_t)kBwdWaves);
+    const uint32_t cap = 2u * (uint32_t)cus;  // two workgroups per CU
     return want < cap ? (want ? want : 1u) : cap;
 }
 
@@ -623,26 +552,14 @@ extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const
                       bwd_blocks(M), parts);
             return DFHIP_EINVAL;
         }
-        const bool w12 = bwd_waves() == 12;
-        if (grad_rgb_dtype == DFHIP_F32) {
-            if (w12)
-                k_field_bwd<half_t, float, false, 12><<<parts, 768, 0, s>>>(
-                    (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                    (const float *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
-            else
-                k_field_bwd<half_t, float, false><<<parts, 256, 0, s>>>(
-                    (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                    (const float *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
-        } else if (grad_rgb_dtype == DFHIP_F16) {
-            if (w12)
-                k_field_bwd<half_t, half_t, false, 12><<<parts, 768, 0, s>>>(
-                    (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                    (const half_t *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
-            else
-                k_field_bwd<half_t, half_t, false><<<parts, 256, 0, s>>>(
-                    (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                    (const half_t *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
-        }
+        if (grad_rgb_dtype == DFHIP_F32)
+            k_field_bwd<half_t, float, false><<<parts, 256, 0, s>>>(
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
+                (const float *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
+        else if (grad_rgb_dtype == DFHIP_F16)
+            k_field_bwd<half_t, half_t, false><<<parts, 256, 0, s>>>(
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
+                (const half_t *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
         else {
             set_error("%s: grad_rgb dtype must be f32 or f16", name);
             return DFHIP_EDTYPE;
@@ -882,14 +799,9 @@ static int grid_field_backward(
             return DFHIP_EINVAL;
         }
 #define DFHIP_BWD(E, R)                                                                       \
-    if (bwd_waves() == 12)                                                                    \
-        k_field_bwd<E, R, true, 12><<<mlp_parts, 768, 0, s>>>(                                \
-            (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, cap, \
-            m_dev, (E *)d_enc_lbc, mlp_partial);                                              \
-    else                                                                                      \
-        k_field_bwd<E, R, true><<<mlp_parts, 256, 0, s>>>(                                    \
-            (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, cap, \
-            m_dev, (E *)d_enc_lbc, mlp_partial)
+    k_field_bwd<E, R, true><<<mlp_parts, 256, 0, s>>>(                                        \
+        (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, cap,     \
+        m_dev, (E *)d_enc_lbc, mlp_partial)
         if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(half_t, float);
         else if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F16) DFHIP_BWD(half_t, half_t);
         else if (elem == DFHIP_BF16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(bf16_t, float);

@@ -57,7 +57,6 @@ struct BinInfo {
     uint32_t L, nbins, shift, tcap;      // tcap: tiles of the capacity (counts row stride)
     uint32_t G;                          // walk workgroups
     uint32_t lane_perm;                  // walk: bit-reversed lane -> run map (1) or identity
-    uint32_t xcd_map;                    // walk: XCD-grouped logical slots (xcd_slot) or identity
     uint32_t o_totals, o_plan;           // word offsets into `counts` (layout below)
     uint32_t bin0[ge::kMaxLevels + 1];   // first bin of level l (bin0[L] = nbins)
     uint32_t base[ge::kMaxLevels];       // first row of level l
@@ -120,12 +119,6 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
             perm = e ? (atoi(e) != 0) : 1;
         }
         bi.lane_perm = (uint32_t)perm;
-        static int xmap = -1;  // DFHIP_WALK_XCD=0: identity slots (A/B)
-        if (xmap < 0) {
-            const char *e = getenv("DFHIP_WALK_XCD");
-            xmap = e ? (atoi(e) != 0) : 1;
-        }
-        bi.xcd_map = (uint32_t)xmap;
     }
     uint32_t nb = 0;
     for (uint32_t l = 0; l < L; ++l) {
@@ -152,18 +145,6 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
 }
 static uint64_t counts_words(const BinInfo &bi) {
     return ((uint64_t)bi.o_plan + 2ull * bi.nbins + 3ull) & ~3ull;
-}
-
-// Logical walk slot of workgroup b: the G workgroups are dealt round-robin
-// over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch: blocks b and b + 8
-// share one; speed only, never correctness), so consecutive logical slots —
-// the parts of one bin, and the bins of one level — are given to blocks of
-// one XCD: that XCD's L2 then holds its levels' feature gradients instead of
-// all eight L2s pulling every level's.  A bijection on [0, G).
-__device__ __forceinline__ uint32_t xcd_slot(uint32_t b, uint32_t G) {
-    const uint32_t x = b & 7u, i = b >> 3;
-    const uint32_t q = G >> 3, r = G & 7u;  // XCD x holds q + (x < r) blocks
-    return x * q + min(x, r) + i;
 }
 
 __device__ __forceinline__ uint32_t bin_total(const uint32_t *__restrict__ totals, uint32_t b) {
@@ -642,8 +623,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     __shared__ uint32_t n_seen;
     uint64_t tr0 = 0;
     if (bi.trace) tr0 = wall_clock64();
-    const uint32_t nb = bi.nbins, G = bi.G;
-    const uint32_t slot = bi.xcd_map ? xcd_slot(blockIdx.x, G) : blockIdx.x;
+    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
     const uint32_t *totals = counts + bi.o_totals;
     if (threadIdx.x < 64) {  // plan (wave 0): this workgroup's bin b and part j of P_b
         const uint32_t ln = threadIdx.x;
@@ -1269,8 +1249,7 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     __shared__ uint32_t pre[kChunkTiles + 1];
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t sh_b, sh_j, sh_p;
-    const uint32_t nb = bi.nbins, G = bi.G;
-    const uint32_t slot = bi.xcd_map ? xcd_slot(blockIdx.x, G) : blockIdx.x;
+    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
     const uint32_t *totals = counts + bi.o_totals;
     if (threadIdx.x < 64) {  // plan (wave 0), as k_walk
         const uint32_t ln = threadIdx.x;
