@@ -846,6 +846,9 @@ constexpr uint32_t kChunkTiles = 1024;
 #ifndef DFHIP_WALK_RUN
 #define DFHIP_WALK_RUN 6
 #endif
+#ifndef DFHIP_WALK_RUN7  // the same for stencil groups (textureless walk: 2 -> 1 costs 20 %)
+#define DFHIP_WALK_RUN7 2
+#endif
 
 template <uint32_t C>
 struct FlatCell {
@@ -1023,8 +1026,7 @@ __device__ __forceinline__ void flat_entry(FlatCell<C> &cell, double *acc, uint3
                 uint32_t ci[3] = {ci0[0], ci0[1], ci0[2]};
                 flat_locate1(ge::dyn_map_t<POW2>(dyn, inv, v), sc, half,
                              fr[ax], ci[ax]);
-                flat_take_at<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm,
-                                      fr, ci, g[a2]);
+                flat_take_at<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm, fr, ci, g[a2]);
             }
         } else {  // rare (a sample on the bound): the general form
 #pragma unroll
@@ -1301,7 +1303,7 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
     // entries whose loads are in flight together per lane (and the next
     // batch's ids): 6 keeps the f16 walk within 128 VGPRs (8 spilled)
-    constexpr uint32_t RUN = GROUP > 1 ? 2u : (uint32_t)DFHIP_WALK_RUN;
+    constexpr uint32_t RUN = GROUP > 1 ? (uint32_t)DFHIP_WALK_RUN7 : (uint32_t)DFHIP_WALK_RUN;
 #define DFHIP_FLAT(LD)                                                                         \
     flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN, WMODE>(gl, inputs, counts, entries, acc, pre,    \
                                                      wsum, nb, b, part, P, ntiles, srows, lo, \

@@ -51,9 +51,18 @@ __device__ __forceinline__ void load_w(W &w, const float *w1, const float *b1, c
 // four xor-shuffles (the same order in all sixteen lanes).  A block is 16
 // rays; 16k rays are 4096 waves (4 per SIMD; four lanes per ray left one wave
 // per SIMD to hide every LDS and global latency).
+// Workgroups of 64 rays (1,024 threads): every workgroup stages the f16
+// weights once and the backward writes one weight-gradient partial per
+// workgroup, so 64 rays per workgroup instead of 16 load the weights and write
+// (and k_head_wsum reads) a quarter of the partials.
+#ifndef DFHIP_HEAD_THREADS
+#define DFHIP_HEAD_THREADS 1024
+#endif
 constexpr int kSub = 16;
 constexpr int kPer = kHid / kSub;  // hidden units per lane
-constexpr int kRays = 256 / kSub;  // rays per 256-thread block
+constexpr int kThreads = DFHIP_HEAD_THREADS;
+constexpr int kRays = kThreads / kSub;  // rays per workgroup
+static_assert(kThreads % 64 == 0 && kThreads <= 1024, "DFHIP_HEAD_THREADS: waves, <= 1024");
 
 // freqencoder.cu:30-58 for D = 3, degree 6 (same expression as k_freq_fwd),
 // then the autocast cast to f16; this sub-lane's share into sx[ray][*].
@@ -124,7 +133,7 @@ __global__ __launch_bounds__(256) void k_head_fwd_plain(
     write_outputs(N, n, bg, ws, depth, image, nears, fars, out_image, out_depth, mask);
 }
 
-__global__ __launch_bounds__(256) void k_head_fwd_net(
+__global__ __launch_bounds__(kThreads) void k_head_fwd_net(
     uint32_t N, const float *__restrict__ ws, const float *__restrict__ depth,
     const float *__restrict__ image, const float *__restrict__ rays_d,
     const float *__restrict__ nears, const float *__restrict__ fars, const float *w1,
@@ -183,7 +192,7 @@ __device__ __forceinline__ float entropy_grad(uint32_t N, float a, const float *
 // sigmoid and the two f16 Linear layers are run backward and this block's
 // weight-gradient partials (f32 sums over its 64 rays of f16 products) formed
 // from LDS images of the activations.
-__global__ __launch_bounds__(256) void k_head_bwd_net(
+__global__ __launch_bounds__(kThreads) void k_head_bwd_net(
     uint32_t N, const float *__restrict__ g_image /* [3, N] */, const float *__restrict__ ws,
     const float *__restrict__ rays_d, const float *w1, const float *b1, const float *w2,
     const float *b2, float *__restrict__ grad_image, float *__restrict__ grad_ws,
@@ -388,7 +397,7 @@ extern "C" int dfhip_ray_head_forward(uint32_t N, const float *ws, const float *
     }
     hipStream_t s = as_stream(stream);
     if (net)
-        hd::k_head_fwd_net<<<ceil_div(N, (uint32_t)hd::kRays), 256, 0, s>>>(
+        hd::k_head_fwd_net<<<ceil_div(N, (uint32_t)hd::kRays), hd::kThreads, 0, s>>>(
             N, ws, depth, image, rays_d, nears, fars, w1, b1, w2, b2, out_image, out_depth, mask);
     else
         hd::k_head_fwd_plain<<<ceil_div(N, 256u), 256, 0, s>>>(N, ws, depth, image, nears, fars,
@@ -419,7 +428,7 @@ static int ray_head_backward(uint32_t N, const float *g_image, const float *ws,
     hipStream_t s = as_stream(stream);
     if (net) {
         const uint32_t blocks = ceil_div(N, (uint32_t)hd::kRays);
-        hd::k_head_bwd_net<<<blocks, 256, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
+        hd::k_head_bwd_net<<<blocks, hd::kThreads, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
                                                   grad_image, grad_ws, partial, ent_grad_loss,
                                                   ent_lambda);
         hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u) + (ent_loss ? 1u : 0u), 1024, 0,
