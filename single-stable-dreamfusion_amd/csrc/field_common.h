@@ -168,16 +168,29 @@ struct FwdG {
 };
 typedef FwdG<half_t> Fwd;
 
+// Four f32 accumulators -> f16 (RNE) -> ReLU as packed f16 pairs (v_cvt_pk
+// + v_pk_max: two values per instruction; the same values as the scalar
+// form except possibly the sign of a zero, which no product, sum or
+// ReLU mask downstream can see unless every term of a sum is zero).
+__device__ __forceinline__ half4 relu_h4(f4 a) {
+    const half4 v = __builtin_convertvector(a, half4);
+    return __builtin_elementwise_max(v, half4{(half_t)0.0f, (half_t)0.0f, (half_t)0.0f,
+                                              (half_t)0.0f});
+}
+
 template <typename E, bool P>
 __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem<E>::v8 xb, int c,
                                              int h, FwdG<E, P> &F) {
     constexpr bool kBf = std::is_same<E, bf16_t>::value;
+    constexpr bool kPkH = P && std::is_same<E, half_t>::value;  // packed f16 (the backward)
     f4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         acc[t] = mfma(a_nat(W.w1, kLd32, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
         if constexpr (kBf) {
             F.a1[t] = relu_bf4(acc[t]);
+        } else if constexpr (kPkH) {
+            F.a1[t] = relu_h4(acc[t]);
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -193,6 +206,8 @@ __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem
         for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kLd64, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
         if constexpr (kBf) {
             F.a2[u] = relu_bf4(a);
+        } else if constexpr (kPkH) {
+            F.a2[u] = relu_h4(a);
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

@@ -283,8 +283,18 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
                               (float)act[3] > 0.0f ? d[3] : 0.0f};
                 dst = __builtin_convertvector(m, bf4);
             } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) dst[r] = act[r] > (E)0.0f ? (E)d[r] : (E)0.0f;
+                // f16 ReLU backward on packed pairs: act is a ReLU output (+-0
+                // or positive), so act > 0 <=> its magnitude bits are nonzero;
+                // ((x & 0x7fff) + 0x7fff) sets bit 15 exactly then, and
+                // (bit >> 15) * 0xffff widens it to the half's mask
+                typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+                const half4 dh = __builtin_convertvector(d, half4);
+                u2 ab, db;
+                __builtin_memcpy(&ab, &act, 8);
+                __builtin_memcpy(&db, &dh, 8);
+                const u2 nz = ((ab & 0x7FFF7FFFu) + 0x7FFF7FFFu) & 0x80008000u;
+                const u2 r = db & ((nz >> 15u) * 0xFFFFu);
+                __builtin_memcpy(&dst, &r, 8);
             }
         };
         // hidden layer 2: dA2^T = W3^T dO^T, ReLU mask
