@@ -436,7 +436,10 @@ def measure_traffic(region, timeout=180, warmup=10):
     # (the occupancy grid, and with it M, grows over the first hundred
     # steps): its last `keep` steps, the ones profiled, sit where the timed
     # region ends
-    keep = 3
+    # profiled steps: 16, so the window holds exactly one density refresh (one
+    # step in 16, as in the timed region) and averages the random cameras'
+    # samples per step (they vary 3x)
+    keep = 16
     child = [sys.executable, str(Path(__file__).resolve()), "--steps", str(keep), "--warmup",
              str(max(1, warmup)),
              "--no-cpu-baseline", "--no-kernel-timing", "--no-alt-backward", "--no-shading",
@@ -535,8 +538,8 @@ def measure_traffic(region, timeout=180, warmup=10):
     MEASURE_TRAFFIC_TRACE_US[region] = sum(trace_us.values())
     return int(total), (
         "measured in this run: rocprofv3 --pmc passes (separate runs: FETCH_SIZE, WRITE_SIZE, "
-        "TCC_HIT_sum + TCC_MISS_sum) of a 10 + 3-step child bench, the last 3 dispatches of each "
-        "kernel; FETCH_SIZE x2 (the gfx950 correction, calibrated for 16-B streaming loads "
+        "TCC_HIT_sum + TCC_MISS_sum) of a child bench ending where the timed region ends, the "
+        "last 16 dispatches of each kernel; FETCH_SIZE x2 (the gfx950 correction, calibrated for 16-B streaming loads "
         "only: an upper bound for gathers; it also counts Infinity-Cache hits), KiB -> bytes, "
         "summed over the region's kernels, mean per launch; l2_hit_rate per kernel")
 
@@ -693,7 +696,7 @@ def main():
         kd = kernels[dom]
         traffic, note = (None, "skipped (--no-traffic or N > 1)")
         if world == 1 and not args.no_traffic:
-            traffic, note = measure_traffic(dom, warmup=args.warmup + args.steps - 3)
+            traffic, note = measure_traffic(dom, warmup=max(1, args.warmup + args.steps - 16))
         roof = {
             "kernel": dom, "bound": "hbm", "achieved": kd["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(kd["achieved_GBs"] / HBM_PEAK_GBS, 4),
@@ -720,7 +723,7 @@ def main():
                 "traffic_per_sample": round(traffic / cm, 2) if traffic else None,
                 "traffic_over_algorithmic": round(traffic / cb, 3) if traffic else None,
                 "timing": ("rocprofv3 kernel trace of the child's graph-replayed steps "
-                           "(last 3 dispatches of each region kernel), bytes from the "
+                           "(last 16 dispatches of each region kernel), bytes from the "
                            "region's model at the child's samples per step"),
                 "eager_twin": {"avg_us": kd["avg_us"], "bytes_per_launch": kd["bytes_per_launch"],
                                "achieved": kd["achieved_GBs"],
@@ -746,8 +749,9 @@ def main():
                 "samples_per_step": round(cm, 1), "bytes_per_step": int(sb),
                 "kernel_us_per_step": round(st_us, 2), "achieved": round(g, 1),
                 "frac": round(g / HBM_PEAK_GBS, 4),
-                "note": "rocprofv3 kernel trace of the child's last 3 graph-replayed steps "
-                        "(every kernel from the step prologue on; no density refresh among them)"}
+                "note": "rocprofv3 kernel trace of the child's last 16 graph-replayed steps "
+                        "(every kernel from a step prologue on: one density refresh, as in "
+                        "every 16 steps of the timed region)"}
         result["kernel_timing"] = timing
     if world == 1 and not args.no_kernel_timing:
         result["field_mlp"] = field_mlp_report(trainer)

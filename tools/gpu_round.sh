@@ -20,7 +20,7 @@ python -c "import json; d=json.load(open('$OUT/bench.json')); print('ms/step', d
 # the same child command bench.py's roofline passes profile: its kernel trace
 # reproduces the line's roofline.frac (tools/roofline_check.py)
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
-    -- python bench.py --steps 3 --warmup ${CHILD_WARMUP:-47} --no-cpu-baseline --no-kernel-timing --no-alt-backward \
+    -- python bench.py --steps 16 --warmup ${CHILD_WARMUP:-34} --no-cpu-baseline --no-kernel-timing --no-alt-backward \
        --no-shading --no-infer --no-traffic --no-c5 \
     > $OUT/bench_prof.log 2>&1 || { echo "prof failed"; tail -20 $OUT/bench_prof.log; exit 4; }
 python tools/prof_top.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/rocprof_top.txt

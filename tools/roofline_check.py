@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 
-def main(bench_json, trace_csv, keep=3):
+def main(bench_json, trace_csv, keep=16):
     import bench
     d = json.loads([l for l in open(bench_json) if l.startswith("{")][-1])
     roof = d["roofline"]
@@ -38,4 +38,4 @@ def main(bench_json, trace_csv, keep=3):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 3)
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 16)
