@@ -178,9 +178,12 @@ __device__ __forceinline__ half4 relu_h4(f4 a) {
                                               (half_t)0.0f});
 }
 
-template <typename E, bool P>
+// W2R: the layer-2 weight operands come from w2op (registers, loaded once per
+// kernel) instead of LDS.
+template <typename E, bool P, bool W2R = false>
 __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem<E>::v8 xb, int c,
-                                             int h, FwdG<E, P> &F) {
+                                             int h, FwdG<E, P> &F,
+                                             const typename Elem<E>::v8 (*w2op)[2] = nullptr) {
     constexpr bool kBf = std::is_same<E, bf16_t>::value;
     constexpr bool kPkH = P && std::is_same<E, half_t>::value;  // packed f16 (the backward)
     f4 acc[4];
@@ -203,7 +206,9 @@ __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem
     for (int u = 0; u < 4; ++u) {
         f4 a = bias4(W.b2, 16 * u + 4 * h);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) a = mfma(a_perm(W.w2, kLd64, 16 * u + c, s, h), b_from_tiles(F.a1, s), a);
+        for (int s = 0; s < 2; ++s)
+            a = mfma(W2R ? w2op[u][s] : a_perm(W.w2, kLd64, 16 * u + c, s, h),
+                     b_from_tiles(F.a1, s), a);
         if constexpr (kBf) {
             F.a2[u] = relu_bf4(a);
         } else if constexpr (kPkH) {

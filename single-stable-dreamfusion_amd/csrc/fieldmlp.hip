@@ -143,6 +143,16 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
 // Each partial entry is written by exactly one lane of the workgroup; the
 // fixed-order k_field_wgrad_sum over workgroups keeps the result deterministic.
 constexpr int kBwdWaves = 4;
+// Weight operands held in registers for the whole kernel instead of re-read
+// from LDS every tile (bit 0: W2 of the forward and W2^T, 64 VGPRs; bit 1:
+// W1^T; bit 2: W3^T).  Field backward per C2 step / textureless step: none
+// 107 / 660 us, bit 0 94 / 578, all three 92 / 558 (230 VGPRs, still 2 waves
+// per SIMD).  The forward kernel's W2 in registers (4 waves per SIMD instead
+// of 5) was slower: 80 -> 83 us.
+#ifndef DFHIP_BWD_WREG
+#define DFHIP_BWD_WREG 7
+#endif
+constexpr int kBwdWreg = DFHIP_BWD_WREG;
 constexpr int kStLd = 312;  // stage row stride (halves): 156 dwords = 4 mod 64 -> the
                             // 32 lanes of an 8-byte write hit 64 distinct banks
 constexpr int kColX = 0, kColA1 = 32, kColA2 = 96, kColD1 = 160, kColD2 = 224, kColDO = 288;
@@ -243,6 +253,20 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
 #pragma unroll
     for (int i = 0; i < 10; ++i) acc[i] = f4{0, 0, 0, 0};
     const v4 ones = v4{(E)1.0f, (E)1.0f, (E)1.0f, (E)1.0f};
+    // weight operands kept in registers (kBwdWreg)
+    v8 w2op[4][2], w2top[4][2], w1top[2][2], w3top[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            if (kBwdWreg & 1) {
+                w2op[u][s2] = a_perm(W.w2, kLd64, 16 * u + c, s2, h);
+                w2top[u][s2] = a_perm(T.w2t, kLd64, 16 * u + c, s2, h);
+            }
+            if ((kBwdWreg & 2) && u < 2) w1top[u][s2] = a_perm(T.w1t, kLd64, 16 * u + c, s2, h);
+        }
+        if (kBwdWreg & 4) w3top[u] = a_nat(T.w3t, kLd32, 16 * u + c, 0, h);
+    }
 
     const uint32_t tiles = ceil_div(M, 16u);
     const uint32_t per_round = gridDim.x * kBwdWaves;
@@ -257,7 +281,7 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
         const uint32_t sample = tile * 16 + c;
         const bool valid = sample < M;
         FwdG<E, true> F;  // packed activations (f16 pairs per VGPR)
-        forward_tile(W, cur.xb, c, h, F);
+        forward_tile<E, true, (kBwdWreg & 1) != 0>(W, cur.xb, c, h, F, w2op);
         // dL/d(output layer), in E as autocast's backward produces it
         E dO[4] = {(E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
         if (h == 0 && valid) {
@@ -301,7 +325,8 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
         typename TilesT<E, true>::type dz2;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const f4 d = mfma(a_nat(T.w3t, kLd32, 16 * u + c, 0, h), dob, f4{0, 0, 0, 0});
+            const f4 d = mfma((kBwdWreg & 4) ? w3top[u] : a_nat(T.w3t, kLd32, 16 * u + c, 0, h),
+                              dob, f4{0, 0, 0, 0});
             mask(F.a2[u], d, dz2[u]);
         }
         // hidden layer 1: dA1^T = W2^T dZ2^T, ReLU mask
@@ -311,7 +336,8 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             f4 d = f4{0, 0, 0, 0};
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
-                d = mfma(a_perm(T.w2t, kLd64, 16 * t + c, s2, h), b_from_tiles(dz2, s2), d);
+                d = mfma((kBwdWreg & 1) ? w2top[t][s2] : a_perm(T.w2t, kLd64, 16 * t + c, s2, h),
+                         b_from_tiles(dz2, s2), d);
             mask(F.a1[t], d, dz1[t]);
         }
         // encoder features: dX^T = W1^T dZ1^T -> [L, B, C] directly
@@ -320,7 +346,8 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             f4 d = f4{0, 0, 0, 0};
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
-                d = mfma(a_perm(T.w1t, kLd64, 16 * f + c, s2, h), b_from_tiles(dz1, s2), d);
+                d = mfma((kBwdWreg & 2) ? w1top[f][s2] : a_perm(T.w1t, kLd64, 16 * f + c, s2, h),
+                         b_from_tiles(dz1, s2), d);
             if (valid) {
                 // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
                 const uint32_t lv = 8 * f + 2 * h;

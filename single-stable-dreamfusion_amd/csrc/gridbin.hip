@@ -52,6 +52,12 @@ constexpr uint32_t kMaxBins = 4096;
 constexpr uint32_t kMaxSlices = 128;          // slices per level (k_bin's 128-bit masks)
 constexpr uint32_t kSliceBytes = 128 * 1024;  // f64 accumulators of one walk workgroup
 constexpr uint32_t kTotSplit = 16;            // bin totals as 16 partial sums (tile % 16)
+// Segment entries are u16: the tile-relative id in bits 0..9; for stencil
+// groups a satellite entry (below) carries its moved-point mask in bits 10..15.
+constexpr uint32_t kIdBits = 10;
+constexpr uint32_t kIdMask = (1u << kIdBits) - 1u;
+static_assert(kTile == (1u << kIdBits), "ids fill the low kIdBits bits of an entry");
+constexpr uint32_t kCentreCost = 4;  // walk cost of a centre entry in satellite entries
 
 struct BinInfo {
     uint32_t L, nbins, shift, tcap;      // tcap: tiles of the capacity (counts row stride)
@@ -326,9 +332,18 @@ struct FastLevels {
 // field row GROUP g + a (GROUP = 7) is point a of sample g, a = 0 the sample
 // itself, a = 1 + s the clamped x + (s odd ? -eps : eps) e_(s >> 1)
 // (k_stencil's arithmetic, network_grid.py:90-104).  Binned per group, one
-// entry per (group, slice) instead of one per (row, slice); the walk derives
-// the seven points from the sample's position and reads the group's seven
-// gradient rows (adjacent in the [L, 7 M, C] planes).
+// entry per (group, slice) instead of one per (row, slice), of two kinds:
+//   * centre entries (front of the segment): the slices the sample's own
+//     corners touch; the walk derives all seven points from the sample's
+//     position and reads the group's seven gradient rows (adjacent in the
+//     [L, 7 M, C] planes);
+//   * satellite entries (back of the segment, counted in the high 16 bits of
+//     the segment count): slices that only moved points touch (at the mid and
+//     fine levels a +-eps move along y or z is one or more slices away), with
+//     the mask of those points in the entry's bits 10..15; the walk takes
+//     only them (usually one) instead of all seven.
+// On the reference grid this cuts the walked points per group from ~243 to
+// ~165 (34.7 entries per group: 21.6 centre, 13.2 satellite).
 struct Stencil {
     float eps, bound;
 };
@@ -414,47 +429,85 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
             for (uint32_t l = 0; l < bi.L; ++l) {
                 const float sc = fl.scale[l];
                 const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
-                uint64_t mask = 0;
-                auto pairs = [&](uint32_t i0) {
+                // slices of the corners of the cell with tiled index i0 into mk
+                auto pairs = [&](uint32_t i0, uint64_t &mk) {
 #pragma unroll
                     for (uint32_t p = 0; p < 4; ++p) {  // x-neighbour pairs {0,1} + {0, m1, m2, m1+m2}
                         if (p >= (1u << (lead - 1u))) break;  // uniform
                         const uint32_t o = ((p & 1u) ? m1 : 0u) + ((p & 2u) ? m2 : 0u);
                         const uint32_t r = (i0 + o) & wm;
-                        mask |= 1ull << (r >> shift);
-                        if ((r & smask) == smask) mask |= 1ull << (((r + 1u) & wm) >> shift);
+                        mk |= 1ull << (r >> shift);
+                        if ((r & smask) == smask) mk |= 1ull << (((r + 1u) & wm) >> shift);
                     }
                 };
-                if (GROUP == 7 && incr) {
-                    uint32_t c[3];
-#pragma unroll
-                    for (uint32_t d = 0; d < 3; ++d) c[d] = (uint32_t)floorf(fmaf(xg[0][d], sc, half));
-                    const uint32_t i0 = c[0] + c[1] * m1 + c[2] * m2;
-                    pairs(i0);
-#pragma unroll
-                    for (uint32_t a = 1; a < 7; ++a) {
-                        const uint32_t ax = (a - 1u) >> 1;
-                        const uint32_t stride = ax == 0 ? 1u : (ax == 1 ? m1 : m2);
-                        if (stride == 0) continue;  // uniform: a dim the index drops
-                        const uint32_t ca = (uint32_t)floorf(fmaf(xg[a][ax], sc, half));
-                        if (ca != c[ax]) pairs(i0 + (ca - c[ax]) * stride);
+                const uint32_t b0 = fl.bin0[l];
+                if constexpr (GROUP == 1) {
+                    uint64_t mask = 0;
+                    const uint32_t c0 = (uint32_t)floorf(fmaf(xg[0][0], sc, half));
+                    const uint32_t c1 = (uint32_t)floorf(fmaf(xg[0][1], sc, half));
+                    const uint32_t c2 = (uint32_t)floorf(fmaf(xg[0][2], sc, half));
+                    pairs(c0 + c1 * m1 + c2 * m2, mask);
+                    while (mask) {
+                        const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mask);
+                        mask &= mask - 1;
+                        const uint32_t slot = atomicAdd(&cnt[b], 1u);
+                        seg[(size_t)b * kTile + slot] = id;
                     }
                 } else {
+                    // mc: slices of the sample's own corners; mo[a - 1]: those of
+                    // moved point a (0 when its cell is the sample's)
+                    uint64_t mc = 0, mo[6] = {0, 0, 0, 0, 0, 0};
+                    if (incr) {
+                        uint32_t c[3];
 #pragma unroll
-                for (uint32_t a = 0; a < GROUP; ++a) {
-                    if (!((in >> a) & 1u)) continue;
-                    const uint32_t c0 = (uint32_t)floorf(fmaf(xg[a][0], sc, half));
-                    const uint32_t c1 = (uint32_t)floorf(fmaf(xg[a][1], sc, half));
-                    const uint32_t c2 = (uint32_t)floorf(fmaf(xg[a][2], sc, half));
-                    pairs(c0 + c1 * m1 + c2 * m2);
-                }
-                }
-                const uint32_t b0 = fl.bin0[l];
-                while (mask) {
-                    const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mask);
-                    mask &= mask - 1;
-                    const uint32_t slot = atomicAdd(&cnt[b], 1u);
-                    seg[(size_t)b * kTile + slot] = id;
+                        for (uint32_t d = 0; d < 3; ++d) c[d] = (uint32_t)floorf(fmaf(xg[0][d], sc, half));
+                        const uint32_t i0 = c[0] + c[1] * m1 + c[2] * m2;
+                        pairs(i0, mc);
+#pragma unroll
+                        for (uint32_t a = 1; a < 7; ++a) {
+                            const uint32_t ax = (a - 1u) >> 1;
+                            const uint32_t stride = ax == 0 ? 1u : (ax == 1 ? m1 : m2);
+                            if (stride == 0) continue;  // uniform: a dim the index drops
+                            const uint32_t ca = (uint32_t)floorf(fmaf(xg[a][ax], sc, half));
+                            if (ca != c[ax]) pairs(i0 + (ca - c[ax]) * stride, mo[a - 1]);
+                        }
+                    } else {
+#pragma unroll
+                        for (uint32_t a = 0; a < 7; ++a) {
+                            if (!((in >> a) & 1u)) continue;
+                            const uint32_t c0 = (uint32_t)floorf(fmaf(xg[a][0], sc, half));
+                            const uint32_t c1 = (uint32_t)floorf(fmaf(xg[a][1], sc, half));
+                            const uint32_t c2 = (uint32_t)floorf(fmaf(xg[a][2], sc, half));
+                            if (a == 0) pairs(c0 + c1 * m1 + c2 * m2, mc);
+                            else pairs(c0 + c1 * m1 + c2 * m2, mo[a - 1]);
+                        }
+                    }
+                    // centre entries (front of the segment): every slice the
+                    // sample's corners touch; the walk takes all seven points
+                    // there.  (A mask of the moved points touching a centre
+                    // entry's slice, to skip the others there, cost more in the
+                    // binning than it saved in the walk: bin 173 -> 192 us, walk
+                    // 972 -> 964 us; so did one append loop over both kinds:
+                    // 173 -> 188 us.)
+                    uint64_t ms = (mo[0] | mo[1] | mo[2] | mo[3] | mo[4] | mo[5]) & ~mc;
+                    while (mc) {
+                        const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mc);
+                        mc &= mc - 1;
+                        const uint32_t slot = atomicAdd(&cnt[b], 1u) & 0xFFFFu;
+                        seg[(size_t)b * kTile + slot] = id;
+                    }
+                    // satellite entries (back of the segment): slices only moved
+                    // points touch, with the mask of those points in bits 10..15
+                    while (ms) {
+                        const uint32_t sl = (uint32_t)__builtin_ctzll(ms);
+                        ms &= ms - 1;
+                        uint32_t m6 = 0;
+#pragma unroll
+                        for (uint32_t a = 0; a < 6; ++a) m6 |= (uint32_t)((mo[a] >> sl) & 1ull) << a;
+                        const uint32_t b = b0 + sl;
+                        const uint32_t slot = kTile - 1u - (atomicAdd(&cnt[b], 1u << 16) >> 16);
+                        seg[(size_t)b * kTile + slot] = (uint16_t)(id | (m6 << kIdBits));
+                    }
                 }
             }
         }
@@ -462,7 +515,10 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
             const uint32_t v = cnt[b];
             counts[(size_t)tile * nb + b] = v;
-            if (v) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], v);
+            // bin totals weigh a centre entry (seven points) as kCentreCost
+            // satellite entries (one point) for the walk's part plan
+            const uint32_t w = (v & 0xFFFFu) * (GROUP > 1 ? kCentreCost : 1u) + (v >> 16);
+            if (w) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], w);
         }
         __syncthreads();
     }
@@ -688,8 +744,9 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     constexpr uint32_t lead = decltype(lead_c)::value;
     // part j of P: tiles j, j + P, ...; wave w takes every waves-th of those
     for (uint32_t t = part + P * wave; t < ntiles; t += P * waves) {
-        const uint32_t cnt = counts[(size_t)t * nb + b];
-        if (bi.trace && lane == 0) atomicAdd(&n_seen, cnt);
+        const uint32_t raw = counts[(size_t)t * nb + b];
+        const uint32_t cnt = raw & 0xFFFFu, nsat = raw >> 16;  // centre / satellite entries
+        if (bi.trace && lane == 0) atomicAdd(&n_seen, cnt + nsat);
         const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile;
         const uint32_t tbase = t * kTile;
         const uint32_t Q = (cnt + 63) >> 6;
@@ -793,6 +850,35 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
             walk(std::integral_constant<uint32_t, 4>{});
         else
             walk(std::integral_constant<uint32_t, kRun>{});
+        if constexpr (GROUP > 1) {
+            // satellite entries (back of the segment): only the moved points
+            // of the entry's mask touch this slice
+            const uint16_t *sseg = seg + (kTile - nsat);
+            const uint32_t Q2 = (nsat + 63) >> 6;
+            const uint32_t f0 = min(rl * Q2, nsat), f1 = min(f0 + Q2, nsat);
+            for (uint32_t e = f0; e < f1; ++e) {
+                const uint32_t v = sseg[e];
+                const uint32_t sid = tbase + (v & kIdMask);
+                float xr[3];
+                load_pos3<3>(inputs, sid, xr);
+                uint32_t m6 = v >> kIdBits;
+                while (m6) {
+                    const uint32_t a = 1u + (uint32_t)__builtin_ctz(m6);
+                    m6 &= m6 - 1u;
+                    float g[C];
+                    load_grad<grad_t, C>(gl + ((size_t)sid * GROUP + a) * C, g);
+                    float p[3], x[D];
+                    group_point<GROUP>(xr, a, st, p);
+                    bool ok = true;
+#pragma unroll
+                    for (uint32_t d = 0; d < D; ++d) {
+                        x[d] = ge::dyn_map_t<POW2>(dyn, inv, p[d]);
+                        ok = ok && !(x[d] < 0.0f) && !(x[d] > 1.0f);
+                    }
+                    if (ok) take(x, g);
+                }
+            }
+        }
         if (have) flush<D, C, MODE, lead>(acc, srows, r0, r1, c, lr, cur, cw);
     }
     };
@@ -848,6 +934,9 @@ constexpr uint32_t kChunkTiles = 1024;
 #endif
 #ifndef DFHIP_WALK_RUN7  // the same for stencil groups (textureless walk: 2 -> 1 costs 20 %)
 #define DFHIP_WALK_RUN7 2
+#endif
+#ifndef DFHIP_WALK_RUN_SAT  // the same for stencil satellite entries (one point each)
+#define DFHIP_WALK_RUN_SAT 4
 #endif
 
 template <uint32_t C>
@@ -1047,10 +1136,87 @@ __device__ __forceinline__ void flat_entry(FlatCell<C> &cell, double *acc, uint3
     }
 }
 
-// A lane's entries [ea, eb) of one piece of a tile segment (ids at seg),
-// RB loads in flight per batch (clamped ids: every load is issued before the
-// first use).
-template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RB>
+// A satellite entry of a stencil group (see k_bin_fast): only the moved
+// points in m6 (bit a - 1: point a) touch the slice; they are taken one after
+// another (usually one).  g0: the gradient of the first of them, loaded with
+// the position; grow: the group's gradient rows.
+template <typename grad_t, uint32_t C, bool POW2, uint32_t LEAD>
+__device__ __forceinline__ void sat_entry(FlatCell<C> &cell, double *acc, uint32_t srows,
+                                          uint32_t lo, uint32_t n, float sc, float half,
+                                          uint32_t m1, uint32_t m2, uint32_t wm,
+                                          const SliceDyn &dyn, float inv, const Stencil &st,
+                                          const float (&xr)[3], uint32_t m6,
+                                          const float (&g0)[C],
+                                          const grad_t *__restrict__ grow) {
+    float g[C];
+#pragma unroll
+    for (uint32_t ch = 0; ch < C; ++ch) g[ch] = g0[ch];
+    bool first = true;
+    while (m6) {
+        const uint32_t a = 1u + (uint32_t)__builtin_ctz(m6);
+        m6 &= m6 - 1u;
+        if (!first) load_grad<grad_t, C>(grow + a * C, g);
+        first = false;
+        float p[3], x[3];
+        group_point<7>(xr, a, st, p);
+        bool ok = true;
+#pragma unroll
+        for (uint32_t d = 0; d < 3; ++d) {
+            x[d] = ge::dyn_map_t<POW2>(dyn, inv, p[d]);
+            ok = ok && !(x[d] < 0.0f) && !(x[d] > 1.0f);
+        }
+        if (ok) flat_take<C, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2, wm, x, g);
+    }
+}
+
+// The loads of one entry (position; the gradient rows of a centre entry, or
+// the first moved point's row of a satellite entry) and its walk.
+template <typename grad_t, uint32_t C, uint32_t GROUP, bool SAT>
+struct EntryIn {
+    float xs[3];
+    float gs[SAT ? 1 : GROUP][C];
+    uint32_t m6;
+};
+
+template <typename grad_t, uint32_t C, uint32_t GROUP, bool SAT>
+__device__ __forceinline__ void load_entry(EntryIn<grad_t, C, GROUP, SAT> &in,
+                                           const grad_t *__restrict__ gl,
+                                           const float *__restrict__ inputs, uint32_t tbase,
+                                           uint32_t v) {
+    const uint32_t s = tbase + (v & kIdMask);
+    load_pos3<3>(inputs, s, in.xs);
+    if constexpr (SAT) {
+        in.m6 = v >> kIdBits;
+        const uint32_t a = 1u + (uint32_t)__builtin_ctz(in.m6 | 0x40u);  // 7: none (not read)
+        load_grad<grad_t, C>(gl + ((size_t)s * GROUP + (a < GROUP ? a : 0u)) * C, in.gs[0]);
+    } else {
+        in.m6 = 0;
+        load_group_grads<grad_t, C, GROUP>(gl + (size_t)s * GROUP * C, in.gs);
+    }
+}
+
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, bool SAT>
+__device__ __forceinline__ void walk_entry(FlatCell<C> &cell, const EntryIn<grad_t, C, GROUP, SAT> &in,
+                                           const grad_t *__restrict__ gl, uint32_t tbase,
+                                           uint32_t v, double *acc, uint32_t srows, uint32_t lo,
+                                           uint32_t n, float sc, float half, uint32_t m1,
+                                           uint32_t m2, uint32_t wm, const SliceDyn &dyn,
+                                           float inv, const Stencil &st) {
+    if constexpr (SAT) {
+        sat_entry<grad_t, C, POW2, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2, wm, dyn, inv,
+                                         st, in.xs, in.m6, in.gs[0],
+                                         gl + (size_t)(tbase + (v & kIdMask)) * GROUP * C);
+    } else {
+        flat_entry<grad_t, C, POW2, GROUP, LEAD>(cell, acc, srows, lo, n, sc, half, m1, m2, wm,
+                                                 dyn, inv, st, in.xs, in.gs);
+    }
+}
+
+// A lane's entries [ea, eb) of one piece of a tile segment (entries at seg),
+// RB loads in flight per batch (clamped slots: every load is issued before
+// the first use).
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RB,
+          bool SAT>
 __device__ __forceinline__ void flat_piece(FlatCell<C> &cell, const grad_t *__restrict__ gl,
                                            const float *__restrict__ inputs,
                                            const uint16_t *__restrict__ seg, uint32_t tbase,
@@ -1060,103 +1226,102 @@ __device__ __forceinline__ void flat_piece(FlatCell<C> &cell, const grad_t *__re
                                            const SliceDyn &dyn, float inv, const Stencil &st) {
     for (uint32_t x = ea; x < eb; x += RB) {
         const uint32_t m = min(eb - x, RB);
-        uint32_t sid[RB];
+        uint32_t v[RB];
 #pragma unroll
-        for (uint32_t i = 0; i < RB; ++i) sid[i] = tbase + seg[x + min(i, m - 1)];
-        float xs[RB][3];
-        float gs[RB][GROUP][C];
+        for (uint32_t i = 0; i < RB; ++i) v[i] = seg[x + min(i, m - 1)];
+        EntryIn<grad_t, C, GROUP, SAT> in[RB];
 #pragma unroll
-        for (uint32_t i = 0; i < RB; ++i) {
-            load_pos3<3>(inputs, sid[i], xs[i]);
-            load_group_grads<grad_t, C, GROUP>(gl + (size_t)sid[i] * GROUP * C, gs[i]);
-        }
+        for (uint32_t i = 0; i < RB; ++i) load_entry(in[i], gl, inputs, tbase, v[i]);
 #pragma unroll
         for (uint32_t i = 0; i < RB; ++i)
             if (i < m)
-                flat_entry<grad_t, C, POW2, GROUP, LEAD>(cell, acc, srows, lo, n, sc, half, m1,
-                                                         m2, wm, dyn, inv, st, xs[i], gs[i]);
+                walk_entry<grad_t, C, POW2, GROUP, LEAD, SAT>(cell, in[i], gl, tbase, v[i], acc,
+                                                              srows, lo, n, sc, half, m1, m2, wm,
+                                                              dyn, inv, st);
     }
 }
 
+// One phase of a part's walk over a chunk of nc tiles (part + (cb + i) P):
+// the centre entries (front of each segment; every entry for GROUP 1) or the
+// satellite entries (back of each segment, stencil groups only).
 template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RUN,
-          uint32_t WMODE>
-__device__ __forceinline__ void flat_walk_level(
-    const grad_t *__restrict__ gl, const float *__restrict__ inputs, const uint32_t *counts,
-    const uint16_t *__restrict__ entries, double *acc, uint32_t *pre, uint32_t *wsum,
-    uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t ntiles, uint32_t srows,
-    uint32_t lo, uint32_t n, float sc, float half, uint32_t m1, uint32_t m2, uint32_t wm,
-    const SliceDyn &dyn, float inv, const Stencil &st) {
+          uint32_t WMODE, bool SAT>
+__device__ __forceinline__ void flat_walk_chunk(
+    FlatCell<C> &cell, const grad_t *__restrict__ gl, const float *__restrict__ inputs,
+    const uint32_t *counts, const uint16_t *__restrict__ entries, double *acc, uint32_t *pre,
+    uint32_t *wsum, uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t cb,
+    uint32_t nc, uint32_t srows, uint32_t lo, uint32_t n, float sc, float half, uint32_t m1,
+    uint32_t m2, uint32_t wm, const SliceDyn &dyn, float inv, const Stencil &st) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t waves = blockDim.x >> 6, nthr = blockDim.x;
-    const uint32_t nt = ntiles > part ? ceil_div(ntiles - part, P) : 0u;
-    FlatCell<C> cell;
-    cell.have = false;
-    cell.i0 = 0;
-    for (uint32_t cb = 0; cb < nt; cb += kChunkTiles) {
-        const uint32_t nc = min(nt - cb, kChunkTiles);
-        // the chunk's segments end to end: exclusive scan of the counts
-        const uint32_t v = tid < nc ? counts[(size_t)(part + (cb + tid) * P) * nb + b] : 0u;
-        uint32_t inc = v;
+    // the chunk's segments end to end: exclusive scan of the counts
+    const uint32_t raw = tid < nc ? counts[(size_t)(part + (cb + tid) * P) * nb + b] : 0u;
+    const uint32_t v = SAT ? (raw >> 16) : (raw & 0xFFFFu);
+    uint32_t inc = v;
 #pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += u;
-        }
-        if (lane == 63) wsum[wave] = inc;
-        __syncthreads();
-        uint32_t wofs = 0;
-        for (uint32_t w = 0; w < wave; ++w) wofs += wsum[w];
-        if (tid < nc) pre[tid] = wofs + inc - v;
-        if (tid == 0) {
-            uint32_t tot = 0;
-            for (uint32_t w = 0; w < waves; ++w) tot += wsum[w];
-            pre[nc] = tot;
-        }
-        __syncthreads();
-        const uint32_t E = pre[nc];
-        if constexpr (WMODE == 2) {
-            // per-wave pieces: wave w takes entries [E w / waves, E (w+1) / waves)
-            // and walks them segment piece by segment piece, the 64 lanes of
-            // the wave on one piece at a time (runs of ceil(piece / 64),
-            // bit-reversed), as k_walk does per whole segment
-            const uint32_t w0 = (uint32_t)((uint64_t)E * wave / waves);
-            const uint32_t w1 = (uint32_t)((uint64_t)E * (wave + 1) / waves);
-            if (w0 < w1) {
-                uint32_t a = 0, z = nc;  // pre[a] <= w0 < pre[z]
-                while (z - a > 1) {
-                    const uint32_t mid = (a + z) >> 1;
-                    if (pre[mid] <= w0) a = mid;
-                    else z = mid;
-                }
-                const uint32_t rl = __builtin_bitreverse32(lane) >> 26;
-                uint32_t ti = a, e = w0;
-                while (e < w1) {
-                    const uint32_t pe = min(pre[ti + 1], w1);
-                    const uint32_t cnt = pe - e;
-                    const uint32_t t = part + (cb + ti) * P;
-                    const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile + (e - pre[ti]);
-                    const uint32_t Qp = (cnt + 63u) >> 6;
-                    const uint32_t ea = min(rl * Qp, cnt), eb = min(ea + Qp, cnt);
-                    if (GROUP > 1 || Qp <= 1)
-                        flat_piece<grad_t, C, POW2, GROUP, LEAD, 1>(
-                            cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
-                            half, m1, m2, wm, dyn, inv, st);
-                    else if (Qp <= 4)
-                        flat_piece<grad_t, C, POW2, GROUP, LEAD, 4>(
-                            cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
-                            half, m1, m2, wm, dyn, inv, st);
-                    else
-                        flat_piece<grad_t, C, POW2, GROUP, LEAD, 8>(
-                            cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
-                            half, m1, m2, wm, dyn, inv, st);
-                    e = pe;
-                    ++ti;
-                    while (e < w1 && pre[ti + 1] == e) ++ti;  // empty segments
-                }
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t wofs = 0;
+    for (uint32_t w = 0; w < wave; ++w) wofs += wsum[w];
+    if (tid < nc) pre[tid] = wofs + inc - v;
+    if (tid == 0) {
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < waves; ++w) tot += wsum[w];
+        pre[nc] = tot;
+    }
+    __syncthreads();
+    const uint32_t E = pre[nc];
+    // entries of chunk tile ti: front slots [0, cnt) or back slots [kTile - cnt, kTile)
+    auto seg_of = [&](uint32_t ti) {
+        const uint32_t t = part + (cb + ti) * P;
+        const uint16_t *sg = entries + ((size_t)t * nb + b) * kTile;
+        return SAT ? sg + (kTile - (pre[ti + 1] - pre[ti])) : sg;
+    };
+    if constexpr (WMODE == 2) {
+        // per-wave pieces: wave w takes entries [E w / waves, E (w+1) / waves)
+        // and walks them segment piece by segment piece, the 64 lanes of the
+        // wave on one piece at a time (runs of ceil(piece / 64), bit-reversed),
+        // as k_walk does per whole segment
+        const uint32_t w0 = (uint32_t)((uint64_t)E * wave / waves);
+        const uint32_t w1 = (uint32_t)((uint64_t)E * (wave + 1) / waves);
+        if (w0 < w1) {
+            uint32_t a = 0, z = nc;  // pre[a] <= w0 < pre[z]
+            while (z - a > 1) {
+                const uint32_t mid = (a + z) >> 1;
+                if (pre[mid] <= w0) a = mid;
+                else z = mid;
             }
-            __syncthreads();  // pre / wsum are rewritten by the next chunk
-            continue;
+            const uint32_t rl = __builtin_bitreverse32(lane) >> 26;
+            uint32_t ti = a, e = w0;
+            while (e < w1) {
+                const uint32_t pe = min(pre[ti + 1], w1);
+                const uint32_t cnt = pe - e;
+                const uint32_t t = part + (cb + ti) * P;
+                const uint16_t *seg = seg_of(ti) + (e - pre[ti]);
+                const uint32_t Qp = (cnt + 63u) >> 6;
+                const uint32_t ea = min(rl * Qp, cnt), eb = min(ea + Qp, cnt);
+                if (GROUP > 1 || Qp <= 1)
+                    flat_piece<grad_t, C, POW2, GROUP, LEAD, 1, SAT>(
+                        cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                        half, m1, m2, wm, dyn, inv, st);
+                else if (Qp <= 4)
+                    flat_piece<grad_t, C, POW2, GROUP, LEAD, 4, SAT>(
+                        cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                        half, m1, m2, wm, dyn, inv, st);
+                else
+                    flat_piece<grad_t, C, POW2, GROUP, LEAD, 8, SAT>(
+                        cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                        half, m1, m2, wm, dyn, inv, st);
+                e = pe;
+                ++ti;
+                while (e < w1 && pre[ti + 1] == e) ++ti;  // empty segments
+            }
         }
+    } else {
         const uint32_t Q = ceil_div(E, nthr);
         // wave w takes the w-th 1/waves of the chunk, so its lanes stay on
         // neighbouring samples (one or two tile segments: positions and
@@ -1178,26 +1343,26 @@ __device__ __forceinline__ void flat_walk_level(
             // batch descriptor: (segment, first slot, size, tile base)
             auto batch_size = [&](uint32_t ee, uint32_t te) { return min(RUN, min(e1, te) - ee); };
             uint32_t m = batch_size(e, tend);
-            const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile;
+            const uint16_t *seg = seg_of(ti);
             uint32_t ids[RUN];
 #pragma unroll
             for (uint32_t i = 0; i < RUN; ++i) ids[i] = seg[slot + min(i, m - 1)];
             while (true) {
                 const uint32_t tbase = t * kTile;
-                // next batch: cursor and its ids, loaded ahead of this batch's data
+                // next batch: cursor and its entries, loaded ahead of this batch's data
                 uint32_t ne = e + m, nslot = slot + m, nti = ti, ntend = tend, nt2 = t;
                 const uint16_t *nseg = seg;
                 if (ne == ntend && ne < e1) {
                     // the next non-empty segment (ne < e1 <= E: one exists); an
                     // empty one would make a batch of zero entries whose clamped
-                    // id loads read slots never written
+                    // loads read slots never written
                     do {
                         ++nti;
                         ntend = pre[nti + 1];
                     } while (ntend == ne);
                     nslot = 0;
                     nt2 = part + (cb + nti) * P;
-                    nseg = entries + ((size_t)nt2 * nb + b) * kTile;
+                    nseg = seg_of(nti);
                 }
                 const bool more = ne < e1;
                 const uint32_t nm = more ? batch_size(ne, ntend) : 1u;
@@ -1206,21 +1371,15 @@ __device__ __forceinline__ void flat_walk_level(
 #pragma unroll
                     for (uint32_t i = 0; i < RUN; ++i) nids[i] = nseg[nslot + min(i, nm - 1)];
                 }
-                float xs[RUN][3];
-                float gs[RUN][GROUP][C];
+                EntryIn<grad_t, C, GROUP, SAT> in[RUN];
+#pragma unroll
+                for (uint32_t i = 0; i < RUN; ++i) load_entry(in[i], gl, inputs, tbase, ids[i]);
 #pragma unroll
                 for (uint32_t i = 0; i < RUN; ++i) {
-                    const uint32_t s = tbase + ids[i];
-                    load_pos3<3>(inputs, s, xs[i]);
-                    load_group_grads<grad_t, C, GROUP>(gl + (size_t)s * GROUP * C, gs[i]);
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < RUN; ++i) {
-                    if (i < m) {
-                        flat_entry<grad_t, C, POW2, GROUP, LEAD>(cell, acc, srows, lo, n, sc,
-                                                                 half, m1, m2, wm, dyn, inv,
-                                                                 st, xs[i], gs[i]);
-                    }
+                    if (i < m)
+                        walk_entry<grad_t, C, POW2, GROUP, LEAD, SAT>(
+                            cell, in[i], gl, tbase, ids[i], acc, srows, lo, n, sc, half, m1, m2,
+                            wm, dyn, inv, st);
                 }
                 if (!more) break;
                 e = ne;
@@ -1234,7 +1393,31 @@ __device__ __forceinline__ void flat_walk_level(
                 for (uint32_t i = 0; i < RUN; ++i) ids[i] = nids[i];
             }
         }
-        __syncthreads();  // pre / wsum are rewritten by the next chunk
+    }
+    __syncthreads();  // pre / wsum are rewritten by the next phase / chunk
+}
+
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RUN,
+          uint32_t RUN_SAT, uint32_t WMODE>
+__device__ __forceinline__ void flat_walk_level(
+    const grad_t *__restrict__ gl, const float *__restrict__ inputs, const uint32_t *counts,
+    const uint16_t *__restrict__ entries, double *acc, uint32_t *pre, uint32_t *wsum,
+    uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t ntiles, uint32_t srows,
+    uint32_t lo, uint32_t n, float sc, float half, uint32_t m1, uint32_t m2, uint32_t wm,
+    const SliceDyn &dyn, float inv, const Stencil &st) {
+    const uint32_t nt = ntiles > part ? ceil_div(ntiles - part, P) : 0u;
+    FlatCell<C> cell;
+    cell.have = false;
+    cell.i0 = 0;
+    for (uint32_t cb = 0; cb < nt; cb += kChunkTiles) {
+        const uint32_t nc = min(nt - cb, kChunkTiles);
+        flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN, WMODE, false>(
+            cell, gl, inputs, counts, entries, acc, pre, wsum, nb, b, part, P, cb, nc, srows, lo,
+            n, sc, half, m1, m2, wm, dyn, inv, st);
+        if constexpr (GROUP > 1)
+            flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN_SAT, WMODE, true>(
+                cell, gl, inputs, counts, entries, acc, pre, wsum, nb, b, part, P, cb, nc, srows,
+                lo, n, sc, half, m1, m2, wm, dyn, inv, st);
     }
     flat_flush<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm);
 }
@@ -1304,8 +1487,9 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     // entries whose loads are in flight together per lane (and the next
     // batch's ids): 6 keeps the f16 walk within 128 VGPRs (8 spilled)
     constexpr uint32_t RUN = GROUP > 1 ? (uint32_t)DFHIP_WALK_RUN7 : (uint32_t)DFHIP_WALK_RUN;
+    constexpr uint32_t RUN_SAT = DFHIP_WALK_RUN_SAT;
 #define DFHIP_FLAT(LD)                                                                         \
-    flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN, WMODE>(gl, inputs, counts, entries, acc, pre,    \
+    flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN, RUN_SAT, WMODE>(gl, inputs, counts, entries, acc, pre, \
                                                      wsum, nb, b, part, P, ntiles, srows, lo, \
                                                      n, sc, half, m1, m2, wm, dyn, inv, st)
     if (lead >= 3) DFHIP_FLAT(3);
