@@ -178,18 +178,21 @@ __device__ __forceinline__ half4 relu_h4(f4 a) {
                                               (half_t)0.0f});
 }
 
-// W2R: the layer-2 weight operands come from w2op (registers, loaded once per
-// kernel) instead of LDS.
-template <typename E, bool P, bool W2R = false>
+// W2R / W1R / W3R: the layer's weight operands come from w2op / w1op / w3op
+// (registers, loaded once per kernel) instead of LDS.
+template <typename E, bool P, bool W2R = false, bool W1R = false, bool W3R = false>
 __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem<E>::v8 xb, int c,
                                              int h, FwdG<E, P> &F,
-                                             const typename Elem<E>::v8 (*w2op)[2] = nullptr) {
+                                             const typename Elem<E>::v8 (*w2op)[2] = nullptr,
+                                             const typename Elem<E>::v8 *w1op = nullptr,
+                                             const typename Elem<E>::v8 *w3op = nullptr) {
     constexpr bool kBf = std::is_same<E, bf16_t>::value;
     constexpr bool kPkH = P && std::is_same<E, half_t>::value;  // packed f16 (the backward)
     f4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        acc[t] = mfma(a_nat(W.w1, kLd32, 16 * t + c, 0, h), xb, bias4(W.b1, 16 * t + 4 * h));
+        acc[t] = mfma(W1R ? w1op[t] : a_nat(W.w1, kLd32, 16 * t + c, 0, h), xb,
+                      bias4(W.b1, 16 * t + 4 * h));
         if constexpr (kBf) {
             F.a1[t] = relu_bf4(acc[t]);
         } else if constexpr (kPkH) {
@@ -223,7 +226,8 @@ __device__ __forceinline__ void forward_tile(const WeightsG<E> &W, typename Elem
     }
     f4 o = bias4(W.b3, 4 * h);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) o = mfma(a_perm(W.w3, kLd64, c, s, h), b_from_tiles(F.a2, s), o);
+    for (int s = 0; s < 2; ++s)
+        o = mfma(W3R ? w3op[s] : a_perm(W.w3, kLd64, c, s, h), b_from_tiles(F.a2, s), o);
     F.o = o;
 }
 

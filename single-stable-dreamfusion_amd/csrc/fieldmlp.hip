@@ -145,12 +145,13 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
 constexpr int kBwdWaves = 4;
 // Weight operands held in registers for the whole kernel instead of re-read
 // from LDS every tile (bit 0: W2 of the forward and W2^T, 64 VGPRs; bit 1:
-// W1^T; bit 2: W3^T).  Field backward per C2 step / textureless step: none
-// 107 / 660 us, bit 0 94 / 578, all three 92 / 558 (230 VGPRs, still 2 waves
+// W1^T; bit 2: W3^T; bit 3: the forward's W1; bit 4: the forward's W3).
+// Field backward per C2 step / textureless step: none 107 / 660 us, bit 0
+// 94 / 578, bits 0-2 92 / 558, all five 90 / 545 (250 VGPRs, still 2 waves
 // per SIMD).  The forward kernel's W2 in registers (4 waves per SIMD instead
 // of 5) was slower: 80 -> 83 us.
 #ifndef DFHIP_BWD_WREG
-#define DFHIP_BWD_WREG 7
+#define DFHIP_BWD_WREG 31
 #endif
 constexpr int kBwdWreg = DFHIP_BWD_WREG;
 constexpr int kStLd = 312;  // stage row stride (halves): 156 dwords = 4 mod 64 -> the
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
     for (int i = 0; i < 10; ++i) acc[i] = f4{0, 0, 0, 0};
     const v4 ones = v4{(E)1.0f, (E)1.0f, (E)1.0f, (E)1.0f};
     // weight operands kept in registers (kBwdWreg)
-    v8 w2op[4][2], w2top[4][2], w1top[2][2], w3top[4];
+    v8 w2op[4][2], w2top[4][2], w1top[2][2], w3top[4], w1op[4], w3op[2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
 #pragma unroll
@@ -266,6 +267,8 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             if ((kBwdWreg & 2) && u < 2) w1top[u][s2] = a_perm(T.w1t, kLd64, 16 * u + c, s2, h);
         }
         if (kBwdWreg & 4) w3top[u] = a_nat(T.w3t, kLd32, 16 * u + c, 0, h);
+        if (kBwdWreg & 8) w1op[u] = a_nat(W.w1, kLd32, 16 * u + c, 0, h);
+        if ((kBwdWreg & 16) && u < 2) w3op[u] = a_perm(W.w3, kLd64, c, u, h);
     }
 
     const uint32_t tiles = ceil_div(M, 16u);
@@ -281,7 +284,8 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
         const uint32_t sample = tile * 16 + c;
         const bool valid = sample < M;
         FwdG<E, true> F;  // packed activations (f16 pairs per VGPR)
-        forward_tile<E, true, (kBwdWreg & 1) != 0>(W, cur.xb, c, h, F, w2op);
+        forward_tile<E, true, (kBwdWreg & 1) != 0, (kBwdWreg & 8) != 0, (kBwdWreg & 16) != 0>(
+            W, cur.xb, c, h, F, w2op, w1op, w3op);
         // dL/d(output layer), in E as autocast's backward produces it
         E dO[4] = {(E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
         if (h == 0 && valid) {
