@@ -26,3 +26,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 python tools/prof_top.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/rocprof_top.txt
 cat $OUT/rocprof_top.txt
 python tools/roofline_check.py $OUT/bench.json $OUT/prof/run_kernel_trace.csv | tee $OUT/roofline_check.json
+# the textureless step's kernels (the shaded steps' profile)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/shprof -o run \
+    -- python tools/shade_steps.py textureless 30 > $OUT/shade_prof.log 2>&1 \
+    || { echo "shade prof failed"; tail -20 $OUT/shade_prof.log; exit 5; }
+python tools/prof_top.py $OUT/shprof/run_kernel_stats.csv 25 > $OUT/rocprof_shade_top.txt
+head -8 $OUT/rocprof_shade_top.txt
