@@ -62,14 +62,16 @@ template <typename T>
 struct WeightsG {
     T w1[kHid * kLd32];  // [n1][f]
     T w2[kHid * kLd64];  // [n2][n1]
-    T w3[16 * kLd64];    // [o][n2], rows 4..15 zero
-    float b1[kHid], b2[kHid], b3[16];  // f32 of the T-rounded biases; b3 rows 4.. zero
+    T w3[16 * kLd64];    // [row][n2]: output r in row 4 r (lane group r of the
+                         // accumulator tile, element 0), the other rows zero
+    float b1[kHid], b2[kHid], b3[16];  // f32 of the T-rounded biases; b3 as w3's rows
 };
 template <typename T>
 struct WeightsTG {       // backward only
     T w1t[kIn * kLd64];  // [f][n1]
     T w2t[kHid * kLd64]; // [n1][n2]
-    T w3t[kHid * kLd32]; // [n2][o], o 4..31 zero
+    T w3t[kHid * kLd32]; // [n2][k]: output r at k = 8 r (the B operand's lane group r,
+                         // element 0), the other columns zero
 };
 typedef WeightsG<half_t> Weights;
 typedef WeightsTG<half_t> WeightsT;
@@ -97,18 +99,21 @@ __device__ void load_weights(WeightsG<E> &W, typename Id<WeightsTG<E>>::type *T,
         W.w2[(i / kHid) * kLd64 + i % kHid] = v;
         if (T) T->w2t[(i % kHid) * kLd64 + i / kHid] = v;
     }
-    for (int i = threadIdx.x; i < 16 * kHid; i += blockDim.x)
-        W.w3[(i / kHid) * kLd64 + i % kHid] = i < kOut * kHid ? (E)w3[i] : (E)0.0f;
+    for (int i = threadIdx.x; i < 16 * kHid; i += blockDim.x) {
+        const int row = i / kHid, n2 = i % kHid;
+        W.w3[row * kLd64 + n2] = (row & 3) == 0 ? (E)w3[(row >> 2) * kHid + n2] : (E)0.0f;
+    }
     if (T)
         for (int i = threadIdx.x; i < kHid * 32; i += blockDim.x) {
             const int n2 = i / 32, o = i % 32;
-            T->w3t[n2 * kLd32 + o] = o < kOut ? (E)w3[o * kHid + n2] : (E)0.0f;
+            T->w3t[n2 * kLd32 + o] = (o & 7) == 0 ? (E)w3[(o >> 3) * kHid + n2] : (E)0.0f;
         }
     for (int i = threadIdx.x; i < kHid; i += blockDim.x) {
         W.b1[i] = (float)(E)b1[i];
         W.b2[i] = (float)(E)b2[i];
     }
-    for (int i = threadIdx.x; i < 16; i += blockDim.x) W.b3[i] = i < kOut ? (float)(E)b3[i] : 0.0f;
+    for (int i = threadIdx.x; i < 16; i += blockDim.x)
+        W.b3[i] = (i & 3) == 0 ? (float)(E)b3[i >> 2] : 0.0f;
 }
 
 // A operand, natural k order: row `row` of a row-major [*, ld] f16 matrix,
@@ -164,7 +169,7 @@ __device__ __forceinline__ f4 bias4(const float *b, int row0) {
 template <typename E, bool P = false>
 struct FwdG {
     typename TilesT<E, P>::type a1, a2;  // [tile][reg]: neuron 16 t + 4 h + r of sample c
-    f4 o;                                // rows 4h + r (only h == 0 valid: outputs 0..3)
+    f4 o;                                // rows 4h + r: o[0] of lane group h is output h
 };
 typedef FwdG<half_t> Fwd;
 

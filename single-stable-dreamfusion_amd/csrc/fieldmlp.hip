@@ -56,31 +56,46 @@ __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     const uint32_t tiles = ceil_div(M, 16u);
-    for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles;
-         tile += waves) {
+    // (x + bound) / (2 bound) (grid.py:142): for a power-of-two bound the
+    // quotient is the product with the exact reciprocal (no division sequence)
+    const float ext = 2.0f * bound;
+    const bool pow2 = (__float_as_uint(ext) & 0x007FFFFFu) == 0u && ext >= 1.17549435e-38f &&
+                      ext < 1.70141183e38f;
+    const float rext = 1.0f / ext;
+    // positions of the wave's next tile, loaded while this one runs (12 B per
+    // lane spilled at 5 waves per SIMD; still 77.5 -> 76.7 us per C2 step,
+    // 415 -> 404 us textureless)
+    uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    float xn[3] = {0.0f, 0.0f, 0.0f};
+    if (tile * 16 + c < M)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) xn[d] = xyz[(size_t)(tile * 16 + c) * 3 + d];
+    for (; tile < tiles; tile += waves) {
         // bf16: the weight operands are re-read from LDS every tile (a memory
         // clobber keeps LICM from hoisting them; hoisted, they spilled)
         if constexpr (!std::is_same<E, half_t>::value) asm volatile("" ::: "memory");
         const uint32_t sample = tile * 16 + c;
         const bool valid = sample < M;
-        float x[3] = {0.0f, 0.0f, 0.0f}, x01[3] = {-1.0f, -1.0f, -1.0f};
+        float x[3] = {xn[0], xn[1], xn[2]}, x01[3] = {-1.0f, -1.0f, -1.0f};
+        const uint32_t nsample = (tile + waves) * 16 + c;
+        if (nsample < M)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) xn[d] = xyz[(size_t)nsample * 3 + d];
         if (valid)
 #pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                x[d] = xyz[(size_t)sample * 3 + d];
-                x01[d] = (x[d] + bound) / (2.0f * bound);
-            }
+            for (int d = 0; d < 3; ++d)
+                x01[d] = pow2 ? (x[d] + bound) * rext : (x[d] + bound) / ext;
         const v8 xb = valid ? grid_features<E, QUAD>(table, LK, align, x01, h, quads) : v8{};
         if (enc && valid) *reinterpret_cast<v8 *>(enc + (size_t)sample * kIn + 8 * h) = xb;
         FwdG<E> F;
         forward_tile(W, xb, c, h, F);
-        if (h == 0 && valid) {
-            const float y = (float)(E)F.o[0] + gaussian(x);
-            sigma[sample] = expf(y);
-#pragma unroll
-            for (int r = 1; r < 4; ++r) {
-                const float v = (float)(E)F.o[r];
-                rgb[(size_t)sample * 3 + r - 1] = (rgb_t)(E)(1.0f / (1.0f + expf(-v)));
+        // lane group h holds output h: density (h = 0) or albedo channel h - 1
+        if (valid) {
+            if (h == 0) {
+                sigma[sample] = expf((float)(E)F.o[0] + gaussian(x));
+            } else {
+                const float v = (float)(E)F.o[0];
+                rgb[(size_t)sample * 3 + h - 1] = (rgb_t)(E)(1.0f / (1.0f + expf(-v)));
             }
         }
     }
@@ -113,13 +128,12 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
         Fwd F;
         forward_tile(W, xb, c, h, F);
         xb = xn;
-        if (h == 0 && sample < M) {
-            const float y = (float)(half_t)F.o[0] + gaussian(x);
-            sigma[sample] = expf(y);
-#pragma unroll
-            for (int r = 1; r < 4; ++r) {
-                const float v = (float)(half_t)F.o[r];
-                rgb[(size_t)sample * 3 + r - 1] = (rgb_t)(half_t)(1.0f / (1.0f + expf(-v)));
+        if (sample < M) {  // lane group h holds output h
+            if (h == 0) {
+                sigma[sample] = expf((float)(half_t)F.o[0] + gaussian(x));
+            } else {
+                const float v = (float)(half_t)F.o[0];
+                rgb[(size_t)sample * 3 + h - 1] = (rgb_t)(half_t)(1.0f / (1.0f + expf(-v)));
             }
         }
     }
@@ -154,6 +168,9 @@ constexpr int kBwdWaves = 4;
 #define DFHIP_BWD_WREG 31
 #endif
 constexpr int kBwdWreg = DFHIP_BWD_WREG;
+#ifndef DFHIP_BWD_PINGPONG
+#define DFHIP_BWD_PINGPONG 0
+#endif
 constexpr int kStLd = 312;  // stage row stride (halves): 156 dwords = 4 mod 64 -> the
                             // 32 lanes of an 8-byte write hit 64 distinct banks
 constexpr int kColX = 0, kColA1 = 32, kColA2 = 96, kColD1 = 160, kColD2 = 224, kColDO = 288;
@@ -204,26 +221,27 @@ __device__ __forceinline__ void st_write4(StageT<E> &S, int sample, int col, E v
 }
 
 // One wave's inputs for a 16-sample tile: encoder features (every lane), and
-// for the output-layer lanes (h == 0) positions and incoming gradients.
-template <typename E>
+// the incoming gradient of the lane group's output (h = 0: the density's, with
+// the position for the Gaussian blob; h > 0: albedo channel h - 1's) — as
+// loaded (no conversion), so a prefetch does not wait for its loads.
+template <typename E, typename rgb_t>
 struct TileIn {
     typename Elem<E>::v8 xb;
-    float xyz[3], gs, grgb[3];
+    float xyz[3], gs;
+    rgb_t grgb;
 };
 
 template <typename E, typename rgb_t>
-__device__ __forceinline__ void load_tile(TileIn<E> &g, uint32_t tile, const E *enc,
+__device__ __forceinline__ void load_tile(TileIn<E, rgb_t> &g, uint32_t tile, const E *enc,
                                           const float *xyz, const float *grad_sigma,
                                           const rgb_t *grad_rgb, uint32_t M, int c, int h) {
     const uint32_t sample = tile * 16 + c;
     g.xb = load_x(enc, sample, M, h);
     const bool v = (h == 0) && sample < M;
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        g.xyz[d] = v ? xyz[(size_t)sample * 3 + d] : 0.0f;
-        g.grgb[d] = v ? (float)grad_rgb[(size_t)sample * 3 + d] : 0.0f;
-    }
+    for (int d = 0; d < 3; ++d) g.xyz[d] = v ? xyz[(size_t)sample * 3 + d] : 0.0f;
     g.gs = v ? grad_sigma[sample] : 0.0f;
+    g.grgb = (h > 0 && sample < M) ? grad_rgb[(size_t)sample * 3 + h - 1] : (rgb_t)0.0f;
 }
 
 // PERM: enc holds the fused forward's permuted feature order (k_field_fwd_fused);
@@ -274,33 +292,33 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
     const uint32_t tiles = ceil_div(M, 16u);
     const uint32_t per_round = gridDim.x * kBwdWaves;
     const uint32_t rounds = ceil_div(tiles, per_round);
-    TileIn<E> cur;
-    uint32_t tile = blockIdx.x * kBwdWaves + wave;
-    load_tile<E, rgb_t>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
-    for (uint32_t round = 0; round < rounds; ++round, tile += per_round) {
-        // the next round's inputs are loaded while this one is processed
-        TileIn<E> nxt;
-        load_tile<E, rgb_t>(nxt, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    // dO^T image columns 4..15 are zero for good (each round writes 0..3)
+    st_write4(S, c, kColDO + 4 * h, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f);
+    // one round: the tile's forward recompute, backward and its share of the
+    // weight gradients (every wave runs the same number of rounds: barriers)
+    auto round_of = [&](const TileIn<E, rgb_t> &cur, uint32_t tile) {
         const uint32_t sample = tile * 16 + c;
         const bool valid = sample < M;
         FwdG<E, true> F;  // packed activations (f16 pairs per VGPR)
         forward_tile<E, true, (kBwdWreg & 1) != 0, (kBwdWreg & 8) != 0, (kBwdWreg & 16) != 0>(
             W, cur.xb, c, h, F, w2op, w1op, w3op);
-        // dL/d(output layer), in E as autocast's backward produces it
-        E dO[4] = {(E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
-        if (h == 0 && valid) {
-            const float y = (float)(E)F.o[0] + gaussian(cur.xyz);
-            // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
-            const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
-            dO[0] = (E)(cur.gs * expf(yc));
-#pragma unroll
-            for (int r = 1; r < 4; ++r) {
-                const float a = (float)(E)(1.0f / (1.0f + expf(-(float)(E)F.o[r])));
-                const float g = (float)(E)cur.grgb[r - 1];
-                dO[r] = (E)(g * (1.0f - a) * a);  // sigmoid_backward in E (opmath f32)
+        // dL/d(output h), in E as autocast's backward produces it: lane group h
+        // holds output h (F.o[0]) and its incoming gradient
+        E dOh = (E)0.0f;
+        if (valid) {
+            if (h == 0) {
+                const float y = (float)(E)F.o[0] + gaussian(cur.xyz);
+                // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
+                const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
+                dOh = (E)(cur.gs * expf(yc));
+            } else {
+                const float a = (float)(E)(1.0f / (1.0f + expf(-(float)(E)F.o[0])));
+                const float g = (float)(E)(float)cur.grgb;
+                dOh = (E)(g * (1.0f - a) * a);  // sigmoid_backward in E (opmath f32)
             }
         }
-        const v8 dob = v8{dO[0], dO[1], dO[2], dO[3], (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
+        // B operand of W3^T dO^T: output h at k = 8 h (T.w3t's layout)
+        const v8 dob = v8{dOh, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
         // ReLU mask of an accumulator tile by the layer's activations
         constexpr bool kBf = std::is_same<E, bf16_t>::value;
         auto mask = [&](const auto &act, const f4 &d, auto &dst) {
@@ -373,7 +391,7 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD1 + col) = dz1[t];
             *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD2 + col) = dz2[t];
         }
-        st_write4(S, c, kColDO + 4 * h, dO[0], dO[1], dO[2], dO[3]);  // h > 0: zeros
+        S.v[c * kStLd + kColDO + h] = dOh;  // columns 4..15 stay zero
         __syncthreads();
         // weight gradients over the round's 4 x 16 samples.  Tile ownership:
         //   wave 0 / 1: W2 rows tn in {0,1} / {2,3} x 4 column tiles, b2 rows tn
@@ -420,8 +438,33 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             }
         }
         __syncthreads();  // the images are rewritten next round
+    };
+    // two input buffers in turn: round r + 1's loads are issued before round
+    // r runs and first waited on in round r + 1 (a copy of the prefetched
+    // registers at the end of each round would wait for them there)
+    uint32_t tile = blockIdx.x * kBwdWaves + wave;
+#if DFHIP_BWD_PINGPONG
+    TileIn<E, rgb_t> ta, tb;
+    load_tile<E, rgb_t>(ta, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    for (uint32_t round = 0; round < rounds; round += 2) {
+        load_tile<E, rgb_t>(tb, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        round_of(ta, tile);
+        tile += per_round;
+        if (round + 1 >= rounds) break;  // uniform
+        load_tile<E, rgb_t>(ta, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        round_of(tb, tile);
+        tile += per_round;
+    }
+#else
+    TileIn<E, rgb_t> cur;
+    load_tile<E, rgb_t>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    for (uint32_t round = 0; round < rounds; ++round, tile += per_round) {
+        TileIn<E, rgb_t> nxt;  // the next round's inputs, loaded while this one runs
+        load_tile<E, rgb_t>(nxt, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        round_of(cur, tile);
         cur = nxt;
     }
+#endif
 
     // ---- this workgroup's partial: every entry written by exactly one lane.
     // Accumulator element r of lane (c, h): row 4h + r, column c of the tile.
@@ -462,6 +505,221 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
         if (wave == 2 && lane == 0)
 #pragma unroll
             for (int r = 0; r < 4; ++r) out[kOffB3 + r] = acc[8][r];
+    }
+}
+
+// ---------------------------------------------------------------- backward, one wave per SIMD
+// k_field_bwd1: the same arithmetic as k_field_bwd with the work split per
+// WAVE instead of per workgroup round.  One workgroup of 4 waves per CU (one
+// wave per SIMD, up to 512 registers: the weight operands in VGPRs, the 37
+// weight-gradient accumulator tiles in AGPRs); the weights are staged in LDS
+// once, after which the waves never synchronise: each takes rounds of two
+// 16-sample tiles, writes their activation images into its own two LDS stage
+// buffers and forms all 37 weight-gradient tiles over those 32 samples (one
+// 16x16x32 MFMA each, k = the 32 samples).  Partials are per wave.
+constexpr int kBwd1Waves = 4;
+
+template <typename E, typename rgb_t, bool PERM>
+__global__ __launch_bounds__(64 * kBwd1Waves, 1) void k_field_bwd1(
+    const E *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
+    const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
+    const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t cap,
+    const int32_t *__restrict__ m_dev,
+    E *__restrict__ d_enc,          // [16, cap, 2] (level-major)
+    float *__restrict__ partial) {  // [gridDim.x * kBwd1Waves, kParams]
+    typedef typename Elem<E>::v8 v8;
+    typedef typename Elem<E>::v4 v4;
+    __shared__ WeightsG<E> W;
+    __shared__ WeightsTG<E> T;
+    __shared__ StageT<E> stage[2 * kBwd1Waves];
+    load_weights<PERM>(W, &T, w1, b1, w2, b2, w3, b3);
+    const uint32_t M = active_count(m_dev, cap);
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    StageT<E> *S2 = stage + 2 * wave;
+    __syncthreads();  // the only workgroup barrier
+
+    v8 w2op[4][2], w2top[4][2], w1top[2][2], w3top[4], w1op[4], w3op[2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            w2op[u][s2] = a_perm(W.w2, kLd64, 16 * u + c, s2, h);
+            w2top[u][s2] = a_perm(T.w2t, kLd64, 16 * u + c, s2, h);
+            if (u < 2) w1top[u][s2] = a_perm(T.w1t, kLd64, 16 * u + c, s2, h);
+        }
+        w3top[u] = a_nat(T.w3t, kLd32, 16 * u + c, 0, h);
+        w1op[u] = a_nat(W.w1, kLd32, 16 * u + c, 0, h);
+        if (u < 2) w3op[u] = a_perm(W.w3, kLd64, c, u, h);
+    }
+    // weight-gradient accumulators: W2 [tn][tm], b2 [tn], W1 [tn][tf], b1 [tn],
+    // W3 [tm], b3 (row-tile tn / tm of 16 neurons; ones operand for biases)
+    f4 gW2[4][4], gB2[4], gW1[4][2], gB1[4], gW3[4], gB3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gW2[i][j] = f4{0, 0, 0, 0};
+        gW1[i][0] = gW1[i][1] = gB2[i] = gB1[i] = gW3[i] = f4{0, 0, 0, 0};
+    }
+    gB3 = f4{0, 0, 0, 0};
+    const v4 ones = v4{(E)1.0f, (E)1.0f, (E)1.0f, (E)1.0f};
+    const v8 ones8 = __builtin_shufflevector(ones, ones, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)  // dO^T image columns 4..15 stay zero
+        st_write4(S2[u], c, kColDO + 4 * h, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f);
+
+    constexpr bool kBf = std::is_same<E, bf16_t>::value;
+    auto mask = [&](const auto &act, const f4 &d, auto &dst) {
+        if constexpr (kBf) {
+            const f4 m = {(float)act[0] > 0.0f ? d[0] : 0.0f, (float)act[1] > 0.0f ? d[1] : 0.0f,
+                          (float)act[2] > 0.0f ? d[2] : 0.0f, (float)act[3] > 0.0f ? d[3] : 0.0f};
+            dst = __builtin_convertvector(m, bf4);
+        } else {  // f16 ReLU backward on packed pairs (k_field_bwd)
+            typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+            const half4 dh = __builtin_convertvector(d, half4);
+            u2 ab, db;
+            __builtin_memcpy(&ab, &act, 8);
+            __builtin_memcpy(&db, &dh, 8);
+            const u2 nz = ((ab & 0x7FFF7FFFu) + 0x7FFF7FFFu) & 0x80008000u;
+            const u2 r = db & ((nz >> 15u) * 0xFFFFu);
+            __builtin_memcpy(&dst, &r, 8);
+        }
+    };
+    // one tile: forward recompute, backward, encoder gradient, LDS image
+    auto tile_of = [&](const TileIn<E, rgb_t> &cur, uint32_t tile, StageT<E> &S) {
+        const uint32_t sample = tile * 16 + c;
+        const bool valid = sample < M;
+        FwdG<E, true> F;
+        forward_tile<E, true, true, true, true>(W, cur.xb, c, h, F, w2op, w1op, w3op);
+        E dOh = (E)0.0f;  // lane group h: output h (k_field_bwd)
+        if (valid) {
+            if (h == 0) {
+                const float y = (float)(E)F.o[0] + gaussian(cur.xyz);
+                const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
+                dOh = (E)(cur.gs * expf(yc));
+            } else {
+                const float a = (float)(E)(1.0f / (1.0f + expf(-(float)(E)F.o[0])));
+                const float g = (float)(E)(float)cur.grgb;
+                dOh = (E)(g * (1.0f - a) * a);
+            }
+        }
+        const v8 dob = v8{dOh, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
+        typename TilesT<E, true>::type dz2, dz1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mask(F.a2[u], mfma(w3top[u], dob, f4{0, 0, 0, 0}), dz2[u]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            f4 d = f4{0, 0, 0, 0};
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) d = mfma(w2top[t][s2], b_from_tiles(dz2, s2), d);
+            mask(F.a1[t], d, dz1[t]);
+        }
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            f4 d = f4{0, 0, 0, 0};
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) d = mfma(w1top[f][s2], b_from_tiles(dz1, s2), d);
+            if (valid) {
+                const uint32_t lv = 8 * f + 2 * h;
+                typedef E e2v __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<e2v *>(d_enc + ((size_t)lv * cap + sample) * 2) =
+                    e2v{(E)d[0], (E)d[1]};
+                *reinterpret_cast<e2v *>(d_enc + ((size_t)(lv + 1) * cap + sample) * 2) =
+                    e2v{(E)d[2], (E)d[3]};
+            }
+        }
+        *reinterpret_cast<v8 *>(S.v + c * kStLd + kColX + 8 * h) = cur.xb;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int col = 16 * t + 4 * h;
+            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColA1 + col) = F.a1[t];
+            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColA2 + col) = F.a2[t];
+            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD1 + col) = dz1[t];
+            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD2 + col) = dz2[t];
+        }
+        S.v[c * kStLd + kColDO + h] = dOh;
+    };
+    // the weight gradients of the wave's two staged tiles (k = 32 samples)
+    auto wgrad = [&]() {
+        auto tr2 = [&](int c0) {
+            const v4 lo = tr_operand(S2[0], c0, lane);
+            const v4 hi = tr_operand(S2[1], c0, lane);
+            return (v8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        };
+        v8 ba1[4], ba2[4], bx[2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            ba1[t] = tr2(kColA1 + 16 * t);
+            ba2[t] = tr2(kColA2 + 16 * t);
+        }
+        bx[0] = tr2(kColX);
+        bx[1] = tr2(kColX + 16);
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+            const v8 a2 = tr2(kColD2 + 16 * tn);
+#pragma unroll
+            for (int tm = 0; tm < 4; ++tm) gW2[tn][tm] = mfma(a2, ba1[tm], gW2[tn][tm]);
+            gB2[tn] = mfma(a2, ones8, gB2[tn]);
+            const v8 a1 = tr2(kColD1 + 16 * tn);
+#pragma unroll
+            for (int tf = 0; tf < 2; ++tf) gW1[tn][tf] = mfma(a1, bx[tf], gW1[tn][tf]);
+            gB1[tn] = mfma(a1, ones8, gB1[tn]);
+        }
+        const v8 ao = tr2(kColDO);
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) gW3[tm] = mfma(ao, ba2[tm], gW3[tm]);
+        gB3 = mfma(ao, ones8, gB3);
+    };
+
+    const uint32_t tiles = ceil_div(M, 16u);
+    const uint32_t nw = gridDim.x * kBwd1Waves;
+    const uint32_t rounds = ceil_div(tiles, 2u * nw);
+    uint32_t pair = blockIdx.x * kBwd1Waves + wave;
+    TileIn<E, rgb_t> c0, c1;
+    load_tile<E, rgb_t>(c0, 2 * pair, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    load_tile<E, rgb_t>(c1, 2 * pair + 1, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    for (uint32_t round = 0; round < rounds; ++round, pair += nw) {
+        TileIn<E, rgb_t> n0, n1;  // the next round's inputs, loaded while this one runs
+        load_tile<E, rgb_t>(n0, 2 * (pair + nw), enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        load_tile<E, rgb_t>(n1, 2 * (pair + nw) + 1, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        tile_of(c0, 2 * pair, S2[0]);
+        tile_of(c1, 2 * pair + 1, S2[1]);
+        __builtin_amdgcn_wave_barrier();  // the wave's own images (LDS ops in order)
+        wgrad();
+        __builtin_amdgcn_wave_barrier();  // read before the next round rewrites them
+        c0 = n0;
+        c1 = n1;
+    }
+
+    // ---- this wave's partial: accumulator element r of lane (c, h) is row
+    // 4h + r, column c of its tile; every entry written by exactly one lane
+    float *out = partial + ((size_t)blockIdx.x * kBwd1Waves + wave) * kParams;
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = 16 * tn + 4 * h + r;
+#pragma unroll
+            for (int tm = 0; tm < 4; ++tm) out[kOffW2 + n * kHid + 16 * tm + c] = gW2[tn][tm][r];
+#pragma unroll
+            for (int tf = 0; tf < 2; ++tf) {
+                const int p = 16 * tf + c;
+                out[kOffW1 + n * kIn + (PERM ? perm_feature(p) : p)] = gW1[tn][tf][r];
+            }
+            if (c == 0) {
+                out[kOffB2 + n] = gB2[tn][r];
+                out[kOffB1 + n] = gB1[tn][r];
+            }
+        }
+    }
+    if (h == 0) {
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[kOffW3 + r * kHid + 16 * tm + c] = gW3[tm][r];
+        if (c == 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[kOffB3 + r] = gB3[r];
     }
 }
 
@@ -522,13 +780,33 @@ static uint32_t resident_blocks(K kern) {
     return cached;
 }
 
+// Backward form (DFHIP_FIELD_BWD1=1: k_field_bwd1, one wave per SIMD, per-wave
+// partials; 0: k_field_bwd, four-wave rounds, per-workgroup partials).
+static bool use_bwd1() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("DFHIP_FIELD_BWD1");
+        v = e ? (atoi(e) != 0) : 0;
+    }
+    return v != 0;
+}
+
 static uint32_t bwd_blocks(uint32_t M) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (use_bwd1()) {  // one workgroup per CU, a tile pair per wave and round
+        const uint32_t want = ceil_div(ceil_div(M, 32u), (uint32_t)kBwd1Waves);
+        const uint32_t cap = (uint32_t)cus;
+        return want < cap ? (want ? want : 1u) : cap;
+    }
     const uint32_t want = ceil_div(ceil_div(M, 16u), (uint32_t)kBwdWaves);
     const uint32_t cap = 2u * (uint32_t)cus;  // two workgroups per CU
     return want < cap ? (want ? want : 1u) : cap;
+}
+// partial rows the backward writes for M rows (k_field_wgrad_sum's parts)
+static uint32_t bwd_parts(uint32_t M) {
+    return use_bwd1() ? bwd_blocks(M) * (uint32_t)kBwd1Waves : bwd_blocks(M);
 }
 
 }  // namespace fm
@@ -539,7 +817,7 @@ using namespace dfhip::fm;
 
 extern "C" uint32_t dfhip_field_mlp_params(void) { return (uint32_t)kParams; }
 
-extern "C" uint32_t dfhip_field_mlp_backward_parts(uint32_t M) { return bwd_blocks(M); }
+extern "C" uint32_t dfhip_field_mlp_backward_parts(uint32_t M) { return bwd_parts(M); }
 
 extern "C" int dfhip_field_mlp_forward(const void *enc, const float *xyz, const float *w1,
                                        const float *b1, const float *w2, const float *b2,
@@ -588,19 +866,28 @@ extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const
             set_error("%s: null pointer", name);
             return DFHIP_EINVAL;
         }
-        if (parts != bwd_blocks(M)) {
+        if (parts != bwd_parts(M)) {
             set_error("%s: parts must be dfhip_field_mlp_backward_parts(M) = %u (got %u)", name,
-                      bwd_blocks(M), parts);
+                      bwd_parts(M), parts);
             return DFHIP_EINVAL;
         }
+        const uint32_t nblk = bwd_blocks(M);
+#define DFHIP_BWDN(R)                                                                          \
+    do {                                                                                       \
+        if (use_bwd1())                                                                        \
+            k_field_bwd1<half_t, R, false><<<nblk, 64 * kBwd1Waves, 0, s>>>(                   \
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,                  \
+                (const R *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);                \
+        else                                                                                   \
+            k_field_bwd<half_t, R, false><<<nblk, 256, 0, s>>>(                                \
+                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,                  \
+                (const R *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);                \
+    } while (0)
         if (grad_rgb_dtype == DFHIP_F32)
-            k_field_bwd<half_t, float, false><<<parts, 256, 0, s>>>(
-                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                (const float *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
+            DFHIP_BWDN(float);
         else if (grad_rgb_dtype == DFHIP_F16)
-            k_field_bwd<half_t, half_t, false><<<parts, 256, 0, s>>>(
-                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,
-                (const half_t *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);
+            DFHIP_BWDN(half_t);
+#undef DFHIP_BWDN
         else {
             set_error("%s: grad_rgb dtype must be f32 or f16", name);
             return DFHIP_EDTYPE;
@@ -834,15 +1121,23 @@ static int grid_field_backward(
             set_error("%s: null pointer", name);
             return DFHIP_EINVAL;
         }
-        if (mlp_parts != bwd_blocks(cap)) {
+        if (mlp_parts != bwd_parts(cap)) {
             set_error("%s: mlp_parts must be dfhip_field_mlp_backward_parts(cap) = %u (got %u)",
-                      name, bwd_blocks(cap), mlp_parts);
+                      name, bwd_parts(cap), mlp_parts);
             return DFHIP_EINVAL;
         }
+        const uint32_t nblk = bwd_blocks(cap);
 #define DFHIP_BWD(E, R)                                                                       \
-    k_field_bwd<E, R, true><<<mlp_parts, 256, 0, s>>>(                                        \
-        (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, cap,     \
-        m_dev, (E *)d_enc_lbc, mlp_partial)
+    do {                                                                                      \
+        if (use_bwd1())                                                                       \
+            k_field_bwd1<E, R, true><<<nblk, 64 * kBwd1Waves, 0, s>>>(                        \
+                (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, \
+                cap, m_dev, (E *)d_enc_lbc, mlp_partial);                                     \
+        else                                                                                  \
+            k_field_bwd<E, R, true><<<nblk, 256, 0, s>>>(                                     \
+                (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, \
+                cap, m_dev, (E *)d_enc_lbc, mlp_partial);                                     \
+    } while (0)
         if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(half_t, float);
         else if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F16) DFHIP_BWD(half_t, half_t);
         else if (elem == DFHIP_BF16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(bf16_t, float);

@@ -282,18 +282,20 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 const uint32_t s = (tile + u) * 16 + c;
                 fm::Fwd F;
                 fm::forward_tile(W, xb[u], c, h, F);
-                if (h == 0 && valid[u]) {
-                    // k_field_fwd_fused's heads: f16-rounded outputs, f32 density
-                    const float sigma = expf((float)(half_t)F.o[0] + fm::gaussian(x[u]));
-                    half_t rgb[3];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const float v = (float)(half_t)F.o[q + 1];
-                        rgb[q] = (half_t)(1.0f / (1.0f + expf(-v)));
+                if (valid[u]) {
+                    // k_field_fwd_fused's heads (f16-rounded outputs, f32 density),
+                    // lane group h on output h: the density into word 3 s, albedo
+                    // channel q = h - 1 into half q of words 3 s + 1, 3 s + 2
+                    if (h == 0) {
+                        S.pos[3 * s] = expf((float)(half_t)F.o[0] + fm::gaussian(x[u]));
+                    } else {
+                        const float v = (float)(half_t)F.o[0];
+                        const half_t a = (half_t)(1.0f / (1.0f + expf(-v)));
+                        if (h == 3)
+                            S.pos[3 * s + 2] = __uint_as_float(pack_h2(a, (half_t)0.0f));
+                        else
+                            reinterpret_cast<half_t *>(S.pos + 3 * s + 1)[h - 1] = a;
                     }
-                    S.pos[3 * s] = sigma;
-                    S.pos[3 * s + 1] = __uint_as_float(pack_h2(rgb[0], rgb[1]));
-                    S.pos[3 * s + 2] = __uint_as_float(pack_h2(rgb[2], (half_t)0.0f));
                 }
             }
         }
