@@ -508,221 +508,6 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
     }
 }
 
-// ---------------------------------------------------------------- backward, one wave per SIMD
-// k_field_bwd1: the same arithmetic as k_field_bwd with the work split per
-// WAVE instead of per workgroup round.  One workgroup of 4 waves per CU (one
-// wave per SIMD, up to 512 registers: the weight operands in VGPRs, the 37
-// weight-gradient accumulator tiles in AGPRs); the weights are staged in LDS
-// once, after which the waves never synchronise: each takes rounds of two
-// 16-sample tiles, writes their activation images into its own two LDS stage
-// buffers and forms all 37 weight-gradient tiles over those 32 samples (one
-// 16x16x32 MFMA each, k = the 32 samples).  Partials are per wave.
-constexpr int kBwd1Waves = 4;
-
-template <typename E, typename rgb_t, bool PERM>
-__global__ __launch_bounds__(64 * kBwd1Waves, 1) void k_field_bwd1(
-    const E *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
-    const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
-    const float *__restrict__ grad_sigma, const rgb_t *__restrict__ grad_rgb, uint32_t cap,
-    const int32_t *__restrict__ m_dev,
-    E *__restrict__ d_enc,          // [16, cap, 2] (level-major)
-    float *__restrict__ partial) {  // [gridDim.x * kBwd1Waves, kParams]
-    typedef typename Elem<E>::v8 v8;
-    typedef typename Elem<E>::v4 v4;
-    __shared__ WeightsG<E> W;
-    __shared__ WeightsTG<E> T;
-    __shared__ StageT<E> stage[2 * kBwd1Waves];
-    load_weights<PERM>(W, &T, w1, b1, w2, b2, w3, b3);
-    const uint32_t M = active_count(m_dev, cap);
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
-    StageT<E> *S2 = stage + 2 * wave;
-    __syncthreads();  // the only workgroup barrier
-
-    v8 w2op[4][2], w2top[4][2], w1top[2][2], w3top[4], w1op[4], w3op[2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            w2op[u][s2] = a_perm(W.w2, kLd64, 16 * u + c, s2, h);
-            w2top[u][s2] = a_perm(T.w2t, kLd64, 16 * u + c, s2, h);
-            if (u < 2) w1top[u][s2] = a_perm(T.w1t, kLd64, 16 * u + c, s2, h);
-        }
-        w3top[u] = a_nat(T.w3t, kLd32, 16 * u + c, 0, h);
-        w1op[u] = a_nat(W.w1, kLd32, 16 * u + c, 0, h);
-        if (u < 2) w3op[u] = a_perm(W.w3, kLd64, c, u, h);
-    }
-    // weight-gradient accumulators: W2 [tn][tm], b2 [tn], W1 [tn][tf], b1 [tn],
-    // W3 [tm], b3 (row-tile tn / tm of 16 neurons; ones operand for biases)
-    f4 gW2[4][4], gB2[4], gW1[4][2], gB1[4], gW3[4], gB3;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gW2[i][j] = f4{0, 0, 0, 0};
-        gW1[i][0] = gW1[i][1] = gB2[i] = gB1[i] = gW3[i] = f4{0, 0, 0, 0};
-    }
-    gB3 = f4{0, 0, 0, 0};
-    const v4 ones = v4{(E)1.0f, (E)1.0f, (E)1.0f, (E)1.0f};
-    const v8 ones8 = __builtin_shufflevector(ones, ones, 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)  // dO^T image columns 4..15 stay zero
-        st_write4(S2[u], c, kColDO + 4 * h, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f);
-
-    constexpr bool kBf = std::is_same<E, bf16_t>::value;
-    auto mask = [&](const auto &act, const f4 &d, auto &dst) {
-        if constexpr (kBf) {
-            const f4 m = {(float)act[0] > 0.0f ? d[0] : 0.0f, (float)act[1] > 0.0f ? d[1] : 0.0f,
-                          (float)act[2] > 0.0f ? d[2] : 0.0f, (float)act[3] > 0.0f ? d[3] : 0.0f};
-            dst = __builtin_convertvector(m, bf4);
-        } else {  // f16 ReLU backward on packed pairs (k_field_bwd)
-            typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-            const half4 dh = __builtin_convertvector(d, half4);
-            u2 ab, db;
-            __builtin_memcpy(&ab, &act, 8);
-            __builtin_memcpy(&db, &dh, 8);
-            const u2 nz = ((ab & 0x7FFF7FFFu) + 0x7FFF7FFFu) & 0x80008000u;
-            const u2 r = db & ((nz >> 15u) * 0xFFFFu);
-            __builtin_memcpy(&dst, &r, 8);
-        }
-    };
-    // one tile: forward recompute, backward, encoder gradient, LDS image
-    auto tile_of = [&](const TileIn<E, rgb_t> &cur, uint32_t tile, StageT<E> &S) {
-        const uint32_t sample = tile * 16 + c;
-        const bool valid = sample < M;
-        FwdG<E, true> F;
-        forward_tile<E, true, true, true, true>(W, cur.xb, c, h, F, w2op, w1op, w3op);
-        E dOh = (E)0.0f;  // lane group h: output h (k_field_bwd)
-        if (valid) {
-            if (h == 0) {
-                const float y = (float)(E)F.o[0] + gaussian(cur.xyz);
-                const float yc = fminf(fmaxf(y, -15.0f), 15.0f);
-                dOh = (E)(cur.gs * expf(yc));
-            } else {
-                const float a = (float)(E)(1.0f / (1.0f + expf(-(float)(E)F.o[0])));
-                const float g = (float)(E)(float)cur.grgb;
-                dOh = (E)(g * (1.0f - a) * a);
-            }
-        }
-        const v8 dob = v8{dOh, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f, (E)0.0f};
-        typename TilesT<E, true>::type dz2, dz1;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) mask(F.a2[u], mfma(w3top[u], dob, f4{0, 0, 0, 0}), dz2[u]);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            f4 d = f4{0, 0, 0, 0};
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) d = mfma(w2top[t][s2], b_from_tiles(dz2, s2), d);
-            mask(F.a1[t], d, dz1[t]);
-        }
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-            f4 d = f4{0, 0, 0, 0};
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) d = mfma(w1top[f][s2], b_from_tiles(dz1, s2), d);
-            if (valid) {
-                const uint32_t lv = 8 * f + 2 * h;
-                typedef E e2v __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<e2v *>(d_enc + ((size_t)lv * cap + sample) * 2) =
-                    e2v{(E)d[0], (E)d[1]};
-                *reinterpret_cast<e2v *>(d_enc + ((size_t)(lv + 1) * cap + sample) * 2) =
-                    e2v{(E)d[2], (E)d[3]};
-            }
-        }
-        *reinterpret_cast<v8 *>(S.v + c * kStLd + kColX + 8 * h) = cur.xb;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int col = 16 * t + 4 * h;
-            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColA1 + col) = F.a1[t];
-            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColA2 + col) = F.a2[t];
-            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD1 + col) = dz1[t];
-            *reinterpret_cast<v4 *>(S.v + c * kStLd + kColD2 + col) = dz2[t];
-        }
-        S.v[c * kStLd + kColDO + h] = dOh;
-    };
-    // the weight gradients of the wave's two staged tiles (k = 32 samples)
-    auto wgrad = [&]() {
-        auto tr2 = [&](int c0) {
-            const v4 lo = tr_operand(S2[0], c0, lane);
-            const v4 hi = tr_operand(S2[1], c0, lane);
-            return (v8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        };
-        v8 ba1[4], ba2[4], bx[2];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            ba1[t] = tr2(kColA1 + 16 * t);
-            ba2[t] = tr2(kColA2 + 16 * t);
-        }
-        bx[0] = tr2(kColX);
-        bx[1] = tr2(kColX + 16);
-#pragma unroll
-        for (int tn = 0; tn < 4; ++tn) {
-            const v8 a2 = tr2(kColD2 + 16 * tn);
-#pragma unroll
-            for (int tm = 0; tm < 4; ++tm) gW2[tn][tm] = mfma(a2, ba1[tm], gW2[tn][tm]);
-            gB2[tn] = mfma(a2, ones8, gB2[tn]);
-            const v8 a1 = tr2(kColD1 + 16 * tn);
-#pragma unroll
-            for (int tf = 0; tf < 2; ++tf) gW1[tn][tf] = mfma(a1, bx[tf], gW1[tn][tf]);
-            gB1[tn] = mfma(a1, ones8, gB1[tn]);
-        }
-        const v8 ao = tr2(kColDO);
-#pragma unroll
-        for (int tm = 0; tm < 4; ++tm) gW3[tm] = mfma(ao, ba2[tm], gW3[tm]);
-        gB3 = mfma(ao, ones8, gB3);
-    };
-
-    const uint32_t tiles = ceil_div(M, 16u);
-    const uint32_t nw = gridDim.x * kBwd1Waves;
-    const uint32_t rounds = ceil_div(tiles, 2u * nw);
-    uint32_t pair = blockIdx.x * kBwd1Waves + wave;
-    TileIn<E, rgb_t> c0, c1;
-    load_tile<E, rgb_t>(c0, 2 * pair, enc, xyz, grad_sigma, grad_rgb, M, c, h);
-    load_tile<E, rgb_t>(c1, 2 * pair + 1, enc, xyz, grad_sigma, grad_rgb, M, c, h);
-    for (uint32_t round = 0; round < rounds; ++round, pair += nw) {
-        TileIn<E, rgb_t> n0, n1;  // the next round's inputs, loaded while this one runs
-        load_tile<E, rgb_t>(n0, 2 * (pair + nw), enc, xyz, grad_sigma, grad_rgb, M, c, h);
-        load_tile<E, rgb_t>(n1, 2 * (pair + nw) + 1, enc, xyz, grad_sigma, grad_rgb, M, c, h);
-        tile_of(c0, 2 * pair, S2[0]);
-        tile_of(c1, 2 * pair + 1, S2[1]);
-        __builtin_amdgcn_wave_barrier();  // the wave's own images (LDS ops in order)
-        wgrad();
-        __builtin_amdgcn_wave_barrier();  // read before the next round rewrites them
-        c0 = n0;
-        c1 = n1;
-    }
-
-    // ---- this wave's partial: accumulator element r of lane (c, h) is row
-    // 4h + r, column c of its tile; every entry written by exactly one lane
-    float *out = partial + ((size_t)blockIdx.x * kBwd1Waves + wave) * kParams;
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int n = 16 * tn + 4 * h + r;
-#pragma unroll
-            for (int tm = 0; tm < 4; ++tm) out[kOffW2 + n * kHid + 16 * tm + c] = gW2[tn][tm][r];
-#pragma unroll
-            for (int tf = 0; tf < 2; ++tf) {
-                const int p = 16 * tf + c;
-                out[kOffW1 + n * kIn + (PERM ? perm_feature(p) : p)] = gW1[tn][tf][r];
-            }
-            if (c == 0) {
-                out[kOffB2 + n] = gB2[tn][r];
-                out[kOffB1 + n] = gB1[tn][r];
-            }
-        }
-    }
-    if (h == 0) {
-#pragma unroll
-        for (int tm = 0; tm < 4; ++tm)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) out[kOffW3 + r * kHid + 16 * tm + c] = gW3[tm][r];
-        if (c == 0)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) out[kOffB3 + r] = gB3[r];
-    }
-}
-
 // Sum the per-workgroup partials (fixed order) into the six f32 gradients:
 // a block takes 64 parameters; its 16 part-lanes sum the parts p = j, j+16,
 // ... of each, then lane j = 0 adds the 16 lane sums in order.
@@ -780,34 +565,16 @@ static uint32_t resident_blocks(K kern) {
     return cached;
 }
 
-// Backward form (DFHIP_FIELD_BWD1=1: k_field_bwd1, one wave per SIMD, per-wave
-// partials; 0: k_field_bwd, four-wave rounds, per-workgroup partials).
-static bool use_bwd1() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("DFHIP_FIELD_BWD1");
-        v = e ? (atoi(e) != 0) : 0;
-    }
-    return v != 0;
-}
-
 static uint32_t bwd_blocks(uint32_t M) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (use_bwd1()) {  // one workgroup per CU, a tile pair per wave and round
-        const uint32_t want = ceil_div(ceil_div(M, 32u), (uint32_t)kBwd1Waves);
-        const uint32_t cap = (uint32_t)cus;
-        return want < cap ? (want ? want : 1u) : cap;
-    }
     const uint32_t want = ceil_div(ceil_div(M, 16u), (uint32_t)kBwdWaves);
     const uint32_t cap = 2u * (uint32_t)cus;  // two workgroups per CU
     return want < cap ? (want ? want : 1u) : cap;
 }
 // partial rows the backward writes for M rows (k_field_wgrad_sum's parts)
-static uint32_t bwd_parts(uint32_t M) {
-    return use_bwd1() ? bwd_blocks(M) * (uint32_t)kBwd1Waves : bwd_blocks(M);
-}
+static uint32_t bwd_parts(uint32_t M) { return bwd_blocks(M); }
 
 }  // namespace fm
 }  // namespace dfhip
@@ -873,16 +640,9 @@ extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const
         }
         const uint32_t nblk = bwd_blocks(M);
 #define DFHIP_BWDN(R)                                                                          \
-    do {                                                                                       \
-        if (use_bwd1())                                                                        \
-            k_field_bwd1<half_t, R, false><<<nblk, 64 * kBwd1Waves, 0, s>>>(                   \
-                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,                  \
-                (const R *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);                \
-        else                                                                                   \
-            k_field_bwd<half_t, R, false><<<nblk, 256, 0, s>>>(                                \
-                (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma,                  \
-                (const R *)grad_rgb, M, nullptr, (half_t *)d_enc_lbc, partial);                \
-    } while (0)
+    k_field_bwd<half_t, R, false><<<nblk, 256, 0, s>>>(                                        \
+        (const half_t *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, M,  \
+        nullptr, (half_t *)d_enc_lbc, partial)
         if (grad_rgb_dtype == DFHIP_F32)
             DFHIP_BWDN(float);
         else if (grad_rgb_dtype == DFHIP_F16)
@@ -1128,16 +888,9 @@ static int grid_field_backward(
         }
         const uint32_t nblk = bwd_blocks(cap);
 #define DFHIP_BWD(E, R)                                                                       \
-    do {                                                                                      \
-        if (use_bwd1())                                                                       \
-            k_field_bwd1<E, R, true><<<nblk, 64 * kBwd1Waves, 0, s>>>(                        \
-                (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, \
-                cap, m_dev, (E *)d_enc_lbc, mlp_partial);                                     \
-        else                                                                                  \
-            k_field_bwd<E, R, true><<<nblk, 256, 0, s>>>(                                     \
-                (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, \
-                cap, m_dev, (E *)d_enc_lbc, mlp_partial);                                     \
-    } while (0)
+    k_field_bwd<E, R, true><<<nblk, 256, 0, s>>>(                                             \
+        (const E *)enc, xyz, w1, b1, w2, b2, w3, b3, grad_sigma, (const R *)grad_rgb, cap,     \
+        m_dev, (E *)d_enc_lbc, mlp_partial)
         if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(half_t, float);
         else if (elem == DFHIP_F16 && grad_rgb_dtype == DFHIP_F16) DFHIP_BWD(half_t, half_t);
         else if (elem == DFHIP_BF16 && grad_rgb_dtype == DFHIP_F32) DFHIP_BWD(bf16_t, float);
