@@ -1537,6 +1537,51 @@ __global__ __launch_bounds__(256) void k_sum(const float *__restrict__ partial, 
     }
 }
 
+// C = 2: one thread per row, both channels as one 8-byte load per image and
+// eight images in flight (the same fixed order and f64 sums as k_sum).
+template <typename out_t>
+__global__ __launch_bounds__(256) void k_sum2(const float *__restrict__ partial, BinInfo bi,
+                                              uint32_t total_rows,
+                                              const uint32_t *__restrict__ counts,
+                                              out_t *__restrict__ out, int accumulate) {
+    const uint32_t srows = 1u << bi.shift;
+    const size_t img = (size_t)srows * 2;
+    for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < total_rows;
+         row += gridDim.x * blockDim.x) {
+        uint32_t l = 0;  // the row's level: binary search over the level bases
+#pragma unroll
+        for (uint32_t step = 8; step > 0; step >>= 1)
+            if (l + step < bi.L && bi.base[l + step] <= row) l += step;
+        const uint32_t rel = row - bi.base[l];
+        const uint32_t b = bi.bin0[l] + (rel >> bi.shift);
+        const uint32_t S = counts[bi.o_plan + 2 * b], P = counts[bi.o_plan + 2 * b + 1];
+        const float2 *src = reinterpret_cast<const float2 *>(partial + (size_t)S * img +
+                                                             (size_t)(rel & (srows - 1)) * 2);
+        const size_t step2 = img / 2;
+        double t0 = 0.0, t1 = 0.0;
+        uint32_t p = 0;
+        for (; p + 8 <= P; p += 8) {
+            float2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(p + u) * step2];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                t0 += (double)v[u].x;
+                t1 += (double)v[u].y;
+            }
+        }
+        for (; p < P; ++p) {
+            const float2 v = src[(size_t)p * step2];
+            t0 += (double)v.x;
+            t1 += (double)v.y;
+        }
+        const float s0 = accumulate ? (float)out[2 * (size_t)row] : 0.0f;
+        const float s1 = accumulate ? (float)out[2 * (size_t)row + 1] : 0.0f;
+        out[2 * (size_t)row] = (out_t)(s0 + (float)t0);
+        out[2 * (size_t)row + 1] = (out_t)(s1 + (float)t1);
+    }
+}
+
 // Corner-row wrap mode shared by every level (0 mask, 1 modulo, 2 hash; the
 // host restatement of ge::level_ctx / level_rows / row_mode), or kModeAny.
 static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t L, uint32_t D,
@@ -1791,9 +1836,15 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
     // every row is written: rows of bins no walk touched get zero (or keep
     // their value when accumulating)
     const uint32_t total_rows = (uint32_t)offsets_host[L];
-    const uint64_t want = ceil_div<uint64_t>((uint64_t)total_rows * C, 256);
-    gb::k_sum<float><<<(uint32_t)(want < 4096 ? want : 4096), 256, 0, s>>>(
-        partial, bi, C, total_rows, counts, grad_embeddings, accumulate);
+    if (C == 2) {
+        const uint64_t want = ceil_div<uint64_t>((uint64_t)total_rows, 256);
+        gb::k_sum2<float><<<(uint32_t)(want < 8192 ? want : 8192), 256, 0, s>>>(
+            partial, bi, total_rows, counts, grad_embeddings, accumulate);
+    } else {
+        const uint64_t want = ceil_div<uint64_t>((uint64_t)total_rows * C, 256);
+        gb::k_sum<float><<<(uint32_t)(want < 4096 ? want : 4096), 256, 0, s>>>(
+            partial, bi, C, total_rows, counts, grad_embeddings, accumulate);
+    }
     return check_launch(name);
 }
 
