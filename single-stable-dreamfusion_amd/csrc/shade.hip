@@ -59,26 +59,31 @@ __global__ __launch_bounds__(kThreads) void k_stencil(const float *__restrict__ 
                                                       uint32_t cap, float eps, float bound,
                                                       float *__restrict__ xyz7,
                                                       int32_t *__restrict__ m7_dev) {
+    // a block's kThreads samples are staged in LDS, then its 21 x kThreads output
+    // floats are written by consecutive threads (contiguous stores; a thread
+    // per sample wrote 21 floats at an 84-byte lane stride)
+    constexpr uint32_t kOut = 3u * (1u + kStencil);  // floats per sample (7 rows)
+    __shared__ float sx[3 * kThreads];
     const uint32_t M = live(m_dev, cap);
     if (blockIdx.x == 0 && threadIdx.x == 0) *m7_dev = (int32_t)(7u * M);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
-        float x[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) x[d] = xyz[3 * (size_t)i + d];
-        float *dst = xyz7 + 21 * (size_t)i;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) dst[d] = x[d];
-#pragma unroll
-        for (int s = 0; s < kStencil; ++s) {
-            const int a = s >> 1;
-            const float off = (s & 1) ? -eps : eps;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
+    for (uint32_t base = blockIdx.x * kThreads; base < M; base += gridDim.x * kThreads) {
+        const uint32_t n = min((uint32_t)kThreads, M - base);
+        for (uint32_t j = threadIdx.x; j < 3 * n; j += kThreads) sx[j] = xyz[3 * (size_t)base + j];
+        __syncthreads();
+        float *dst = xyz7 + kOut * (size_t)base;
+        for (uint32_t j = threadIdx.x; j < kOut * n; j += kThreads) {
+            const uint32_t i = j / kOut, k = j - kOut * i, r = k / 3u, d = k - 3u * r;
+            const float x = sx[3 * i + d];
+            float v = x;
+            if (r > 0) {
                 // x + tensor([[eps, 0, 0]]) then clamp(-bound, bound)
-                const float v = x[d] + (d == a ? off : 0.0f);
-                dst[3 * (1 + s) + d] = fminf(fmaxf(v, -bound), bound);
+                const uint32_t s1 = r - 1u, a = s1 >> 1;
+                const float off = (s1 & 1u) ? -eps : eps;
+                v = fminf(fmaxf(x + (d == a ? off : 0.0f), -bound), bound);
             }
+            dst[j] = v;
         }
+        __syncthreads();  // sx is rewritten next
     }
 }
 
