@@ -217,10 +217,18 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
     for (int d = 0; d < 3; ++d) l16[d] = rnd<E>(light[d]);
     // d loss / d orient_i: (scale * lambda) / M' (MulBackward, MeanBackward)
     const float go = (grad_loss[0] * lambda) / padded_rows(M);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+    // a block's samples are computed one per thread into LDS images of their
+    // 21 albedo-gradient and 7 density-gradient values, which consecutive
+    // threads then copy out (contiguous stores)
+    __shared__ E s_ga[21 * kThreads];
+    __shared__ float s_gs[7 * kThreads];
+    for (uint32_t base = blockIdx.x * kThreads; base < M; base += gridDim.x * kThreads) {
+      const uint32_t nblk = min((uint32_t)kThreads, M - base);
+      const uint32_t i = base + threadIdx.x;
+      if (i < M) {
         const Normal nm = fd_normal(sigma7, i, eps);
         const Shade sh = lambert<E>(nm.n, l16, ratio, omr);
-        E *ga = grad_albedo7 + 21 * (size_t)i;
+        E *ga = s_ga + 21 * threadIdx.x;
         float g[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) g[d] = (float)grad_color[3 * (size_t)i + d];
@@ -262,7 +270,7 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
         const float gr = ((-gn[0] * nm.v[0]) / r2 + (-gn[1] * nm.v[1]) / r2) +
                          (-gn[2] * nm.v[2]) / r2;
         const float gs = nm.ss >= 1e-20f ? gr / (2.0f * nm.r) : 0.0f;
-        float *gs7 = grad_sigma7 + 7 * (size_t)i;
+        float *gs7 = s_gs + 7 * threadIdx.x;
         gs7[0] = grad_sigma[i];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -275,6 +283,13 @@ __global__ __launch_bounds__(kThreads) void k_shade_bwd(
         // the stencil rows carry no albedo gradient
 #pragma unroll
         for (int k = 3; k < 21; ++k) ga[k] = (E)0.0f;
+      }
+      __syncthreads();
+      for (uint32_t j = threadIdx.x; j < 21 * nblk; j += kThreads)
+          grad_albedo7[21 * (size_t)base + j] = s_ga[j];
+      for (uint32_t j = threadIdx.x; j < 7 * nblk; j += kThreads)
+          grad_sigma7[7 * (size_t)base + j] = s_gs[j];
+      __syncthreads();  // the images are rewritten next
     }
 }
 
