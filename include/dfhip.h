@@ -522,6 +522,41 @@ int dfhip_grid_encode_backward_binned_stencil(int phase, int grad_dtype, const v
                                               uint32_t *entries, uint32_t *counts,
                                               float *partial, int accumulate,
                                               dfhip_stream_t stream);
+/* Per-call options of the binned backward: A/B and test switches of one call,
+ * nothing kept between calls (the library holds no mode state).  A field < 0
+ * (or 0 where noted) keeps the default; NULL options = all defaults. */
+typedef struct dfhip_binned_opts {
+    int32_t walk_mode;          /* -1 default: per-segment walk for single samples, flat walk
+                                   for stencil groups; 0 per-segment, 1 flat, 2 flat
+                                   per-wave pieces (mask-form layouts) */
+    int32_t fast_bin;           /* -1 / 1: mask-form fast binning where it applies; 0 the
+                                   generic binning kernel */
+    int32_t walk_groups_per_cu; /* 0 default (3); 1..16 walk workgroups per CU (changes the
+                                   partial scratch size: pass the same opts to the scratch call) */
+    int32_t lane_perm;          /* -1 default (1): per-segment walk lanes take runs in
+                                   bit-reversed order (1) or in lane order (0) */
+    uint64_t *trace;            /* debug: per-workgroup walk timeline, 8 u64 per walk
+                                   workgroup {bin, bin + 1, parts, entries, t0, t0, part, t1}
+                                   (per-segment walk only); NULL = off */
+} dfhip_binned_opts;
+/* dfhip_grid_backward_binned_scratch / dfhip_grid_encode_backward_binned_stencil
+ * with per-call options (group 1 = single samples, eps ignored; group 7 =
+ * stencil groups).  The scratch depends on the group and the options: size it
+ * with the group and opts the launches will use. */
+int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32_t *offsets_host,
+                                            uint32_t L, uint32_t C, uint32_t group,
+                                            const dfhip_binned_opts *opts, uint64_t *entries_u32,
+                                            uint64_t *counts_u32, uint64_t *partial_f32);
+int dfhip_grid_encode_backward_binned_opts(int phase, int grad_dtype, const void *grad_lbc,
+                                           const float *inputs, float bound,
+                                           const int32_t *offsets, const int32_t *offsets_host,
+                                           float *grad_embeddings, uint32_t B,
+                                           const int32_t *m_dev, uint32_t D, uint32_t C,
+                                           uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                           int align_corners, uint32_t group, float eps,
+                                           uint32_t *entries, uint32_t *counts, float *partial,
+                                           int accumulate, const dfhip_binned_opts *opts,
+                                           dfhip_stream_t stream);
 
 /* nerf/utils.py:708-713 scaler.step(optimizer); scaler.update() for
  * torch.optim.Adam (csrc/optim.hip): non-finite check of every grad, then (if
@@ -673,6 +708,20 @@ int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d
                             const float *b1, const float *w2, const float *b2, const float *w3,
                             const float *b3, float *weights_sum, float *depth, float *image,
                             uint32_t *work, const void *quads, dfhip_stream_t stream);
+/* The same with a debug profile of this call: prof (DEVICE u64 [6], caller
+ * zeroed) receives the per-wave phase cycles of the persistent kernel summed
+ * {refill, march, field, composite, rounds, field tiles}; NULL = the call
+ * above.  Used by tools/infer_case.py. */
+int dfhip_render_rays_infer_prof(uint32_t N, const float *rays_o, const float *rays_d,
+                                 const float *nears, const float *fars, const float *noises,
+                                 float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
+                                 uint32_t H, const uint8_t *grid, float T_thresh,
+                                 const void *table, const int32_t *offsets, uint32_t L, float S,
+                                 uint32_t base_res, uint32_t gridtype, int align_corners,
+                                 const float *w1, const float *b1, const float *w2,
+                                 const float *b2, const float *w3, const float *b3,
+                                 float *weights_sum, float *depth, float *image, uint32_t *work,
+                                 const void *quads, uint64_t *prof, dfhip_stream_t stream);
 
 /* ---- non-albedo shading of the train step (csrc/shade.hip) ------------------
  * Replaces, for the `textureless` / `lambertian` steps, network_grid.py:90-144

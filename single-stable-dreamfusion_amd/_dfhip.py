@@ -82,6 +82,11 @@ _SIGS = {
     "dfhip_grid_encode_backward_binned_stencil": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp,
                                                   _u32, _vp, _u32, _u32, _u32, _f32, _u32, _u32,
                                                   _i32, _u32, _f32, _vp, _vp, _vp, _i32, _vp],
+    "dfhip_grid_backward_binned_scratch_opts": [_u32, _vp, _u32, _u32, _u32, _vp, _vp, _vp,
+                                                _vp],
+    "dfhip_grid_encode_backward_binned_opts": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _u32,
+                                               _vp, _u32, _u32, _u32, _f32, _u32, _u32, _i32,
+                                               _u32, _f32, _vp, _vp, _vp, _i32, _vp, _vp],
     "dfhip_grid_grad_blc_to_lbc": [_i32, _vp, _vp, _u32, _u32, _u32, _vp],
     "dfhip_field_mlp_forward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp],
     "dfhip_field_mlp_backward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,
@@ -141,6 +146,9 @@ _SIGS = {
     "dfhip_render_rays_infer": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32, _vp,
                                 _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_render_rays_infer_prof": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32,
+                                     _vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp, _vp,
+                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],

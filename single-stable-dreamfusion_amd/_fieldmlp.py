@@ -171,13 +171,15 @@ def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lb
 
 def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                       bitfield, T_thresh, table, offsets, S, base_res, gridtype, align_corners,
-                      weights, weights_sum, depth, image, work, quads=None):
+                      weights, weights_sum, depth, image, work, quads=None, prof=None):
     """Inference render of N rays in one launch (csrc/render.hip; reference
     nerf/renderer.py:496-532).  rays_o/rays_d [N, 3] f32, nears/fars [N] f32,
     noises [N] f32 or None, bitfield u8, table [rows, 2] f16, offsets int32.
     Writes weights_sum [N], depth [N], image [N, 3] f32; work: [4] int32
     scratch whose words 1, 2 hold the evaluated sample count afterwards;
-    quads: the table's corner quads ([rows, 4] int32, grid_quads) or None."""
+    quads: the table's corner quads ([rows, 4] int32, grid_quads) or None.
+    prof: [6] int64 device tensor (zeroed) receiving the kernel's per-wave
+    phase cycles (dfhip_render_rays_infer_prof; tools only) or None."""
     n = rays_o.shape[0]
     for t, what in ((rays_o, "rays_o"), (rays_d, "rays_d"), (nears, "nears"), (fars, "fars"),
                     (weights_sum, "weights_sum"), (depth, "depth"), (image, "image")):
@@ -207,8 +209,13 @@ def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_
         checked(quads, "quads", "int")
         if tuple(quads.shape) != (table.shape[0], 4):
             raise RuntimeError("quads must be [rows, 4] int32 (grid_quads of the table)")
-    call("dfhip_render_rays_infer", n, ptr(rays_o), ptr(rays_d), ptr(nears), ptr(fars),
-         ptr(noises), float(bound), float(dt_gamma), int(max_steps), int(C), int(H), ptr(bitfield),
-         float(T_thresh), ptr(table), ptr(offsets), offsets.shape[0] - 1, float(S),
-         int(base_res), int(gridtype), int(bool(align_corners)), *_weights(weights),
-         ptr(weights_sum), ptr(depth), ptr(image), ptr(work), ptr(quads), stream())
+    args = (n, ptr(rays_o), ptr(rays_d), ptr(nears), ptr(fars), ptr(noises), float(bound),
+            float(dt_gamma), int(max_steps), int(C), int(H), ptr(bitfield), float(T_thresh),
+            ptr(table), ptr(offsets), offsets.shape[0] - 1, float(S), int(base_res),
+            int(gridtype), int(bool(align_corners)), *_weights(weights), ptr(weights_sum),
+            ptr(depth), ptr(image), ptr(work), ptr(quads))
+    if prof is None:
+        call("dfhip_render_rays_infer", *args, stream())
+    else:
+        checked(prof, "prof")
+        call("dfhip_render_rays_infer_prof", *args, ptr(prof), stream())

@@ -3,6 +3,8 @@
 plus the native [B, L*C]-layout entry points.  Checks mirror
 gridencoder.cu:425-441 (CHECK_CUDA / CHECK_CONTIGUOUS / dtype) and raise
 RuntimeError."""
+import ctypes
+
 import _dfhip as _d
 from _dfhip import call, ptr, stream, checked
 
@@ -106,14 +108,33 @@ def grid_encode_backward_sliced_dyn(grad_lbc, inputs, bound, offsets, grad_embed
 
 # ---- binned owner-computes backward (csrc/gridbin.hip; see dfhip.h)
 
-def grid_backward_binned_scratch(cap, offsets_host, L, C):
-    """(entries u32, counts u32, partial f32) element counts for capacity cap."""
+class BinnedOpts(ctypes.Structure):
+    """dfhip_binned_opts: per-call A/B and test switches of the binned
+    backward (fields < 0 keep the library default; see include/dfhip.h)."""
+    _fields_ = [("walk_mode", ctypes.c_int32), ("fast_bin", ctypes.c_int32),
+                ("walk_groups_per_cu", ctypes.c_int32), ("lane_perm", ctypes.c_int32),
+                ("trace", ctypes.c_void_p)]
+
+    def __init__(self, walk_mode=-1, fast_bin=-1, walk_groups_per_cu=0, lane_perm=-1,
+                 trace=None):
+        super().__init__(int(walk_mode), int(fast_bin), int(walk_groups_per_cu), int(lane_perm),
+                         None if trace is None else ptr(trace))
+
+
+def _opts_ref(opts):
+    return None if opts is None else ctypes.byref(opts)
+
+
+def grid_backward_binned_scratch(cap, offsets_host, L, C, opts=None, group=1):
+    """(entries u32, counts u32, partial f32) element counts for capacity cap
+    (samples, or stencil groups with group=7; opts: the BinnedOpts the
+    launches will use)."""
     import ctypes
     import numpy as np
     off = np.ascontiguousarray(offsets_host, dtype=np.int32)
     e, c, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-    call("dfhip_grid_backward_binned_scratch", int(cap), off.ctypes.data, int(L), int(C),
-         ctypes.byref(e), ctypes.byref(c), ctypes.byref(p))
+    call("dfhip_grid_backward_binned_scratch_opts", int(cap), off.ctypes.data, int(L), int(C),
+         int(group), _opts_ref(opts), ctypes.byref(e), ctypes.byref(c), ctypes.byref(p))
     return int(e.value), int(c.value), int(p.value)
 
 
@@ -124,14 +145,15 @@ def grid_encode_backward_binned(*args, **kw):
 
 def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddings,
                     B, m_dev, D, C, L, S, H, gridtype, align_corners, entries, counts,
-                    partial, accumulate=False, phase=3, stencil_eps=None):
+                    partial, accumulate=False, phase=3, stencil_eps=None, opts=None):
     """grad_lbc [L, B, C] (B = capacity), inputs [B, D] raw positions in
     [-bound, bound] (bound > 0) or [0, 1] (bound = 0); rows [0, m_dev[0]) walked
     when m_dev is given.  grad_embeddings [rows, C] f32 is overwritten (or
     added into with accumulate).  stencil_eps: finite-difference stencil
     groups of 7 (dfhip_grid_encode_backward_binned_stencil): grad_lbc is
     [L, 7 B, C], inputs / B / m_dev count samples, row 7 g + a is point a of
-    sample g's stencil."""
+    sample g's stencil.  opts: BinnedOpts of this call (None = defaults; the
+    scratch must be sized with the same opts)."""
     import numpy as np
     checked(grad_lbc, "grad")
     checked(inputs, "inputs")
@@ -151,15 +173,14 @@ def binned_launcher(grad_lbc, inputs, bound, offsets, offsets_host, grad_embeddi
             ptr(offsets), off.ctypes.data, ptr(grad_embeddings), int(B), ptr(m_dev), int(D),
             int(C), int(L), float(S), int(H), int(gridtype), int(bool(align_corners)))
     tail = (ptr(entries), ptr(counts), ptr(partial), int(bool(accumulate)))
-    keep = (grad_lbc, inputs, offsets, off, grad_embeddings, m_dev, entries, counts, partial)
-    if stencil_eps is None:
-        name, args = "dfhip_grid_encode_backward_binned_phase", head + tail
-    else:
-        if grad_lbc.shape[1] < 7 * int(B) or inputs.shape[0] < int(B):
-            raise RuntimeError("stencil groups: grad_lbc must hold 7 B rows per level and "
-                               "inputs B samples")
-        name, args = ("dfhip_grid_encode_backward_binned_stencil",
-                      head + (7, float(stencil_eps)) + tail)
+    keep = (grad_lbc, inputs, offsets, off, grad_embeddings, m_dev, entries, counts, partial,
+            opts)
+    if stencil_eps is not None and (grad_lbc.shape[1] < 7 * int(B) or inputs.shape[0] < int(B)):
+        raise RuntimeError("stencil groups: grad_lbc must hold 7 B rows per level and "
+                           "inputs B samples")
+    group = (1, 0.0) if stencil_eps is None else (7, float(stencil_eps))
+    name, args = ("dfhip_grid_encode_backward_binned_opts",
+                  head + group + tail + (_opts_ref(opts),))
 
     def launch(_keep=keep):
         """Launch on the current stream with the validated, pre-marshalled

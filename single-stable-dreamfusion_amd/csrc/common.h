@@ -25,6 +25,18 @@ inline int check_launch(const char *what) {
     return DFHIP_OK;
 }
 
+// ---------------------------------------------------------------- launch setup
+// The current device and its CU count (queried per call).
+int current_device();
+uint32_t device_cus();
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize, bytes) once per (kernel,
+// device), thread-safe.
+void ensure_dynamic_lds(const void *kernel, int bytes);
+// Workgroups of `threads` threads of `kernel` co-resident on the current
+// device (occupancy query once per (kernel, device, threads); fallback_per_cu
+// per CU if the query fails).
+uint32_t resident_blocks(const void *kernel, int threads, int fallback_per_cu);
+
 inline hipStream_t as_stream(dfhip_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 template <typename T>

@@ -548,29 +548,10 @@ __global__ __launch_bounds__(1024) void k_field_wgrad_sum(const float *__restric
     dst[k] = accumulate ? dst[k] + s : s;
 }
 
-// Workgroups of 256 threads that fit on the whole device at once for `kern`.
-template <typename K>
-static uint32_t resident_blocks(K kern) {
-    static uint32_t cached = 0;  // one per kernel instantiation
-    if (cached == 0) {
-        int dev = 0, cus = 256, per_cu = 0;
-        if (hipGetDevice(&dev) == hipSuccess)
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, 256, 0) !=
-                hipSuccess ||
-            per_cu <= 0)
-            per_cu = 4;
-        cached = (uint32_t)(per_cu * cus);
-    }
-    return cached;
-}
-
 static uint32_t bwd_blocks(uint32_t M) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t cus = device_cus();
     const uint32_t want = ceil_div(ceil_div(M, 16u), (uint32_t)kBwdWaves);
-    const uint32_t cap = 2u * (uint32_t)cus;  // two workgroups per CU
+    const uint32_t cap = 2u * cus;  // two workgroups per CU
     return want < cap ? (want ? want : 1u) : cap;
 }
 // partial rows the backward writes for M rows (k_field_wgrad_sum's parts)
@@ -681,7 +662,7 @@ static void launch_field_fwd(hipStream_t s, const float *xyz, float bound, const
     // walks ~M / (16 * waves) tiles); more blocks than fit leave a partial
     // last round of blocks (4096 blocks at 5 waves/SIMD were 3.2 rounds)
     const uint32_t tiles = ceil_div(cap, 16u);
-    const uint32_t fit = resident_blocks(k_field_fwd_fused<E, rgb_t, QUAD>);
+    const uint32_t fit = resident_blocks((const void *)k_field_fwd_fused<E, rgb_t, QUAD>, 256, 4);
     const uint32_t blocks = ceil_div(tiles, 4u) < fit ? ceil_div(tiles, 4u) : fit;
     k_field_fwd_fused<E, rgb_t, QUAD><<<blocks, 256, 0, s>>>(
         xyz, bound, (const E *)table, (const u32x4 *)quads, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3,

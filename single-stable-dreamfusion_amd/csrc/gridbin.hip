@@ -35,8 +35,6 @@
 // reference: f16 / f32 global atomics in arbitrary order).
 #include "grid_common.h"
 
-#include <stdlib.h>
-
 #include <type_traits>
 
 namespace dfhip {
@@ -70,39 +68,55 @@ struct BinInfo {
     uint64_t *trace;                     // debug: per-workgroup walk timeline (null: off)
 };
 
-static uint64_t *g_walk_trace = nullptr;  // set by dfhip_debug_walk_trace (tools only)
-static bool g_fast_bin = true;            // dfhip_debug_fast_bin(0): the generic k_bin (A/B, tests)
+// Walk workgroups per CU (default 3: walk + sum 216.5 -> 208.4 us per C2
+// step against 4; 2 and 5-6 slower).  A/B: dfhip_binned_opts.walk_groups_per_cu.
+#ifndef DFHIP_WALK_G_DEFAULT
+#define DFHIP_WALK_G_DEFAULT 3
+#endif
+// Walk form of a NULL / -1 walk_mode (-1: per group, see flat_walk_mode);
+// variant libraries (tools/variant_lib.sh) set it for A/B of the replayed step.
+#ifndef DFHIP_WALK_MODE_DEFAULT
+#define DFHIP_WALK_MODE_DEFAULT -1
+#endif
+
+// The per-call options (dfhip_binned_opts, NULL = defaults) resolved once per
+// call; the library keeps no mode state between calls.
+struct Opts {
+    int walk_mode;        // -1: per group (per-segment for single samples, flat for groups)
+    bool fast_bin;        // mask-form fast binning where it applies
+    uint32_t walk_g;      // walk workgroups per CU
+    uint32_t lane_perm;   // per-segment walk: bit-reversed lane -> run map
+    uint64_t *trace;      // debug walk timeline or null
+};
+
+static bool resolve_opts(const dfhip_binned_opts *o, Opts &r) {
+    r.walk_mode = DFHIP_WALK_MODE_DEFAULT;
+    r.fast_bin = true;
+    r.walk_g = DFHIP_WALK_G_DEFAULT;
+    r.lane_perm = 1;
+    r.trace = nullptr;
+    if (!o) return true;
+    if (o->walk_mode < -1 || o->walk_mode > 2) {
+        set_error("binned backward: walk_mode must be -1, 0, 1 or 2 (got %d)", (int)o->walk_mode);
+        return false;
+    }
+    if (o->walk_groups_per_cu < 0 || o->walk_groups_per_cu > 16) {
+        set_error("binned backward: walk_groups_per_cu must be 0..16 (got %d)",
+                  (int)o->walk_groups_per_cu);
+        return false;
+    }
+    if (o->walk_mode >= 0) r.walk_mode = o->walk_mode;
+    r.fast_bin = o->fast_bin != 0;
+    if (o->walk_groups_per_cu > 0) r.walk_g = (uint32_t)o->walk_groups_per_cu;
+    if (o->lane_perm >= 0) r.lane_perm = o->lane_perm != 0;
+    r.trace = o->trace;
+    return true;
+}
 
 static uint32_t slice_shift(uint32_t C) {
     uint32_t shift = 0;
     while ((2ull << shift) * 8ull * C <= kSliceBytes) ++shift;
     return shift;  // largest 2^shift rows with 2^shift * C doubles <= kSliceBytes
-}
-
-static uint32_t device_cus() {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            v > 0)
-            cus = v;
-        else
-            cus = 256;
-    }
-    return (uint32_t)cus;
-}
-
-// Walk workgroups per CU (DFHIP_WALK_G, 1..16, for A/B runs; default 3:
-// walk + sum 216.5 -> 208.4 us per C2 step against 4; 2 and 5-6 slower).
-static uint32_t walk_groups_per_cu() {
-    static uint32_t g = 0;
-    if (g == 0) {
-        const char *e = getenv("DFHIP_WALK_G");
-        const int v = e ? atoi(e) : 0;
-        g = (v >= 1 && v <= 16) ? (uint32_t)v : 3u;
-    }
-    return g;
 }
 
 // scratch layout (u32 words of `counts`):
@@ -111,21 +125,14 @@ static uint32_t walk_groups_per_cu() {
 //   [nbins][2]     first image slot, parts         (k_walk; zeroed before k_bin)
 // Host: bins and layout from the HOST copy of the offsets.
 static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint32_t cap,
-                      BinInfo &bi) {
+                      const Opts &op, BinInfo &bi) {
     if (L == 0 || L > ge::kMaxLevels || C == 0) return false;
     bi.L = L;
-    bi.trace = g_walk_trace;
+    bi.trace = op.trace;
     bi.shift = slice_shift(C);
     bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, kTile);
-    bi.G = walk_groups_per_cu() * device_cus();
-    {
-        static int perm = -1;
-        if (perm < 0) {
-            const char *e = getenv("DFHIP_WALK_PERM");
-            perm = e ? (atoi(e) != 0) : 1;
-        }
-        bi.lane_perm = (uint32_t)perm;
-    }
+    bi.G = op.walk_g * device_cus();
+    bi.lane_perm = op.lane_perm;
     uint32_t nb = 0;
     for (uint32_t l = 0; l < L; ++l) {
         const uint32_t rows = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
@@ -1549,8 +1556,9 @@ __global__ __launch_bounds__(256) void k_sum2(const float *__restrict__ partial,
     for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < total_rows;
          row += gridDim.x * blockDim.x) {
         uint32_t l = 0;  // the row's level: binary search over the level bases
+        static_assert(ge::kMaxLevels <= 64, "the search below reaches level 63 at most");
 #pragma unroll
-        for (uint32_t step = 8; step > 0; step >>= 1)
+        for (uint32_t step = 32; step > 0; step >>= 1)
             if (l + step < bi.L && bi.base[l + step] <= row) l += step;
         const uint32_t rel = row - bi.base[l];
         const uint32_t b = bi.bin0[l] + (rel >> bi.shift);
@@ -1607,20 +1615,14 @@ static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t 
     return mode == 0 ? 0 : kModeAny;  // only the mask form is specialised
 }
 
-// Walk form for mask-form layouts (DFHIP_WALK_FLAT: 0 the per-segment
-// k_walk, 1 the flat k_walk_flat, 2 its per-wave pieces; A/B runs, tests).
-// Default: flat for stencil groups (textureless step, rocprof: walk 1307 ->
-// 1051 us), per-segment for single samples (albedo step: 189 us against 197
-// per-wave pieces and 269 flat — one entry's work is too short to pay for
-// lanes spread over a part's tiles).
-static int g_walk_mode = -2;  // -1: default per group; set by dfhip_debug_walk_mode (tests)
-static int flat_walk_mode(uint32_t group) {
-    if (g_walk_mode == -2) {
-        const char *e = getenv("DFHIP_WALK_FLAT");
-        g_walk_mode = e ? atoi(e) : -1;
-        if (g_walk_mode < -1 || g_walk_mode > 2) g_walk_mode = -1;
-    }
-    if (g_walk_mode >= 0) return g_walk_mode;
+// Walk form for mask-form layouts (dfhip_binned_opts.walk_mode: 0 the
+// per-segment k_walk, 1 the flat k_walk_flat, 2 its per-wave pieces; A/B
+// runs, tests).  Default: flat for stencil groups (textureless step, rocprof:
+// walk 1307 -> 1051 us), per-segment for single samples (albedo step: 189 us
+// against 197 per-wave pieces and 269 flat — one entry's work is too short to
+// pay for lanes spread over a part's tiles).
+static int flat_walk_mode(uint32_t group, const Opts &op) {
+    if (op.walk_mode >= 0) return op.walk_mode;
     return group > 1 ? 1 : 0;
 }
 
@@ -1629,25 +1631,20 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
                         const int32_t *offsets, const int32_t *offsets_host, const Levels &lv,
                         const BinInfo &bi, uint32_t gridtype, int align, SliceDyn dyn,
                         uint32_t B, uint32_t *counts, const uint16_t *entries, float *partial,
-                        const FastLevels *fl, Stencil st = Stencil{0.0f, 0.0f}) {
+                        const FastLevels *fl, const Opts &op,
+                        Stencil st = Stencil{0.0f, 0.0f}) {
     const bool pow2 = ge::dyn_pow2(dyn.bound);
     const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-    if constexpr (C == 2) if (fl && flat_walk_mode(GROUP)) {
+    if constexpr (C == 2) if (fl && flat_walk_mode(GROUP, op)) {
         typedef void (*flat_fn)(const grad_t *, const float *, FastLevels, BinInfo, int,
                                 SliceDyn, float, uint32_t, uint32_t *, const uint16_t *,
                                 float *, Stencil);
-        const int wmode = flat_walk_mode(GROUP);
+        const int wmode = flat_walk_mode(GROUP, op);
         const flat_fn kf = wmode == 2 ? (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 2>
                                               : k_walk_flat<grad_t, C, false, GROUP, 2>)
                                       : (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 1>
                                               : k_walk_flat<grad_t, C, false, GROUP, 1>);
-        static bool fattr[3][2] = {{false, false}, {false, false}, {false, false}};
-        if (!fattr[wmode][pow2]) {
-            (void)hipFuncSetAttribute((const void *)kf,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)kSliceBytes);
-            fattr[wmode][pow2] = true;
-        }
+        ensure_dynamic_lds((const void *)kf, (int)kSliceBytes);
         kf<<<bi.G, 1024, lds, s>>>(grad, inputs, *fl, bi, align, dyn, inv, B, counts, entries,
                                    partial, st);
         return;
@@ -1666,12 +1663,7 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
         else
             kern = m0 ? k_walk<grad_t, 3, C, false, 0> : k_walk<grad_t, 3, C, false, kModeAny>;
     }
-    static bool attr[2][2] = {{false, false}, {false, false}};
-    if (!attr[pow2][m0]) {
-        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kSliceBytes);
-        attr[pow2][m0] = true;
-    }
+    ensure_dynamic_lds((const void *)kern, (int)kSliceBytes);
     kern<<<bi.G, 1024, lds, s>>>(grad, inputs, offsets, lv, bi, gridtype, align, dyn, inv, B,
                                  counts, entries, partial, st);
 }
@@ -1681,37 +1673,16 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
 
 using namespace dfhip;
 
-// Debug: per-workgroup walk timeline {first bin, end bin, 0, entries, t0,
-// t_planned, range start, t_end} (wall clock ticks) into `trace` (8 u64 per
-// walk workgroup); null turns it off.  Used by tools/walk_trace.py only.
-// Debug: choose the generic binning kernel (0) or the mask-form fast path
-// where it applies (1, default).  Used by tests / A-B tools only.
-extern "C" int dfhip_debug_fast_bin(int on) {
-    gb::g_fast_bin = on != 0;
-    return DFHIP_OK;
-}
-
-// Debug: the walk form for mask-form layouts (0 per segment, 1 flat, 2 flat
-// per-wave pieces; -1 the default per group).  Used by tests / A-B tools only.
-extern "C" int dfhip_debug_walk_mode(int mode) {
-    if (mode < -1 || mode > 2) {
-        set_error("debug_walk_mode: mode must be -1, 0, 1 or 2 (got %d)", mode);
-        return DFHIP_EINVAL;
-    }
-    gb::g_walk_mode = mode;
-    return DFHIP_OK;
-}
-
-extern "C" int dfhip_debug_walk_trace(uint64_t *trace) {
-    gb::g_walk_trace = trace;
-    return DFHIP_OK;
-}
-
-extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host,
-                                                  uint32_t L, uint32_t C, uint64_t *entries_u32,
-                                                  uint64_t *counts_u32, uint64_t *partial_f32) {
+extern "C" int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32_t *offsets_host,
+                                                       uint32_t L, uint32_t C, uint32_t group,
+                                                       const dfhip_binned_opts *opts,
+                                                       uint64_t *entries_u32,
+                                                       uint64_t *counts_u32,
+                                                       uint64_t *partial_f32) {
+    gb::Opts op;
+    if (!gb::resolve_opts(opts, op)) return DFHIP_EINVAL;
     gb::BinInfo bi;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, bi)) {
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, op, bi)) {
         set_error("grid_backward_binned_scratch: unsupported level layout");
         return DFHIP_EINVAL;
     }
@@ -1722,13 +1693,22 @@ extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *o
     return DFHIP_OK;
 }
 
+extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host,
+                                                  uint32_t L, uint32_t C, uint64_t *entries_u32,
+                                                  uint64_t *counts_u32, uint64_t *partial_f32) {
+    return dfhip_grid_backward_binned_scratch_opts(cap, offsets_host, L, C, 1, nullptr,
+                                                   entries_u32, counts_u32, partial_f32);
+}
+
 static int binned_backward(const char *name, int phase, int grad_dtype, const void *grad_lbc,
                            const float *inputs, float bound, const int32_t *offsets,
                            const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
                            const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S,
                            uint32_t H, uint32_t gridtype, int align_corners, uint32_t group,
                            float eps, uint32_t *entries, uint32_t *counts, float *partial,
-                           int accumulate, hipStream_t s) {
+                           int accumulate, const dfhip_binned_opts *opts, hipStream_t s) {
+    gb::Opts op;
+    if (!gb::resolve_opts(opts, op)) return DFHIP_EINVAL;
     if (phase < 1 || phase > 3) {
         set_error("%s: phase must be 1 (bin), 2 (walk + sum) or 3 (both), got %d", name, phase);
         return DFHIP_EINVAL;
@@ -1738,7 +1718,7 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
         return DFHIP_EINVAL;
     }
     gb::BinInfo bi;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, B, bi)) {
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, B, op, bi)) {
         set_error("%s: unsupported level layout", name);
         return DFHIP_EINVAL;
     }
@@ -1784,7 +1764,7 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
                     gb::k_bin_fast<false, 7><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
                                                                     dyn, inv, B, counts,
                                                                     (uint16_t *)entries, st);
-            } else if (gb::g_fast_bin && fast) {
+            } else if (op.fast_bin && fast) {
                 if (pow2)
                     gb::k_bin_fast<true><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
                                                                 dyn, inv, B, counts,
@@ -1811,11 +1791,11 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
 #define DFHIP_WALK(GT, CC)                                                                    \
     gb::launch_walk<GT, CC>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
                             bi, gridtype, align_corners, dyn, B, counts,                     \
-                            (const uint16_t *)entries, partial, flp)
+                            (const uint16_t *)entries, partial, flp, op)
 #define DFHIP_WALK7(GT)                                                                       \
     gb::launch_walk<GT, 2, 7>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
                               bi, gridtype, align_corners, dyn, B, counts,                   \
-                              (const uint16_t *)entries, partial, flp, st)
+                              (const uint16_t *)entries, partial, flp, op, st)
         if (group == 7) {
             if (grad_dtype == DFHIP_F16) DFHIP_WALK7(half_t);
             else DFHIP_WALK7(bf16_t);
@@ -1857,7 +1837,7 @@ extern "C" int dfhip_grid_encode_backward_binned_phase(
     return binned_backward("grid_encode_backward_binned", phase, grad_dtype, grad_lbc, inputs,
                            bound, offsets, offsets_host, grad_embeddings, B, m_dev, D, C, L, S,
                            H, gridtype, align_corners, 1, 0.0f, entries, counts, partial,
-                           accumulate, as_stream(stream));
+                           accumulate, nullptr, as_stream(stream));
 }
 
 extern "C" int dfhip_grid_encode_backward_binned_stencil(
@@ -1869,7 +1849,20 @@ extern "C" int dfhip_grid_encode_backward_binned_stencil(
     return binned_backward("grid_encode_backward_binned_stencil", phase, grad_dtype, grad_lbc,
                            inputs, bound, offsets, offsets_host, grad_embeddings, B, m_dev, D, C,
                            L, S, H, gridtype, align_corners, group, eps, entries, counts,
-                           partial, accumulate, as_stream(stream));
+                           partial, accumulate, nullptr, as_stream(stream));
+}
+
+extern "C" int dfhip_grid_encode_backward_binned_opts(
+    int phase, int grad_dtype, const void *grad_lbc, const float *inputs, float bound,
+    const int32_t *offsets, const int32_t *offsets_host, float *grad_embeddings, uint32_t B,
+    const int32_t *m_dev, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+    uint32_t gridtype, int align_corners, uint32_t group, float eps, uint32_t *entries,
+    uint32_t *counts, float *partial, int accumulate, const dfhip_binned_opts *opts,
+    dfhip_stream_t stream) {
+    return binned_backward("grid_encode_backward_binned", phase, grad_dtype, grad_lbc, inputs,
+                           bound, offsets, offsets_host, grad_embeddings, B, m_dev, D, C, L, S,
+                           H, gridtype, align_corners, group, eps, entries, counts, partial,
+                           accumulate, opts, as_stream(stream));
 }
 
 extern "C" int dfhip_grid_encode_backward_binned(

@@ -653,13 +653,7 @@ static void launch_sliced_dc(hipStream_t s, dim3 g, size_t lds, const grad_t *gr
         kern = k_grid_bwd_sliced<grad_t, D, C, kRunLen>;
     else
         kern = k_grid_bwd_sliced_simple<grad_t, D, C>;
-    static bool attr_set = false;  // idempotent; racing first calls set the same value
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)kern,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kSliceLdsBytes);
-        attr_set = true;
-    }
+    ensure_dynamic_lds((const void *)kern, (int)kSliceLdsBytes);
     // 16-B vector loads of whole runs: bases aligned and every level's grad
     // plane a multiple of 16 B
     const int vec_ok = (((uintptr_t)grad | (uintptr_t)in) & 15) == 0 &&
@@ -692,20 +686,6 @@ static void launch_sliced(uint32_t D, uint32_t C, hipStream_t s, dim3 g, size_t 
     }
 #undef DFHIP_SL_C
 #undef DFHIP_SL
-}
-
-static uint32_t device_cus() {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            v > 0)
-            cus = v;
-        else
-            cus = 256;
-    }
-    return (uint32_t)cus;
 }
 
 static bool check_dc(const char *what, uint32_t D, uint32_t C, uint32_t L) {

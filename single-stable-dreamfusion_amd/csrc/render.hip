@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     uint32_t taken = 0;
     bool finished = false;  // T < T_thresh or max_samples: later samples are dropped
     uint32_t samples = 0;   // per-lane count of evaluated samples (stats)
-    // debug phase profile (dfhip_debug_render_profile): cycles of refill,
+    // debug phase profile (dfhip_render_rays_infer_prof): cycles of refill,
     // march, field and compositing, rounds and field tiles, per wave
     uint64_t pc[6] = {0, 0, 0, 0, 0, 0};
     uint64_t c0 = prof ? clock64() : 0;
@@ -361,24 +361,14 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
 
 using namespace dfhip;
 
-static uint64_t *g_render_prof = nullptr;  // set by dfhip_debug_render_profile (tools only)
-
-// Debug: per-wave phase cycles of k_render_infer summed into prof[0..5] =
-// {refill, march, field, composite cycles, rounds, field tiles} (u64, caller
-// zeroed); null turns it off.  Used by tools/infer_case.py only.
-extern "C" int dfhip_debug_render_profile(uint64_t *prof) {
-    g_render_prof = prof;
-    return DFHIP_OK;
-}
-
-extern "C" int dfhip_render_rays_infer(
+static int render_infer(
     uint32_t N, const float *rays_o, const float *rays_d, const float *nears, const float *fars,
     const float *noises, float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
     uint32_t H, const uint8_t *grid, float T_thresh, const void *table, const int32_t *offsets,
     uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
-    const void *quads, dfhip_stream_t stream) {
+    const void *quads, uint64_t *prof, dfhip_stream_t stream) {
     const char *name = "render_rays_infer";
     if (L != 16) {
         set_error("%s: the fused renderer supports the reference's 16-level x 2-channel 3-D "
@@ -401,22 +391,42 @@ extern "C" int dfhip_render_rays_infer(
     const rm::MarchConsts k = rm::make_consts(bound, dt_gamma, max_steps, C, H);
     const ge::Levels lv = ge::make_levels(L, S, base_res);
     // persistent waves: as many workgroups as are co-resident on the chip
-    // (occupancy query, once); the queue balances the rays among them
-    static uint32_t resident = 0;
-    if (resident == 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rd::k_render_infer,
-                                                         64 * rd::kWaves, 0) != hipSuccess)
-            per_cu = cus = 0;
-        resident = (uint32_t)((per_cu > 0 ? per_cu : 2) * (cus > 0 ? cus : 256));
-    }
+    // (occupancy query, cached per device); the queue balances the rays
+    const uint32_t resident =
+        resident_blocks((const void *)rd::k_render_infer, 64 * rd::kWaves, 2);
     const uint32_t want = ceil_div(N, 64u * rd::kWaves);
     const uint32_t blocks = want < resident ? want : resident;
     rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
         N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
         (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
-        weights_sum, depth, image, work, (const fm::u32x4 *)quads, g_render_prof);
+        weights_sum, depth, image, work, (const fm::u32x4 *)quads, prof);
     return check_launch(name);
+}
+
+extern "C" int dfhip_render_rays_infer(
+    uint32_t N, const float *rays_o, const float *rays_d, const float *nears, const float *fars,
+    const float *noises, float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
+    uint32_t H, const uint8_t *grid, float T_thresh, const void *table, const int32_t *offsets,
+    uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
+    const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+    const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
+    const void *quads, dfhip_stream_t stream) {
+    return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
+                        grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
+                        w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, nullptr,
+                        stream);
+}
+
+extern "C" int dfhip_render_rays_infer_prof(
+    uint32_t N, const float *rays_o, const float *rays_d, const float *nears, const float *fars,
+    const float *noises, float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
+    uint32_t H, const uint8_t *grid, float T_thresh, const void *table, const int32_t *offsets,
+    uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
+    const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+    const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
+    const void *quads, uint64_t *prof, dfhip_stream_t stream) {
+    return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
+                        grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
+                        w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, prof,
+                        stream);
 }

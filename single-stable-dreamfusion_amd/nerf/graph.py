@@ -97,17 +97,20 @@ class GraphedTrainStep:
                     self.optimizer_in_graph = True
             self.load(data, self.text_z)
             self.stream.wait_stream(torch.cuda.current_stream())
-            # the capture (and its dry run) forks the quad build and the
-            # binning onto a side stream: graph branches
+            # graph branches (quad build and binning on a side stream) only
+            # under DFHIP_STEP_FORK=1 (native_step._FORK, off by default: the
+            # branches overlap but slow the kernels beside them as much)
             nat.fork = True
             with torch.cuda.stream(self.stream):
-                # dry run (first-use setup outside the capture, including the
-                # communicator's first collective); the optimizer is not run,
-                # its launches are plain kernels
+                # dry run (first-use setup outside the capture); neither the
+                # optimizer nor the all-reduce runs.  The communicator is
+                # already up (Trainer's rank-0 parameter broadcast), and a
+                # step that captures must issue exactly as many collectives as
+                # a step that replays (one, inside the graph): ranks that
+                # capture a (shading, H, W) key on different steps then still
+                # pair their collectives step for step.
                 nat.body()
                 nat.embedding_backward()
-                if nat.dp_world is not None:
-                    nat.allreduce_tail()
             with torch.cuda.graph(self.graph, stream=self.stream):
                 self.loss = nat.body()
                 nat.embedding_backward()

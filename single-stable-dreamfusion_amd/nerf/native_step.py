@@ -214,7 +214,8 @@ class NativeAlbedoStep:
         # 7-point stencil as one group (DFHIP_STENCIL_BIN=0: the 7 M rows one by one)
         self.stencil_bin = bool(self.shade_code) and _STENCIL_BIN
         ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
-            cap if self.stencil_bin else fcap, enc.offsets_host, self.L, self.C)
+            cap if self.stencil_bin else fcap, enc.offsets_host, self.L, self.C,
+            group=7 if self.stencil_bin else 1)
         self.bin_scratch = (torch.empty(ne, **i32), torch.empty(nc, **i32),
                             torch.empty(npf, **f32))
         sc = trainer.scaler
@@ -241,6 +242,9 @@ class NativeAlbedoStep:
         self.grads = [(p, p.grad) for p in self.params]
         self._emb_launch = None
         self._emb_bin = self._emb_walk = None
+        # dfhip_binned_opts of the embedding backward (tools: a walk trace of
+        # the eager twin; None = the library defaults the scratch is sized for)
+        self.binned_opts = None
         # graph branches (set by the capture; the eager twin runs one stream)
         self.fork = False
         self._side = None
@@ -508,6 +512,8 @@ class NativeAlbedoStep:
                     self.encoder.embeddings.grad, self.fcap, self.m_field, 3, self.C, self.L, S,
                     Hb, gridtype, align, *self.bin_scratch)
             kw = {}
+        if self.binned_opts is not None:
+            kw["opts"] = self.binned_opts
         self._emb_launch = _gridencoder.binned_launcher(*args, **kw)
         self._emb_bin = _gridencoder.binned_launcher(*args, phase=1, **kw)
         self._emb_walk = _gridencoder.binned_launcher(*args, phase=2, **kw)

@@ -292,6 +292,12 @@ class Trainer(object):
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
                     dist.broadcast(t.data, src=0)
+        if (self.device.type == "cuda" and dist.is_available() and dist.is_initialized()
+                and dist.get_backend() == "nccl"):
+            # the communicator's first collective, issued by every rank here
+            # (not inside a step): the graph capture's dry run issues none, so
+            # a capturing step and a replaying step both issue exactly one
+            dist.all_reduce(torch.zeros(1, device=self.device))
         if getattr(model, "cuda_ray", False) and self.device.type == "cuda":
             # the density-grid jitter draws the same numbers on every rank, so
             # the occupancy grids stay identical without a collective

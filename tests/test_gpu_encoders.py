@@ -280,9 +280,9 @@ def test_sh_encoder(gpu, degree):
 
 
 def _binned(glbc, x, bound, offs, rows, B, m_dev, D, C, L, S, H, gt, gpu, accumulate=False,
-            gemb=None):
+            gemb=None, opts=None):
     import _gridencoder
-    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, C)
+    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, C, opts)
     ent = torch.empty(ne, dtype=torch.int32, device=gpu)
     cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
     part = torch.full((npf,), float("nan"), device=gpu)
@@ -290,7 +290,7 @@ def _binned(glbc, x, bound, offs, rows, B, m_dev, D, C, L, S, H, gt, gpu, accumu
         gemb = torch.full((rows, C), float("nan"), device=gpu)  # overwritten
     _gridencoder.grid_encode_backward_binned(glbc, x, bound, T(offs, gpu), offs, gemb, B, m_dev,
                                              D, C, L, S, H, gt, False, ent, cnt, part,
-                                             accumulate)
+                                             accumulate, opts=opts)
     return gemb
 
 
@@ -331,8 +331,11 @@ def test_grid_backward_binned_device_count(gpu):
     np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5, atol=1e-6 * scale)
 
 
-@pytest.mark.parametrize("C,L,H,log2T", [(1, 8, 4, 17), (4, 6, 8, 15), (2, 16, 16, 19)])
+@pytest.mark.parametrize("C,L,H,log2T", [(1, 8, 4, 17), (4, 6, 8, 15), (2, 16, 16, 19),
+                                         (2, 20, 4, 14), (2, 24, 2, 12)])
 def test_grid_backward_binned_shapes(gpu, C, L, H, log2T):
+    """Other layouts, including C = 2 with more than 16 levels (the row ->
+    level search of k_sum2 reaches every level, not only the first 16)."""
     from gridencoder.grid import level_offsets
     offs = level_offsets(L, C, 3, H, 2.0, log2T, False)
     rows = int(offs[-1])
@@ -392,11 +395,7 @@ def test_grid_backward_fast_bins_equal_generic(gpu, gt):
     level constants, corner slices from x-neighbour pairs) files exactly the
     generic k_bin's entries: same per-(tile, slice) counts, same id set in
     every segment; tiled grid (fast path) and hashed grid (falls back)."""
-    import ctypes
-    import _dfhip
     import _gridencoder
-    lib = _dfhip.load()
-    lib.dfhip_debug_fast_bin.argtypes = [ctypes.c_int]
     offs, S, _ = _grid_consts()
     rows = int(offs[-1])
     # include points on slice and level edges: lattice-aligned and clamped ones
@@ -409,19 +408,16 @@ def test_grid_backward_fast_bins_equal_generic(gpu, gt):
     xt = T(x, gpu)
     ne, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, 16, 2)
     got = {}
-    try:
-        for fast in (0, 1):
-            lib.dfhip_debug_fast_bin(fast)
-            ent = torch.zeros(ne, dtype=torch.int32, device=gpu)
-            cnt = torch.zeros(nc, dtype=torch.int32, device=gpu)
-            part = torch.empty(npf, device=gpu)
-            gemb = torch.empty(rows, 2, device=gpu)
-            _gridencoder.binned_launcher(glbc, xt, 0.0, T(offs, gpu), offs, gemb, B, None, 3, 2,
-                                         16, S, 16, gt, False, ent, cnt, part)()
-            torch.cuda.synchronize()
-            got[fast] = (ent.cpu().numpy().view(np.uint16), cnt.cpu().numpy(), gemb.cpu().numpy())
-    finally:
-        lib.dfhip_debug_fast_bin(1)
+    for fast in (0, 1):
+        opts = _gridencoder.BinnedOpts(fast_bin=fast)
+        ent = torch.zeros(ne, dtype=torch.int32, device=gpu)
+        cnt = torch.zeros(nc, dtype=torch.int32, device=gpu)
+        part = torch.empty(npf, device=gpu)
+        gemb = torch.empty(rows, 2, device=gpu)
+        _gridencoder.binned_launcher(glbc, xt, 0.0, T(offs, gpu), offs, gemb, B, None, 3, 2,
+                                     16, S, 16, gt, False, ent, cnt, part, opts=opts)()
+        torch.cuda.synchronize()
+        got[fast] = (ent.cpu().numpy().view(np.uint16), cnt.cpu().numpy(), gemb.cpu().numpy())
     tiles = -(-B // 1024)
     (e0, c0, g0), (e1, c1, g1) = got[0], got[1]
     # counts region [tiles][bins]; bins = slices of 8,192 rows per level (C = 2)
@@ -486,6 +482,50 @@ def test_grid_backward_stencil_groups_equal_rows(gpu, dtype):
     np.testing.assert_allclose(out["groups"], want, rtol=1e-5, atol=1e-7 * scale)
 
 
+def test_binned_options_are_per_call(gpu):
+    """dfhip_binned_opts is a per-call argument: a call with debug options (a
+    walk trace, the generic binning, 5 walk workgroups per CU) leaves the
+    next default call unaffected — no trace written, the default scratch
+    size, and the default call's result equal to a default call made before
+    any debug call (re-entrant, no global mutable state)."""
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    x = _samples(20000, 71)
+    B = x.shape[0]
+    g = (np.random.default_rng(72).normal(size=(B, 32)) * 0.1).astype(np.float16)
+    glbc = T(g, gpu).view(B, 16, 2).transpose(0, 1).contiguous()
+    xt = T(x, gpu)
+    scratch0 = _gridencoder.grid_backward_binned_scratch(B, offs, 16, 2)
+
+    def run(opts=None, trace=None):
+        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, 16, 2, opts)
+        ent = torch.zeros(ne, dtype=torch.int32, device=gpu)
+        cnt = torch.zeros(nc, dtype=torch.int32, device=gpu)
+        part = torch.zeros(npf, device=gpu)
+        gemb = torch.empty(rows, 2, device=gpu)
+        _gridencoder.binned_launcher(glbc, xt, 0.0, T(offs, gpu), offs, gemb, B, None, 3, 2, 16,
+                                     S, 16, 1, False, ent, cnt, part, opts=opts)()
+        torch.cuda.synchronize()
+        return gemb.cpu().numpy()
+
+    before = run()
+    trace = torch.zeros(8 * 16 * 256 * 8, dtype=torch.int64, device=gpu)
+    dbg = _gridencoder.BinnedOpts(walk_mode=0, fast_bin=0, walk_groups_per_cu=5, trace=trace)
+    assert _gridencoder.grid_backward_binned_scratch(B, offs, 16, 2, dbg)[2] > scratch0[2]
+    got_dbg = run(dbg)
+    assert int(trace.count_nonzero()) > 0  # the debug call wrote its walk timeline
+    trace.zero_()
+    after = run()
+    torch.cuda.synchronize()
+    assert int(trace.count_nonzero()) == 0  # the default call wrote none
+    assert _gridencoder.grid_backward_binned_scratch(B, offs, 16, 2) == scratch0
+    # same plan and walk: the default result is reproduced (f64 sums of exact
+    # products; the debug call's different part split rounds at f32 only)
+    np.testing.assert_allclose(after, before, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(got_dbg, before, rtol=1e-5, atol=1e-8)
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_grid_backward_walk_forms(gpu, mode):
     """Every walk form of the binned backward (gridbin.hip: 0 = one wave per
@@ -494,51 +534,46 @@ def test_grid_backward_walk_forms(gpu, mode):
     single samples (the albedo step, with a device count and raw positions)
     and for 7-point stencil groups (the shaded steps, samples on the box
     faces)."""
-    import ctypes
     import _dfhip
     import _gridencoder
-    lib = _dfhip.load()
-    lib.dfhip_debug_walk_mode.argtypes = [ctypes.c_int]
+    opts = _gridencoder.BinnedOpts(walk_mode=mode)
     offs, S, _ = _grid_consts()
     rows = int(offs[-1])
-    try:
-        assert lib.dfhip_debug_walk_mode(mode) == 0
-        # single samples: capacity planes, live count on the device
-        cap, m = 40000, 33333
-        x01 = _samples(cap, 61, edge=False)
-        g = (np.random.default_rng(62).normal(size=(cap, 32)) * 0.1).astype(np.float16)
-        want = oracle.grid_encode_backward(g[:m], x01[:m], offs, 2, S, 16)
-        glbc = T(g, gpu).view(cap, 16, 2).transpose(0, 1).contiguous()
-        m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
-        gemb = _binned(glbc, T(x01 * 2 - 1, gpu), 1.0, offs, rows, cap, m_dev, 3, 2, 16, S, 16,
-                       1, gpu)
-        scale = np.abs(want).max()
-        np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
-                                   atol=1e-7 * scale)
-        # stencil groups
-        cap, m, eps = 5000, 4321, 1e-2
-        x = (_samples(cap, 63, edge=False) * 2 - 1).astype(np.float32)
-        x[:40, 1] = np.float32(1.0)
-        xt = T(x, gpu)
-        m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
-        x7 = torch.empty(7 * cap, 3, device=gpu)
-        m7 = torch.zeros(1, dtype=torch.int32, device=gpu)
-        _dfhip.call("dfhip_shading_stencil", xt.data_ptr(), m_dev.data_ptr(), cap, eps, 1.0,
-                    x7.data_ptr(), m7.data_ptr(), _dfhip.stream())
-        g7 = (torch.randn(16, 7 * cap, 2, generator=torch.Generator().manual_seed(64)) * 0.1)
-        g7 = g7.half().to(gpu)
-        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offs, 16, 2)
-        ent = torch.empty(ne, dtype=torch.int32, device=gpu)
-        cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
-        part = torch.empty(npf, device=gpu)
-        gemb = torch.full((rows, 2), float("nan"), device=gpu)
-        _gridencoder.binned_launcher(g7, xt, 1.0, T(offs, gpu), offs, gemb, cap, m_dev, 3, 2, 16,
-                                     S, 16, 1, False, ent, cnt, part, stencil_eps=eps)()
-        torch.cuda.synchronize()
-        x01 = ((x7[:7 * m].cpu().numpy() + np.float32(1)) / np.float32(2)).astype(np.float32)
-        gl = g7[:, :7 * m].float().cpu().numpy()
-        want = oracle.grid_encode_backward(gl, x01, offs, 2, S, 16, gridtype=1, blc=False)
-        np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
-                                   atol=1e-7 * np.abs(want).max())
-    finally:
-        lib.dfhip_debug_walk_mode(-1)
+    # single samples: capacity planes, live count on the device
+    cap, m = 40000, 33333
+    x01 = _samples(cap, 61, edge=False)
+    g = (np.random.default_rng(62).normal(size=(cap, 32)) * 0.1).astype(np.float16)
+    want = oracle.grid_encode_backward(g[:m], x01[:m], offs, 2, S, 16)
+    glbc = T(g, gpu).view(cap, 16, 2).transpose(0, 1).contiguous()
+    m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+    gemb = _binned(glbc, T(x01 * 2 - 1, gpu), 1.0, offs, rows, cap, m_dev, 3, 2, 16, S, 16,
+                   1, gpu, opts=opts)
+    scale = np.abs(want).max()
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
+                               atol=1e-7 * scale)
+    # stencil groups
+    cap, m, eps = 5000, 4321, 1e-2
+    x = (_samples(cap, 63, edge=False) * 2 - 1).astype(np.float32)
+    x[:40, 1] = np.float32(1.0)
+    xt = T(x, gpu)
+    m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+    x7 = torch.empty(7 * cap, 3, device=gpu)
+    m7 = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _dfhip.call("dfhip_shading_stencil", xt.data_ptr(), m_dev.data_ptr(), cap, eps, 1.0,
+                x7.data_ptr(), m7.data_ptr(), _dfhip.stream())
+    g7 = (torch.randn(16, 7 * cap, 2, generator=torch.Generator().manual_seed(64)) * 0.1)
+    g7 = g7.half().to(gpu)
+    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offs, 16, 2)
+    ent = torch.empty(ne, dtype=torch.int32, device=gpu)
+    cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
+    part = torch.empty(npf, device=gpu)
+    gemb = torch.full((rows, 2), float("nan"), device=gpu)
+    _gridencoder.binned_launcher(g7, xt, 1.0, T(offs, gpu), offs, gemb, cap, m_dev, 3, 2, 16,
+                                 S, 16, 1, False, ent, cnt, part, stencil_eps=eps,
+                                 opts=opts)()
+    torch.cuda.synchronize()
+    x01 = ((x7[:7 * m].cpu().numpy() + np.float32(1)) / np.float32(2)).astype(np.float32)
+    gl = g7[:, :7 * m].float().cpu().numpy()
+    want = oracle.grid_encode_backward(gl, x01, offs, 2, S, 16, gridtype=1, blc=False)
+    np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
+                               atol=1e-7 * np.abs(want).max())

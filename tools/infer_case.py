@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--profile", action="store_true",
-                    help="per-wave phase cycles of k_render_infer (dfhip_debug_render_profile)")
+                    help="per-wave phase cycles of k_render_infer (dfhip_render_rays_infer_prof)")
     ap.add_argument("--sphere", action="store_true", help="analytic sphere occupancy (R1)")
     args = ap.parse_args()
     import main as m
@@ -58,15 +58,16 @@ def main():
     print(f"res={args.res} ms_per_frame={ms:.3f} image_mean={float(img.mean()):.6f} "
           f"ws_mean={float(out['weights_sum'].float().mean()):.6f}", flush=True)
     if args.profile:
-        import ctypes
-        import _dfhip
-        lib = _dfhip.load()
-        lib.dfhip_debug_render_profile.argtypes = [ctypes.c_void_p]
+        import functools
+        import _fieldmlp
         prof = torch.zeros(6, dtype=torch.int64, device=dev)
-        lib.dfhip_debug_render_profile(prof.data_ptr())
-        frame()
+        plain = _fieldmlp.render_rays_infer
+        _fieldmlp.render_rays_infer = functools.partial(plain, prof=prof)
+        try:
+            frame()
+        finally:
+            _fieldmlp.render_rays_infer = plain
         torch.cuda.synchronize()
-        lib.dfhip_debug_render_profile(None)
         p = prof.cpu().tolist()
         tot = sum(p[:4])
         print("phase cycles (summed over waves): " + ", ".join(

@@ -43,21 +43,19 @@ def main():
     L = 16
     g = (torch.randn(L, B, 2, device=dev) * 0.01).half()
     gemb = torch.empty(int(offs[-1]), 2, device=dev)
-    ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2)
+    trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
+    opts = _gridencoder.BinnedOpts(walk_mode=0, trace=trace)
+    ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts)
     ent = torch.empty(ne_, dtype=torch.int32, device=dev)
     cnt = torch.empty(nc, dtype=torch.int32, device=dev)
     part = torch.empty(npf, device=dev)
     ot = T(offs)
-    trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
     import os
     win = os.environ.get("DFHIP_GRID_NOWIN") is None
-    lib.dfhip_debug_walk_trace.argtypes = [ctypes.c_void_p]
     for rep in range(args.reps + 1):
         trace.zero_()
-        lib.dfhip_debug_walk_trace(trace.data_ptr())
         _gridencoder.grid_encode_backward_binned(g, x01, 0.0, ot, offs, gemb, B, None, 3, 2, L,
-                                                 S, 16, 1, False, ent, cnt, part)
-        lib.dfhip_debug_walk_trace(None)
+                                                 S, 16, 1, False, ent, cnt, part, opts=opts)
         torch.cuda.synchronize()
     report(trace, B, L, offs, shift=0 if win else 13)
 

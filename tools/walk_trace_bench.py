@@ -25,8 +25,8 @@ def main():
     import bench
     from gridencoder.grid import level_offsets
     from walk_trace import report
-    lib = _dfhip.load()
-    lib.dfhip_debug_walk_trace.argtypes = [ctypes.c_void_p]
+    import _gridencoder
+    _dfhip.load()
     trainer, data = bench.make_trainer(args.res, 0, 0, 1, True, graph=True)
 
     def step():
@@ -39,14 +39,15 @@ def main():
     pls = np.exp2(np.log2(2048 / 16) / 15)
     offs = level_offsets(16, 2, 3, 16, pls, 16, False).astype(np.int32)
     trainer.step_hook = lambda g: g.step_timed()
+    g = next(iter(trainer._graphs.values()))
+    # the eager twin's embedding backward with a walk trace (per-call options)
+    g.native.binned_opts = _gridencoder.BinnedOpts(trace=trace)
+    g.native._emb_launch = None
     for i in range(args.steps):
         trace.zero_()
         torch.cuda.synchronize()
-        lib.dfhip_debug_walk_trace(trace.data_ptr())
         step()
         torch.cuda.synchronize()
-        lib.dfhip_debug_walk_trace(None)
-        g = next(iter(trainer._graphs.values()))
         ns = getattr(g, "native", None) or getattr(g, "step", None)
         M = int(ns.m_dev.item()) if ns is not None and hasattr(ns, "m_dev") else 1
         print(f"--- step {i} (samples {M})")
