@@ -396,7 +396,8 @@ def summarize_kernels(records):
 # timed region -> its kernels, each as alternative name fragments (rocprofv3
 # reports some names demangled, some mangled)
 REGION_KERNELS = {
-    "grid_encode_backward": (("gb::k_bin", "gb5k_bin"), ("gb::k_walk", "gb6k_walk"),
+    "grid_encode_backward": (("gb::k_bin", "gb5k_bin", "gb::k_rbin", "gb6k_rbin"),
+                             ("gb::k_walk", "gb6k_walk", "gb::k_rwalk", "gb7k_rwalk"),
                              ("gb::k_sum", "gb5k_sum")),
     "grid_field_forward": ("k_field_fwd_fused",),
     "field_mlp_backward": ("k_field_bwd", "k_field_wgrad_sum"),

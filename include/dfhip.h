@@ -528,7 +528,10 @@ int dfhip_grid_encode_backward_binned_stencil(int phase, int grad_dtype, const v
 typedef struct dfhip_binned_opts {
     int32_t walk_mode;          /* -1 default: per-segment walk for single samples, flat walk
                                    for stencil groups; 0 per-segment, 1 flat, 2 flat
-                                   per-wave pieces (mask-form layouts) */
+                                   per-wave pieces (mask-form layouts); 3 the resolved
+                                   stream for single samples (16-byte entries binned with
+                                   their fractions and gradient, streamed by the walk;
+                                   f16 / bf16, C = 2, align_corners = 0, else flat) */
     int32_t fast_bin;           /* -1 / 1: mask-form fast binning where it applies; 0 the
                                    generic binning kernel */
     int32_t walk_groups_per_cu; /* 0 default (3); 1..16 walk workgroups per CU (changes the
@@ -541,10 +544,12 @@ typedef struct dfhip_binned_opts {
 } dfhip_binned_opts;
 /* dfhip_grid_backward_binned_scratch / dfhip_grid_encode_backward_binned_stencil
  * with per-call options (group 1 = single samples, eps ignored; group 7 =
- * stencil groups).  The scratch depends on the group and the options: size it
- * with the group and opts the launches will use. */
+ * stencil groups).  The scratch depends on the layout (S, H, gridtype,
+ * align_corners as the launch), the group and the options: size it with the
+ * values the launches will use. */
 int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32_t *offsets_host,
-                                            uint32_t L, uint32_t C, uint32_t group,
+                                            uint32_t L, uint32_t C, float S, uint32_t H,
+                                            uint32_t gridtype, int align_corners, uint32_t group,
                                             const dfhip_binned_opts *opts, uint64_t *entries_u32,
                                             uint64_t *counts_u32, uint64_t *partial_f32);
 int dfhip_grid_encode_backward_binned_opts(int phase, int grad_dtype, const void *grad_lbc,

@@ -82,8 +82,8 @@ _SIGS = {
     "dfhip_grid_encode_backward_binned_stencil": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp,
                                                   _u32, _vp, _u32, _u32, _u32, _f32, _u32, _u32,
                                                   _i32, _u32, _f32, _vp, _vp, _vp, _i32, _vp],
-    "dfhip_grid_backward_binned_scratch_opts": [_u32, _vp, _u32, _u32, _u32, _vp, _vp, _vp,
-                                                _vp],
+    "dfhip_grid_backward_binned_scratch_opts": [_u32, _vp, _u32, _u32, _f32, _u32, _u32,
+                                                _i32, _u32, _vp, _vp, _vp, _vp],
     "dfhip_grid_encode_backward_binned_opts": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _u32,
                                                _vp, _u32, _u32, _u32, _f32, _u32, _u32, _i32,
                                                _u32, _f32, _vp, _vp, _vp, _i32, _vp, _vp],

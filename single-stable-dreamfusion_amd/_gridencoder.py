@@ -125,16 +125,19 @@ def _opts_ref(opts):
     return None if opts is None else ctypes.byref(opts)
 
 
-def grid_backward_binned_scratch(cap, offsets_host, L, C, opts=None, group=1):
+def grid_backward_binned_scratch(cap, offsets_host, L, C, opts=None, group=1, S=0.0, H=1,
+                                 gridtype=1, align_corners=False):
     """(entries u32, counts u32, partial f32) element counts for capacity cap
     (samples, or stencil groups with group=7; opts: the BinnedOpts the
-    launches will use)."""
+    launches will use; S, H, gridtype, align_corners: the launches' layout,
+    which sizes the resolved stream's pool)."""
     import ctypes
     import numpy as np
     off = np.ascontiguousarray(offsets_host, dtype=np.int32)
     e, c, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
     call("dfhip_grid_backward_binned_scratch_opts", int(cap), off.ctypes.data, int(L), int(C),
-         int(group), _opts_ref(opts), ctypes.byref(e), ctypes.byref(c), ctypes.byref(p))
+         float(S), int(H), int(gridtype), int(bool(align_corners)), int(group), _opts_ref(opts),
+         ctypes.byref(e), ctypes.byref(c), ctypes.byref(p))
     return int(e.value), int(c.value), int(p.value)
 
 

@@ -35,6 +35,8 @@
 // reference: f16 / f32 global atomics in arbitrary order).
 #include "grid_common.h"
 
+#include <algorithm>
+
 #include <type_traits>
 
 namespace dfhip {
@@ -61,7 +63,7 @@ struct BinInfo {
     uint32_t L, nbins, shift, tcap;      // tcap: tiles of the capacity (counts row stride)
     uint32_t G;                          // walk workgroups
     uint32_t lane_perm;                  // walk: bit-reversed lane -> run map (1) or identity
-    uint32_t o_totals, o_plan;           // word offsets into `counts` (layout below)
+    uint32_t o_roff, o_totals, o_plan;   // word offsets into `counts` (layout below)
     uint32_t bin0[ge::kMaxLevels + 1];   // first bin of level l (bin0[L] = nbins)
     uint32_t base[ge::kMaxLevels];       // first row of level l
     uint32_t rows[ge::kMaxLevels];       // rows of level l
@@ -96,8 +98,9 @@ static bool resolve_opts(const dfhip_binned_opts *o, Opts &r) {
     r.lane_perm = 1;
     r.trace = nullptr;
     if (!o) return true;
-    if (o->walk_mode < -1 || o->walk_mode > 2) {
-        set_error("binned backward: walk_mode must be -1, 0, 1 or 2 (got %d)", (int)o->walk_mode);
+    if (o->walk_mode < -1 || o->walk_mode > 3) {
+        set_error("binned backward: walk_mode must be -1, 0, 1, 2 or 3 (got %d)",
+                  (int)o->walk_mode);
         return false;
     }
     if (o->walk_groups_per_cu < 0 || o->walk_groups_per_cu > 16) {
@@ -121,6 +124,8 @@ static uint32_t slice_shift(uint32_t C) {
 
 // scratch layout (u32 words of `counts`):
 //   [tcap][nbins]  per-(tile, bin) counts          (k_bin)
+//   [tcap][nbins]  per-(tile, bin) segment offsets in the tile's pool region
+//                  (k_rbin, the resolved stream only)
 //   [nbins][16]    totals, as 16 partial sums      (k_bin; zeroed before it)
 //   [nbins][2]     first image slot, parts         (k_walk; zeroed before k_bin)
 // Host: bins and layout from the HOST copy of the offsets.
@@ -151,8 +156,9 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     // so the per-call clear is ONE aligned fill (an unaligned one took two
     // fill launches)
     const uint64_t tot = ((uint64_t)nb * bi.tcap + 3ull) & ~3ull;
-    if (tot + (kTotSplit + 2ull) * nb + 4ull >= (1ull << 32)) return false;
-    bi.o_totals = (uint32_t)tot;
+    if (2ull * tot + (kTotSplit + 2ull) * nb + 4ull >= (1ull << 32)) return false;
+    bi.o_roff = (uint32_t)tot;
+    bi.o_totals = (uint32_t)(2ull * tot);
     bi.o_plan = bi.o_totals + nb * kTotSplit;
     return true;
 }
@@ -1509,6 +1515,395 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
         out[i] = (float)acc[(i % C) * srows + i / C];
 }
 
+// ---------------------------------------------------------------- 4. resolved stream
+// Single samples (the albedo step) with f16 / bf16 gradients on a mask-form
+// layout: the binning resolves every (sample, level, slice) entry once, so
+// the walk streams its bin instead of gathering.
+//
+//   k_rbin (one workgroup per tile of kTile samples, one thread per sample):
+//     pass A: each level's cell, fractions and slice mask (kept in registers);
+//       per (level, slice) a wave ballot counts the wave's entries (no LDS
+//       atomics: the one-slice coarse levels put every lane of a wave on one
+//       counter); a workgroup scan gives every (wave, bin) its base inside
+//       the tile's segment and every bin its segment offset in the tile's
+//       region of the pool;
+//     pass B: per level the sample's gradient row (coalesced: [L, B, 2]) and,
+//       per slice, its 16-byte entry at base + ballot rank.
+//   An entry is {g (2 x 16 bit), fx | i0 lo << 24, fy | i0 hi << 24, fz}: the
+//   level-relative tiled index of the cell (masked by the level's wrap, < 2^16
+//   rows) and the three fractions as exact 24-bit fixed point (p = x * scale
+//   + 0.5 >= 0.5, so frac = p - floor(p) is a multiple of ulp(p) >= 2^-24).
+//   Entries of a segment are in sample order (wave-major, then lane order),
+//   i.e. in ray order: a lane's run of consecutive entries follows a ray.
+//   k_rwalk: the flat walk's plan and part layout over the pool's segments;
+//     per entry one 16-byte load of the lane's own run (prefetched one batch
+//     ahead), no id -> position / gradient gathers and no cell location.
+constexpr uint32_t kRMaxBins = 256;    // bins of a resolved layout (k_rbin LDS: 16 x 256 counts)
+constexpr uint32_t kRMaxSlices = 32;   // slices per level (u32 slice masks)
+constexpr uint32_t kRWaves = kTile / 64;
+constexpr uint32_t kRBatch = 4;        // entries per lane per walk batch
+
+__device__ __forceinline__ uint32_t frac24(float f) {
+    return (uint32_t)(f * 16777216.0f);  // exact: f is a multiple of 2^-24 in [0, 1)
+}
+
+template <bool POW2>
+__global__ __launch_bounds__(1024) void k_rbin(const float *__restrict__ inputs,
+                                              const uint32_t *__restrict__ grad,  // [L, B] rows
+                                              FastLevels fl, BinInfo bi, SliceDyn dyn, float inv,
+                                              uint32_t B, uint32_t tile_entries,
+                                              uint32_t *__restrict__ counts,
+                                              uint4 *__restrict__ pool) {
+    __shared__ uint32_t cw[kRWaves][kRMaxBins];  // the wave's count, then its base
+    __shared__ uint32_t toff[kRMaxBins];
+    __shared__ uint32_t wtot[kRWaves];
+    const uint32_t M = ge::dyn_count(dyn, B);
+    const uint32_t ntiles = ceil_div(M, kTile);
+    const uint32_t nb = bi.nbins, L = bi.L, shift = bi.shift, smask = (1u << bi.shift) - 1u;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint32_t s = tile * kTile + threadIdx.x;
+        float x[3] = {0.0f, 0.0f, 0.0f};
+        const bool in = s < M && load_pos<3, POW2>(inputs, dyn, inv, s, x);
+        uint32_t mk[kFastLevels], px[kFastLevels], py[kFastLevels], pz[kFastLevels];
+#pragma unroll
+        for (uint32_t l = 0; l < kFastLevels; ++l) {
+            mk[l] = px[l] = py[l] = pz[l] = 0;
+            if (l >= L) continue;  // uniform
+            const float sc = fl.scale[l];
+            const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
+            uint32_t c[3], fq[3];
+#pragma unroll
+            for (uint32_t d = 0; d < 3; ++d) {
+                const float p = fmaf(x[d], sc, 0.5f);
+                const float fl0 = floorf(p);
+                c[d] = (uint32_t)fl0;
+                fq[d] = frac24(p - fl0);
+            }
+            const uint32_t i0 = c[0] + c[1] * m1 + c[2] * m2;
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {  // x-neighbour pairs, as k_bin_fast
+                if (q >= (1u << (lead - 1u))) break;  // uniform
+                const uint32_t o = ((q & 1u) ? m1 : 0u) + ((q & 2u) ? m2 : 0u);
+                const uint32_t r = (i0 + o) & wm;
+                mask |= 1u << (r >> shift);
+                if ((r & smask) == smask) mask |= 1u << (((r + 1u) & wm) >> shift);
+            }
+            const uint32_t im = i0 & wm;
+            mk[l] = in ? mask : 0u;
+            px[l] = fq[0] | (im << 24);
+            py[l] = fq[1] | ((im >> 8) << 24);
+            pz[l] = fq[2];
+            const uint32_t b0 = fl.bin0[l], ns = bi.bin0[l + 1] - b0;
+            for (uint32_t k = 0; k < ns; ++k) {  // uniform
+                const u64 bal = __ballot((mk[l] >> k) & 1u);
+                if (lane == 0) cw[wave][b0 + k] = (uint32_t)__popcll(bal);
+            }
+        }
+        __syncthreads();
+        // per bin: the waves' bases inside the segment and the tile's count;
+        // then the segments' offsets in the tile region (exclusive scan)
+        const uint32_t b = threadIdx.x;
+        uint32_t tc = 0;
+        if (b < nb) {
+#pragma unroll
+            for (uint32_t w = 0; w < kRWaves; ++w) {
+                const uint32_t v = cw[w][b];
+                cw[w][b] = tc;
+                tc += v;
+            }
+        }
+        uint32_t inc = tc;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        uint32_t wofs = 0;
+        for (uint32_t w = 0; w < wave; ++w) wofs += wtot[w];
+        if (b < nb) {
+            const uint32_t off = wofs + inc - tc;
+            toff[b] = off;
+            counts[(size_t)tile * nb + b] = tc;
+            counts[bi.o_roff + (size_t)tile * nb + b] = off;
+            if (tc) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], tc);
+        }
+        __syncthreads();
+        // pass B: the entries
+        uint4 *tp = pool + (size_t)tile * tile_entries;
+#pragma unroll
+        for (uint32_t l = 0; l < kFastLevels; ++l) {
+            if (l >= L) continue;  // uniform
+            const uint32_t g = in ? grad[(size_t)l * B + s] : 0u;
+            const uint32_t b0 = fl.bin0[l], ns = bi.bin0[l + 1] - b0;
+            for (uint32_t k = 0; k < ns; ++k) {  // uniform
+                const bool mine = (mk[l] >> k) & 1u;
+                const u64 bal = __ballot(mine);
+                if (mine) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    const uint32_t bb = b0 + k;
+                    tp[toff[bb] + cw[wave][bb] + rank] = make_uint4(g, px[l], py[l], pz[l]);
+                }
+            }
+        }
+        __syncthreads();  // cw / toff are rewritten by the next tile
+    }
+}
+
+// Walk plan (wave 0 of every walk workgroup): this workgroup's bin b and part
+// j of P_b; part 0 records the bin's image slots for k_sum.  Returns in
+// sh_b / sh_j / sh_p (sh_p = 0: an idle workgroup).
+__device__ __forceinline__ void walk_plan(const BinInfo &bi, uint32_t *counts, uint32_t &sh_b,
+                                          uint32_t &sh_j, uint32_t &sh_p) {
+    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
+    const uint32_t *totals = counts + bi.o_totals;
+    const uint32_t ln = threadIdx.x;
+    u64 T = 0, nz = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+        const uint32_t e = b0 + ln < nb ? bin_total(totals, b0 + ln) : 0u;
+        u64 t, z;
+        (void)wave_excl_scan(e, ln, &t);
+        (void)wave_excl_scan(e ? 1u : 0u, ln, &z);
+        T += t;
+        nz += z;
+    }
+    const u64 extra = G > nz ? G - nz : 0;
+    uint32_t carry = 0;
+    if (ln == 0) sh_p = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+        const uint32_t b = b0 + ln;
+        const uint32_t e = b < nb ? bin_total(totals, b) : 0u;
+        const uint32_t p = e ? 1u + (uint32_t)((u64)e * extra / (T ? T : 1)) : 0u;
+        u64 tot;
+        const uint32_t s = carry + (uint32_t)wave_excl_scan(p, ln, &tot);
+        if (b < nb && p && slot >= s && slot < s + p) {
+            sh_b = b;
+            sh_j = slot - s;
+            sh_p = p;
+        }
+        if (b < nb && p && slot == s) {
+            counts[bi.o_plan + 2 * b] = s;
+            counts[bi.o_plan + 2 * b + 1] = p;
+        }
+        carry += (uint32_t)tot;
+    }
+}
+
+// One resolved entry into the lane's cell state (flat_take_at's arithmetic:
+// the same trailing-dimension factor and per-corner weight products).
+template <typename grad_t, uint32_t LEAD>
+__device__ __forceinline__ void rtake(FlatCell<2> &st, double *acc, uint32_t srows, uint32_t lo,
+                                      uint32_t n, uint32_t m1, uint32_t m2, uint32_t wm,
+                                      const uint4 v) {
+    const uint32_t i0 = (v.y >> 24) | ((v.z >> 16) & 0xFF00u);
+    float fr[3];
+    fr[0] = (float)(v.y & 0xFFFFFFu) * 5.9604644775390625e-8f;  // 2^-24, exact
+    fr[1] = (float)(v.z & 0xFFFFFFu) * 5.9604644775390625e-8f;
+    fr[2] = (float)(v.w & 0xFFFFFFu) * 5.9604644775390625e-8f;
+    float g[2];
+    {
+        grad_t lo16, hi16;
+        const uint16_t a = (uint16_t)(v.x & 0xFFFFu), b = (uint16_t)(v.x >> 16);
+        __builtin_memcpy(&lo16, &a, 2);
+        __builtin_memcpy(&hi16, &b, 2);
+        g[0] = (float)lo16;
+        g[1] = (float)hi16;
+    }
+    float tw = 1.0f;  // trailing dims dropped from the index: their corners coincide
+#pragma unroll
+    for (uint32_t d = LEAD; d < 3; ++d) tw *= (1.0f - fr[d]) + fr[d];
+    const double gd0 = (double)g[0], gd1 = (double)g[1];
+    if (!(st.have && i0 == st.i0)) {
+        if (st.have) {
+#pragma unroll
+            for (uint32_t k = 0; k < (1u << LEAD); ++k) {
+                const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
+                const uint32_t rel = ((st.i0 + o) & wm) - lo;
+                if (rel < n) {
+                    atomicAdd(acc + rel, st.cw[k][0]);
+                    atomicAdd(acc + srows + rel, st.cw[k][1]);
+                }
+            }
+        }
+        st.i0 = i0;
+        st.have = true;
+#pragma unroll
+        for (uint32_t k = 0; k < (1u << LEAD); ++k) st.cw[k][0] = st.cw[k][1] = 0.0;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < (1u << LEAD); ++k) {
+        float w = tw;
+#pragma unroll
+        for (uint32_t d = 0; d < LEAD; ++d) w *= (k & (1u << d)) ? fr[d] : 1.0f - fr[d];
+        const double wd = (double)w;
+        st.cw[k][0] = fma(wd, gd0, st.cw[k][0]);
+        st.cw[k][1] = fma(wd, gd1, st.cw[k][1]);
+    }
+}
+
+// A part's walk at one level lead: its tiles (part, part + P, ...) in chunks
+// of up to kChunkTiles; each chunk's segments laid end to end (scan of the
+// counts), cut into 1024 equal runs (wave w the w-th sixteenth, lanes
+// bit-reversed); a lane's run may cross segments.  Entries are loaded one
+// batch ahead of their use.
+template <typename grad_t, uint32_t LEAD>
+__device__ __forceinline__ void rwalk_level(const uint4 *__restrict__ pool, const uint32_t *counts,
+                                            const BinInfo &bi, uint32_t tile_entries,
+                                            double *acc, uint32_t *pre, uint32_t *sbase,
+                                            uint32_t *wsum, uint32_t b, uint32_t part, uint32_t P,
+                                            uint32_t ntiles, uint32_t srows, uint32_t lo,
+                                            uint32_t n, uint32_t m1, uint32_t m2, uint32_t wm) {
+    const uint32_t nb = bi.nbins;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t waves = blockDim.x >> 6, nthr = blockDim.x;
+    const uint32_t nt = ntiles > part ? ceil_div(ntiles - part, P) : 0u;
+    FlatCell<2> cell;
+    cell.have = false;
+    cell.i0 = 0;
+    for (uint32_t cb = 0; cb < nt; cb += kChunkTiles) {
+        const uint32_t nc = min(nt - cb, kChunkTiles);
+        uint32_t v = 0;
+        if (tid < nc) {
+            const uint32_t t = part + (cb + tid) * P;
+            v = counts[(size_t)t * nb + b];
+            sbase[tid] = t * tile_entries + counts[bi.o_roff + (size_t)t * nb + b];
+        }
+        uint32_t inc = v;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t wofs = 0;
+        for (uint32_t w = 0; w < wave; ++w) wofs += wsum[w];
+        if (tid < nc) pre[tid] = wofs + inc - v;
+        if (tid == 0) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < waves; ++w) tot += wsum[w];
+            pre[nc] = tot;
+        }
+        __syncthreads();
+        const uint32_t E = pre[nc];
+        const uint32_t Q = ceil_div(E, nthr);
+        const uint32_t r = wave * 64u + (__builtin_bitreverse32(lane) >> 26);
+        uint32_t e = min(r * Q, E);
+        const uint32_t e1 = min(e + Q, E);
+        if (e < e1) {
+            uint32_t a = 0, z = nc;  // segment of entry e: pre[a] <= e < pre[z]
+            while (z - a > 1) {
+                const uint32_t mid = (a + z) >> 1;
+                if (pre[mid] <= e) a = mid;
+                else z = mid;
+            }
+            uint32_t ti = a, tend = pre[a + 1], addr = sbase[a] + (e - pre[a]);
+            // one entry on: the next pool index (into the next non-empty
+            // segment at a segment's end)
+            auto advance = [&]() {
+                ++addr;
+                ++e;
+                if (e < e1 && e == tend) {
+                    do {
+                        ++ti;
+                        tend = pre[ti + 1];
+                    } while (tend == e);
+                    addr = sbase[ti];
+                }
+            };
+            // the pool indices of the next m <= kRBatch entries (the rest
+            // clamped to the last: every load is issued before the first use)
+            auto next_batch = [&](uint32_t (&ix)[kRBatch], uint32_t &m) {
+                m = min(kRBatch, e1 - e);
+#pragma unroll
+                for (uint32_t i = 0; i < kRBatch; ++i) {
+                    if (i < m) {
+                        ix[i] = addr;
+                        advance();
+                    } else {
+                        ix[i] = ix[i ? i - 1 : 0];
+                    }
+                }
+            };
+            uint32_t ix[kRBatch], m;
+            next_batch(ix, m);
+            uint4 cur[kRBatch];
+#pragma unroll
+            for (uint32_t i = 0; i < kRBatch; ++i) cur[i] = pool[ix[i]];
+            while (true) {
+                const bool more = e < e1;
+                uint32_t nm = 0;
+                uint4 nxt[kRBatch];
+                if (more) {
+                    next_batch(ix, nm);
+#pragma unroll
+                    for (uint32_t i = 0; i < kRBatch; ++i) nxt[i] = pool[ix[i]];
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < kRBatch; ++i)
+                    if (i < m) rtake<grad_t, LEAD>(cell, acc, srows, lo, n, m1, m2, wm, cur[i]);
+                if (!more) break;
+                m = nm;
+#pragma unroll
+                for (uint32_t i = 0; i < kRBatch; ++i) cur[i] = nxt[i];
+            }
+        }
+        __syncthreads();  // pre / sbase / wsum are rewritten by the next chunk
+    }
+    if (cell.have) {
+#pragma unroll
+        for (uint32_t k = 0; k < (1u << LEAD); ++k) {
+            const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
+            const uint32_t rel = ((cell.i0 + o) & wm) - lo;
+            if (rel < n) {
+                atomicAdd(acc + rel, cell.cw[k][0]);
+                atomicAdd(acc + srows + rel, cell.cw[k][1]);
+            }
+        }
+    }
+}
+
+template <typename grad_t>
+__global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, FastLevels fl,
+                                               BinInfo bi, SliceDyn dyn, uint32_t B,
+                                               uint32_t tile_entries, uint32_t *counts,
+                                               float *__restrict__ partial) {
+    extern __shared__ double acc[];
+    __shared__ uint32_t pre[kChunkTiles + 1];
+    __shared__ uint32_t sbase[kChunkTiles];
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t sh_b, sh_j, sh_p;
+    if (threadIdx.x < 64) walk_plan(bi, counts, sh_b, sh_j, sh_p);
+    __syncthreads();
+    const uint32_t P = sh_p;
+    if (P == 0) return;  // uniform
+    const uint32_t b = sh_b, part = sh_j;
+    uint32_t l = 0;
+    while (l + 1 < bi.L && bi.bin0[l + 1] <= b) ++l;
+    const uint32_t srows = 1u << bi.shift;
+    const uint32_t lo = (b - bi.bin0[l]) << bi.shift;  // slice start, relative to the level
+    const uint32_t n = min(srows, bi.rows[l] - lo);
+    for (uint32_t i = threadIdx.x; i < srows * 2; i += blockDim.x) acc[i] = 0.0;
+    __syncthreads();
+    const uint32_t ntiles = ceil_div(ge::dyn_count(dyn, B), kTile);
+    const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
+#define DFHIP_RW(LD)                                                                            \
+    rwalk_level<grad_t, LD>(pool, counts, bi, tile_entries, acc, pre, sbase, wsum, b, part, P, \
+                            ntiles, srows, lo, n, m1, m2, wm)
+    if (lead >= 3) DFHIP_RW(3);
+    else if (lead == 2) DFHIP_RW(2);
+    else DFHIP_RW(1);
+#undef DFHIP_RW
+    __syncthreads();
+    float *out = partial + (size_t)blockIdx.x * ((size_t)srows * 2);
+    for (uint32_t i = threadIdx.x; i < n * 2; i += blockDim.x)
+        out[i] = (float)acc[(i & 1u) * srows + (i >> 1)];
+}
+
 // ---------------------------------------------------------------- 3. sum
 // Every (row, channel) of the table sums its bin's P_b images (slots
 // S_b .. S_b + P_b - 1, recorded by k_walk) in order.
@@ -1588,6 +1983,25 @@ __global__ __launch_bounds__(256) void k_sum2(const float *__restrict__ partial,
         out[2 * (size_t)row] = (out_t)(s0 + (float)t0);
         out[2 * (size_t)row + 1] = (out_t)(s1 + (float)t1);
     }
+}
+
+// The resolved stream (k_rbin + k_rwalk) fits the layout: at most kRMaxBins
+// bins, kRMaxSlices slices and 2^16 rows per level (16-bit cell index), and
+// the pool index below 2^32.  tile_entries: the pool region of one tile, the
+// bound kTile x sum over levels of min(2^lead, slices) (a cell's corners lie
+// in at most that many slices).
+static bool resolved_layout(const FastLevels &fl, const BinInfo &bi, uint32_t &tile_entries) {
+    if (bi.nbins > kRMaxBins || bi.L > kFastLevels) return false;
+    uint64_t per = 0;
+    for (uint32_t l = 0; l < bi.L; ++l) {
+        const uint32_t ns = bi.bin0[l + 1] - bi.bin0[l];
+        if (ns > kRMaxSlices || bi.rows[l] > 65536u) return false;
+        per += std::min<uint32_t>(1u << fl.lead[l], ns);
+    }
+    const uint64_t te = per * kTile;
+    if (te * bi.tcap >= (1ull << 32)) return false;
+    tile_entries = (uint32_t)te;
+    return true;
 }
 
 // Corner-row wrap mode shared by every level (0 mask, 1 modulo, 2 hash; the
@@ -1673,12 +2087,10 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
 
 using namespace dfhip;
 
-extern "C" int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32_t *offsets_host,
-                                                       uint32_t L, uint32_t C, uint32_t group,
-                                                       const dfhip_binned_opts *opts,
-                                                       uint64_t *entries_u32,
-                                                       uint64_t *counts_u32,
-                                                       uint64_t *partial_f32) {
+extern "C" int dfhip_grid_backward_binned_scratch_opts(
+    uint32_t cap, const int32_t *offsets_host, uint32_t L, uint32_t C, float S, uint32_t H,
+    uint32_t gridtype, int align_corners, uint32_t group, const dfhip_binned_opts *opts,
+    uint64_t *entries_u32, uint64_t *counts_u32, uint64_t *partial_f32) {
     gb::Opts op;
     if (!gb::resolve_opts(opts, op)) return DFHIP_EINVAL;
     gb::BinInfo bi;
@@ -1686,8 +2098,18 @@ extern "C" int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32
         set_error("grid_backward_binned_scratch: unsupported level layout");
         return DFHIP_EINVAL;
     }
-    // tile-relative sample ids, u16 (kTile <= 65536), counted in u32 words
-    if (entries_u32) *entries_u32 = ((uint64_t)bi.tcap * bi.nbins * gb::kTile + 1) / 2;
+    // tile-relative sample ids, u16 (kTile <= 65536), counted in u32 words;
+    // the resolved stream's pool (16-byte entries) where it may run
+    uint64_t ew = ((uint64_t)bi.tcap * bi.nbins * gb::kTile + 1) / 2;
+    if (group == 1 && C == 2 && gb::flat_walk_mode(1, op) == 3 && L <= ge::kMaxLevels) {
+        const ge::Levels lv = ge::make_levels(L, S, H);
+        gb::FastLevels fl;
+        uint32_t te = 0;
+        if (gb::make_fast_levels(offsets_host, lv, bi, gridtype, align_corners != 0, fl) &&
+            gb::resolved_layout(fl, bi, te))
+            ew = std::max<uint64_t>(ew, (uint64_t)bi.tcap * te * 4ull);
+    }
+    if (entries_u32) *entries_u32 = ew;
     if (counts_u32) *counts_u32 = gb::counts_words(bi);
     if (partial_f32) *partial_f32 = gb::partial_floats(bi, C);
     return DFHIP_OK;
@@ -1696,8 +2118,9 @@ extern "C" int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32
 extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host,
                                                   uint32_t L, uint32_t C, uint64_t *entries_u32,
                                                   uint64_t *counts_u32, uint64_t *partial_f32) {
-    return dfhip_grid_backward_binned_scratch_opts(cap, offsets_host, L, C, 1, nullptr,
-                                                   entries_u32, counts_u32, partial_f32);
+    return dfhip_grid_backward_binned_scratch_opts(cap, offsets_host, L, C, 0.0f, 1, 1, 0, 1,
+                                                   nullptr, entries_u32, counts_u32,
+                                                   partial_f32);
 }
 
 static int binned_backward(const char *name, int phase, int grad_dtype, const void *grad_lbc,
@@ -1747,6 +2170,12 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
         }
     }
     const gb::Stencil st{eps, bound};
+    // the resolved stream: single samples, 2 channels of f16 / bf16 gradients,
+    // a mask-form layout, half-cell origin (frac exact in 24 bits)
+    uint32_t r_tile = 0;
+    const bool rs = group == 1 && C == 2 && fast && align_corners == 0 &&
+                    grad_dtype != DFHIP_F32 && gb::flat_walk_mode(1, op) == 3 &&
+                    gb::resolved_layout(fl, bi, r_tile);
     if (phase & 1) {
         // totals (k_bin adds) and the plan (k_walk sets; P = 0: no images)
         (void)hipMemsetAsync(counts + bi.o_totals, 0,
@@ -1755,7 +2184,16 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
             const uint32_t gbin = bi.tcap < 4096u ? bi.tcap : 4096u;
             const bool pow2 = ge::dyn_pow2(dyn.bound);
             const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-            if (group == 7) {
+            if (rs) {
+                if (pow2)
+                    gb::k_rbin<true><<<gbin, 1024, 0, s>>>(inputs, (const uint32_t *)grad_lbc, fl,
+                                                           bi, dyn, inv, B, r_tile, counts,
+                                                           (uint4 *)entries);
+                else
+                    gb::k_rbin<false><<<gbin, 1024, 0, s>>>(inputs, (const uint32_t *)grad_lbc,
+                                                            fl, bi, dyn, inv, B, r_tile, counts,
+                                                            (uint4 *)entries);
+            } else if (group == 7) {
                 if (pow2)
                     gb::k_bin_fast<true, 7><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
                                                                    dyn, inv, B, counts,
@@ -1796,7 +2234,12 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
     gb::launch_walk<GT, 2, 7>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
                               bi, gridtype, align_corners, dyn, B, counts,                   \
                               (const uint16_t *)entries, partial, flp, op, st)
-        if (group == 7) {
+        if (rs) {
+            auto kr = grad_dtype == DFHIP_F16 ? gb::k_rwalk<half_t> : gb::k_rwalk<bf16_t>;
+            ensure_dynamic_lds((const void *)kr, (int)gb::kSliceBytes);
+            kr<<<bi.G, 1024, lds, s>>>((const uint4 *)entries, fl, bi, dyn, B, r_tile, counts,
+                                       partial);
+        } else if (group == 7) {
             if (grad_dtype == DFHIP_F16) DFHIP_WALK7(half_t);
             else DFHIP_WALK7(bf16_t);
         } else if (grad_dtype == DFHIP_F16) {

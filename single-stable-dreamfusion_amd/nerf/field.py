@@ -119,7 +119,8 @@ class _GridField(Function):
         if ctx.needs_input_grad[2]:
             grad_emb = torch.empty(rows, C, device=dev, dtype=torch.float32)
             if binned:
-                ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offsets_host, L, C)
+                ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
+                    cap, offsets_host, L, C, S=S, H=H, gridtype=gridtype, align_corners=align)
                 scratch = (torch.empty(ne, device=dev, dtype=torch.int32),
                            torch.empty(nc, device=dev, dtype=torch.int32),
                            torch.empty(npf, device=dev))

@@ -213,9 +213,11 @@ class NativeAlbedoStep:
         # shaded steps: the embedding backward bins and walks each sample's
         # 7-point stencil as one group (DFHIP_STENCIL_BIN=0: the 7 M rows one by one)
         self.stencil_bin = bool(self.shade_code) and _STENCIL_BIN
+        S_, Hb_, gridtype_, align_, _ = self.meta
         ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
             cap if self.stencil_bin else fcap, enc.offsets_host, self.L, self.C,
-            group=7 if self.stencil_bin else 1)
+            group=7 if self.stencil_bin else 1, S=S_, H=Hb_, gridtype=gridtype_,
+            align_corners=align_)
         self.bin_scratch = (torch.empty(ne, **i32), torch.empty(nc, **i32),
                             torch.empty(npf, **f32))
         sc = trainer.scaler

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ranges", default="0-15,0-2,3-8,9-15")
+    ap.add_argument("--modes", default="-1", help="walk modes (dfhip_binned_opts.walk_mode)")
     args = ap.parse_args()
     import _dfhip
     import _gridencoder
@@ -45,17 +46,27 @@ def main():
         L = len(offs) - 1
         rows = int(offs[-1])
         g = (torch.randn(L, B, 2, device=dev) * 0.01).half()
-        gemb = torch.empty(rows, 2, device=dev)
-        ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2)
-        ent = torch.empty(ne_, dtype=torch.int32, device=dev)
-        cnt = torch.empty(nc, dtype=torch.int32, device=dev)
-        part = torch.empty(npf, device=dev)
         ot = T(offs)
-        # S and H of the sub-range: level l' = l - first has scale 2^(l*S)*16 - 1
-        t = timeit(lambda: _gridencoder.grid_encode_backward_binned(
-            g, x01, 0.0, ot, offs, gemb, B, None, 3, 2, L, S, int(round(H)), 1, False, ent, cnt,
-            part), args.reps)  # H rounded: representative cell sizes
-        print(f"B={B} levels={first}..{last} rows={rows} median_us={t:.1f}", flush=True)
+        ref = None
+        for mode in (int(v) for v in args.modes.split(",")):
+            opts = _gridencoder.BinnedOpts(walk_mode=mode)
+            gemb = torch.empty(rows, 2, device=dev)
+            Hr = int(round(H))  # H rounded: representative cell sizes
+            ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts, S=S,
+                                                                     H=Hr)
+            ent = torch.empty(ne_, dtype=torch.int32, device=dev)
+            cnt = torch.empty(nc, dtype=torch.int32, device=dev)
+            part = torch.empty(npf, device=dev)
+            # S and H of the sub-range: level l' = l - first has scale 2^(l*S)*16 - 1
+            t = timeit(lambda: _gridencoder.grid_encode_backward_binned(
+                g, x01, 0.0, ot, offs, gemb, B, None, 3, 2, L, S, Hr, 1, False, ent, cnt,
+                part, opts=opts), args.reps)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = gemb.clone()
+            err = float(((gemb - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
+            print(f"B={B} levels={first}..{last} rows={rows} mode={mode} median_us={t:.1f} "
+                  f"max_rel_diff_vs_first={err:.2e}", flush=True)
 
 
 if __name__ == "__main__":
