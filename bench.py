@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--c5-res", type=int, default=256)
     p.add_argument("--no-traffic", action="store_true",
                    help="skip the live rocprofv3 PMC passes for roofline.traffic")
+    p.add_argument("--shade", default="albedo", choices=("albedo", "textureless", "lambertian"),
+                   help="shading of the timed steps (the shading roofline's profiled child "
+                        "runs the textureless step; the headline is albedo)")
     p.add_argument("--launcher-selftest", action="store_true",
                    help="CPU/gloo check of the N-rank launch only (no GPU work)")
     return p.parse_args()
@@ -415,7 +418,7 @@ MEASURE_TRAFFIC_TRACE_US = {}  # region -> its kernels' replayed duration per st
 MEASURE_STEP_TRACE_US = {}  # "step" -> every kernel's replayed duration per step (child trace)
 
 
-def measure_traffic(region, timeout=180, warmup=10):
+def measure_traffic(region, timeout=180, warmup=10, shade="albedo", key=None):
     """HBM bytes per launch of timed region `region`, measured now: rocprofv3
     passes over a short child run of this same bench (graph-replayed steps, no
     extras), each its own run as MI355X_MICROARCH.md prescribes: a plain
@@ -424,7 +427,10 @@ def measure_traffic(region, timeout=180, warmup=10):
     FETCH_SIZE is doubled (the gfx950 correction for wide reads; the guide
     leaves gathers uncalibrated), both are KiB.  The child's samples per step
     are recorded so bytes, time and traffic are compared at ONE workload.
-    Returns (bytes or None, note)."""
+    shade: the child's step shading (the shaded step's roofline profiles the
+    textureless step); key: the name its figures are recorded under
+    (default: region).  Returns (bytes or None, note)."""
+    key = key or region
     import shutil
     import signal
     import subprocess
@@ -444,7 +450,7 @@ def measure_traffic(region, timeout=180, warmup=10):
     child = [sys.executable, str(Path(__file__).resolve()), "--steps", str(keep), "--warmup",
              str(max(1, warmup)),
              "--no-cpu-baseline", "--no-kernel-timing", "--no-alt-backward", "--no-shading",
-             "--no-infer", "--no-traffic", "--no-c5"]
+             "--no-infer", "--no-traffic", "--no-c5", "--shade", shade]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
     env["TMPDIR"] = "/tmp"
@@ -504,7 +510,7 @@ def measure_traffic(region, timeout=180, warmup=10):
                     allk.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                                  r["Kernel_Name"]))
             starts = sorted(t0 for t0, _, n in allk if "k_step_prologue" in n)
-            if len(starts) >= keep:
+            if len(starts) >= keep and key == region:
                 b0 = starts[-keep]
                 MEASURE_STEP_TRACE_US["step"] = sum(
                     t1 - t0 for t0, t1, _ in allk if t0 >= b0) / keep / 1e3
@@ -528,21 +534,59 @@ def measure_traffic(region, timeout=180, warmup=10):
     shutil.rmtree(tmp, ignore_errors=True)
     total = sum(per["FETCH_SIZE"].values()) + sum(per["WRITE_SIZE"].values())
     names = [a if isinstance(a, str) else a[0] for a in pats]
-    MEASURE_TRAFFIC_CHILD_M[region] = (sum(child_m) / len(child_m)) if child_m else None
-    MEASURE_TRAFFIC_DETAIL[region] = {
+    MEASURE_TRAFFIC_CHILD_M[key] = (sum(child_m) / len(child_m)) if child_m else None
+    MEASURE_TRAFFIC_DETAIL[key] = {
         names[i]: {"fetch_x2": int(per["FETCH_SIZE"][i]), "write": int(per["WRITE_SIZE"][i]),
                    "l2_hit_rate": round(per["TCC_HIT_sum"][i] /
                                         max(1.0, per["TCC_HIT_sum"][i] + per["TCC_MISS_sum"][i]),
                                         4),
                    "replayed_us": round(trace_us[i], 2)}
         for i in range(len(pats))}
-    MEASURE_TRAFFIC_TRACE_US[region] = sum(trace_us.values())
+    MEASURE_TRAFFIC_TRACE_US[key] = sum(trace_us.values())
     return int(total), (
         "measured in this run: rocprofv3 --pmc passes (separate runs: FETCH_SIZE, WRITE_SIZE, "
         "TCC_HIT_sum + TCC_MISS_sum) of a child bench ending where the timed region ends, the "
         "last 16 dispatches of each kernel; FETCH_SIZE x2 (the gfx950 correction, calibrated for 16-B streaming loads "
         "only: an upper bound for gathers; it also counts Infinity-Cache hits), KiB -> bytes, "
         "summed over the region's kernels, mean per launch; l2_hit_rate per kernel")
+
+
+def shading_roofline(trainer, args):
+    """The textureless step's dominant kernel region, the grid embedding
+    backward over 7-point stencil groups (k_bin_fast<7> + k_walk_flat<7> +
+    k_sum2), on ONE workload: a child bench replaying textureless steps
+    (--shade textureless), its last 16 steps profiled by rocprofv3 (kernel
+    trace, FETCH_SIZE, WRITE_SIZE, TCC hit / miss; measure_traffic).  Bytes
+    per launch: SURVEY 8(d)'s model per group (its position 12 B + the seven
+    rows' feature gradients 7 L C 2 B) at the child's groups per step, plus
+    the table gradient once (4 rows C)."""
+    m = trainer.model
+    enc = m.encoder
+    L, C = int(enc.num_levels), int(enc.level_dim)
+    rows = int(enc.offsets_host[-1])
+    traffic, note = measure_traffic("grid_encode_backward", warmup=max(1, args.warmup + args.steps - 16),
+                                    shade="textureless", key="shaded_grid_encode_backward")
+    cm = MEASURE_TRAFFIC_CHILD_M.get("shaded_grid_encode_backward")
+    tus = MEASURE_TRAFFIC_TRACE_US.get("shaded_grid_encode_backward")
+    if not (cm and tus):
+        return {"kernel": "grid_encode_backward (stencil groups)", "traffic": traffic,
+                "traffic_source": note}
+    per = 12 + 7 * L * C * 2
+    cb = 4 * rows * C + per * cm
+    gbs = cb / (tus * 1e-6) / 1e9
+    return {
+        "kernel": "grid_encode_backward (stencil groups: k_bin_fast<7> + k_walk_flat<7> + k_sum2)",
+        "region": "grid_encode_backward", "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": note,
+        "traffic_by_kernel": MEASURE_TRAFFIC_DETAIL.get("shaded_grid_encode_backward"),
+        "avg_us": round(tus, 2), "bytes_per_launch": int(cb), "groups_per_step": round(cm, 1),
+        "algorithmic_bytes_per_group": round(cb / cm, 2),
+        "traffic_per_group": round(traffic / cm, 2) if traffic else None,
+        "traffic_over_algorithmic": round(traffic / cb, 3) if traffic else None,
+        "timing": ("rocprofv3 kernel trace of a child bench's graph-replayed textureless steps "
+                   "(last 16 dispatches of each region kernel); bytes: SURVEY 8(d) per group "
+                   f"({per} B: position + 7 x {L} x {C} f16 gradients) at the child's groups "
+                   "per step + the f32 table gradient")}
 
 
 def _free_port():
@@ -613,6 +657,8 @@ def main():
     _dfhip.load()
     trainer, data = make_trainer(args.res, args.seed, rank, world, not args.two_pass_backward,
                                  graph=not args.eager, mock_sds=args.mock_sds)
+    if args.shade != "albedo":
+        trainer.pick_shading = (lambda k: (lambda: (k, 0.1)))(args.shade)
 
     def step():
         trainer.train_iteration(data.collate([0]))
@@ -802,6 +848,8 @@ def main():
         shade["note"] = ("steps >= albedo_iters: 0.2 albedo + 0.4 textureless + 0.4 lambertian "
                          "(utils.py:346-359), native graph-replayed, fused backward; "
                          "iters_weighted: 0.1 albedo (albedo_iters 1000 of 10000) + 0.9 schedule")
+        if not args.no_traffic:
+            shade["roofline"] = shading_roofline(trainer, args)
         result["shading"] = shade
     if world == 1 and not args.no_c5:
         result["c5"] = bench_c5(args, rank, world)

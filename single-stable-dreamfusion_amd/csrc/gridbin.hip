@@ -569,6 +569,24 @@ static bool make_fast_levels(const int32_t *offsets_host, const Levels &lv, cons
 }
 
 // ---------------------------------------------------------------- 2. walk
+// Timing probes of the slice-image adds (variant libraries only; results are
+// wrong): 1 = the same number of ds_add_f64 on bank-distinct rows (lane-indexed
+// inside the row's 512-row block), 2 = no LDS adds (the value kept alive by a
+// never-taken store).
+#ifndef DFHIP_PROBE_ADDS
+#define DFHIP_PROBE_ADDS 0
+#endif
+__device__ __forceinline__ void lds_add(double *acc, uint32_t idx, double v, uint32_t k) {
+    if constexpr (DFHIP_PROBE_ADDS == 1) {
+        atomicAdd(acc + ((idx & ~511u) | ((threadIdx.x & 63u) + 64u * (k & 7u))), v);
+    } else if constexpr (DFHIP_PROBE_ADDS == 2) {
+        if (__builtin_expect(v == 1.0e300, 0)) acc[idx] = v;
+    } else {
+        (void)k;
+        atomicAdd(acc + idx, v);
+    }
+}
+
 // Flush one cell's merged corner contributions into the LDS slice [r0, r1).
 template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD>
 __device__ __forceinline__ void flush_m(double *acc, uint32_t cs, uint32_t r0, uint32_t r1,
@@ -611,9 +629,8 @@ __device__ __forceinline__ void flush_m(double *acc, uint32_t cs, uint32_t r0, u
             const uint32_t o = (k & 1u) + ((k & 2u) ? lr.m1 : 0u) + ((k & 4u) ? lr.m2 : 0u);
             const uint32_t rel = ((i0 + o) & lr.wmask) - lo;
             if (rel < n) {
-                double *dst = acc + rel;
 #pragma unroll
-                for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(dst + ch * cs, cw[k][ch]);
+                for (uint32_t ch = 0; ch < C; ++ch) lds_add(acc, rel + ch * cs, cw[k][ch], k);
             }
         }
         return;
@@ -1012,7 +1029,7 @@ __device__ __forceinline__ void flat_take_at(FlatCell<C> &st, double *acc, uint3
                 if (rel < n) {
 #pragma unroll
                     for (uint32_t ch = 0; ch < C; ++ch)
-                        atomicAdd(acc + ch * srows + rel, st.cw[k][ch]);
+                        lds_add(acc, ch * srows + rel, st.cw[k][ch], k);
                 }
             }
         }
@@ -1047,7 +1064,7 @@ __device__ __forceinline__ void flat_flush(FlatCell<C> &st, double *acc, uint32_
         const uint32_t rel = ((st.i0 + o) & wm) - lo;
         if (rel < n) {
 #pragma unroll
-            for (uint32_t ch = 0; ch < C; ++ch) atomicAdd(acc + ch * srows + rel, st.cw[k][ch]);
+            for (uint32_t ch = 0; ch < C; ++ch) lds_add(acc, ch * srows + rel, st.cw[k][ch], k);
         }
     }
     st.have = false;
@@ -1724,8 +1741,8 @@ __device__ __forceinline__ void rtake(FlatCell<2> &st, double *acc, uint32_t sro
                 const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
                 const uint32_t rel = ((st.i0 + o) & wm) - lo;
                 if (rel < n) {
-                    atomicAdd(acc + rel, st.cw[k][0]);
-                    atomicAdd(acc + srows + rel, st.cw[k][1]);
+                    lds_add(acc, rel, st.cw[k][0], k);
+                    lds_add(acc, srows + rel, st.cw[k][1], k);
                 }
             }
         }
@@ -1860,8 +1877,8 @@ __device__ __forceinline__ void rwalk_level(const uint4 *__restrict__ pool, cons
             const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
             const uint32_t rel = ((cell.i0 + o) & wm) - lo;
             if (rel < n) {
-                atomicAdd(acc + rel, cell.cw[k][0]);
-                atomicAdd(acc + srows + rel, cell.cw[k][1]);
+                lds_add(acc, rel, cell.cw[k][0], k);
+                lds_add(acc, srows + rel, cell.cw[k][1], k);
             }
         }
     }

@@ -32,3 +32,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/s
     || { echo "shade prof failed"; tail -20 $OUT/shade_prof.log; exit 5; }
 python tools/prof_top.py $OUT/shprof/run_kernel_stats.csv 25 > $OUT/rocprof_shade_top.txt
 head -8 $OUT/rocprof_shade_top.txt
+# the shading roofline's child (bench.py --shade textureless): its trace
+# reproduces shading.roofline.frac
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/shchild -o run \
+    -- python bench.py --steps 16 --warmup ${CHILD_WARMUP:-34} --no-cpu-baseline --no-kernel-timing --no-alt-backward \
+       --no-shading --no-infer --no-traffic --no-c5 --shade textureless \
+    > $OUT/shchild.log 2>&1 || { echo "shade child prof failed"; tail -20 $OUT/shchild.log; exit 6; }
+python tools/roofline_check.py $OUT/bench.json $OUT/shchild/run_kernel_trace.csv --shading | tee $OUT/roofline_check_shading.json

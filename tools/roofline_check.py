@@ -1,7 +1,10 @@
 """Reproduce bench.py's roofline line from a rocprofv3 kernel trace of the
 same child command bench.py profiles (tools/gpu_round.sh):
 
-    python tools/roofline_check.py BENCH_JSON KERNEL_TRACE_CSV [keep]
+    python tools/roofline_check.py BENCH_JSON KERNEL_TRACE_CSV [keep] [--shading]
+
+--shading: the line's shading.roofline (the textureless step's grid embedding
+backward) against a trace of `bench.py --shade textureless` (the same child).
 
 Region time = the last `keep` dispatches of each of the region's kernels
 (bench.REGION_KERNELS), averaged; bytes = the line's bytes_per_launch (the
@@ -16,11 +19,12 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 
-def main(bench_json, trace_csv, keep=16):
+def main(bench_json, trace_csv, keep=16, shading=False):
     import bench
     d = json.loads([l for l in open(bench_json) if l.startswith("{")][-1])
-    roof = d["roofline"]
-    pats = bench.REGION_KERNELS.get(roof["kernel"], (roof["kernel"],))
+    roof = d["shading"]["roofline"] if shading else d["roofline"]
+    region = roof.get("region", roof["kernel"])
+    pats = bench.REGION_KERNELS.get(region, (region,))
     durs = {}
     for r in csv.DictReader(open(trace_csv)):
         for i, alts in enumerate(pats):
@@ -31,11 +35,13 @@ def main(bench_json, trace_csv, keep=16):
     us = sum(sum(v for _, v in sorted(x)[-keep:]) / keep / 1e3 for x in durs.values())
     gbs = roof["bytes_per_launch"] / (us * 1e-6) / 1e9
     frac = gbs / roof["peak"]
-    print(json.dumps({"region": roof["kernel"], "trace_us": round(us, 2),
+    print(json.dumps({"region": region, "shading": shading, "trace_us": round(us, 2),
                       "line_us": roof["avg_us"], "trace_GBs": round(gbs, 1),
                       "line_GBs": roof["achieved"], "trace_frac": round(frac, 4),
                       "line_frac": roof["frac"], "ratio": round(frac / roof["frac"], 3)}))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 16)
+    flags = [a for a in sys.argv[1:] if a.startswith("--")]
+    pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+    main(pos[0], pos[1], int(pos[2]) if len(pos) > 2 else 16, shading="--shading" in flags)
