@@ -540,7 +540,7 @@ typedef struct dfhip_binned_opts {
                                    bit-reversed order (1) or in lane order (0) */
     uint64_t *trace;            /* debug: per-workgroup walk timeline, 8 u64 per walk
                                    workgroup {bin, bin + 1, parts, entries, t0, t0, part, t1}
-                                   (per-segment walk only); NULL = off */
+                                   (per-segment walk and resolved stream); NULL = off */
 } dfhip_binned_opts;
 /* dfhip_grid_backward_binned_scratch / dfhip_grid_encode_backward_binned_stencil
  * with per-call options (group 1 = single samples, eps ignored; group 7 =

@@ -378,6 +378,84 @@ __device__ __forceinline__ void group_point(const float (&xr)[3], uint32_t a, co
     }
 }
 
+// Wave-aggregated appends of one level, called by all 64 lanes of a wave:
+// centre entries (slice mask mc, front of the segment, +1 on the packed
+// count) and, for stencil groups, satellite entries (mask ms, back of the
+// segment, +2^16) carrying their moved-point masks (from mo).  Per slice k of
+// the level a ballot per kind gives each lane its rank; lane k adds the wave's
+// counts of slice k to that slice's counter, i.e. the level's ns counters in
+// ONE LDS atomic instruction on distinct addresses, instead of one atomic per
+// entry (a one-slice coarse level put all 64 lanes of an instruction on the
+// same counter: r04 PMC, conflict cycles 8.7x the LDS-active ones).
+// Levels of at most this many slices append wave-aggregated (wave_append);
+// the others one LDS atomic per entry (lane_append).  All levels wave-
+// aggregated (every slice of every level a ballot, twice) removed the bank
+// conflicts but cost more VALU than they saved: k_bin_fast 64 -> 102 us
+// (1.1 M samples), <7> 173 -> 269 us per textureless step.
+#ifndef DFHIP_BIN_BALLOT_NS
+#define DFHIP_BIN_BALLOT_NS 0
+#endif
+
+// One lane's appends (an LDS atomic per entry: slot = the counter's old value).
+template <bool SAT>
+__device__ __forceinline__ void lane_append(uint32_t *cnt, uint16_t *seg, uint32_t b0,
+                                            uint64_t mc, uint64_t ms, const uint64_t (&mo)[6],
+                                            uint16_t id) {
+    while (mc) {
+        const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mc);
+        mc &= mc - 1;
+        const uint32_t slot = atomicAdd(&cnt[b], 1u) & 0xFFFFu;
+        seg[(size_t)b * kTile + slot] = id;
+    }
+    if constexpr (SAT) {
+        while (ms) {
+            const uint32_t sl = (uint32_t)__builtin_ctzll(ms);
+            ms &= ms - 1;
+            uint32_t m6 = 0;
+#pragma unroll
+            for (uint32_t a = 0; a < 6; ++a) m6 |= (uint32_t)((mo[a] >> sl) & 1ull) << a;
+            const uint32_t b = b0 + sl;
+            const uint32_t slot = kTile - 1u - (atomicAdd(&cnt[b], 1u << 16) >> 16);
+            seg[(size_t)b * kTile + slot] = (uint16_t)(id | (m6 << kIdBits));
+        }
+    }
+}
+
+template <bool SAT>
+__device__ __forceinline__ void wave_append(uint32_t *cnt, uint16_t *seg, uint32_t b0, uint32_t ns,
+                                            uint64_t mc, uint64_t ms, const uint64_t (&mo)[6],
+                                            uint16_t id, uint32_t lane) {
+    uint32_t myc = 0;
+    for (uint32_t k = 0; k < ns; ++k) {  // uniform
+        uint32_t v = (uint32_t)__popcll(__ballot((mc >> k) & 1ull));
+        if constexpr (SAT) v |= (uint32_t)__popcll(__ballot((ms >> k) & 1ull)) << 16;
+        if (lane == k) myc = v;
+    }
+    uint32_t base = 0;
+    if (lane < ns && myc) base = atomicAdd(&cnt[b0 + lane], myc);
+    for (uint32_t k = 0; k < ns; ++k) {  // uniform
+        const u64 bc = __ballot((mc >> k) & 1ull);
+        const u64 bs = SAT ? __ballot((ms >> k) & 1ull) : 0ull;
+        if (!(bc | bs)) continue;  // uniform
+        const uint32_t bk = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)k);
+        uint16_t *sg = seg + (size_t)(b0 + k) * kTile;
+        if ((mc >> k) & 1ull)
+            sg[(bk & 0xFFFFu) + __builtin_amdgcn_mbcnt_hi((uint32_t)(bc >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bc, 0u))] = id;
+        if constexpr (SAT) {
+            if ((ms >> k) & 1ull) {
+                uint32_t m6 = 0;
+#pragma unroll
+                for (uint32_t a = 0; a < 6; ++a) m6 |= (uint32_t)((mo[a] >> k) & 1ull) << a;
+                const uint32_t r = (bk >> 16) + __builtin_amdgcn_mbcnt_hi(
+                                                    (uint32_t)(bs >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bs, 0u));
+                sg[kTile - 1u - r] = (uint16_t)(id | (m6 << kIdBits));
+            }
+        }
+    }
+}
+
 template <bool POW2, uint32_t GROUP = 1>
 __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inputs,
                                                   FastLevels fl, BinInfo bi, int align_corners,
@@ -395,14 +473,18 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
         __syncthreads();
         uint16_t *seg = entries + (size_t)tile * nb * kTile;
         const uint32_t s_end = min(M, (tile + 1) * kTile);
-        for (uint32_t s = tile * kTile + threadIdx.x; s < s_end; s += blockDim.x) {
+        {
+            // one sample (group) per thread (blockDim == kTile): every lane of a
+            // wave reaches the per-level appends, which are wave-wide
+            const uint32_t s = tile * kTile + threadIdx.x;
             // the group's points, mapped to [0, 1]; out-of-range points skip
             float xg[GROUP][3];
             uint32_t in = 0;
+#pragma unroll
+            for (uint32_t a = 0; a < GROUP; ++a) xg[a][0] = xg[a][1] = xg[a][2] = 0.0f;
             if constexpr (GROUP == 1) {
-                if (!load_pos<3, POW2>(inputs, dyn, inv, s, xg[0])) continue;
-                in = 1;
-            } else {
+                if (s < s_end && load_pos<3, POW2>(inputs, dyn, inv, s, xg[0])) in = 1;
+            } else if (s < s_end) {
                 float xr[3];
 #pragma unroll
                 for (uint32_t d = 0; d < 3; ++d) xr[d] = inputs[(size_t)s * 3 + d];
@@ -418,9 +500,9 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                     }
                     in |= (ok ? 1u : 0u) << a;
                 }
-                if (!in) continue;
             }
-            const uint16_t id = (uint16_t)(s - tile * kTile);
+            const uint16_t id = (uint16_t)threadIdx.x;
+            const uint32_t lane = threadIdx.x & 63u;
             // stencil groups: point 1 + 2 axis + k moves only along `axis`, so
             // when its other two mapped coordinates equal the sample's (the
             // sample inside the bound: the clamp is the identity) its cell
@@ -453,19 +535,20 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                         if ((r & smask) == smask) mk |= 1ull << (((r + 1u) & wm) >> shift);
                     }
                 };
-                const uint32_t b0 = fl.bin0[l];
+                const uint32_t b0 = fl.bin0[l], ns = bi.bin0[l + 1] - b0;
                 if constexpr (GROUP == 1) {
                     uint64_t mask = 0;
-                    const uint32_t c0 = (uint32_t)floorf(fmaf(xg[0][0], sc, half));
-                    const uint32_t c1 = (uint32_t)floorf(fmaf(xg[0][1], sc, half));
-                    const uint32_t c2 = (uint32_t)floorf(fmaf(xg[0][2], sc, half));
-                    pairs(c0 + c1 * m1 + c2 * m2, mask);
-                    while (mask) {
-                        const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mask);
-                        mask &= mask - 1;
-                        const uint32_t slot = atomicAdd(&cnt[b], 1u);
-                        seg[(size_t)b * kTile + slot] = id;
+                    if (in) {
+                        const uint32_t c0 = (uint32_t)floorf(fmaf(xg[0][0], sc, half));
+                        const uint32_t c1 = (uint32_t)floorf(fmaf(xg[0][1], sc, half));
+                        const uint32_t c2 = (uint32_t)floorf(fmaf(xg[0][2], sc, half));
+                        pairs(c0 + c1 * m1 + c2 * m2, mask);
                     }
+                    const uint64_t none[6] = {0, 0, 0, 0, 0, 0};
+                    if (ns <= DFHIP_BIN_BALLOT_NS)  // uniform
+                        wave_append<false>(cnt, seg, b0, ns, mask, 0, none, id, lane);
+                    else
+                        lane_append<false>(cnt, seg, b0, mask, 0, none, id);
                 } else {
                     // mc: slices of the sample's own corners; mo[a - 1]: those of
                     // moved point a (0 when its cell is the sample's)
@@ -484,7 +567,7 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                             const uint32_t ca = (uint32_t)floorf(fmaf(xg[a][ax], sc, half));
                             if (ca != c[ax]) pairs(i0 + (ca - c[ax]) * stride, mo[a - 1]);
                         }
-                    } else {
+                    } else if (in) {
 #pragma unroll
                         for (uint32_t a = 0; a < 7; ++a) {
                             if (!((in >> a) & 1u)) continue;
@@ -497,30 +580,17 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                     }
                     // centre entries (front of the segment): every slice the
                     // sample's corners touch; the walk takes all seven points
-                    // there.  (A mask of the moved points touching a centre
+                    // there.  Satellite entries (back of the segment): slices
+                    // only moved points touch, with the mask of those points in
+                    // bits 10..15.  (A mask of the moved points touching a centre
                     // entry's slice, to skip the others there, cost more in the
                     // binning than it saved in the walk: bin 173 -> 192 us, walk
-                    // 972 -> 964 us; so did one append loop over both kinds:
-                    // 173 -> 188 us.)
-                    uint64_t ms = (mo[0] | mo[1] | mo[2] | mo[3] | mo[4] | mo[5]) & ~mc;
-                    while (mc) {
-                        const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mc);
-                        mc &= mc - 1;
-                        const uint32_t slot = atomicAdd(&cnt[b], 1u) & 0xFFFFu;
-                        seg[(size_t)b * kTile + slot] = id;
-                    }
-                    // satellite entries (back of the segment): slices only moved
-                    // points touch, with the mask of those points in bits 10..15
-                    while (ms) {
-                        const uint32_t sl = (uint32_t)__builtin_ctzll(ms);
-                        ms &= ms - 1;
-                        uint32_t m6 = 0;
-#pragma unroll
-                        for (uint32_t a = 0; a < 6; ++a) m6 |= (uint32_t)((mo[a] >> sl) & 1ull) << a;
-                        const uint32_t b = b0 + sl;
-                        const uint32_t slot = kTile - 1u - (atomicAdd(&cnt[b], 1u << 16) >> 16);
-                        seg[(size_t)b * kTile + slot] = (uint16_t)(id | (m6 << kIdBits));
-                    }
+                    // 972 -> 964 us.)
+                    const uint64_t ms = (mo[0] | mo[1] | mo[2] | mo[3] | mo[4] | mo[5]) & ~mc;
+                    if (ns <= DFHIP_BIN_BALLOT_NS)  // uniform
+                        wave_append<true>(cnt, seg, b0, ns, mc, ms, mo, id, lane);
+                    else
+                        lane_append<true>(cnt, seg, b0, mc, ms, mo, id);
                 }
             }
         }
@@ -1894,6 +1964,7 @@ __global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, 
     __shared__ uint32_t sbase[kChunkTiles];
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t sh_b, sh_j, sh_p;
+    const uint64_t tr0 = bi.trace ? wall_clock64() : 0;
     if (threadIdx.x < 64) walk_plan(bi, counts, sh_b, sh_j, sh_p);
     __syncthreads();
     const uint32_t P = sh_p;
@@ -1906,6 +1977,7 @@ __global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, 
     const uint32_t n = min(srows, bi.rows[l] - lo);
     for (uint32_t i = threadIdx.x; i < srows * 2; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
+    const uint64_t tr1 = bi.trace ? wall_clock64() : 0;
     const uint32_t ntiles = ceil_div(ge::dyn_count(dyn, B), kTile);
     const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
 #define DFHIP_RW(LD)                                                                            \
@@ -1919,6 +1991,22 @@ __global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, 
     float *out = partial + (size_t)blockIdx.x * ((size_t)srows * 2);
     for (uint32_t i = threadIdx.x; i < n * 2; i += blockDim.x)
         out[i] = (float)acc[(i & 1u) * srows + (i >> 1)];
+    if (bi.trace) {  // debug timeline (dfhip_binned_opts.trace), as k_walk's
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t e = 0;  // the part's entries
+            for (uint32_t t = part; t < ntiles; t += P) e += counts[(size_t)t * bi.nbins + b];
+            uint64_t *r = bi.trace + (size_t)blockIdx.x * 8;
+            r[0] = b;
+            r[1] = b + 1;
+            r[2] = P;
+            r[3] = e;
+            r[4] = tr0;
+            r[5] = tr1;
+            r[6] = part;
+            r[7] = wall_clock64();
+        }
+    }
 }
 
 // ---------------------------------------------------------------- 3. sum

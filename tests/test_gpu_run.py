@@ -40,10 +40,12 @@ def _models(gpu, seed=0, emb_scale=0.5):
     return opt, net, ref
 
 
-def test_run_matches_cpu_oracle(gpu):
+@pytest.mark.parametrize("res", [32, 64])
+def test_run_matches_cpu_oracle(gpu, res):
+    """64 x 64 is BASELINE configs[0]'s render size (C1)."""
     from nerf.provider import NeRFDataset
     opt, net, ref = _models(gpu)
-    data = NeRFDataset(opt, device=gpu, type="test", H=32, W=32, size=8).collate([2])
+    data = NeRFDataset(opt, device=gpu, type="test", H=res, W=res, size=8).collate([2])
     rays_o, rays_d = data["rays_o"], data["rays_d"]
     light = torch.tensor([0.0, 0.0, 1.0], device=gpu)
     with torch.no_grad():

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--radius", type=float, default=0.56)
+    ap.add_argument("--mode", type=int, default=0, help="walk mode (0 per segment, 3 resolved)")
     args = ap.parse_args()
     import _dfhip
     import _gridencoder
@@ -44,8 +45,8 @@ def main():
     g = (torch.randn(L, B, 2, device=dev) * 0.01).half()
     gemb = torch.empty(int(offs[-1]), 2, device=dev)
     trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
-    opts = _gridencoder.BinnedOpts(walk_mode=0, trace=trace)
-    ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts)
+    opts = _gridencoder.BinnedOpts(walk_mode=args.mode, trace=trace)
+    ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts, S=S, H=16)
     ent = torch.empty(ne_, dtype=torch.int32, device=dev)
     cnt = torch.empty(nc, dtype=torch.int32, device=dev)
     part = torch.empty(npf, device=dev)
