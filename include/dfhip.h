@@ -540,7 +540,7 @@ typedef struct dfhip_binned_opts {
                                    bit-reversed order (1) or in lane order (0) */
     uint64_t *trace;            /* debug: per-workgroup walk timeline, 8 u64 per walk
                                    workgroup {bin, bin + 1, parts, entries, t0, t0, part, t1}
-                                   (per-segment walk and resolved stream); NULL = off */
+                                   (every walk form); NULL = off */
 } dfhip_binned_opts;
 /* dfhip_grid_backward_binned_scratch / dfhip_grid_encode_backward_binned_stencil
  * with per-call options (group 1 = single samples, eps ignored; group 7 =
@@ -552,6 +552,10 @@ int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32_t *offsets
                                             uint32_t gridtype, int align_corners, uint32_t group,
                                             const dfhip_binned_opts *opts, uint64_t *entries_u32,
                                             uint64_t *counts_u32, uint64_t *partial_f32);
+/* Samples per binning tile (the id slots of one (tile, slice) segment of the
+ * entries scratch) of a call with this group and these options; 0 on bad
+ * options. */
+uint32_t dfhip_grid_backward_binned_tile(uint32_t group, const dfhip_binned_opts *opts);
 int dfhip_grid_encode_backward_binned_opts(int phase, int grad_dtype, const void *grad_lbc,
                                            const float *inputs, float bound,
                                            const int32_t *offsets, const int32_t *offsets_host,

@@ -184,6 +184,8 @@ def load() -> ctypes.CDLL:
     lib.dfhip_grid_backward_partial_floats.argtypes = [_u32, _u32, _u32]
     lib.dfhip_shading_partial_doubles.restype = _u32
     lib.dfhip_shading_partial_doubles.argtypes = [_u32]
+    lib.dfhip_grid_backward_binned_tile.restype = _u32
+    lib.dfhip_grid_backward_binned_tile.argtypes = [_u32, _vp]
     lib.dfhip_march_rays_train_stage_floats.restype = ctypes.c_uint64
     lib.dfhip_march_rays_train_stage_floats.argtypes = [_u32, _u32]
     for name, args in _SIGS.items():
@@ -199,7 +201,7 @@ def exported_symbols() -> list[str]:
             "dfhip_grid_backward_default_parts", "dfhip_grid_backward_partial_floats",
             "dfhip_field_mlp_params", "dfhip_field_mlp_backward_parts",
             "dfhip_ray_head_partial_floats", "dfhip_march_rays_train_stage_floats",
-            "dfhip_shading_partial_doubles",
+            "dfhip_shading_partial_doubles", "dfhip_grid_backward_binned_tile",
             *_SIGS.keys()]
 
 

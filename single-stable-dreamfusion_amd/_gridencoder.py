@@ -125,6 +125,11 @@ def _opts_ref(opts):
     return None if opts is None else ctypes.byref(opts)
 
 
+def grid_backward_binned_tile(opts=None, group=1):
+    """Samples per binning tile (id slots per (tile, slice) segment)."""
+    return int(_d.load().dfhip_grid_backward_binned_tile(int(group), _opts_ref(opts)))
+
+
 def grid_backward_binned_scratch(cap, offsets_host, L, C, opts=None, group=1, S=0.0, H=1,
                                  gridtype=1, align_corners=False):
     """(entries u32, counts u32, partial f32) element counts for capacity cap

@@ -48,6 +48,18 @@ using ge::SliceDyn;
 typedef unsigned long long u64;
 
 constexpr uint32_t kTile = 1024;              // samples per binning tile (ids per segment)
+// Samples per binning tile for single samples (the albedo step; stencil
+// groups keep kTile: their entries carry a 6-bit point mask above 10 id
+// bits).  Longer tiles make longer (tile, slice) segments: the per-segment
+// walk pays one dependent count -> ids -> data round trip per segment, and at
+// the fine levels a 1,024-sample tile leaves ~40 entries per segment, less
+// than one per lane.
+#ifndef DFHIP_TILE1
+#define DFHIP_TILE1 1024
+#endif
+constexpr uint32_t kTile1 = DFHIP_TILE1;
+static_assert(kTile1 >= kTile && kTile1 <= 65536 && (kTile1 & (kTile1 - 1)) == 0,
+              "DFHIP_TILE1: a power of two in [1024, 65536] (u16 tile-relative ids)");
 constexpr uint32_t kMaxBins = 4096;
 constexpr uint32_t kMaxSlices = 128;          // slices per level (k_bin's 128-bit masks)
 constexpr uint32_t kSliceBytes = 128 * 1024;  // f64 accumulators of one walk workgroup
@@ -58,9 +70,24 @@ constexpr uint32_t kIdBits = 10;
 constexpr uint32_t kIdMask = (1u << kIdBits) - 1u;
 static_assert(kTile == (1u << kIdBits), "ids fill the low kIdBits bits of an entry");
 constexpr uint32_t kCentreCost = 4;  // walk cost of a centre entry in satellite entries
+// Walk cost of a non-empty (tile, slice) segment, in entries, added to the
+// bin totals that deal out the walk parts (P_b ~ cost): a segment pays a
+// dependent count -> ids -> data round trip whatever its size, so a slice
+// whose samples are few per tile but spread over every tile (the scene's
+// edge slices) is slow per entry.  Entries alone (r05 walk timeline, 1.1 M
+// samples): such single-part bins walked 67-180 entries/us against ~300 for
+// the others, and the slowest of them (173 us) set the 260 us kernel span
+// beside a 75 us mean workgroup.
+#ifndef DFHIP_SEG_COST
+#define DFHIP_SEG_COST 48
+#endif
+#ifndef DFHIP_SEG_COST7  // the same for stencil groups, in satellite entries
+#define DFHIP_SEG_COST7 48
+#endif
 
 struct BinInfo {
     uint32_t L, nbins, shift, tcap;      // tcap: tiles of the capacity (counts row stride)
+    uint32_t tile;                       // samples per tile = id slots per segment
     uint32_t G;                          // walk workgroups
     uint32_t lane_perm;                  // walk: bit-reversed lane -> run map (1) or identity
     uint32_t o_roff, o_totals, o_plan;   // word offsets into `counts` (layout below)
@@ -129,13 +156,17 @@ static uint32_t slice_shift(uint32_t C) {
 //   [nbins][16]    totals, as 16 partial sums      (k_bin; zeroed before it)
 //   [nbins][2]     first image slot, parts         (k_walk; zeroed before k_bin)
 // Host: bins and layout from the HOST copy of the offsets.
+static int flat_walk_mode(uint32_t group, const Opts &op);
 static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint32_t cap,
-                      const Opts &op, BinInfo &bi) {
+                      uint32_t group, const Opts &op, BinInfo &bi) {
     if (L == 0 || L > ge::kMaxLevels || C == 0) return false;
     bi.L = L;
     bi.trace = op.trace;
     bi.shift = slice_shift(C);
-    bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, kTile);
+    // single samples bin into kTile1-sample tiles (not the resolved stream,
+    // whose k_rbin runs one thread per sample of a kTile tile)
+    bi.tile = (group == 1 && flat_walk_mode(1, op) != 3) ? kTile1 : kTile;
+    bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, bi.tile);
     bi.G = op.walk_g * device_cus();
     bi.lane_perm = op.lane_perm;
     uint32_t nb = 0;
@@ -257,7 +288,7 @@ __device__ __forceinline__ void slice_mask(const ge::LevelRows &lr, const uint32
 // Append sample s (tile-relative id) to the segments of the slices in mask.
 template <uint32_t W>
 __device__ __forceinline__ void append(const uint64_t (&mask)[W], uint32_t b0, uint32_t *cnt,
-                                       uint16_t *seg, uint16_t id) {
+                                       uint16_t *seg, uint16_t id, uint32_t tile) {
 #pragma unroll
     for (uint32_t h = 0; h < W; ++h) {
         uint64_t mk = mask[h];
@@ -265,7 +296,7 @@ __device__ __forceinline__ void append(const uint64_t (&mask)[W], uint32_t b0, u
             const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mk) + 64u * h;
             mk &= mk - 1;
             const uint32_t slot = atomicAdd(&cnt[b], 1u);
-            seg[(size_t)b * kTile + slot] = id;
+            seg[(size_t)b * tile + slot] = id;
         }
     }
 }
@@ -281,14 +312,15 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
     __shared__ uint32_t cnt[kMaxBins];
     const bool align = align_corners != 0;
     const uint32_t M = ge::dyn_count(dyn, B);
-    const uint32_t ntiles = ceil_div(M, kTile);
+    const uint32_t T = bi.tile;
+    const uint32_t ntiles = ceil_div(M, T);
     const uint32_t nb = bi.nbins;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
         __syncthreads();
-        uint16_t *seg = entries + (size_t)tile * nb * kTile;
-        const uint32_t s_end = min(M, (tile + 1) * kTile);
-        for (uint32_t s = tile * kTile + threadIdx.x; s < s_end; s += blockDim.x) {
+        uint16_t *seg = entries + (size_t)tile * nb * T;
+        const uint32_t s_end = min(M, (tile + 1) * T);
+        for (uint32_t s = tile * T + threadIdx.x; s < s_end; s += blockDim.x) {
             float x[D];
             if (!load_pos<D, POW2>(inputs, dyn, inv, s, x)) continue;
             for (uint32_t l = 0; l < bi.L; ++l) {
@@ -299,19 +331,19 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
                 locate<D>(c, align, x, cell, frac);
                 const int mode = ge::row_mode(lr);
                 const uint32_t b0 = bi.bin0[l];
-                const uint16_t id = (uint16_t)(s - tile * kTile);
+                const uint16_t id = (uint16_t)(s - tile * T);
                 if (bi.bin0[l + 1] - b0 <= 64) {  // uniform: one mask word
                     uint64_t mask[1];
                     if (mode == 0) slice_mask<D, 0, 1>(lr, cell, bi.shift, mask);
                     else if (mode == 1) slice_mask<D, 1, 1>(lr, cell, bi.shift, mask);
                     else slice_mask<D, 2, 1>(lr, cell, bi.shift, mask);
-                    append<1>(mask, b0, cnt, seg, id);
+                    append<1>(mask, b0, cnt, seg, id, T);
                 } else {
                     uint64_t mask[2];
                     if (mode == 0) slice_mask<D, 0, 2>(lr, cell, bi.shift, mask);
                     else if (mode == 1) slice_mask<D, 1, 2>(lr, cell, bi.shift, mask);
                     else slice_mask<D, 2, 2>(lr, cell, bi.shift, mask);
-                    append<2>(mask, b0, cnt, seg, id);
+                    append<2>(mask, b0, cnt, seg, id, T);
                 }
             }
         }
@@ -319,7 +351,9 @@ __global__ __launch_bounds__(1024) void k_bin(const float *__restrict__ inputs,
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
             const uint32_t v = cnt[b];
             counts[(size_t)tile * nb + b] = v;
-            if (v) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], v);
+            if (v)
+                atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit],
+                          v + (uint32_t)DFHIP_SEG_COST);
         }
         __syncthreads();
     }
@@ -400,12 +434,12 @@ __device__ __forceinline__ void group_point(const float (&xr)[3], uint32_t a, co
 template <bool SAT>
 __device__ __forceinline__ void lane_append(uint32_t *cnt, uint16_t *seg, uint32_t b0,
                                             uint64_t mc, uint64_t ms, const uint64_t (&mo)[6],
-                                            uint16_t id) {
+                                            uint16_t id, uint32_t tile) {
     while (mc) {
         const uint32_t b = b0 + (uint32_t)__builtin_ctzll(mc);
         mc &= mc - 1;
         const uint32_t slot = atomicAdd(&cnt[b], 1u) & 0xFFFFu;
-        seg[(size_t)b * kTile + slot] = id;
+        seg[(size_t)b * tile + slot] = id;
     }
     if constexpr (SAT) {
         while (ms) {
@@ -415,8 +449,8 @@ __device__ __forceinline__ void lane_append(uint32_t *cnt, uint16_t *seg, uint32
 #pragma unroll
             for (uint32_t a = 0; a < 6; ++a) m6 |= (uint32_t)((mo[a] >> sl) & 1ull) << a;
             const uint32_t b = b0 + sl;
-            const uint32_t slot = kTile - 1u - (atomicAdd(&cnt[b], 1u << 16) >> 16);
-            seg[(size_t)b * kTile + slot] = (uint16_t)(id | (m6 << kIdBits));
+            const uint32_t slot = tile - 1u - (atomicAdd(&cnt[b], 1u << 16) >> 16);
+            seg[(size_t)b * tile + slot] = (uint16_t)(id | (m6 << kIdBits));
         }
     }
 }
@@ -424,7 +458,7 @@ __device__ __forceinline__ void lane_append(uint32_t *cnt, uint16_t *seg, uint32
 template <bool SAT>
 __device__ __forceinline__ void wave_append(uint32_t *cnt, uint16_t *seg, uint32_t b0, uint32_t ns,
                                             uint64_t mc, uint64_t ms, const uint64_t (&mo)[6],
-                                            uint16_t id, uint32_t lane) {
+                                            uint16_t id, uint32_t lane, uint32_t tile) {
     uint32_t myc = 0;
     for (uint32_t k = 0; k < ns; ++k) {  // uniform
         uint32_t v = (uint32_t)__popcll(__ballot((mc >> k) & 1ull));
@@ -438,7 +472,7 @@ __device__ __forceinline__ void wave_append(uint32_t *cnt, uint16_t *seg, uint32
         const u64 bs = SAT ? __ballot((ms >> k) & 1ull) : 0ull;
         if (!(bc | bs)) continue;  // uniform
         const uint32_t bk = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)k);
-        uint16_t *sg = seg + (size_t)(b0 + k) * kTile;
+        uint16_t *sg = seg + (size_t)(b0 + k) * tile;
         if ((mc >> k) & 1ull)
             sg[(bk & 0xFFFFu) + __builtin_amdgcn_mbcnt_hi((uint32_t)(bc >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bc, 0u))] = id;
@@ -450,7 +484,7 @@ __device__ __forceinline__ void wave_append(uint32_t *cnt, uint16_t *seg, uint32
                 const uint32_t r = (bk >> 16) + __builtin_amdgcn_mbcnt_hi(
                                                     (uint32_t)(bs >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bs, 0u));
-                sg[kTile - 1u - r] = (uint16_t)(id | (m6 << kIdBits));
+                sg[tile - 1u - r] = (uint16_t)(id | (m6 << kIdBits));
             }
         }
     }
@@ -466,17 +500,18 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
     __shared__ uint32_t cnt[kMaxBins];
     const float half = align_corners ? 0.0f : 0.5f;
     const uint32_t M = ge::dyn_count(dyn, B);
-    const uint32_t ntiles = ceil_div(M, kTile);
+    const uint32_t T = GROUP == 1 ? bi.tile : kTile;
+    const uint32_t ntiles = ceil_div(M, T);
     const uint32_t nb = bi.nbins, shift = bi.shift, smask = (1u << bi.shift) - 1u;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
         __syncthreads();
-        uint16_t *seg = entries + (size_t)tile * nb * kTile;
-        const uint32_t s_end = min(M, (tile + 1) * kTile);
-        {
-            // one sample (group) per thread (blockDim == kTile): every lane of a
-            // wave reaches the per-level appends, which are wave-wide
-            const uint32_t s = tile * kTile + threadIdx.x;
+        uint16_t *seg = entries + (size_t)tile * nb * T;
+        const uint32_t s_end = min(M, (tile + 1) * T);
+        // a uniform trip count: every lane of a wave reaches the per-level
+        // appends, which may be wave-wide
+        for (uint32_t s0 = tile * T; s0 < s_end; s0 += blockDim.x) {
+            const uint32_t s = s0 + threadIdx.x;
             // the group's points, mapped to [0, 1]; out-of-range points skip
             float xg[GROUP][3];
             uint32_t in = 0;
@@ -501,7 +536,7 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                     in |= (ok ? 1u : 0u) << a;
                 }
             }
-            const uint16_t id = (uint16_t)threadIdx.x;
+            const uint16_t id = (uint16_t)(s - tile * T);
             const uint32_t lane = threadIdx.x & 63u;
             // stencil groups: point 1 + 2 axis + k moves only along `axis`, so
             // when its other two mapped coordinates equal the sample's (the
@@ -546,9 +581,9 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                     }
                     const uint64_t none[6] = {0, 0, 0, 0, 0, 0};
                     if (ns <= DFHIP_BIN_BALLOT_NS)  // uniform
-                        wave_append<false>(cnt, seg, b0, ns, mask, 0, none, id, lane);
+                        wave_append<false>(cnt, seg, b0, ns, mask, 0, none, id, lane, T);
                     else
-                        lane_append<false>(cnt, seg, b0, mask, 0, none, id);
+                        lane_append<false>(cnt, seg, b0, mask, 0, none, id, T);
                 } else {
                     // mc: slices of the sample's own corners; mo[a - 1]: those of
                     // moved point a (0 when its cell is the sample's)
@@ -588,9 +623,9 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
                     // 972 -> 964 us.)
                     const uint64_t ms = (mo[0] | mo[1] | mo[2] | mo[3] | mo[4] | mo[5]) & ~mc;
                     if (ns <= DFHIP_BIN_BALLOT_NS)  // uniform
-                        wave_append<true>(cnt, seg, b0, ns, mc, ms, mo, id, lane);
+                        wave_append<true>(cnt, seg, b0, ns, mc, ms, mo, id, lane, T);
                     else
-                        lane_append<true>(cnt, seg, b0, mc, ms, mo, id);
+                        lane_append<true>(cnt, seg, b0, mc, ms, mo, id, T);
                 }
             }
         }
@@ -601,7 +636,9 @@ __global__ __launch_bounds__(1024) void k_bin_fast(const float *__restrict__ inp
             // bin totals weigh a centre entry (seven points) as kCentreCost
             // satellite entries (one point) for the walk's part plan
             const uint32_t w = (v & 0xFFFFu) * (GROUP > 1 ? kCentreCost : 1u) + (v >> 16);
-            if (w) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], w);
+            if (w)
+                atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit],
+                          w + (uint32_t)(GROUP > 1 ? DFHIP_SEG_COST7 : DFHIP_SEG_COST));
         }
         __syncthreads();
     }
@@ -833,7 +870,8 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     const LevelCtx c = ge::level_ctx<D>(offsets, lv, l, gridtype, align);
     const ge::LevelRows lr = ge::level_rows<D>(c);
     const uint32_t M = ge::dyn_count(dyn, B);
-    const uint32_t ntiles = ceil_div(M, kTile);
+    const uint32_t T = GROUP == 1 ? bi.tile : kTile;
+    const uint32_t ntiles = ceil_div(M, T);
     const grad_t *gl = grad + (size_t)l * GROUP * B * C;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
     // the level's lead (corners 2^lead) is uniform over the workgroup: the
@@ -847,8 +885,8 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         const uint32_t raw = counts[(size_t)t * nb + b];
         const uint32_t cnt = raw & 0xFFFFu, nsat = raw >> 16;  // centre / satellite entries
         if (bi.trace && lane == 0) atomicAdd(&n_seen, cnt + nsat);
-        const uint16_t *seg = entries + ((size_t)t * nb + b) * kTile;
-        const uint32_t tbase = t * kTile;
+        const uint16_t *seg = entries + ((size_t)t * nb + b) * T;
+        const uint32_t tbase = t * T;
         const uint32_t Q = (cnt + 63) >> 6;
         // lane -> run: bit-reversed lane index (lanes next to each other in a
         // wave instruction take runs far apart in the segment, i.e. different
@@ -953,7 +991,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         if constexpr (GROUP > 1) {
             // satellite entries (back of the segment): only the moved points
             // of the entry's mask touch this slice
-            const uint16_t *sseg = seg + (kTile - nsat);
+            const uint16_t *sseg = seg + (T - nsat);
             const uint32_t Q2 = (nsat + 63) >> 6;
             const uint32_t f0 = min(rl * Q2, nsat), f1 = min(f0 + Q2, nsat);
             for (uint32_t e = f0; e < f1; ++e) {
@@ -1351,7 +1389,8 @@ __device__ __forceinline__ void flat_walk_chunk(
     const uint32_t *counts, const uint16_t *__restrict__ entries, double *acc, uint32_t *pre,
     uint32_t *wsum, uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t cb,
     uint32_t nc, uint32_t srows, uint32_t lo, uint32_t n, float sc, float half, uint32_t m1,
-    uint32_t m2, uint32_t wm, const SliceDyn &dyn, float inv, const Stencil &st) {
+    uint32_t m2, uint32_t wm, const SliceDyn &dyn, float inv, const Stencil &st,
+    uint32_t *entries_seen, uint32_t tile1) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t waves = blockDim.x >> 6, nthr = blockDim.x;
     // the chunk's segments end to end: exclusive scan of the counts
@@ -1375,11 +1414,13 @@ __device__ __forceinline__ void flat_walk_chunk(
     }
     __syncthreads();
     const uint32_t E = pre[nc];
+    if (tid == 0) *entries_seen += E;  // the debug trace's entry count
     // entries of chunk tile ti: front slots [0, cnt) or back slots [kTile - cnt, kTile)
+    const uint32_t T = GROUP == 1 ? tile1 : kTile;
     auto seg_of = [&](uint32_t ti) {
         const uint32_t t = part + (cb + ti) * P;
-        const uint16_t *sg = entries + ((size_t)t * nb + b) * kTile;
-        return SAT ? sg + (kTile - (pre[ti + 1] - pre[ti])) : sg;
+        const uint16_t *sg = entries + ((size_t)t * nb + b) * T;
+        return SAT ? sg + (T - (pre[ti + 1] - pre[ti])) : sg;
     };
     if constexpr (WMODE == 2) {
         // per-wave pieces: wave w takes entries [E w / waves, E (w+1) / waves)
@@ -1406,15 +1447,15 @@ __device__ __forceinline__ void flat_walk_chunk(
                 const uint32_t ea = min(rl * Qp, cnt), eb = min(ea + Qp, cnt);
                 if (GROUP > 1 || Qp <= 1)
                     flat_piece<grad_t, C, POW2, GROUP, LEAD, 1, SAT>(
-                        cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                        cell, gl, inputs, seg, t * T, ea, eb, acc, srows, lo, n, sc,
                         half, m1, m2, wm, dyn, inv, st);
                 else if (Qp <= 4)
                     flat_piece<grad_t, C, POW2, GROUP, LEAD, 4, SAT>(
-                        cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                        cell, gl, inputs, seg, t * T, ea, eb, acc, srows, lo, n, sc,
                         half, m1, m2, wm, dyn, inv, st);
                 else
                     flat_piece<grad_t, C, POW2, GROUP, LEAD, 8, SAT>(
-                        cell, gl, inputs, seg, t * kTile, ea, eb, acc, srows, lo, n, sc,
+                        cell, gl, inputs, seg, t * T, ea, eb, acc, srows, lo, n, sc,
                         half, m1, m2, wm, dyn, inv, st);
                 e = pe;
                 ++ti;
@@ -1448,7 +1489,7 @@ __device__ __forceinline__ void flat_walk_chunk(
 #pragma unroll
             for (uint32_t i = 0; i < RUN; ++i) ids[i] = seg[slot + min(i, m - 1)];
             while (true) {
-                const uint32_t tbase = t * kTile;
+                const uint32_t tbase = t * T;
                 // next batch: cursor and its entries, loaded ahead of this batch's data
                 uint32_t ne = e + m, nslot = slot + m, nti = ti, ntend = tend, nt2 = t;
                 const uint16_t *nseg = seg;
@@ -1504,7 +1545,7 @@ __device__ __forceinline__ void flat_walk_level(
     const uint16_t *__restrict__ entries, double *acc, uint32_t *pre, uint32_t *wsum,
     uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t ntiles, uint32_t srows,
     uint32_t lo, uint32_t n, float sc, float half, uint32_t m1, uint32_t m2, uint32_t wm,
-    const SliceDyn &dyn, float inv, const Stencil &st) {
+    const SliceDyn &dyn, float inv, const Stencil &st, uint32_t *entries_seen, uint32_t tile1) {
     const uint32_t nt = ntiles > part ? ceil_div(ntiles - part, P) : 0u;
     FlatCell<C> cell;
     cell.have = false;
@@ -1513,11 +1554,11 @@ __device__ __forceinline__ void flat_walk_level(
         const uint32_t nc = min(nt - cb, kChunkTiles);
         flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN, WMODE, false>(
             cell, gl, inputs, counts, entries, acc, pre, wsum, nb, b, part, P, cb, nc, srows, lo,
-            n, sc, half, m1, m2, wm, dyn, inv, st);
+            n, sc, half, m1, m2, wm, dyn, inv, st, entries_seen, tile1);
         if constexpr (GROUP > 1)
             flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN_SAT, WMODE, true>(
                 cell, gl, inputs, counts, entries, acc, pre, wsum, nb, b, part, P, cb, nc, srows,
-                lo, n, sc, half, m1, m2, wm, dyn, inv, st);
+                lo, n, sc, half, m1, m2, wm, dyn, inv, st, entries_seen, tile1);
     }
     flat_flush<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm);
 }
@@ -1533,9 +1574,11 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     extern __shared__ double acc[];
     __shared__ uint32_t pre[kChunkTiles + 1];
     __shared__ uint32_t wsum[16];
-    __shared__ uint32_t sh_b, sh_j, sh_p;
+    __shared__ uint32_t sh_b, sh_j, sh_p, sh_entries;
+    const uint64_t tr0 = bi.trace ? wall_clock64() : 0;
     const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
     const uint32_t *totals = counts + bi.o_totals;
+    if (threadIdx.x == 0) sh_entries = 0;
     if (threadIdx.x < 64) {  // plan (wave 0), as k_walk
         const uint32_t ln = threadIdx.x;
         u64 T = 0, nz = 0;
@@ -1579,8 +1622,9 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     const uint32_t n = min(srows, bi.rows[l] - lo);
     for (uint32_t i = threadIdx.x; i < srows * C; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
+    const uint64_t tr1 = bi.trace ? wall_clock64() : 0;
     const uint32_t M = ge::dyn_count(dyn, B);
-    const uint32_t ntiles = ceil_div(M, kTile);
+    const uint32_t ntiles = ceil_div(M, GROUP == 1 ? bi.tile : kTile);
     const grad_t *gl = grad + (size_t)l * GROUP * B * C;
     const float sc = fl.scale[l], half = align_corners ? 0.0f : 0.5f;
     const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
@@ -1591,7 +1635,8 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
 #define DFHIP_FLAT(LD)                                                                         \
     flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN, RUN_SAT, WMODE>(gl, inputs, counts, entries, acc, pre, \
                                                      wsum, nb, b, part, P, ntiles, srows, lo, \
-                                                     n, sc, half, m1, m2, wm, dyn, inv, st)
+                                                     n, sc, half, m1, m2, wm, dyn, inv, st, \
+                                                     &sh_entries, bi.tile)
     if (lead >= 3) DFHIP_FLAT(3);
     else if (lead == 2) DFHIP_FLAT(2);
     else DFHIP_FLAT(1);
@@ -1600,6 +1645,17 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     float *out = partial + (size_t)slot * ((size_t)srows * C);
     for (uint32_t i = threadIdx.x; i < n * C; i += blockDim.x)
         out[i] = (float)acc[(i % C) * srows + i / C];
+    if (bi.trace && threadIdx.x == 0) {  // debug timeline (dfhip_binned_opts.trace)
+        uint64_t *r = bi.trace + (size_t)blockIdx.x * 8;
+        r[0] = b;
+        r[1] = b + 1;
+        r[2] = P;
+        r[3] = sh_entries;
+        r[4] = tr0;
+        r[5] = tr1;
+        r[6] = part;
+        r[7] = wall_clock64();
+    }
 }
 
 // ---------------------------------------------------------------- 4. resolved stream
@@ -1716,7 +1772,9 @@ __global__ __launch_bounds__(1024) void k_rbin(const float *__restrict__ inputs,
             toff[b] = off;
             counts[(size_t)tile * nb + b] = tc;
             counts[bi.o_roff + (size_t)tile * nb + b] = off;
-            if (tc) atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit], tc);
+            if (tc)
+                atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit],
+                          tc + (uint32_t)DFHIP_SEG_COST);
         }
         __syncthreads();
         // pass B: the entries
@@ -1843,7 +1901,8 @@ __device__ __forceinline__ void rwalk_level(const uint4 *__restrict__ pool, cons
                                             double *acc, uint32_t *pre, uint32_t *sbase,
                                             uint32_t *wsum, uint32_t b, uint32_t part, uint32_t P,
                                             uint32_t ntiles, uint32_t srows, uint32_t lo,
-                                            uint32_t n, uint32_t m1, uint32_t m2, uint32_t wm) {
+                                            uint32_t n, uint32_t m1, uint32_t m2, uint32_t wm,
+                                            uint32_t *entries_seen) {
     const uint32_t nb = bi.nbins;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t waves = blockDim.x >> 6, nthr = blockDim.x;
@@ -1877,6 +1936,7 @@ __device__ __forceinline__ void rwalk_level(const uint4 *__restrict__ pool, cons
         }
         __syncthreads();
         const uint32_t E = pre[nc];
+        if (tid == 0) *entries_seen += E;  // debug trace only
         const uint32_t Q = ceil_div(E, nthr);
         const uint32_t r = wave * 64u + (__builtin_bitreverse32(lane) >> 26);
         uint32_t e = min(r * Q, E);
@@ -1963,8 +2023,9 @@ __global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, 
     __shared__ uint32_t pre[kChunkTiles + 1];
     __shared__ uint32_t sbase[kChunkTiles];
     __shared__ uint32_t wsum[16];
-    __shared__ uint32_t sh_b, sh_j, sh_p;
+    __shared__ uint32_t sh_b, sh_j, sh_p, sh_entries;
     const uint64_t tr0 = bi.trace ? wall_clock64() : 0;
+    if (threadIdx.x == 0) sh_entries = 0;
     if (threadIdx.x < 64) walk_plan(bi, counts, sh_b, sh_j, sh_p);
     __syncthreads();
     const uint32_t P = sh_p;
@@ -1982,7 +2043,7 @@ __global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, 
     const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
 #define DFHIP_RW(LD)                                                                            \
     rwalk_level<grad_t, LD>(pool, counts, bi, tile_entries, acc, pre, sbase, wsum, b, part, P, \
-                            ntiles, srows, lo, n, m1, m2, wm)
+                            ntiles, srows, lo, n, m1, m2, wm, &sh_entries)
     if (lead >= 3) DFHIP_RW(3);
     else if (lead == 2) DFHIP_RW(2);
     else DFHIP_RW(1);
@@ -1994,13 +2055,11 @@ __global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, 
     if (bi.trace) {  // debug timeline (dfhip_binned_opts.trace), as k_walk's
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t e = 0;  // the part's entries
-            for (uint32_t t = part; t < ntiles; t += P) e += counts[(size_t)t * bi.nbins + b];
             uint64_t *r = bi.trace + (size_t)blockIdx.x * 8;
             r[0] = b;
             r[1] = b + 1;
             r[2] = P;
-            r[3] = e;
+            r[3] = sh_entries;
             r[4] = tr0;
             r[5] = tr1;
             r[6] = part;
@@ -2199,13 +2258,13 @@ extern "C" int dfhip_grid_backward_binned_scratch_opts(
     gb::Opts op;
     if (!gb::resolve_opts(opts, op)) return DFHIP_EINVAL;
     gb::BinInfo bi;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, op, bi)) {
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, group, op, bi)) {
         set_error("grid_backward_binned_scratch: unsupported level layout");
         return DFHIP_EINVAL;
     }
     // tile-relative sample ids, u16 (kTile <= 65536), counted in u32 words;
     // the resolved stream's pool (16-byte entries) where it may run
-    uint64_t ew = ((uint64_t)bi.tcap * bi.nbins * gb::kTile + 1) / 2;
+    uint64_t ew = ((uint64_t)bi.tcap * bi.nbins * bi.tile + 1) / 2;
     if (group == 1 && C == 2 && gb::flat_walk_mode(1, op) == 3 && L <= ge::kMaxLevels) {
         const ge::Levels lv = ge::make_levels(L, S, H);
         gb::FastLevels fl;
@@ -2218,6 +2277,14 @@ extern "C" int dfhip_grid_backward_binned_scratch_opts(
     if (counts_u32) *counts_u32 = gb::counts_words(bi);
     if (partial_f32) *partial_f32 = gb::partial_floats(bi, C);
     return DFHIP_OK;
+}
+
+// Samples per binning tile (= id slots per (tile, slice) segment) of a call
+// with this group and these options (tests read segments with it).
+extern "C" uint32_t dfhip_grid_backward_binned_tile(uint32_t group, const dfhip_binned_opts *opts) {
+    gb::Opts op;
+    if (!gb::resolve_opts(opts, op)) return 0;
+    return (group == 1 && gb::flat_walk_mode(1, op) != 3) ? gb::kTile1 : gb::kTile;
 }
 
 extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host,
@@ -2246,7 +2313,7 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
         return DFHIP_EINVAL;
     }
     gb::BinInfo bi;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, B, op, bi)) {
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, B, group, op, bi)) {
         set_error("%s: unsupported level layout", name);
         return DFHIP_EINVAL;
     }

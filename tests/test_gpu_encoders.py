@@ -419,7 +419,8 @@ def test_grid_backward_fast_bins_equal_generic(gpu, gt):
                                      16, S, 16, gt, False, ent, cnt, part, opts=opts)()
         torch.cuda.synchronize()
         got[fast] = (ent.cpu().numpy().view(np.uint16), cnt.cpu().numpy(), gemb.cpu().numpy())
-    tiles = -(-B // 1024)
+    tsz = _gridencoder.grid_backward_binned_tile()
+    tiles = -(-B // tsz)
     (e0, c0, g0), (e1, c1, g1) = got[0], got[1]
     # counts region [tiles][bins]; bins = slices of 8,192 rows per level (C = 2)
     nb = int(sum(-(-int(offs[l + 1] - offs[l]) // 8192) for l in range(16)))
@@ -428,7 +429,7 @@ def test_grid_backward_fast_bins_equal_generic(gpu, gt):
     for t in range(tiles):
         for b in range(nb):
             n = int(c0[t * nb + b])
-            base = (t * nb + b) * 1024
+            base = (t * nb + b) * tsz
             assert np.array_equal(np.sort(e0[base:base + n]), np.sort(e1[base:base + n])), (t, b)
     np.testing.assert_allclose(g1, g0, rtol=1e-6, atol=1e-9)
 

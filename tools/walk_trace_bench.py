@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--res", type=int, default=128)
+    ap.add_argument("--shade", default="albedo", help="albedo | textureless | lambertian")
     args = ap.parse_args()
     import _dfhip
     import bench
@@ -28,6 +29,8 @@ def main():
     import _gridencoder
     _dfhip.load()
     trainer, data = bench.make_trainer(args.res, 0, 0, 1, True, graph=True)
+    if args.shade != "albedo":
+        trainer.pick_shading = (lambda k: (lambda: (k, 0.1)))(args.shade)
 
     def step():
         trainer.train_iteration(data.collate([0]))
