@@ -1321,7 +1321,9 @@ __device__ __forceinline__ void load_entry(EntryIn<grad_t, C, GROUP, SAT> &in,
                                            const grad_t *__restrict__ gl,
                                            const float *__restrict__ inputs, uint32_t tbase,
                                            uint32_t v) {
-    const uint32_t s = tbase + (v & kIdMask);
+    // satellite entries carry their point mask above the id; other entries
+    // are the plain tile-relative id (up to 16 bits for single samples)
+    const uint32_t s = tbase + (SAT ? (v & kIdMask) : v);
     load_pos3<3>(inputs, s, in.xs);
     if constexpr (SAT) {
         in.m6 = v >> kIdBits;
@@ -2257,14 +2259,19 @@ extern "C" int dfhip_grid_backward_binned_scratch_opts(
     uint64_t *entries_u32, uint64_t *counts_u32, uint64_t *partial_f32) {
     gb::Opts op;
     if (!gb::resolve_opts(opts, op)) return DFHIP_EINVAL;
-    gb::BinInfo bi;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, group, op, bi)) {
+    gb::BinInfo bi, bo;
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, group, op, bi) ||
+        !gb::make_bins(offsets_host, L, C, cap, group == 1 ? 7u : 1u, op, bo)) {
         set_error("grid_backward_binned_scratch: unsupported level layout");
         return DFHIP_EINVAL;
     }
+    // sized for both groups' tile layouts (single samples and stencil groups
+    // tile differently), so a scratch sized for one group is never short for
+    // the other
     // tile-relative sample ids, u16 (kTile <= 65536), counted in u32 words;
     // the resolved stream's pool (16-byte entries) where it may run
-    uint64_t ew = ((uint64_t)bi.tcap * bi.nbins * bi.tile + 1) / 2;
+    uint64_t ew = std::max<uint64_t>(((uint64_t)bi.tcap * bi.nbins * bi.tile + 1) / 2,
+                                      ((uint64_t)bo.tcap * bo.nbins * bo.tile + 1) / 2);
     if (group == 1 && C == 2 && gb::flat_walk_mode(1, op) == 3 && L <= ge::kMaxLevels) {
         const ge::Levels lv = ge::make_levels(L, S, H);
         gb::FastLevels fl;
@@ -2274,7 +2281,7 @@ extern "C" int dfhip_grid_backward_binned_scratch_opts(
             ew = std::max<uint64_t>(ew, (uint64_t)bi.tcap * te * 4ull);
     }
     if (entries_u32) *entries_u32 = ew;
-    if (counts_u32) *counts_u32 = gb::counts_words(bi);
+    if (counts_u32) *counts_u32 = std::max(gb::counts_words(bi), gb::counts_words(bo));
     if (partial_f32) *partial_f32 = gb::partial_floats(bi, C);
     return DFHIP_OK;
 }

@@ -461,7 +461,7 @@ def test_grid_backward_stencil_groups_equal_rows(gpu, dtype):
     out = {}
     for mode in ("rows", "groups"):
         ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
-            7 * cap if mode == "rows" else cap, offs, 16, 2)
+            7 * cap if mode == "rows" else cap, offs, 16, 2, group=1 if mode == "rows" else 7)
         ent = torch.empty(ne, dtype=torch.int32, device=gpu)
         cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
         part = torch.empty(npf, device=gpu)
@@ -566,7 +566,7 @@ def test_grid_backward_walk_forms(gpu, mode):
                 x7.data_ptr(), m7.data_ptr(), _dfhip.stream())
     g7 = (torch.randn(16, 7 * cap, 2, generator=torch.Generator().manual_seed(64)) * 0.1)
     g7 = g7.half().to(gpu)
-    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offs, 16, 2)
+    ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offs, 16, 2, opts, group=7)
     ent = torch.empty(ne, dtype=torch.int32, device=gpu)
     cnt = torch.empty(nc, dtype=torch.int32, device=gpu)
     part = torch.empty(npf, device=gpu)

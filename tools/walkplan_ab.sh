@@ -1,7 +1,7 @@
 #!/bin/bash
-# Walk-plan A/B: the default library against variants lib/libdfhip_{s0,t2k,t4k}.so
-# (s0: no per-segment cost in the part plan, the round-4 plan; t2k / t4k:
-# 2,048 / 4,096-sample binning tiles for single samples).  Per library: the
+# Walk-plan A/B: the default library against variants lib/libdfhip_{s0,t4k}.so
+# (s0: no per-segment cost in the part plan, the round-4 plan; t4k:
+# 4,096-sample binning tiles for single samples).  Per library: the
 # albedo bin-case walk timeline and rocprofv3 kernel stats of the C2 headline
 # steps; for s0 and the default also the textureless step (eager-twin walk
 # timeline, kernel stats).
@@ -14,7 +14,7 @@ L=$PWD/single-stable-dreamfusion_amd/lib
 DFHIP_LIB=$L/libdfhip_t4k.so timeout -k 10 300 python -u -m pytest tests/test_gpu_encoders.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread \
     > $OUT/pytest_t4k.log 2>&1 || { echo "pytest t4k failed"; tail -30 $OUT/pytest_t4k.log; exit 1; }
 tail -1 $OUT/pytest_t4k.log
-for v in ${VARS:-s0 base t2k t4k}; do
+for v in ${VARS:-s0 base t4k}; do
   if [ $v = base ]; then unset DFHIP_LIB; else export DFHIP_LIB=$L/libdfhip_$v.so; fi
   timeout -k 10 200 python -u tools/walk_trace.py --mode 0 --reps 3 > $OUT/trace_$v.log 2>&1 \
       || { echo "trace $v failed"; tail -20 $OUT/trace_$v.log; exit 2; }
