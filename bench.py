@@ -58,6 +58,9 @@ def parse():
                    help="skip timing the textureless / lambertian steps")
     p.add_argument("--no-alt-backward", action="store_true",
                    help="skip timing the other backward structure (two-pass / fused)")
+    p.add_argument("--no-module-path", action="store_true",
+                   help="skip timing the reference-module path (autograd through the "
+                        "reference-API encoder / MLP modules, no fused field, no native step)")
     p.add_argument("--no-c5", action="store_true",
                    help="skip the C5 leg (256x256 bf16 renderer step)")
     p.add_argument("--c5-res", type=int, default=256)
@@ -450,7 +453,7 @@ def measure_traffic(region, timeout=180, warmup=10, shade="albedo", key=None):
     child = [sys.executable, str(Path(__file__).resolve()), "--steps", str(keep), "--warmup",
              str(max(1, warmup)),
              "--no-cpu-baseline", "--no-kernel-timing", "--no-alt-backward", "--no-shading",
-             "--no-infer", "--no-traffic", "--no-c5", "--shade", shade]
+             "--no-infer", "--no-traffic", "--no-c5", "--no-module-path", "--shade", shade]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
     env["TMPDIR"] = "/tmp"
@@ -549,6 +552,33 @@ def measure_traffic(region, timeout=180, warmup=10, shade="albedo", key=None):
         "last 16 dispatches of each kernel; FETCH_SIZE x2 (the gfx950 correction, calibrated for 16-B streaming loads "
         "only: an upper bound for gathers; it also counts Infinity-Cache hits), KiB -> bytes, "
         "summed over the region's kernels, mean per launch; l2_hit_rate per kernel")
+
+
+def module_path_leg(args, timeout=300):
+    """The C2 step through the reference-API modules one by one — grid
+    encoder, MLP and compositing as separate autograd nodes on the
+    `_gridencoder` / `_raymarching` kernels (DFHIP_FUSED_FIELD=0), autograd
+    body instead of the native step (DFHIP_NATIVE_STEP=0), still HIP-graph
+    replayed: the path the reference's own nerf/network_grid.py takes on this
+    package.  A child bench (the switches are read at import)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
+    env.update(DFHIP_NATIVE_STEP="0", DFHIP_FUSED_FIELD="0")
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--steps", str(min(args.steps, 20)),
+           "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-kernel-timing",
+           "--no-alt-backward", "--no-shading", "--no-infer", "--no-traffic", "--no-c5",
+           "--no-module-path"]
+    try:
+        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+        line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+        d = json.loads(line)
+    except (subprocess.TimeoutExpired, IndexError, ValueError) as e:
+        return {"error": f"{type(e).__name__}"}
+    return {"ms_per_step": d["ms_per_step"], "value": d["value"], "unit": d["unit"],
+            "mean_samples_per_step": d["config"]["mean_samples_per_step"],
+            "note": "DFHIP_FUSED_FIELD=0 DFHIP_NATIVE_STEP=0: encoder, MLP and compositing "
+                    "as separate autograd nodes (reference-API modules), graph-replayed"}
 
 
 def shading_roofline(trainer, args):
@@ -851,6 +881,8 @@ def main():
         if not args.no_traffic:
             shade["roofline"] = shading_roofline(trainer, args)
         result["shading"] = shade
+    if world == 1 and not args.no_module_path:
+        result["module_path"] = module_path_leg(args)
     if world == 1 and not args.no_c5:
         result["c5"] = bench_c5(args, rank, world)
     if rank == 0 and world == 1 and not args.no_infer:

@@ -5,8 +5,11 @@ resolution 16 -> 2048*bound) + ReLU MLP 32 -> 64 -> 64 -> 4, a Gaussian density
 blob at the origin, finite-difference normals and a frequency-encoded
 background MLP 39 -> 64 -> 3.  Module names, parameter shapes and creation
 order (hence seeded initialisation and state_dict keys) match the reference
-(network_grid.py:35-181), so the reference file itself also runs on this
-package unchanged.
+(network_grid.py:35-181).  Its forward goes through the same reference-API
+modules (GridEncoder, FreqEncoder, trunc_exp, raymarching.*) that the
+reference file calls; with DFHIP_FUSED_FIELD=0 and DFHIP_NATIVE_STEP=0 they
+run one by one as separate autograd nodes — the path the reference file
+takes on this package — and bench.py times that path as `module_path`.
 """
 import os
 

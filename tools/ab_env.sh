@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 VAR=${VAR:?} A=${A:?} B=${B:?} REGIONS=${REGIONS:-march_rays_train_count,grid_encode_backward}
-ARGS="--steps 40 --warmup 10 --no-cpu-baseline --no-traffic --no-infer --no-c5 --no-shading --no-alt-backward ${BENCH_ARGS:-}"
+ARGS="--steps 40 --warmup 10 --no-cpu-baseline --no-traffic --no-infer --no-c5 --no-module-path --no-shading --no-alt-backward ${BENCH_ARGS:-}"
 for rep in 1 2; do
   for v in $A $B; do
     env $VAR=$v timeout -k 10 300 python bench.py $ARGS > gpurun_out/ab_$v.log 2>&1 \

@@ -21,7 +21,7 @@ python -c "import json; d=json.load(open('$OUT/bench.json')); print('ms/step', d
 # reproduces the line's roofline.frac (tools/roofline_check.py)
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
     -- python bench.py --steps 16 --warmup ${CHILD_WARMUP:-34} --no-cpu-baseline --no-kernel-timing --no-alt-backward \
-       --no-shading --no-infer --no-traffic --no-c5 \
+       --no-shading --no-infer --no-traffic --no-c5 --no-module-path \
     > $OUT/bench_prof.log 2>&1 || { echo "prof failed"; tail -20 $OUT/bench_prof.log; exit 4; }
 python tools/prof_top.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/rocprof_top.txt
 cat $OUT/rocprof_top.txt
@@ -36,6 +36,6 @@ head -8 $OUT/rocprof_shade_top.txt
 # reproduces shading.roofline.frac
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/shchild -o run \
     -- python bench.py --steps 16 --warmup ${CHILD_WARMUP:-34} --no-cpu-baseline --no-kernel-timing --no-alt-backward \
-       --no-shading --no-infer --no-traffic --no-c5 --shade textureless \
+       --no-shading --no-infer --no-traffic --no-c5 --no-module-path --shade textureless \
     > $OUT/shchild.log 2>&1 || { echo "shade child prof failed"; tail -20 $OUT/shchild.log; exit 6; }
 python tools/roofline_check.py $OUT/bench.json $OUT/shchild/run_kernel_trace.csv --shading | tee $OUT/roofline_check_shading.json

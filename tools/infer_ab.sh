@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 VAR=${VAR:?} A=${A:?} B=${B:?}
-ARGS="--steps 2 --warmup 2 --no-cpu-baseline --no-traffic --no-c5 --no-shading --no-alt-backward --no-kernel-timing"
+ARGS="--steps 2 --warmup 2 --no-cpu-baseline --no-traffic --no-c5 --no-module-path --no-shading --no-alt-backward --no-kernel-timing"
 for rep in 1 2; do
   for v in $A $B; do
     env $VAR=$v timeout -k 10 300 python bench.py $ARGS > gpurun_out/iab_$v.log 2>&1 \

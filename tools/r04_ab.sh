@@ -17,7 +17,7 @@ for cfg in ${CONFIGS:?}; do
   mkdir -p $OUT
   env $envs timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c2 -o run \
       -- python bench.py --steps 40 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-traffic \
-         --no-infer --no-c5 --no-shading --no-alt-backward > $OUT/c2.log 2>&1 \
+         --no-infer --no-c5 --no-module-path --no-shading --no-alt-backward > $OUT/c2.log 2>&1 \
       || { echo "c2 prof failed"; tail -5 $OUT/c2.log; exit 4; }
   python tools/prof_top.py $OUT/c2/run_kernel_stats.csv ${TOPN:-8}
   grep '^{' $OUT/c2.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('ms/step', d['ms_per_step'], 'M', d['config']['mean_samples_per_step'])"
@@ -29,7 +29,7 @@ for cfg in ${CONFIGS:?}; do
     for c in FETCH_SIZE WRITE_SIZE; do
       env $envs timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/pmc_$c -o run \
           -- python bench.py --steps 3 --warmup 47 --no-cpu-baseline --no-kernel-timing --no-traffic \
-             --no-infer --no-c5 --no-shading --no-alt-backward > $OUT/pmc_$c.log 2>&1 \
+             --no-infer --no-c5 --no-module-path --no-shading --no-alt-backward > $OUT/pmc_$c.log 2>&1 \
           || { echo "pmc $c failed"; exit 5; }
       for k in k_walk k_bin k_sum; do python tools/pmc_table.py $OUT/pmc_$c $k; done
     done
