@@ -426,21 +426,6 @@ int dfhip_grid_field_forward_quads(int elem, const float *xyz, float bound, cons
                                    const float *b2, const float *w3, const float *b3, void *enc,
                                    float *sigma, void *rgb, int rgb_dtype, uint32_t cap,
                                    const int32_t *m_dev, dfhip_stream_t stream);
-/* dfhip_grid_field_forward_quads over rows laid out in groups: group 1 is the
- * call above; group 7 says row 7 i is sample i and rows 7 i + 1 .. 7 i + 6 its
- * finite-difference stencil points (the FD normal's six common_forward calls,
- * nerf/network_grid.py:90-114, interleaved as dfhip_shading_stencil writes
- * them), and the satellites take their centre's corner quads at the coarse
- * levels where they share its cell.  Identical results to group 1. */
-int dfhip_grid_field_forward_quads_grouped(int elem, const float *xyz, float bound,
-                                           const void *table, const void *quads,
-                                           const int32_t *offsets, uint32_t L, float S,
-                                           uint32_t H, uint32_t gridtype, int align_corners,
-                                           const float *w1, const float *b1, const float *w2,
-                                           const float *b2, const float *w3, const float *b3,
-                                           void *enc, float *sigma, void *rgb, int rgb_dtype,
-                                           uint32_t cap, const int32_t *m_dev, uint32_t group,
-                                           dfhip_stream_t stream);
 /* Backward of dfhip_grid_field_forward: MLP backward (d_enc_lbc [16, cap, 2] f16
  * scratch, mlp_partial: dfhip_field_mlp_backward_parts(cap) * params floats),
  * f32 weight gradients (overwritten), then the sliced embedding backward into

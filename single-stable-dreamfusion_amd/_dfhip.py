@@ -110,9 +110,6 @@ _SIGS = {
     "dfhip_grid_field_forward_quads": [_i32, _vp, _f32, _vp, _vp, _vp, _u32, _f32, _u32, _u32,
                                        _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                        _u32, _vp, _vp],
-    "dfhip_grid_field_forward_quads_grouped": [_i32, _vp, _f32, _vp, _vp, _vp, _u32, _f32, _u32,
-                                               _u32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                               _vp, _vp, _i32, _u32, _vp, _u32, _vp],
     "dfhip_grid_field_forward_bf16": [_vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,
                                       _vp],

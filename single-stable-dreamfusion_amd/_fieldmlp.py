@@ -88,20 +88,14 @@ def grid_quads(embeddings, offsets, S, H, gridtype, align_corners, table, quads)
 
 def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners, weights, enc,
                        sigma, rgb, m_dev=None,
-                       quads=None, group=1):
+                       quads=None):
     """xyz [cap, 3] f32 in [-bound, bound]; table [rows, 2] f16 (fp16 autocast,
     the reference's -O) or bf16 (the C5 bf16 option: features and activations
     bf16 too); offsets [17] int32.  Writes sigma [cap] f32, rgb [cap, 3] (the
     table's dtype or f32) and, when given, enc [cap, 32] in the table's dtype
     (permuted feature order, for grid_field_backward).  Only rows
-    [0, m_dev[0]) are computed when m_dev (int32 device tensor) is given.
-    group=7 (with quads): the rows are 7-point stencil groups (row 7 i the
-    sample, rows 7 i + 1.. its FD points; dfhip_shading_stencil's layout) and
-    the satellites share their centre's coarse-level corner quads; the results
-    are the group=1 results."""
+    [0, m_dev[0]) are computed when m_dev (int32 device tensor) is given."""
     cap = xyz.shape[0]
-    if group not in (1, 7):
-        raise RuntimeError("group must be 1 or 7")
     _f32(xyz, "xyz")
     checked(table, "table")
     if table.dtype not in (torch.float16, torch.bfloat16) or table.dim() != 2 or \
@@ -121,17 +115,11 @@ def grid_field_forward(xyz, bound, table, offsets, S, H, gridtype, align_corners
         if quads.dtype != torch.int32 or tuple(quads.shape) != (table.shape[0], 4):
             raise RuntimeError("quads must be a [rows, 4] int32 tensor (rows = table rows)")
         elem = _d.BF16 if table.dtype == torch.bfloat16 else _d.F16
-        args = (elem, ptr(xyz), float(bound), ptr(table), ptr(quads), ptr(offsets),
-                offsets.shape[0] - 1, float(S), int(H), int(gridtype), int(bool(align_corners)),
-                *_weights(weights), ptr(enc), ptr(sigma), ptr(rgb), _d.dtype_code(rgb, "rgb"),
-                cap, ptr(m_dev))
-        if group == 1:
-            call("dfhip_grid_field_forward_quads", *args, stream())
-        else:
-            call("dfhip_grid_field_forward_quads_grouped", *args, int(group), stream())
+        call("dfhip_grid_field_forward_quads", elem, ptr(xyz), float(bound), ptr(table),
+             ptr(quads), ptr(offsets), offsets.shape[0] - 1, float(S), int(H), int(gridtype),
+             int(bool(align_corners)), *_weights(weights), ptr(enc), ptr(sigma), ptr(rgb),
+             _d.dtype_code(rgb, "rgb"), cap, ptr(m_dev), stream())
         return
-    if group != 1:
-        raise RuntimeError("grouped rows (group=%d) need the corner quads" % group)
     fn = "dfhip_grid_field_forward_bf16" if table.dtype == torch.bfloat16 else \
         "dfhip_grid_field_forward"
     call(fn, ptr(xyz), float(bound), ptr(table), ptr(offsets),

@@ -315,34 +315,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // level, the rows r, r + 1, r + m1, r + m1 + 1 (wrapped like the corners), so
 // a level's corners 0-3 are ONE 16-byte load and corners 4-7 another (none on
 // a z-dropped level): 25 gathers per sample.  Same values, same order.
-//
-// SHARE (QUAD only; stencil groups, dfhip_grid_field_forward_quads_grouped):
-// at levels 0-7 (the first batch) a lane whose cell is the cell of lane
-// `src` (its group's centre row, in the same lane group) skips its quad
-// loads and takes the centre's quads by lane permutes: at those resolutions
-// (16-110 cells per unit against a 2 eps = 0.01 stencil) most of a group's
-// seven points share the centre's cell, so most satellite lanes issue no
-// table request there.  Same rows, same values, same arithmetic.  Every lane
-// of the wave must call it (the permutes read other lanes); out-of-range
-// points take no loads and encode to zero.
-#ifndef DFHIP_FWD_SHARE_PROBE
-#define DFHIP_FWD_SHARE_PROBE 0
-#endif
-template <typename E, bool QUAD = false, bool SHARE = false>
+template <typename E, bool QUAD = false>
 __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restrict__ table,
                                                               const LevelK *lk, bool align,
                                                               const float (&x)[3], int h,
                                                               const u32x4 *__restrict__ quads =
-                                                                  nullptr,
-                                                              int src = 0) {
-    static_assert(!SHARE || QUAD, "shared corner quads need the quad layout");
+                                                                  nullptr) {
     typename Elem<E>::v8 out{};
     typedef float f8 __attribute__((ext_vector_type(8)));
     f8 outf{};  // bf16: the f32 features, converted to bf16 pairs at the end
-    const bool inr =
-        !(x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f);
-    if (!SHARE && !inr) return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
-    const bool self = src == (int)(threadIdx.x & 63u);
+    if (x[0] < 0.0f || x[0] > 1.0f || x[1] < 0.0f || x[1] > 1.0f || x[2] < 0.0f || x[2] > 1.0f)
+        return out;  // gridencoder.cu:91-100: out-of-range samples encode to zero
     const uint32_t *tab = reinterpret_cast<const uint32_t *>(table);
     // two batches of two levels: up to 8 pair loads in flight per lane per
     // batch (all four levels at once held 64 VGPRs of rows and bits and
@@ -369,45 +352,6 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                 const uint32_t i0 = cell[0] + cell[1] * k.m1 + cell[2] * k.m2;
                 const uint32_t ob[4] = {0u, k.m1, k.m2, k.m2 + k.m1};
                 const bool zdrop = k.m2 == 0u;
-                if constexpr (SHARE) {
-                    if (half == 0) {
-                        // the centre's cell index (all-ones: out of range)
-                        const uint32_t mine = inr ? i0 : 0xFFFFFFFFu;
-                        const uint32_t theirs = (uint32_t)__shfl((int)mine, src);
-                        // timing probes (variant libraries; results wrong): 1 =
-                        // no data permutes, 2 = no satellite loads at all
-                        const bool own = DFHIP_FWD_SHARE_PROBE == 2
-                                             ? inr && self
-                                             : inr && (self || theirs != i0);
-                        u32x4 q0{}, q1{};
-                        if (own) {
-                            q0 = quads[k.base + (i0 & k.wmask)];
-                            q1 = zdrop ? q0 : quads[k.base + ((i0 + k.m2) & k.wmask)];
-                        }
-                        if (DFHIP_FWD_SHARE_PROBE == 0 && __ballot(inr && !own)) {  // uniform
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                const uint32_t a = (uint32_t)__shfl((int)q0[j], src);
-                                const uint32_t b = (uint32_t)__shfl((int)q1[j], src);
-                                if (!own) {
-                                    q0[j] = a;
-                                    q1[j] = b;
-                                }
-                            }
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            bits[qq][j] = q0[j];
-                            bits[qq][4 + j] = q1[j];
-                        }
-                        continue;
-                    }
-                    if (!inr) {  // no loads for out-of-range points
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) bits[qq][j] = 0u;
-                        continue;
-                    }
-                }
                 if constexpr (QUAD) {
                     const u32x4 q0 = quads[k.base + (i0 & k.wmask)];
                     u32x4 q1 = q0;
@@ -438,11 +382,6 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
                     }
                 }
             } else {
-                if (SHARE && !inr) {  // no loads for out-of-range points
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) bits[qq][j] = 0u;
-                    continue;
-                }
 #pragma unroll
                 for (uint32_t c = 0; c < 8; ++c) {
                     const uint32_t px = cell[0] + (c & 1u), py = cell[1] + ((c >> 1) & 1u),
@@ -499,7 +438,6 @@ __device__ __forceinline__ typename Elem<E>::v8 grid_features(const E *__restric
         }
     }
     if constexpr (!std::is_same<E, half_t>::value) out = __builtin_convertvector(outf, bf8);
-    if (SHARE && !inr) out = typename Elem<E>::v8{};
     return out;
 }
 

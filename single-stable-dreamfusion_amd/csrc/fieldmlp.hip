@@ -38,13 +38,7 @@ namespace fm {
 // table loads in flight per lane), the features go straight into the MLP's
 // B operand, and are also written (permuted order, 16 B per lane) for the
 // backward.  xyz in [-bound, bound] is mapped to [0, 1] as grid.py:142 does.
-//
-// GROUP 7 (QUAD only): the rows are 7-point stencil groups (row 7 i = sample
-// i, shade.hip's k_stencil), and a satellite row shares its centre's corner
-// quads at the coarse levels where they fall in one cell (grid_features'
-// SHARE): the centre is lane c - (row % 7) of the same lane group when the
-// tile holds it.
-template <typename E, typename rgb_t, bool QUAD, uint32_t GROUP = 1>
+template <typename E, typename rgb_t, bool QUAD>
 __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
     const float *__restrict__ xyz, float bound, const E *__restrict__ table,
     const u32x4 *__restrict__ quads, const int32_t *__restrict__ offsets, ge::Levels lv, uint32_t gridtype, int align_corners,
@@ -91,15 +85,7 @@ __global__ __launch_bounds__(256, 5) void k_field_fwd_fused(
 #pragma unroll
             for (int d = 0; d < 3; ++d)
                 x01[d] = pow2 ? (x[d] + bound) * rext : (x[d] + bound) / ext;
-        v8 xb;
-        if constexpr (GROUP > 1) {
-            // every lane calls (x01 = -1 encodes invalid rows to zero)
-            const uint32_t a = sample % GROUP;
-            const int src = (uint32_t)c >= a ? lane - (int)a : lane;
-            xb = grid_features<E, true, true>(table, LK, align, x01, h, quads, src);
-        } else {
-            xb = valid ? grid_features<E, QUAD>(table, LK, align, x01, h, quads) : v8{};
-        }
+        const v8 xb = valid ? grid_features<E, QUAD>(table, LK, align, x01, h, quads) : v8{};
         if (enc && valid) *reinterpret_cast<v8 *>(enc + (size_t)sample * kIn + 8 * h) = xb;
         FwdG<E> F;
         forward_tile(W, xb, c, h, F);
@@ -666,7 +652,7 @@ static bool check_field_grid(const char *name, uint32_t L) {
     return true;
 }
 
-template <typename E, typename rgb_t, bool QUAD, uint32_t GROUP = 1>
+template <typename E, typename rgb_t, bool QUAD>
 static void launch_field_fwd(hipStream_t s, const float *xyz, float bound, const void *table,
                              const void *quads, const int32_t *offsets, const ge::Levels &lv, uint32_t gridtype,
                              int align_corners, const float *w1, const float *b1, const float *w2,
@@ -676,37 +662,24 @@ static void launch_field_fwd(hipStream_t s, const float *xyz, float bound, const
     // walks ~M / (16 * waves) tiles); more blocks than fit leave a partial
     // last round of blocks (4096 blocks at 5 waves/SIMD were 3.2 rounds)
     const uint32_t tiles = ceil_div(cap, 16u);
-    const uint32_t fit =
-        resident_blocks((const void *)k_field_fwd_fused<E, rgb_t, QUAD, GROUP>, 256, 4);
+    const uint32_t fit = resident_blocks((const void *)k_field_fwd_fused<E, rgb_t, QUAD>, 256, 4);
     const uint32_t blocks = ceil_div(tiles, 4u) < fit ? ceil_div(tiles, 4u) : fit;
-    k_field_fwd_fused<E, rgb_t, QUAD, GROUP><<<blocks, 256, 0, s>>>(
+    k_field_fwd_fused<E, rgb_t, QUAD><<<blocks, 256, 0, s>>>(
         xyz, bound, (const E *)table, (const u32x4 *)quads, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3,
         b3, (E *)enc, sigma, (rgb_t *)rgb, cap, m_dev);
 }
 
 // elem: DFHIP_F16 (table, features, activations in f16: the reference's fp16
 // autocast) or DFHIP_BF16 (all of them bf16: bf16 autocast, the C5 option).
-// group 7: the rows are stencil groups (k_field_fwd_fused GROUP); with quads
-// the satellites share their centre's coarse-level quads (DFHIP_FWD_SHARE=0
-// builds the A/B library that ignores it).
-#ifndef DFHIP_FWD_SHARE
-#define DFHIP_FWD_SHARE 1
-#endif
 static int grid_field_forward(const char *name, int elem, const float *xyz, float bound,
                               const void *table, const void *quads, const int32_t *offsets, uint32_t L, float S,
                               uint32_t H, uint32_t gridtype, int align_corners, const float *w1,
                               const float *b1, const float *w2, const float *b2, const float *w3,
                               const float *b3, void *enc, float *sigma, void *rgb, int rgb_dtype,
-                              uint32_t cap, const int32_t *m_dev, dfhip_stream_t stream,
-                              uint32_t group = 1) {
+                              uint32_t cap, const int32_t *m_dev, dfhip_stream_t stream) {
     if (!check_field_grid(name, L)) return DFHIP_EINVAL;
     if (!(bound > 0.0f)) {
         set_error("%s: bound must be > 0", name);
-        return DFHIP_EINVAL;
-    }
-    if (group != 1 && group != 7) {
-        set_error("%s: group must be 1 (independent rows) or 7 (stencil groups), got %u", name,
-                  group);
         return DFHIP_EINVAL;
     }
     if (cap == 0) return DFHIP_OK;
@@ -716,17 +689,13 @@ static int grid_field_forward(const char *name, int elem, const float *xyz, floa
     }
     hipStream_t s = as_stream(stream);
     const ge::Levels lv = ge::make_levels(L, S, H);
-    const bool share = quads && group == 7 && DFHIP_FWD_SHARE;
 #define DFHIP_FWD(E, R)                                                                       \
-    (share ? launch_field_fwd<E, R, true, 7>(s, xyz, bound, table, quads, offsets, lv, gridtype, \
-                                             align_corners, w1, b1, w2, b2, w3, b3, enc, sigma,   \
-                                             rgb, cap, m_dev)                                     \
-     : quads ? launch_field_fwd<E, R, true>(s, xyz, bound, table, quads, offsets, lv, gridtype,  \
-                                            align_corners, w1, b1, w2, b2, w3, b3, enc, sigma,    \
-                                            rgb, cap, m_dev)                                      \
-             : launch_field_fwd<E, R, false>(s, xyz, bound, table, nullptr, offsets, lv,          \
-                                             gridtype, align_corners, w1, b1, w2, b2, w3, b3,     \
-                                             enc, sigma, rgb, cap, m_dev))
+    (quads ? launch_field_fwd<E, R, true>(s, xyz, bound, table, quads, offsets, lv, gridtype,    \
+                                          align_corners, w1, b1, w2, b2, w3, b3, enc, sigma, rgb,  \
+                                          cap, m_dev)                                              \
+           : launch_field_fwd<E, R, false>(s, xyz, bound, table, nullptr, offsets, lv, gridtype,  \
+                                           align_corners, w1, b1, w2, b2, w3, b3, enc, sigma, rgb, \
+                                           cap, m_dev))
     if (elem == DFHIP_F16 && rgb_dtype == DFHIP_F32) DFHIP_FWD(half_t, float);
     else if (elem == DFHIP_F16 && rgb_dtype == DFHIP_F16) DFHIP_FWD(half_t, half_t);
     else if (elem == DFHIP_BF16 && rgb_dtype == DFHIP_F32) DFHIP_FWD(bf16_t, float);
@@ -866,23 +835,6 @@ extern "C" int dfhip_grid_field_forward_quads(int elem, const float *xyz, float 
     return grid_field_forward("grid_field_forward_quads", elem, xyz, bound, table, quads,
                               offsets, L, S, H, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
                               enc, sigma, rgb, rgb_dtype, cap, m_dev, stream);
-}
-
-// The same over rows laid out as `group`-point stencil groups (7: shade.hip's
-// k_stencil interleaving; 1: dfhip_grid_field_forward_quads).
-extern "C" int dfhip_grid_field_forward_quads_grouped(
-    int elem, const float *xyz, float bound, const void *table, const void *quads,
-    const int32_t *offsets, uint32_t L, float S, uint32_t H, uint32_t gridtype, int align_corners,
-    const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
-    const float *b3, void *enc, float *sigma, void *rgb, int rgb_dtype, uint32_t cap,
-    const int32_t *m_dev, uint32_t group, dfhip_stream_t stream) {
-    if (!quads || (reinterpret_cast<uintptr_t>(quads) & 15)) {
-        set_error("grid_field_forward_quads_grouped: quads must be non-null and 16-byte aligned");
-        return DFHIP_EINVAL;
-    }
-    return grid_field_forward("grid_field_forward_quads_grouped", elem, xyz, bound, table, quads,
-                              offsets, L, S, H, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
-                              enc, sigma, rgb, rgb_dtype, cap, m_dev, stream, group);
 }
 
 static int grid_field_backward(

@@ -683,16 +683,6 @@ static bool make_fast_levels(const int32_t *offsets_host, const Levels &lv, cons
 #ifndef DFHIP_PROBE_ADDS
 #define DFHIP_PROBE_ADDS 0
 #endif
-// Register accumulators of a lane's current cell (the products of its points
-// merged before one slice-image add per corner and channel): f64 by default
-// (products and merges exact); DFHIP_ACC_F32=1 merges in f32 and widens at
-// the flush (relative error ~ sqrt(points per cell) x 2^-24 before the f64
-// slice sums).
-#ifndef DFHIP_ACC_F32
-#define DFHIP_ACC_F32 0
-#endif
-typedef std::conditional_t<DFHIP_ACC_F32 != 0, float, double> cacc_t;
-
 __device__ __forceinline__ void lds_add(double *acc, uint32_t idx, double v, uint32_t k) {
     if constexpr (DFHIP_PROBE_ADDS == 1) {
         atomicAdd(acc + ((idx & ~511u) | ((threadIdx.x & 63u) + 64u * (k & 7u))), v);
@@ -708,7 +698,7 @@ __device__ __forceinline__ void lds_add(double *acc, uint32_t idx, double v, uin
 template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD>
 __device__ __forceinline__ void flush_m(double *acc, uint32_t cs, uint32_t r0, uint32_t r1,
                                         const LevelCtx &c, const ge::LevelRows &lr,
-                                        const uint32_t cell[D], const cacc_t (&cw)[1u << D][C]);
+                                        const uint32_t cell[D], const double (&cw)[1u << D][C]);
 
 constexpr int kModeAny = 3;  // MODE: the corner-row wrap fixed at compile time, or any
 
@@ -717,7 +707,7 @@ constexpr int kModeAny = 3;  // MODE: the corner-row wrap fixed at compile time,
 template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD = 0>
 __device__ __forceinline__ void flush(double *acc, uint32_t cs, uint32_t r0, uint32_t r1,
                                       const LevelCtx &c, const ge::LevelRows &lr,
-                                      const uint32_t cell[D], const cacc_t (&cw)[1u << D][C]) {
+                                      const uint32_t cell[D], const double (&cw)[1u << D][C]) {
     if constexpr (MODE != kModeAny) {
         flush_m<D, C, MODE, LEAD>(acc, cs, r0, r1, c, lr, cell, cw);
     } else {
@@ -731,7 +721,7 @@ __device__ __forceinline__ void flush(double *acc, uint32_t cs, uint32_t r0, uin
 template <uint32_t D, uint32_t C, int MODE, uint32_t LEAD>
 __device__ __forceinline__ void flush_m(double *acc, uint32_t cs, uint32_t r0, uint32_t r1,
                                         const LevelCtx &c, const ge::LevelRows &lr,
-                                        const uint32_t cell[D], const cacc_t (&cw)[1u << D][C]) {
+                                        const uint32_t cell[D], const double (&cw)[1u << D][C]) {
     const uint32_t lead = LEAD ? LEAD : lr.lead;
     if constexpr (MODE == 0 && D == 3) {
         // mask form: corner k's row is base + ((i0 + o_k) & wmask) with the
@@ -904,7 +894,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         // levels, where a cell holds many consecutive samples)
         const uint32_t rl = bi.lane_perm ? (__builtin_bitreverse32(lane) >> 26) : lane;
         const uint32_t e0 = min(rl * Q, cnt), e1 = min(e0 + Q, cnt);
-        cacc_t cw[1u << D][C];
+        double cw[1u << D][C];
         uint32_t cur[D];
         bool have = false;
         // one contribution: the point x (in [0, 1]) with gradient g, merged
@@ -940,7 +930,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
                     if (d < lead) w *= (kc & (1u << d)) ? frac[d] : 1.0f - frac[d];
 #pragma unroll
                 for (uint32_t ch = 0; ch < C; ++ch)
-                    cw[kc][ch] = fma((cacc_t)w, (cacc_t)g[ch], cw[kc][ch]);
+                    cw[kc][ch] = fma((double)w, (double)g[ch], cw[kc][ch]);
             }
         };
         // a lane walks a run of Q entries in batches of RUN loads; segments
@@ -1089,7 +1079,7 @@ constexpr uint32_t kChunkTiles = 1024;
 
 template <uint32_t C>
 struct FlatCell {
-    cacc_t cw[8][C];
+    double cw[8][C];
     uint32_t i0;
     bool have;
 };
@@ -1134,9 +1124,9 @@ __device__ __forceinline__ void flat_take_at(FlatCell<C> &st, double *acc, uint3
     float tw = 1.0f;  // trailing dims dropped from the index: their corners coincide
 #pragma unroll
     for (uint32_t d = LEAD; d < 3; ++d) tw *= (1.0f - fr[d]) + fr[d];
-    cacc_t gd[C];
+    double gd[C];
 #pragma unroll
-    for (uint32_t ch = 0; ch < C; ++ch) gd[ch] = (cacc_t)g[ch];
+    for (uint32_t ch = 0; ch < C; ++ch) gd[ch] = (double)g[ch];
     const bool same = st.have && i0 == st.i0;
     if (!same) {
         if (st.have) {
@@ -1165,7 +1155,7 @@ __device__ __forceinline__ void flat_take_at(FlatCell<C> &st, double *acc, uint3
         float w = tw;
 #pragma unroll
         for (uint32_t d = 0; d < LEAD; ++d) w *= (k & (1u << d)) ? fr[d] : 1.0f - fr[d];
-        const cacc_t wd = (cacc_t)w;
+        const double wd = (double)w;
 #pragma unroll
         for (uint32_t ch = 0; ch < C; ++ch) st.cw[k][ch] = fma(wd, gd[ch], st.cw[k][ch]);
     }
@@ -1873,7 +1863,7 @@ __device__ __forceinline__ void rtake(FlatCell<2> &st, double *acc, uint32_t sro
     float tw = 1.0f;  // trailing dims dropped from the index: their corners coincide
 #pragma unroll
     for (uint32_t d = LEAD; d < 3; ++d) tw *= (1.0f - fr[d]) + fr[d];
-    const cacc_t gd0 = (cacc_t)g[0], gd1 = (cacc_t)g[1];
+    const double gd0 = (double)g[0], gd1 = (double)g[1];
     if (!(st.have && i0 == st.i0)) {
         if (st.have) {
 #pragma unroll
@@ -1896,7 +1886,7 @@ __device__ __forceinline__ void rtake(FlatCell<2> &st, double *acc, uint32_t sro
         float w = tw;
 #pragma unroll
         for (uint32_t d = 0; d < LEAD; ++d) w *= (k & (1u << d)) ? fr[d] : 1.0f - fr[d];
-        const cacc_t wd = (cacc_t)w;
+        const double wd = (double)w;
         st.cw[k][0] = fma(wd, gd0, st.cw[k][0]);
         st.cw[k][1] = fma(wd, gd1, st.cw[k][1]);
     }

@@ -371,7 +371,7 @@ class NativeAlbedoStep:
             _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table,
                                          self.encoder.offsets, S, Hb, gridtype, align, self.mlp,
                                          self.enc, self.sigma_field, self.albedo, self.m_field,
-                                         quads=self.quads, group=self.rows_per)
+                                         quads=self.quads)
         rgb = self.albedo
         if self.shade_code:
             # normals, lambertian, colour, orientation loss (network_grid.py:116-144,
@@ -534,7 +534,7 @@ class NativeAlbedoStep:
             _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table,
                                          self.encoder.offsets, S, Hb, gridtype, align, self.mlp,
                                          self.enc, self.sigma_field, self.albedo, self.m_field,
-                                         quads=self.quads, group=self.rows_per)
+                                         quads=self.quads)
 
         def bwd():
             _fieldmlp.grid_field_backward(

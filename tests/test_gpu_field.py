@@ -151,59 +151,3 @@ def test_quad_forward_bit_identical(gpu, dtype, align, lo, hi, gridtype):
     for u, v in zip(*outs):
         assert torch.equal(u.view(torch.int16) if u.dtype != torch.float32 else u,
                            v.view(torch.int16) if v.dtype != torch.float32 else v)
-
-
-@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("align,gridtype", [(False, "tiled"), (True, "tiled"), (False, "hash")])
-def test_grouped_quad_forward_bit_identical(gpu, dtype, align, gridtype):
-    """dfhip_grid_field_forward_quads_grouped (group 7: the textureless /
-    lambertian step's stencil rows, satellites sharing their centre's
-    coarse-level corner quads) against the group-1 quad forward: features,
-    sigma and rgb bit-identical.  Rows: M samples with their six clamped
-    eps = 1e-2 FD points interleaved (shade.hip k_stencil's layout), a few
-    points pushed out of [-1, 1] (they encode to zero, centre or satellite),
-    and a live count that ends inside a group and inside a 16-row tile."""
-    import _fieldmlp
-    from gridencoder import GridEncoder
-    enc, layers = _field(gpu, seed=6)
-    if gridtype == "hash":
-        enc = GridEncoder(input_dim=3, num_levels=16, level_dim=2, base_resolution=16,
-                          log2_hashmap_size=16, desired_resolution=2048, gridtype="hash").to(gpu)
-        with torch.no_grad():
-            enc.embeddings.uniform_(-0.5, 0.5)
-    enc.align_corners = align
-    S = float(np.log2(enc.per_level_scale))
-    Hb, gt = int(enc.base_resolution), enc.gridtype_id
-    ws = [p.detach().float().contiguous() for lin in layers for p in (lin.weight, lin.bias)]
-    g = torch.Generator(device=gpu).manual_seed(11)
-    M, eps = 9_001, 1e-2
-    c = torch.rand(M, 3, device=gpu, generator=g) * 2 - 1
-    pts = [c]
-    for a in range(3):
-        for sgn in (1.0, -1.0):
-            p = c.clone()
-            p[:, a] += sgn * eps
-            pts.append(p.clamp(-1.0, 1.0))
-    x = torch.stack(pts, 1).reshape(7 * M, 3).contiguous()
-    x[7 * 5] = 1.5                      # a centre out of range
-    x[7 * 9 + 3] = -1.25                # a satellite out of range
-    x[7 * 13:7 * 14] = 2.0              # a whole group
-    emb = enc.embeddings.detach()
-    rows = emb.shape[0]
-    table = torch.empty(rows, 2, device=gpu, dtype=dtype)
-    quads = torch.empty(rows, 4, device=gpu, dtype=torch.int32)
-    _fieldmlp.grid_quads(emb, enc.offsets, S, Hb, gt, align, table, quads)
-    live = 7 * M - 12  # ends inside a group and inside a tile
-    m_dev = torch.tensor([live], device=gpu, dtype=torch.int32)
-    outs = []
-    for grp in (1, 7):
-        e = torch.zeros(7 * M, 32, device=gpu, dtype=dtype)
-        s = torch.zeros(7 * M, device=gpu)
-        a = torch.zeros(7 * M, 3, device=gpu, dtype=dtype)
-        _fieldmlp.grid_field_forward(x, 1.0, table, enc.offsets, S, Hb, gt, align, ws, e, s, a,
-                                     m_dev, quads=quads, group=grp)
-        outs.append((e, s, a))
-    for u, v in zip(*outs):
-        assert torch.equal(u.view(torch.int16) if u.dtype != torch.float32 else u,
-                           v.view(torch.int16) if v.dtype != torch.float32 else v)
-    assert bool(outs[1][0][7 * 5].eq(0).all()) and float(outs[1][0][:live].abs().sum()) > 0
