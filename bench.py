@@ -403,7 +403,8 @@ def summarize_kernels(records):
 # reports some names demangled, some mangled)
 REGION_KERNELS = {
     "grid_encode_backward": (("gb::k_bin", "gb5k_bin", "gb::k_rbin", "gb6k_rbin"),
-                             ("gb::k_walk", "gb6k_walk", "gb::k_rwalk", "gb7k_rwalk"),
+                             ("gb::k_walk", "gb6k_walk", "gb11k_walk_flat", "gb::k_rwalk",
+                              "gb7k_rwalk"),
                              ("gb::k_sum", "gb5k_sum")),
     "grid_field_forward": ("k_field_fwd_fused",),
     "field_mlp_backward": ("k_field_bwd", "k_field_wgrad_sum"),
@@ -525,8 +526,8 @@ def measure_traffic(region, timeout=180, warmup=10, shade="albedo", key=None):
                 for i, alts in enumerate(pats):
                     alts = (alts,) if isinstance(alts, str) else alts
                     if any(a in r["Kernel_Name"] for a in alts):
-                        key = int(r.get("Dispatch_Id", 0) or 0)
-                        sums.setdefault((i, name), []).append((key, float(r["Counter_Value"])))
+                        did = int(r.get("Dispatch_Id", 0) or 0)
+                        sums.setdefault((i, name), []).append((did, float(r["Counter_Value"])))
         for cname in counters:
             got = {i: [v for _, v in sorted(vs)[-keep:]] for (i, n), vs in sums.items()
                    if n == cname}

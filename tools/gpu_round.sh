@@ -7,12 +7,15 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-round}
 mkdir -p $OUT
+# SKIP_TESTS=1: the bench and profiles only (tests and smoke green on this tree)
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread --durations=30 \
     > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
     || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 2; }
 tail -1 $OUT/smoke.log
+fi
 timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 \
     || { echo "bench failed"; tail -30 $OUT/bench.log; exit 3; }
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
