@@ -1067,12 +1067,6 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
 // accumulators start at the products (f64, exact) instead of zero + fma, and
 // the level's corner count is a template parameter.
 constexpr uint32_t kChunkTiles = 1024;
-#ifndef DFHIP_WALK_QR  // entries per thread per round of the flat walk (0: one round)
-#define DFHIP_WALK_QR 0
-#endif
-#ifndef DFHIP_WALK_RSYNC  // a workgroup barrier between rounds
-#define DFHIP_WALK_RSYNC 0
-#endif
 #ifndef DFHIP_WALK_RUN
 #define DFHIP_WALK_RUN 6
 #endif
@@ -1471,26 +1465,14 @@ __device__ __forceinline__ void flat_walk_chunk(
             }
         }
     } else {
-        // rounds (DFHIP_WALK_QR > 0): the chunk's entries in consecutive windows
-        // of about nthr x QR entries, cut into nthr runs each, so that the
-        // workgroup works on one window of samples at a time (its positions and
-        // gradient rows stay in L2) instead of every wave on its own sixteenth
-        // of the part's samples at once; a lane's cell state carries across
-        // (a new run's first cell flushes the old one as any other cell change)
-        const uint32_t nr = DFHIP_WALK_QR > 0 ? max(1u, ceil_div(E, nthr * (uint32_t)DFHIP_WALK_QR))
-                                              : 1u;
-        for (uint32_t rd = 0; rd < nr; ++rd) {
-        const uint32_t E0 = (uint32_t)((uint64_t)E * rd / nr);
-        const uint32_t E1 = (uint32_t)((uint64_t)E * (rd + 1) / nr);
-        const uint32_t Q = ceil_div(E1 - E0, nthr);
-        if (DFHIP_WALK_RSYNC && rd > 0) __syncthreads();
-        // wave w takes the w-th 1/waves of the chunk (round), so its lanes stay
-        // on neighbouring samples (one or two tile segments: positions and
+        const uint32_t Q = ceil_div(E, nthr);
+        // wave w takes the w-th 1/waves of the chunk, so its lanes stay on
+        // neighbouring samples (one or two tile segments: positions and
         // gradients hit in L1); inside it lane -> run is bit-reversed, so the
         // lanes of one LDS instruction flush different rays
         const uint32_t r = wave * 64u + (__builtin_bitreverse32(lane) >> 26);
-        uint32_t e = min(E0 + r * Q, E1);
-        const uint32_t e1 = min(e + Q, E1);
+        uint32_t e = min(r * Q, E);
+        const uint32_t e1 = min(e + Q, E);
         if (e < e1) {
             // segment of entry e: the last ti with pre[ti] <= e
             uint32_t a = 0, z = nc;  // pre[a] <= e < pre[z]
@@ -1553,7 +1535,6 @@ __device__ __forceinline__ void flat_walk_chunk(
 #pragma unroll
                 for (uint32_t i = 0; i < RUN; ++i) ids[i] = nids[i];
             }
-        }
         }
     }
     __syncthreads();  // pre / wsum are rewritten by the next phase / chunk
