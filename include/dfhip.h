@@ -717,10 +717,14 @@ int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d
                             const float *b1, const float *w2, const float *b2, const float *w3,
                             const float *b3, float *weights_sum, float *depth, float *image,
                             uint32_t *work, const void *quads, dfhip_stream_t stream);
-/* The same with a debug profile of this call: prof (DEVICE u64 [6], caller
- * zeroed) receives the per-wave phase cycles of the persistent kernel summed
- * {refill, march, field, composite, rounds, field tiles}; NULL = the call
- * above.  Used by tools/infer_case.py. */
+/* The same with a debug profile of this call: prof (DEVICE u64 [10]; caller
+ * sets [6] and [7] to UINT64_MAX, the others to 0) receives the per-wave
+ * phase cycles of the persistent kernel summed {refill, march, field,
+ * composite, rounds, field tiles}, then wall-clock ticks (100 MHz): [6] the
+ * first wave's start, [7] the first time a wave found the ray queue empty,
+ * [8] the last wave's end, [9] the waves' lifetimes summed (the drain after
+ * the queue ran dry and the mean resident waves).  NULL = the call above.
+ * Used by tools/infer_case.py. */
 int dfhip_render_rays_infer_prof(uint32_t N, const float *rays_o, const float *rays_d,
                                  const float *nears, const float *fars, const float *noises,
                                  float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
@@ -731,6 +735,38 @@ int dfhip_render_rays_infer_prof(uint32_t N, const float *rays_o, const float *r
                                  const float *b2, const float *w3, const float *b3,
                                  float *weights_sum, float *depth, float *image, uint32_t *work,
                                  const void *quads, uint64_t *prof, dfhip_stream_t stream);
+/* dfhip_render_rays_infer[_prof] taking rays from the queue chunk by chunk:
+ * order[0 .. ceil(N / 2^chunk_log2)) (DEVICE int32, a permutation of the
+ * chunk indices; NULL = pixel order) names the chunks of 2^chunk_log2
+ * consecutive rays in queue order.  The persistent kernel's tail is the rays
+ * still marching after the queue ran dry, so a caller puts the costly chunks
+ * first (dfhip_render_ray_order); whole chunks keep a wave's refills on
+ * neighbouring pixels.  Outputs are per ray: any order gives the same
+ * results; ids >= N (the partial last chunk) are skipped. */
+int dfhip_render_rays_infer_ordered(uint32_t N, const float *rays_o, const float *rays_d,
+                                    const float *nears, const float *fars, const float *noises,
+                                    float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
+                                    uint32_t H, const uint8_t *grid, float T_thresh,
+                                    const void *table, const int32_t *offsets, uint32_t L,
+                                    float S, uint32_t base_res, uint32_t gridtype,
+                                    int align_corners, const float *w1, const float *b1,
+                                    const float *w2, const float *b2, const float *w3,
+                                    const float *b3, float *weights_sum, float *depth,
+                                    float *image, uint32_t *work, const void *quads,
+                                    const int32_t *order, uint32_t chunk_log2, uint64_t *prof,
+                                    dfhip_stream_t stream);
+/* The queue order for dfhip_render_rays_infer_ordered: the chunks of
+ * 2^chunk_log2 consecutive rays (rays_o / rays_d [N, 3] f32) by ascending
+ * summed squared distance of their rays' lines from the scene centre (the
+ * bound box's centre, the origin), i.e. the rays crossing the most of the
+ * scene first — the cost quantised to 64 levels between its min and max,
+ * ties in chunk order (a stable counting sort).  cost: [nchunks] f32
+ * scratch (the per-chunk cost, a partial last chunk scaled to a whole one);
+ * order: [nchunks] int32 out; nchunks = ceil(N / 2^chunk_log2) <= 16384.
+ * Two launches, deterministic. */
+int dfhip_render_ray_order(const float *rays_o, const float *rays_d, uint32_t N,
+                           uint32_t chunk_log2, float *cost, int32_t *order,
+                           dfhip_stream_t stream);
 
 /* ---- non-albedo shading of the train step (csrc/shade.hip) ------------------
  * Replaces, for the `textureless` / `lambertian` steps, network_grid.py:90-144

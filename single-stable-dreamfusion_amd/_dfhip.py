@@ -149,6 +149,11 @@ _SIGS = {
     "dfhip_render_rays_infer_prof": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32, _u32,
                                      _vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dfhip_render_rays_infer_ordered": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32,
+                                        _u32, _vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32,
+                                        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                        _u32, _vp, _vp],
+    "dfhip_render_ray_order": [_vp, _vp, _u32, _u32, _vp, _vp, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],
@@ -331,6 +336,9 @@ def checked(t: torch.Tensor, what: str, kind: str = "float") -> torch.Tensor:
     check_contig(t, what)
     if kind == "int":
         check_int(t, what)
+    elif kind == "i64":
+        if t.dtype != torch.int64:
+            raise RuntimeError(f"{what} must be an int64 tensor")
     elif kind == "u8":
         if t.dtype != torch.uint8:
             raise RuntimeError(f"{what} must be a uint8 tensor")

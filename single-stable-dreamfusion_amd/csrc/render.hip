@@ -127,7 +127,8 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *__restrict__ weights_sum, float *__restrict__ depth,
     float *__restrict__ image, uint32_t *__restrict__ work,
-    const fm::u32x4 *__restrict__ quads, uint64_t *prof) {
+    const fm::u32x4 *__restrict__ quads, uint64_t *prof, const int32_t *__restrict__ order,
+    uint32_t chunk_log2) {
     __shared__ fm::Weights W;
     __shared__ fm::LevelK LK[fm::kLevels];
     __shared__ Stage stages[kWaves];
@@ -139,6 +140,8 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     Stage &S = stages[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const float inv_extent = 1.0f / (2.0f * k.bound);
+    // queue positions: N, or whole chunks of the order
+    const uint32_t Nq = order ? ceil_div(N, 1u << chunk_log2) << chunk_log2 : N;
 
     int ray = -1;
     bool exhausted = false;
@@ -158,6 +161,8 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     // march, field and compositing, rounds and field tiles, per wave
     uint64_t pc[6] = {0, 0, 0, 0, 0, 0};
     uint64_t c0 = prof ? clock64() : 0;
+    const uint64_t w0 = prof ? wall_clock64() : 0;
+    bool dry = false;  // this wave has seen the queue empty (prof)
 
     while (true) {
         // ---- refill lanes without a ray from the global queue
@@ -171,8 +176,20 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
             if (need) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                     (uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
-                const uint32_t id = base + rank;
-                if (id < N) {
+                const uint32_t q = base + rank;
+                // the queue's q-th ray: ray q, or ray r of chunk order[q >> cl]
+                // (chunks of 2^cl consecutive rays, the costly ones first, so
+                // that they do not finish alone after the queue ran dry); an id
+                // >= N (the partial last chunk, or an order that is not a
+                // permutation) is skipped, never read or written
+                const uint32_t id =
+                    q < Nq ? (order ? ((uint32_t)order[q >> chunk_log2] << chunk_log2) +
+                                          (q & ((1u << chunk_log2) - 1u))
+                                    : q)
+                           : N;
+                if (q >= Nq) {
+                    exhausted = true;
+                } else if (id < N) {
                     ray = (int)id;
                     r = rm::load_ray(rays_o + 3 * (size_t)id, rays_d + 3 * (size_t)id);
                     // rays_t starts at the near plane (renderer.py:509); the
@@ -188,12 +205,17 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                     ws = dp = cr = cg = cb = 0.0f;
                     taken = 0;
                     finished = false;
-                } else {
-                    exhausted = true;
                 }
             }
+            if (prof && !dry && __ballot(exhausted)) {  // uniform
+                dry = true;
+                if (lane == 0)
+                    atomicMin((unsigned long long *)&prof[7], (unsigned long long)wall_clock64());
+            }
         }
-        if (__ballot(ray >= 0) == 0) break;
+        // done when no lane holds a ray and the queue is dry for all (a lane
+        // whose queue entry was skipped refills next round)
+        if (__ballot(ray >= 0 || !exhausted) == 0) break;
         if (prof) {
             const uint64_t c1 = clock64();
             pc[0] += c1 - c0;
@@ -343,9 +365,14 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
             c0 = c1;
         }
     }
-    if (prof && lane == 0)
+    if (prof && lane == 0) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) atomicAdd((unsigned long long *)&prof[i], pc[i]);
+        const uint64_t w1 = wall_clock64();
+        atomicMin((unsigned long long *)&prof[6], (unsigned long long)w0);
+        atomicMax((unsigned long long *)&prof[8], (unsigned long long)w1);
+        atomicAdd((unsigned long long *)&prof[9], (unsigned long long)(w1 - w0));
+    }
     // stats: composited samples (64-bit, low / high words)
     uint32_t tot = samples;
 #pragma unroll
@@ -368,8 +395,13 @@ static int render_infer(
     uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
-    const void *quads, uint64_t *prof, dfhip_stream_t stream) {
+    const void *quads, uint64_t *prof, const int32_t *order, uint32_t chunk_log2,
+    dfhip_stream_t stream) {
     const char *name = "render_rays_infer";
+    if (order && chunk_log2 > 16) {
+        set_error("%s: chunk_log2 must be <= 16 (got %u)", name, chunk_log2);
+        return DFHIP_EINVAL;
+    }
     if (L != 16) {
         set_error("%s: the fused renderer supports the reference's 16-level x 2-channel 3-D "
                   "grid (got L=%u)", name, L);
@@ -399,7 +431,7 @@ static int render_infer(
     rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
         N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
         (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
-        weights_sum, depth, image, work, (const fm::u32x4 *)quads, prof);
+        weights_sum, depth, image, work, (const fm::u32x4 *)quads, prof, order, chunk_log2);
     return check_launch(name);
 }
 
@@ -414,7 +446,7 @@ extern "C" int dfhip_render_rays_infer(
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, nullptr,
-                        stream);
+                        nullptr, 0, stream);
 }
 
 extern "C" int dfhip_render_rays_infer_prof(
@@ -428,5 +460,167 @@ extern "C" int dfhip_render_rays_infer_prof(
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, prof,
-                        stream);
+                        nullptr, 0, stream);
+}
+
+extern "C" int dfhip_render_rays_infer_ordered(
+    uint32_t N, const float *rays_o, const float *rays_d, const float *nears, const float *fars,
+    const float *noises, float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
+    uint32_t H, const uint8_t *grid, float T_thresh, const void *table, const int32_t *offsets,
+    uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
+    const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
+    const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
+    const void *quads, const int32_t *order, uint32_t chunk_log2, uint64_t *prof,
+    dfhip_stream_t stream) {
+    return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
+                        grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
+                        w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, prof,
+                        order, chunk_log2, stream);
+}
+
+// ---------------------------------------------------------------- queue order
+namespace dfhip {
+namespace rd {
+
+constexpr uint32_t kMaxOrderChunks = 16384;  // one workgroup's counting sort (64 x 256 slots)
+
+// Cost of each chunk of 2^cl consecutive rays: the summed squared distance
+// of the rays' lines from the scene centre (the origin of the reference's
+// bound box).  One wave per chunk.
+__global__ __launch_bounds__(256) void k_chunk_cost(const float *__restrict__ rays_o,
+                                                    const float *__restrict__ rays_d, uint32_t N,
+                                                    uint32_t cl, uint32_t nchunks,
+                                                    float *__restrict__ cost) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (ch >= nchunks) return;  // uniform per wave
+    const uint32_t r0 = ch << cl, r1 = min(N, (ch + 1) << cl);
+    float acc = 0.0f;
+    for (uint32_t r = r0 + lane; r < r1; r += 64) {
+        const float ox = rays_o[3 * (size_t)r], oy = rays_o[3 * (size_t)r + 1],
+                    oz = rays_o[3 * (size_t)r + 2];
+        const float dx = rays_d[3 * (size_t)r], dy = rays_d[3 * (size_t)r + 1],
+                    dz = rays_d[3 * (size_t)r + 2];
+        const float dd = fmaxf(dx * dx + dy * dy + dz * dz, 1e-20f);
+        const float t = -(ox * dx + oy * dy + oz * dz) / dd;
+        const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
+        acc += px * px + py * py + pz * pz;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    // a partial last chunk: the mean over its rays, scaled to a whole chunk
+    if (lane == 0) cost[ch] = acc * (float)(1u << cl) / (float)(r1 - r0);
+}
+
+// The chunks by ascending cost, quantised to kOrderBuckets levels between the
+// costs' min and max (NaN last), ties by chunk index: a stable counting sort
+// in one workgroup.  Thread t takes the chunks [t per, (t + 1) per) and counts
+// them per bucket in its own LDS column; an exclusive scan over (bucket,
+// thread) gives every thread its first slot per bucket; each thread then
+// places its chunks in index order.  (A full bitonic sort of 16 k keys in one
+// workgroup took 229 us per frame; a queue order needs only the coarse rank.)
+constexpr uint32_t kOrderBuckets = 64;
+constexpr uint32_t kOrderThreads = 256;
+constexpr uint32_t kOrderRow = kOrderThreads + 1;  // padded row: thread b's scan row, and
+                                                  // thread t's column, hit distinct banks
+__global__ __launch_bounds__(kOrderThreads) void k_chunk_order(const float *__restrict__ cost,
+                                                               uint32_t nchunks,
+                                                               int32_t *__restrict__ order) {
+    __shared__ uint16_t slot[kOrderBuckets * kOrderRow];  // [bucket][thread] (<= 16 k chunks)
+    __shared__ uint8_t bk[kMaxOrderChunks];                // each chunk's bucket
+    __shared__ float rmin[kOrderThreads], rmax[kOrderThreads];
+    __shared__ uint32_t rsum[kOrderBuckets];
+    const uint32_t t = threadIdx.x;
+    // the costs once, coalesced: range, then every chunk's bucket into LDS
+    float lo = INFINITY, hi = -INFINITY;
+    for (uint32_t c = t; c < nchunks; c += kOrderThreads) {
+        const float v = cost[c];
+        if (v == v) {
+            lo = fminf(lo, v);
+            hi = fmaxf(hi, v);
+        }
+    }
+    rmin[t] = lo;
+    rmax[t] = hi;
+    for (uint32_t b = 0; b < kOrderBuckets; ++b) slot[b * kOrderRow + t] = 0;
+    __syncthreads();
+    for (uint32_t o = kOrderThreads / 2; o > 0; o >>= 1) {
+        if (t < o) {
+            rmin[t] = fminf(rmin[t], rmin[t + o]);
+            rmax[t] = fmaxf(rmax[t], rmax[t + o]);
+        }
+        __syncthreads();
+    }
+    const float cmin = rmin[0], span = rmax[0] - rmin[0];
+    const float scale = span > 0.0f ? (float)kOrderBuckets / span : 0.0f;
+    for (uint32_t c = t; c < nchunks; c += kOrderThreads) {
+        const float v = cost[c];
+        uint32_t b = kOrderBuckets - 1;  // NaN last
+        if (v == v) {
+            const float q = (v - cmin) * scale;
+            b = q >= (float)(kOrderBuckets - 1) ? kOrderBuckets - 1 : (uint32_t)fmaxf(q, 0.0f);
+        }
+        bk[c] = (uint8_t)b;
+    }
+    __syncthreads();
+    // thread t's chunks: the contiguous range [c0, c1), counted per bucket in
+    // its own column
+    const uint32_t per = ceil_div(nchunks, kOrderThreads);
+    const uint32_t c0 = min(nchunks, t * per), c1 = min(nchunks, c0 + per);
+    for (uint32_t c = c0; c < c1; ++c) ++slot[bk[c] * kOrderRow + t];
+    __syncthreads();
+    // exclusive scan of the bucket-major [bucket][thread] counts: thread b
+    // scans bucket b's row, then the row sums are scanned and added
+    if (t < kOrderBuckets) {
+        uint32_t sum = 0;
+        for (uint32_t u = 0; u < kOrderThreads; ++u) {
+            const uint32_t v = slot[t * kOrderRow + u];
+            slot[t * kOrderRow + u] = (uint16_t)sum;
+            sum += v;
+        }
+        rsum[t] = sum;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < kOrderBuckets; ++b) {
+            const uint32_t v = rsum[b];
+            rsum[b] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    for (uint32_t c = c0; c < c1; ++c) {
+        const uint32_t b = bk[c];
+        order[rsum[b] + slot[b * kOrderRow + t]++] = (int32_t)c;
+    }
+}
+
+}  // namespace rd
+}  // namespace dfhip
+
+extern "C" int dfhip_render_ray_order(const float *rays_o, const float *rays_d, uint32_t N,
+                                      uint32_t chunk_log2, float *cost, int32_t *order,
+                                      dfhip_stream_t stream) {
+    const char *name = "render_ray_order";
+    if (chunk_log2 > 16) {
+        set_error("%s: chunk_log2 must be <= 16 (got %u)", name, chunk_log2);
+        return DFHIP_EINVAL;
+    }
+    if (N == 0) return DFHIP_OK;
+    const uint32_t nchunks = ceil_div(N, 1u << chunk_log2);
+    if (nchunks > rd::kMaxOrderChunks) {
+        set_error("%s: %u chunks of 2^%u rays exceed %u (use larger chunks)", name, nchunks,
+                  chunk_log2, rd::kMaxOrderChunks);
+        return DFHIP_EINVAL;
+    }
+    if (!rays_o || !rays_d || !cost || !order) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    rd::k_chunk_cost<<<ceil_div(nchunks, 4u), 256, 0, s>>>(rays_o, rays_d, N, chunk_log2,
+                                                           nchunks, cost);
+    rd::k_chunk_order<<<1, rd::kOrderThreads, 0, s>>>(cost, nchunks, order);
+    return check_launch(name);
 }

@@ -224,3 +224,46 @@ def test_fused_infer_bit_exact_at_c4_size(gpu, occupancy):
     np.testing.assert_array_equal(fw, lw)
     np.testing.assert_array_equal(fd, ld)
     np.testing.assert_array_equal(fi, li)
+
+
+def test_ray_order_and_ordered_queue(gpu, monkeypatch):
+    """dfhip_render_ray_order against numpy (chunks of 2^cl consecutive rays by
+    ascending summed squared distance of their lines from the origin,
+    quantised to 64 levels, ties in chunk order; a partial last chunk scaled
+    to a whole one), and the queue in that
+    order renders bit-identically to pixel order — for chunk sizes 1, 8, 64
+    and N not a multiple of the chunk (the partial chunk anywhere in the
+    order)."""
+    import _fieldmlp
+    import nerf.renderer as rr
+    m = _model(gpu, 8, 1.0, "grid")
+    rays_o, rays_d = _rays(gpu, 37, 29, 8)  # N = 1073
+    n = rays_o.shape[0]
+    o, d = rays_o.cpu().double().numpy(), rays_d.cpu().double().numpy()
+    t = -(o * d).sum(1) / (d * d).sum(1)
+    dist = ((o + t[:, None] * d) ** 2).sum(1)
+    for cl in (0, 3, 6):
+        cost_dev = torch.empty(-(-n // (1 << cl)), device=gpu)
+        order = _fieldmlp.render_ray_order(rays_o, rays_d, cl, cost=cost_dev).cpu().numpy()
+        nc = -(-n // (1 << cl))
+        assert sorted(order.tolist()) == list(range(nc))
+        cost = np.array([dist[c << cl:(c + 1) << cl].mean() * (1 << cl) for c in range(nc)])
+        np.testing.assert_allclose(cost_dev.cpu().numpy(), cost, rtol=1e-4, atol=1e-6 * cost.max())
+        # buckets of the device costs: non-decreasing along the order, chunk
+        # indices increasing inside a bucket
+        c32 = cost_dev.cpu().numpy()
+        q = np.minimum((c32 - c32.min()) * np.float32(64 / (c32.max() - c32.min())), 63)
+        b = q.astype(np.int64)[order]
+        assert np.all(np.diff(b) >= 0)
+        same = np.diff(b) == 0
+        assert np.all(np.diff(order)[same] > 0)
+    outs = []
+    for flag, cl in ((0, 6), (1, 0), (1, 3), (1, 6)):
+        monkeypatch.setattr(rr, "_INFER_ORDER", flag)
+        monkeypatch.setattr(rr, "_INFER_CHUNK_LOG2", cl)
+        (fw, fd, fi), _ = _both(m, rays_o, rays_d, 1)
+        outs.append((fw, fd, fi))
+    assert (outs[0][0] > 0).sum() > 100
+    for got in outs[1:]:
+        for a, b in zip(outs[0], got):
+            np.testing.assert_array_equal(a, b)

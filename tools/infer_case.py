@@ -60,7 +60,8 @@ def main():
     if args.profile:
         import functools
         import _fieldmlp
-        prof = torch.zeros(6, dtype=torch.int64, device=dev)
+        prof = torch.zeros(10, dtype=torch.int64, device=dev)
+        prof[6] = prof[7] = -1  # UINT64_MAX (atomicMin slots)
         plain = _fieldmlp.render_rays_infer
         _fieldmlp.render_rays_infer = functools.partial(plain, prof=prof)
         try:
@@ -74,6 +75,11 @@ def main():
             f"{n} {v / tot:.3f}" for n, v in zip(("refill", "march", "field", "composite"), p[:4]))
             + f"; rounds {p[4]}, tiles {p[5]}, cycles/round {tot / max(1, p[4]):.0f}, "
             f"field cycles/tile {p[2] / max(1, p[5]):.0f}", flush=True)
+        span = max(1, p[8] - p[6])
+        waves = p[9] / span  # mean resident waves over the kernel's span
+        print(f"wall span {span / 100:.1f} us (100 MHz ticks); queue dry after "
+              f"{(p[7] - p[6]) / 100:.1f} us ({(p[7] - p[6]) / span:.3f} of the span); "
+              f"mean resident waves {waves:.0f}", flush=True)
 
 
 if __name__ == "__main__":
