@@ -33,13 +33,19 @@ constexpr float kHalfPi = 3.141592653589793f / 2.0f;
 
 __device__ __forceinline__ float r16(float x) { return (float)(half_t)f32_rounded(x); }
 
-struct W {
-    float w1[kW1], b1[kB1], w2[kW2], b2[kB2];
+// w1 transposed ([kIn][kHid]: sub-lane q's four hidden units of input i are
+// one 16-byte LDS read; 39 instead of 156 reads per lane), w2 as in the
+// reference ([kOut][kHid]: q's four units of output k are contiguous too)
+struct alignas(16) W {
+    float w1t[kW1], b1[kB1], w2[kW2], b2[kB2];
 };
 
 __device__ __forceinline__ void load_w(W &w, const float *w1, const float *b1, const float *w2,
                                        const float *b2) {
-    for (int i = threadIdx.x; i < kW1; i += blockDim.x) w.w1[i] = r16(w1[i]);
+    for (int i = threadIdx.x; i < kW1; i += blockDim.x) {
+        const int j = i / kIn, c = i - j * kIn;  // w1 [kHid, kIn] row-major
+        w.w1t[c * kHid + j] = r16(w1[i]);
+    }
     for (int i = threadIdx.x; i < kB1; i += blockDim.x) w.b1[i] = r16(b1[i]);
     for (int i = threadIdx.x; i < kW2; i += blockDim.x) w.w2[i] = r16(w2[i]);
     for (int i = threadIdx.x; i < kB2; i += blockDim.x) w.b2[i] = r16(b2[i]);
@@ -84,24 +90,49 @@ __device__ __forceinline__ void features_part(const float *d, int q, float *sx) 
 // pre-activation (partials combined across the ray's four lanes).
 __device__ __forceinline__ void mlp_part(const W &w, const float *x, int q, float h[kPer],
                                         float o[kOut]) {
+    static_assert(kPer == 4, "one float4 of hidden units per sub-lane");
+    // the four units' sums side by side, each in input order (the same fmaf
+    // chain per unit as one unit at a time)
+    float a[kPer] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < kIn; ++i) {
+        const float4 wv = *reinterpret_cast<const float4 *>(&w.w1t[i * kHid + kPer * q]);
+        a[0] = fmaf(x[i], wv.x, a[0]);
+        a[1] = fmaf(x[i], wv.y, a[1]);
+        a[2] = fmaf(x[i], wv.z, a[2]);
+        a[3] = fmaf(x[i], wv.w, a[3]);
+    }
 #pragma unroll
     for (int jj = 0; jj < kPer; ++jj) {
-        const int j = kPer * q + jj;
-        float a = 0.0f;
-#pragma unroll
-        for (int i = 0; i < kIn; ++i) a = fmaf(x[i], w.w1[j * kIn + i], a);
-        a = a + w.b1[j];
-        h[jj] = r16(a > 0.0f ? a : 0.0f);
+        const float v = a[jj] + w.b1[kPer * q + jj];
+        h[jj] = r16(v > 0.0f ? v : 0.0f);
     }
 #pragma unroll
     for (int k = 0; k < kOut; ++k) {
         float a = 0.0f;
+        const float4 wv = *reinterpret_cast<const float4 *>(&w.w2[k * kHid + kPer * q]);
+        const float w2q[kPer] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
-        for (int jj = 0; jj < kPer; ++jj) a = fmaf(h[jj], w.w2[k * kHid + kPer * q + jj], a);
+        for (int jj = 0; jj < kPer; ++jj) a = fmaf(h[jj], w2q[jj], a);
 #pragma unroll
         for (int o2 = 1; o2 < kSub; o2 <<= 1) a = a + __shfl_xor(a, o2, 64);
         o[k] = r16(a + w.b2[k]);
     }
+}
+
+// A ray's staged features (16-byte aligned row of kIn + 1 floats) into x:
+// nine 16-byte reads and three words instead of 39 reads
+__device__ __forceinline__ void load_x(const float *row, bool live, float (&x)[kIn]) {
+#pragma unroll
+    for (int i = 0; i < kIn / 4; ++i) {
+        const float4 v = *reinterpret_cast<const float4 *>(row + 4 * i);
+        x[4 * i] = live ? v.x : 0.0f;
+        x[4 * i + 1] = live ? v.y : 0.0f;
+        x[4 * i + 2] = live ? v.z : 0.0f;
+        x[4 * i + 3] = live ? v.w : 0.0f;
+    }
+#pragma unroll
+    for (int i = kIn / 4 * 4; i < kIn; ++i) x[i] = live ? row[i] : 0.0f;
 }
 
 __device__ __forceinline__ float sigmoid16(float o) { return r16(1.0f / (1.0f + expf(-o))); }
@@ -140,7 +171,7 @@ __global__ __launch_bounds__(kThreads) void k_head_fwd_net(
     const float *b1, const float *w2, const float *b2, float *__restrict__ out_image,
     float *__restrict__ out_depth, uint8_t *__restrict__ mask) {
     __shared__ W w;
-    __shared__ float s_x[kRays][kIn + 1];
+    __shared__ alignas(16) float s_x[kRays][kIn + 1];
     load_w(w, w1, b1, w2, b2);
     const int q = threadIdx.x & (kSub - 1), r = threadIdx.x / kSub;
     const uint32_t n = blockIdx.x * kRays + r;
@@ -148,8 +179,7 @@ __global__ __launch_bounds__(kThreads) void k_head_fwd_net(
     if (live) features_part(rays_d + 3 * (size_t)n, q, s_x[r]);
     __syncthreads();
     float x[kIn], h[kPer], o[kOut];
-#pragma unroll
-    for (int i = 0; i < kIn; ++i) x[i] = live ? s_x[r][i] : 0.0f;
+    load_x(s_x[r], live, x);
     mlp_part(w, x, q, h, o);
     if (!live || q != 0) return;
     float bg[3];
@@ -198,7 +228,7 @@ __global__ __launch_bounds__(kThreads) void k_head_bwd_net(
     const float *b2, float *__restrict__ grad_image, float *__restrict__ grad_ws,
     float *__restrict__ partial, const float *__restrict__ ent_grad_loss, float ent_lambda) {
     __shared__ W w;
-    __shared__ float s_x[kRays][kIn + 1];
+    __shared__ alignas(16) float s_x[kRays][kIn + 1];
     __shared__ half_t s_dh[kRays][kHid];  // relu-masked hidden grads (f16 values)
     __shared__ half_t s_h[kRays][kHid];   // hidden activations
     __shared__ float s_do[kRays][4];      // output pre-activation grads (f16 values)
@@ -211,8 +241,7 @@ __global__ __launch_bounds__(kThreads) void k_head_bwd_net(
         for (int i = 0; i < kIn; ++i) s_x[r][i] = 0.0f;
     __syncthreads();
     float x[kIn], h[kPer], o[kOut];
-#pragma unroll
-    for (int i = 0; i < kIn; ++i) x[i] = s_x[r][i];
+    load_x(s_x[r], true, x);
     mlp_part(w, x, q, h, o);
     float g[3] = {0.0f, 0.0f, 0.0f}, bg[3];
     if (live)
