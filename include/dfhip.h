@@ -767,6 +767,14 @@ int dfhip_render_rays_infer_ordered(uint32_t N, const float *rays_o, const float
 int dfhip_render_ray_order(const float *rays_o, const float *rays_d, uint32_t N,
                            uint32_t chunk_log2, float *cost, int32_t *order,
                            dfhip_stream_t stream);
+/* The same order from the occupancy grid (grid: the march's bitfield, C
+ * cascades of H^3; nears / fars [N] f32): a chunk's cost is minus the occupied
+ * cells met at 16 evenly spaced points of each ray's [near, far), so the
+ * rays crossing the most occupied space come first. */
+int dfhip_render_ray_order_occ(const float *rays_o, const float *rays_d, const float *nears,
+                               const float *fars, const uint8_t *grid, float bound, uint32_t C,
+                               uint32_t H, uint32_t max_steps, uint32_t N, uint32_t chunk_log2,
+                               float *cost, int32_t *order, dfhip_stream_t stream);
 
 /* ---- non-albedo shading of the train step (csrc/shade.hip) ------------------
  * Replaces, for the `textureless` / `lambertian` steps, network_grid.py:90-144

@@ -169,11 +169,13 @@ def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lb
 
 # ---- fused inference render (march + field + composite, persistent queue)
 
-def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None):
+def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None, occ=None):
     """Queue order of the fused render (csrc/render.hip k_chunk_cost +
     k_chunk_sort): the chunks of 2^chunk_log2 consecutive rays by ascending
     summed squared distance of their lines from the origin.  Returns the
-    [ceil(N / 2^chunk_log2)] int32 order (cost: f32 scratch of that size)."""
+    [ceil(N / 2^chunk_log2)] int32 order (cost: f32 scratch of that size).
+    occ = (nears, fars, bitfield, bound, C, H, max_steps): cost from the
+    occupancy grid instead (dfhip_render_ray_order_occ)."""
     n = rays_o.shape[0]
     _f32(rays_o, "rays_o")
     _f32(rays_d, "rays_d")
@@ -188,8 +190,21 @@ def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None):
     checked(order, "order", "int")
     if cost.numel() < nc or order.numel() < nc:
         raise RuntimeError("cost / order must hold ceil(N / 2^chunk_log2) values")
-    call("dfhip_render_ray_order", ptr(rays_o), ptr(rays_d), n, int(chunk_log2), ptr(cost),
-         ptr(order), stream())
+    if occ is None:
+        call("dfhip_render_ray_order", ptr(rays_o), ptr(rays_d), n, int(chunk_log2), ptr(cost),
+             ptr(order), stream())
+    else:  # (nears, fars, bitfield, bound, C, H, max_steps): occupancy cost
+        nears, fars, bitfield, bound, C, H, max_steps = occ
+        _f32(nears, "nears")
+        _f32(fars, "fars")
+        checked(bitfield, "bitfield", "u8")
+        if tuple(nears.shape) != (n,) or tuple(fars.shape) != (n,):
+            raise RuntimeError("nears / fars must be [N]")
+        if bitfield.numel() * 8 < C * H ** 3:
+            raise RuntimeError("bitfield is smaller than C * H^3 / 8 bytes")
+        call("dfhip_render_ray_order_occ", ptr(rays_o), ptr(rays_d), ptr(nears), ptr(fars),
+             ptr(bitfield), float(bound), int(C), int(H), int(max_steps), n, int(chunk_log2),
+             ptr(cost), ptr(order), stream())
     return order
 
 

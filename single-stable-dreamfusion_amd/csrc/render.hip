@@ -512,6 +512,47 @@ __global__ __launch_bounds__(256) void k_chunk_cost(const float *__restrict__ ra
     if (lane == 0) cost[ch] = acc * (float)(1u << cl) / (float)(r1 - r0);
 }
 
+// The same chunks' cost from the occupancy grid: minus the occupied cells
+// found at kOccProbes evenly spaced points of each ray's [near, far) (the
+// bitfield the march reads, level of each point as the march takes it at
+// dt_min), so that the rays crossing the most occupied space come first.
+constexpr uint32_t kOccProbes = 16;
+__global__ __launch_bounds__(256) void k_chunk_cost_occ(
+    const float *__restrict__ rays_o, const float *__restrict__ rays_d,
+    const float *__restrict__ nears, const float *__restrict__ fars,
+    const uint8_t *__restrict__ grid, rm::MarchConsts k, uint32_t N, uint32_t cl,
+    uint32_t nchunks, float *__restrict__ cost) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (ch >= nchunks) return;  // uniform per wave
+    const uint32_t r0 = ch << cl, r1 = min(N, (ch + 1) << cl);
+    uint32_t occ = 0;
+    for (uint32_t r = r0 + lane; r < r1; r += 64) {
+        const float n0 = nears[r], f0 = fars[r];
+        if (!(f0 > n0)) continue;  // a ray missing the box
+        const float ox = rays_o[3 * (size_t)r], oy = rays_o[3 * (size_t)r + 1],
+                    oz = rays_o[3 * (size_t)r + 2];
+        const float dx = rays_d[3 * (size_t)r], dy = rays_d[3 * (size_t)r + 1],
+                    dz = rays_d[3 * (size_t)r + 2];
+        const float step = (f0 - n0) / (float)kOccProbes;
+#pragma unroll 4
+        for (uint32_t i = 0; i < kOccProbes; ++i) {
+            const float t = fmaf((float)i + 0.5f, step, n0);
+            const float x = rm::clampf(fmaf(t, dx, ox), -k.bound, k.bound);
+            const float y = rm::clampf(fmaf(t, dy, oy), -k.bound, k.bound);
+            const float z = rm::clampf(fmaf(t, dz, oz), -k.bound, k.bound);
+            const rm::Mip m = rm::mip_of(k, x, y, z, k.dt_min);
+            const uint32_t idx = rm::grid_index(k, m.level, rm::cell_of(k, x, m.rbound),
+                                                rm::cell_of(k, y, m.rbound),
+                                                rm::cell_of(k, z, m.rbound));
+            occ += (grid[idx >> 3] >> (idx & 7)) & 1u;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) occ += __shfl_xor(occ, off);
+    if (lane == 0) cost[ch] = -(float)occ * (float)(1u << cl) / (float)(r1 - r0);
+}
+
 // The chunks by ascending cost, quantised to kOrderBuckets levels between the
 // costs' min and max (NaN last), ties by chunk index: a stable counting sort
 // in one workgroup.  Thread t takes the chunks [t per, (t + 1) per) and counts
@@ -598,6 +639,38 @@ __global__ __launch_bounds__(kOrderThreads) void k_chunk_order(const float *__re
 
 }  // namespace rd
 }  // namespace dfhip
+
+extern "C" int dfhip_render_ray_order_occ(const float *rays_o, const float *rays_d,
+                                          const float *nears, const float *fars,
+                                          const uint8_t *grid, float bound, uint32_t C,
+                                          uint32_t H, uint32_t max_steps, uint32_t N,
+                                          uint32_t chunk_log2, float *cost, int32_t *order,
+                                          dfhip_stream_t stream) {
+    const char *name = "render_ray_order_occ";
+    if (chunk_log2 > 16 || C < 1 || C > 16 || H < 2 || H > 1024 || max_steps == 0 ||
+        !(bound > 0.0f)) {
+        set_error("%s: invalid chunk_log2=%u C=%u H=%u max_steps=%u bound=%g", name,
+                  chunk_log2, C, H, max_steps, (double)bound);
+        return DFHIP_EINVAL;
+    }
+    if (N == 0) return DFHIP_OK;
+    const uint32_t nchunks = ceil_div(N, 1u << chunk_log2);
+    if (nchunks > rd::kMaxOrderChunks) {
+        set_error("%s: %u chunks of 2^%u rays exceed %u (use larger chunks)", name, nchunks,
+                  chunk_log2, rd::kMaxOrderChunks);
+        return DFHIP_EINVAL;
+    }
+    if (!rays_o || !rays_d || !nears || !fars || !grid || !cost || !order) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const rm::MarchConsts k = rm::make_consts(bound, 0.0f, max_steps, C, H);
+    rd::k_chunk_cost_occ<<<ceil_div(nchunks, 4u), 256, 0, s>>>(rays_o, rays_d, nears, fars, grid,
+                                                               k, N, chunk_log2, nchunks, cost);
+    rd::k_chunk_order<<<1, rd::kOrderThreads, 0, s>>>(cost, nchunks, order);
+    return check_launch(name);
+}
 
 extern "C" int dfhip_render_ray_order(const float *rays_o, const float *rays_d, uint32_t N,
                                       uint32_t chunk_log2, float *cost, int32_t *order,

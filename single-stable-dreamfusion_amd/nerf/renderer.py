@@ -23,7 +23,8 @@ from .utils import custom_meshgrid, safe_normalize
 _INFER_QUADS = os.environ.get("DFHIP_INFER_QUADS", "1") != "0"
 # Queue order of the fused inference render (DFHIP_INFER_ORDER=0: pixel
 # order): chunks of 2^_INFER_CHUNK_LOG2 consecutive rays, those passing
-# closest to the scene centre first (dfhip_render_ray_order)
+# closest to the scene centre first (1, dfhip_render_ray_order) or those
+# meeting the most occupied cells first (2, dfhip_render_ray_order_occ)
 _INFER_ORDER = int(os.environ.get("DFHIP_INFER_ORDER", "1"))
 _INFER_CHUNK_LOG2 = int(os.environ.get("DFHIP_INFER_CHUNK_LOG2", "6"))
 
@@ -395,8 +396,11 @@ class NeRFRenderer(nn.Module):
         cl = _INFER_CHUNK_LOG2
         while (N + (1 << cl) - 1) >> cl > 16384:  # the order kernel's chunk limit
             cl += 1
+        occ = ((nears.float().contiguous(), fars.float().contiguous(), self.density_bitfield,
+                self.bound, self.cascade, self.grid_size, max_steps)
+               if _INFER_ORDER == 2 else None)
         order = (_fieldmlp.render_ray_order(rays_o.float().contiguous(),
-                                            rays_d.float().contiguous(), cl)
+                                            rays_d.float().contiguous(), cl, occ=occ)
                  if _INFER_ORDER and N > 0 else None)
         with _dfhip.timed("render_rays_infer", nbytes):
             _fieldmlp.render_rays_infer(

@@ -258,7 +258,7 @@ def test_ray_order_and_ordered_queue(gpu, monkeypatch):
         same = np.diff(b) == 0
         assert np.all(np.diff(order)[same] > 0)
     outs = []
-    for flag, cl in ((0, 6), (1, 0), (1, 3), (1, 6)):
+    for flag, cl in ((0, 6), (1, 0), (1, 3), (1, 6), (2, 3), (2, 6)):
         monkeypatch.setattr(rr, "_INFER_ORDER", flag)
         monkeypatch.setattr(rr, "_INFER_CHUNK_LOG2", cl)
         (fw, fd, fi), _ = _both(m, rays_o, rays_d, 1)
