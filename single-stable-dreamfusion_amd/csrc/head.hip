@@ -172,20 +172,38 @@ __global__ __launch_bounds__(kThreads) void k_head_fwd_net(
     float *__restrict__ out_depth, uint8_t *__restrict__ mask) {
     __shared__ W w;
     __shared__ alignas(16) float s_x[kRays][kIn + 1];
-    load_w(w, w1, b1, w2, b2);
     const int q = threadIdx.x & (kSub - 1), r = threadIdx.x / kSub;
     const uint32_t n = blockIdx.x * kRays + r;
     const bool live = n < N;
-    if (live) features_part(rays_d + 3 * (size_t)n, q, s_x[r]);
+    // the ray's direction and (sub-lane 0) the mix / depth operands are
+    // loaded ahead of the weight staging, so their latency overlaps it
+    float d[3] = {0.0f, 0.0f, 0.0f}, tl[7] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = rays_d[3 * (size_t)n + c];
+        if (q == 0) {
+            tl[0] = ws[n];
+            tl[1] = depth[n];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) tl[2 + k] = image[3 * (size_t)n + k];
+            tl[5] = nears[n];
+            tl[6] = fars[n];
+        }
+    }
+    load_w(w, w1, b1, w2, b2);
+    if (live) features_part(d, q, s_x[r]);
     __syncthreads();
     float x[kIn], h[kPer], o[kOut];
     load_x(s_x[r], live, x);
     mlp_part(w, x, q, h, o);
     if (!live || q != 0) return;
-    float bg[3];
+    // write_outputs' arithmetic on the preloaded operands
+    const float t = 1.0f - tl[0];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
-    write_outputs(N, n, bg, ws, depth, image, nears, fars, out_image, out_depth, mask);
+    for (int k = 0; k < 3; ++k) out_image[(size_t)k * N + n] = tl[2 + k] + t * sigmoid16(o[k]);
+    const float dd = tl[1] - tl[5];
+    out_depth[n] = (dd < 0.0f ? 0.0f : dd) / (tl[6] - tl[5]);
+    mask[n] = tl[5] < tl[6] ? 1 : 0;
 }
 
 // Backward.  grad_image [N, 3] = g; grad_ws = -sum_c g_c bg_c; grad_bg =
