@@ -398,8 +398,9 @@ static int render_infer(
     const void *quads, uint64_t *prof, const int32_t *order, uint32_t chunk_log2,
     dfhip_stream_t stream) {
     const char *name = "render_rays_infer";
-    if (order && chunk_log2 > 16) {
-        set_error("%s: chunk_log2 must be <= 16 (got %u)", name, chunk_log2);
+    if (order && (chunk_log2 > 16 || N > 0xFFFFFFFFu - (1u << chunk_log2))) {
+        set_error("%s: chunk_log2 must be <= 16 and N + 2^chunk_log2 < 2^32 (got %u, N=%u)",
+                  name, chunk_log2, N);
         return DFHIP_EINVAL;
     }
     if (L != 16) {
