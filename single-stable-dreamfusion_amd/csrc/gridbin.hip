@@ -801,6 +801,55 @@ __device__ __forceinline__ void load_grad(const grad_t *__restrict__ p, float (&
 // GROUP > 1 (stencil groups, see Stencil): an entry is a group; the lane
 // takes the group's points one after another through the same cell merge
 // (at the coarse levels a sample and its stencil points share a cell).
+// Walk plan of every walk workgroup: this workgroup's bin b and part j of
+// P_b (P_b = 1 + E_b (G - nz) / T, parts laid out in bin order); part 0
+// records the bin's image slots for k_sum.  Every thread stages the bin
+// totals in LDS (tot_s, kMaxBins words: one round of independent loads), then
+// wave 0 scans them (twice reading the totals from global memory was 2 nb / 64
+// dependent load rounds on one wave, ~4.7 us of every workgroup's start).
+// All threads call it; returns in sh_b / sh_j / sh_p (sh_p = 0: an idle
+// workgroup) after a barrier.
+__device__ __forceinline__ void walk_plan(const BinInfo &bi, uint32_t *counts, uint32_t *tot_s,
+                                          uint32_t &sh_b, uint32_t &sh_j, uint32_t &sh_p) {
+    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
+    const uint32_t *totals = counts + bi.o_totals;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) tot_s[b] = bin_total(totals, b);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t ln = threadIdx.x;
+        u64 T = 0, nz = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t e = b0 + ln < nb ? tot_s[b0 + ln] : 0u;
+            u64 t, z;
+            (void)wave_excl_scan(e, ln, &t);
+            (void)wave_excl_scan(e ? 1u : 0u, ln, &z);
+            T += t;
+            nz += z;
+        }
+        const u64 extra = G > nz ? G - nz : 0;
+        uint32_t carry = 0;
+        if (ln == 0) sh_p = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t b = b0 + ln;
+            const uint32_t e = b < nb ? tot_s[b] : 0u;
+            const uint32_t p = e ? 1u + (uint32_t)((u64)e * extra / (T ? T : 1)) : 0u;
+            u64 tot;
+            const uint32_t s = carry + (uint32_t)wave_excl_scan(p, ln, &tot);
+            if (b < nb && p && slot >= s && slot < s + p) {
+                sh_b = b;
+                sh_j = slot - s;
+                sh_p = p;
+            }
+            if (b < nb && p && slot == s) {
+                counts[bi.o_plan + 2 * b] = s;
+                counts[bi.o_plan + 2 * b + 1] = p;
+            }
+            carry += (uint32_t)tot;
+        }
+    }
+    __syncthreads();
+}
+
 template <typename grad_t, uint32_t D, uint32_t C, bool POW2, int MODE, uint32_t GROUP = 1>
 __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad,  // [L, GROUP B, C]
                                                const float *__restrict__ inputs,
@@ -814,58 +863,26 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
     extern __shared__ double acc[];
     __shared__ uint32_t sh_b, sh_j, sh_p;
     __shared__ uint32_t n_seen;
+    __shared__ uint32_t tot_s[kMaxBins];
     uint64_t tr0 = 0;
     if (bi.trace) tr0 = wall_clock64();
-    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
-    const uint32_t *totals = counts + bi.o_totals;
-    if (threadIdx.x < 64) {  // plan (wave 0): this workgroup's bin b and part j of P_b
-        const uint32_t ln = threadIdx.x;
-        u64 T = 0, nz = 0;
-        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-            const uint32_t e = b0 + ln < nb ? bin_total(totals, b0 + ln) : 0u;
-            u64 t, z;
-            (void)wave_excl_scan(e, ln, &t);
-            (void)wave_excl_scan(e ? 1u : 0u, ln, &z);
-            T += t;
-            nz += z;
-        }
-        const u64 extra = G > nz ? G - nz : 0;
-        uint32_t carry = 0;
-        if (ln == 0) sh_p = 0;  // none: an idle workgroup
-        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-            const uint32_t b = b0 + ln;
-            const uint32_t e = b < nb ? bin_total(totals, b) : 0u;
-            const uint32_t p = e ? 1u + (uint32_t)((u64)e * extra / (T ? T : 1)) : 0u;
-            u64 tot;
-            const uint32_t s = carry + (uint32_t)wave_excl_scan(p, ln, &tot);
-            if (b < nb && p && slot >= s && slot < s + p) {
-                sh_b = b;
-                sh_j = slot - s;
-                sh_p = p;
-            }
-            if (b < nb && p && slot == s) {  // part 0 records the bin's images for k_sum
-                counts[bi.o_plan + 2 * b] = s;
-                counts[bi.o_plan + 2 * b + 1] = p;
-            }
-            carry += (uint32_t)tot;
-        }
-        if (ln == 0) n_seen = 0;
-    }
-    __syncthreads();
+    const uint32_t nb = bi.nbins, slot = blockIdx.x;
+    const uint32_t srows = 1u << bi.shift;
+    // channel-major slice image (acc[ch * srows + row]): a wave's f64 adds to
+    // random rows then spread over 32 bank pairs instead of 16 row groups;
+    // zeroed before the plan (its barriers cover it)
+    for (uint32_t i = threadIdx.x; i < srows * C; i += blockDim.x) acc[i] = 0.0;
+    if (threadIdx.x == 0) n_seen = 0;
+    walk_plan(bi, counts, tot_s, sh_b, sh_j, sh_p);
     const uint32_t P = sh_p;
     if (P == 0) return;  // uniform: more workgroups than parts
     const uint32_t b = sh_b, part = sh_j;
     uint32_t l = 0;
     while (l + 1 < bi.L && bi.bin0[l + 1] <= b) ++l;
     const uint32_t k = b - bi.bin0[l];
-    const uint32_t srows = 1u << bi.shift;
     const uint32_t r0 = bi.base[l] + (k << bi.shift);
     const uint32_t r1 = min(r0 + srows, bi.base[l] + bi.rows[l]);
     const uint32_t n = (r1 - r0) * C;
-    // channel-major slice image (acc[ch * srows + row]): a wave's f64 adds to
-    // random rows then spread over 32 bank pairs instead of 16 row groups
-    for (uint32_t i = threadIdx.x; i < srows * C; i += blockDim.x) acc[i] = 0.0;
-    __syncthreads();
     const bool align = align_corners != 0;
     const LevelCtx c = ge::level_ctx<D>(offsets, lv, l, gridtype, align);
     const ge::LevelRows lr = ge::level_rows<D>(c);
@@ -1577,53 +1594,20 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     __shared__ uint32_t pre[kChunkTiles + 1];
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t sh_b, sh_j, sh_p, sh_entries;
+    __shared__ uint32_t tot_s[kMaxBins];
     const uint64_t tr0 = bi.trace ? wall_clock64() : 0;
-    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
-    const uint32_t *totals = counts + bi.o_totals;
+    const uint32_t nb = bi.nbins, slot = blockIdx.x;
+    const uint32_t srows = 1u << bi.shift;
+    for (uint32_t i = threadIdx.x; i < srows * C; i += blockDim.x) acc[i] = 0.0;
     if (threadIdx.x == 0) sh_entries = 0;
-    if (threadIdx.x < 64) {  // plan (wave 0), as k_walk
-        const uint32_t ln = threadIdx.x;
-        u64 T = 0, nz = 0;
-        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-            const uint32_t e = b0 + ln < nb ? bin_total(totals, b0 + ln) : 0u;
-            u64 t, z;
-            (void)wave_excl_scan(e, ln, &t);
-            (void)wave_excl_scan(e ? 1u : 0u, ln, &z);
-            T += t;
-            nz += z;
-        }
-        const u64 extra = G > nz ? G - nz : 0;
-        uint32_t carry = 0;
-        if (ln == 0) sh_p = 0;
-        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-            const uint32_t b = b0 + ln;
-            const uint32_t e = b < nb ? bin_total(totals, b) : 0u;
-            const uint32_t p = e ? 1u + (uint32_t)((u64)e * extra / (T ? T : 1)) : 0u;
-            u64 tot;
-            const uint32_t s = carry + (uint32_t)wave_excl_scan(p, ln, &tot);
-            if (b < nb && p && slot >= s && slot < s + p) {
-                sh_b = b;
-                sh_j = slot - s;
-                sh_p = p;
-            }
-            if (b < nb && p && slot == s) {
-                counts[bi.o_plan + 2 * b] = s;
-                counts[bi.o_plan + 2 * b + 1] = p;
-            }
-            carry += (uint32_t)tot;
-        }
-    }
-    __syncthreads();
+    walk_plan(bi, counts, tot_s, sh_b, sh_j, sh_p);  // (its barriers cover the zeroing)
     const uint32_t P = sh_p;
     if (P == 0) return;  // uniform
     const uint32_t b = sh_b, part = sh_j;
     uint32_t l = 0;
     while (l + 1 < bi.L && bi.bin0[l + 1] <= b) ++l;
-    const uint32_t srows = 1u << bi.shift;
     const uint32_t lo = (b - bi.bin0[l]) << bi.shift;  // slice start, relative to the level
     const uint32_t n = min(srows, bi.rows[l] - lo);
-    for (uint32_t i = threadIdx.x; i < srows * C; i += blockDim.x) acc[i] = 0.0;
-    __syncthreads();
     const uint64_t tr1 = bi.trace ? wall_clock64() : 0;
     const uint32_t M = ge::dyn_count(dyn, B);
     const uint32_t ntiles = ceil_div(M, GROUP == 1 ? bi.tile : kTile);
@@ -1798,45 +1782,6 @@ __global__ __launch_bounds__(1024) void k_rbin(const float *__restrict__ inputs,
             }
         }
         __syncthreads();  // cw / toff are rewritten by the next tile
-    }
-}
-
-// Walk plan (wave 0 of every walk workgroup): this workgroup's bin b and part
-// j of P_b; part 0 records the bin's image slots for k_sum.  Returns in
-// sh_b / sh_j / sh_p (sh_p = 0: an idle workgroup).
-__device__ __forceinline__ void walk_plan(const BinInfo &bi, uint32_t *counts, uint32_t &sh_b,
-                                          uint32_t &sh_j, uint32_t &sh_p) {
-    const uint32_t nb = bi.nbins, G = bi.G, slot = blockIdx.x;
-    const uint32_t *totals = counts + bi.o_totals;
-    const uint32_t ln = threadIdx.x;
-    u64 T = 0, nz = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-        const uint32_t e = b0 + ln < nb ? bin_total(totals, b0 + ln) : 0u;
-        u64 t, z;
-        (void)wave_excl_scan(e, ln, &t);
-        (void)wave_excl_scan(e ? 1u : 0u, ln, &z);
-        T += t;
-        nz += z;
-    }
-    const u64 extra = G > nz ? G - nz : 0;
-    uint32_t carry = 0;
-    if (ln == 0) sh_p = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-        const uint32_t b = b0 + ln;
-        const uint32_t e = b < nb ? bin_total(totals, b) : 0u;
-        const uint32_t p = e ? 1u + (uint32_t)((u64)e * extra / (T ? T : 1)) : 0u;
-        u64 tot;
-        const uint32_t s = carry + (uint32_t)wave_excl_scan(p, ln, &tot);
-        if (b < nb && p && slot >= s && slot < s + p) {
-            sh_b = b;
-            sh_j = slot - s;
-            sh_p = p;
-        }
-        if (b < nb && p && slot == s) {
-            counts[bi.o_plan + 2 * b] = s;
-            counts[bi.o_plan + 2 * b + 1] = p;
-        }
-        carry += (uint32_t)tot;
     }
 }
 
@@ -2026,20 +1971,19 @@ __global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, 
     __shared__ uint32_t sbase[kChunkTiles];
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t sh_b, sh_j, sh_p, sh_entries;
+    __shared__ uint32_t tot_s[kMaxBins];
     const uint64_t tr0 = bi.trace ? wall_clock64() : 0;
+    const uint32_t srows = 1u << bi.shift;
+    for (uint32_t i = threadIdx.x; i < srows * 2; i += blockDim.x) acc[i] = 0.0;
     if (threadIdx.x == 0) sh_entries = 0;
-    if (threadIdx.x < 64) walk_plan(bi, counts, sh_b, sh_j, sh_p);
-    __syncthreads();
+    walk_plan(bi, counts, tot_s, sh_b, sh_j, sh_p);  // (its barriers cover the zeroing)
     const uint32_t P = sh_p;
     if (P == 0) return;  // uniform
     const uint32_t b = sh_b, part = sh_j;
     uint32_t l = 0;
     while (l + 1 < bi.L && bi.bin0[l + 1] <= b) ++l;
-    const uint32_t srows = 1u << bi.shift;
     const uint32_t lo = (b - bi.bin0[l]) << bi.shift;  // slice start, relative to the level
     const uint32_t n = min(srows, bi.rows[l] - lo);
-    for (uint32_t i = threadIdx.x; i < srows * 2; i += blockDim.x) acc[i] = 0.0;
-    __syncthreads();
     const uint64_t tr1 = bi.trace ? wall_clock64() : 0;
     const uint32_t ntiles = ceil_div(ge::dyn_count(dyn, B), kTile);
     const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
