@@ -51,14 +51,12 @@ def main():
     cnt = torch.empty(nc, dtype=torch.int32, device=dev)
     part = torch.empty(npf, device=dev)
     ot = T(offs)
-    import os
-    win = os.environ.get("DFHIP_GRID_NOWIN") is None
     for rep in range(args.reps + 1):
         trace.zero_()
         _gridencoder.grid_encode_backward_binned(g, x01, 0.0, ot, offs, gemb, B, None, 3, 2, L,
                                                  S, 16, 1, False, ent, cnt, part, opts=opts)
         torch.cuda.synchronize()
-    report(trace, B, L, offs, shift=0 if win else 13)
+    report(trace, B, L, offs, shift=13)  # C = 2: 8,192-row slices
 
 
 def report(trace, B, L, offs=None, shift=13):
@@ -95,9 +93,14 @@ def report(trace, B, L, offs=None, shift=13):
             bin0.append(bin0[-1] + ((rows - 1) >> shift) + 1)
         lvl = np.searchsorted(np.array(bin0), tr[:, 0], side="right") - 1
         one = (tr[:, 1] - tr[:, 0]) == 1
-        print("level: entries/us per workgroup (single-bin workgroups)")
+        print("level: entries/us per workgroup (single-bin workgroups); max duration us")
         print("  " + "  ".join(f"{lv}:{(tr[one & (lvl == lv), 3] / dur[one & (lvl == lv)]).mean():.0f}"
                                for lv in range(L) if (one & (lvl == lv)).any()))
+        print("  " + "  ".join(f"{lv}:{dur[one & (lvl == lv)].max():.0f}"
+                               for lv in range(L) if (one & (lvl == lv)).any()))
+        tot = {lv: int(tr[lvl == lv, 3].sum()) for lv in range(L)}
+        print("level: entries, workgroups")
+        print("  " + "  ".join(f"{lv}:{tot[lv]}/{int((lvl == lv).sum())}" for lv in range(L)))
 
 
 if __name__ == "__main__":
