@@ -61,6 +61,10 @@ def parse():
     p.add_argument("--no-module-path", action="store_true",
                    help="skip timing the reference-module path (autograd through the "
                         "reference-API encoder / MLP modules, no fused field, no native step)")
+    p.add_argument("--module-path-child", action="store_true",
+                   help="(internal) run the step through the reference-API modules: the "
+                        "Trainer's autograd body, GridEncoder -> MLP -> trunc_exp / sigmoid "
+                        "-> composite_rays_train as separate nodes")
     p.add_argument("--no-c5", action="store_true",
                    help="skip the C5 leg (256x256 bf16 renderer step)")
     p.add_argument("--c5-res", type=int, default=256)
@@ -72,6 +76,34 @@ def parse():
     p.add_argument("--launcher-selftest", action="store_true",
                    help="CPU/gloo check of the N-rank launch only (no GPU work)")
     return p.parse_args()
+
+
+def env_options(model=None, trainer=None):
+    """A/B switches of tools/ scripts, read from the environment here only (the
+    package itself takes them as explicit options): DFHIP_NATIVE_STEP,
+    DFHIP_NATIVE_ADAM, DFHIP_STENCIL_BIN (Trainer), DFHIP_FUSED_FIELD,
+    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2 (renderer),
+    DFHIP_GRID_BWD=atomic (GridEncoder)."""
+    env = os.environ
+    if trainer is not None:
+        for name, attr in (("DFHIP_NATIVE_STEP", "native_step"),
+                           ("DFHIP_NATIVE_ADAM", "native_optimizer"),
+                           ("DFHIP_STENCIL_BIN", "stencil_bin")):
+            if name in env:
+                setattr(trainer, attr, env[name] != "0")
+        model = trainer.model if model is None else model
+    if model is not None:
+        if "DFHIP_FUSED_FIELD" in env:
+            model.fused_field = env["DFHIP_FUSED_FIELD"] != "0"
+        if "DFHIP_INFER_QUADS" in env:
+            model.infer_quads = env["DFHIP_INFER_QUADS"] != "0"
+        if "DFHIP_INFER_ORDER" in env:
+            model.infer_order = int(env["DFHIP_INFER_ORDER"])
+        if "DFHIP_INFER_CHUNK_LOG2" in env:
+            model.infer_chunk_log2 = int(env["DFHIP_INFER_CHUNK_LOG2"])
+        enc = getattr(model, "encoder", None)
+        if env.get("DFHIP_GRID_BWD") == "atomic" and hasattr(enc, "backward_mode"):
+            enc.backward_mode = "atomic"
 
 
 def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False, bf16=False):
@@ -104,7 +136,48 @@ def make_trainer(res, seed, rank, world, fused, graph=False, mock_sds=False, bf1
                       graph_step=graph)
     data = NeRFDataset(opt, device=device, type="train", H=res, W=res, size=100)
     trainer.model.train()
+    env_options(trainer=trainer)
     return trainer, data
+
+
+def replica_digest(trainer):
+    """f64 digest of one rank's replica state (every parameter, the Adam step
+    counts and moments, the GradScaler scale, the density grid and bitfield):
+    per tensor its sum and its sum of squares.  Data-parallel ranks that stay
+    replicas (the reference's DDP contract, nerf/utils.py:200-202) have equal
+    digests bit for bit."""
+    m = trainer.model
+    ts = [p.detach() for p in m.parameters()]
+    for st in trainer.optimizer.state.values():
+        for k in ("step", "exp_avg", "exp_avg_sq"):
+            if k in st and torch.is_tensor(st[k]):
+                ts.append(st[k])
+    if trainer.scaler.is_enabled():
+        ts.append(torch.as_tensor(trainer.scaler.get_scale(), dtype=torch.float64))
+    if getattr(m, "cuda_ray", False):
+        ts += [m.density_grid, m.density_bitfield]
+    dev = next(m.parameters()).device
+    out = []
+    for t in ts:
+        t = t.to(device=dev, dtype=torch.float64)
+        out += [t.sum(), (t * t).sum()]
+    return torch.stack(out)
+
+
+def replica_check(trainer, samples, world):
+    """After the timed region: replicas_identical (MIN == MAX of every digest
+    entry over the ranks) and every rank's mean samples per step."""
+    d = replica_digest(trainer)
+    lo, hi = d.clone(), d.clone()
+    per_rank = [samples]
+    if world > 1:
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        s = torch.tensor([samples], dtype=torch.float64, device=d.device)
+        got = [torch.zeros_like(s) for _ in range(world)]
+        dist.all_gather(got, s)
+        per_rank = [float(g.item()) for g in got]
+    return bool(torch.equal(lo, hi)), [round(v, 1) for v in per_rank]
 
 
 def cpu_baseline(res, steps, c1_steps=10, c1_warmup=3):
@@ -180,6 +253,7 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1,
     opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res)])
     torch.manual_seed(seed)
     model = NeRFNetwork(opt).to(device)
+    env_options(model=model)
     with torch.no_grad():
         model.encoder.embeddings.uniform_(-0.5, 0.5)
     with torch.autocast("cuda", dtype=torch.float16):
@@ -402,9 +476,8 @@ def summarize_kernels(records):
 # timed region -> its kernels, each as alternative name fragments (rocprofv3
 # reports some names demangled, some mangled)
 REGION_KERNELS = {
-    "grid_encode_backward": (("gb::k_bin", "gb5k_bin", "gb::k_rbin", "gb6k_rbin"),
-                             ("gb::k_walk", "gb6k_walk", "gb11k_walk_flat", "gb::k_rwalk",
-                              "gb7k_rwalk"),
+    "grid_encode_backward": (("gb::k_bin", "gb5k_bin"),
+                             ("gb::k_walk", "gb6k_walk", "gb11k_walk_flat"),
                              ("gb::k_sum", "gb5k_sum")),
     "grid_field_forward": ("k_field_fwd_fused",),
     "field_mlp_backward": ("k_field_bwd", "k_field_wgrad_sum"),
@@ -555,31 +628,100 @@ def measure_traffic(region, timeout=180, warmup=10, shade="albedo", key=None):
         "summed over the region's kernels, mean per launch; l2_hit_rate per kernel")
 
 
+MODULE_GROUPS = (  # rocprofv3 kernel name fragment -> breakdown group
+    ("k_march_train", "march_rays_train"), ("k_grid_fwd", "grid_encode_forward"),
+    ("k_mlp_fwd", "mlp_forward"), ("k_field_bwd", "mlp_backward"),
+    ("k_field_wgrad_sum", "mlp_backward"), ("k_blc_to_lbc", "grid_encode_backward"),
+    ("gb::k_", "grid_encode_backward"), ("gb5k_", "grid_encode_backward"),
+    ("gb6k_", "grid_encode_backward"), ("gb11k_", "grid_encode_backward"),
+    ("k_composite_train", "composite_rays_train"), ("hd::k_", "ray_head_and_entropy"),
+    ("hd4k_", "ray_head_and_entropy"), ("k_entropy", "ray_head_and_entropy"),
+    ("opt::k_", "adam"), ("opt5k_", "adam"), ("k_get_rays", "camera_and_near_far"),
+    ("k_near_far", "camera_and_near_far"), ("occ::k_", "occupancy_refresh"),
+    ("k_grid_ema", "occupancy_refresh"), ("k_packbits", "occupancy_refresh"),
+    ("k_mean_count", "occupancy_refresh"), ("Cijk_", "hipblaslt_gemm"),
+    ("at::native", "torch_elementwise_and_reductions"), ("rocclr", "runtime_copies_and_fills"))
+
+
+def _module_breakdown(csv_files, steps):
+    """Kernel time per step by group over the child's last `steps` steps (a
+    step starts at its march count launch) from rocprofv3 kernel traces."""
+    import csv
+    ks = []
+    for f in csv_files:
+        for r in csv.DictReader(open(f)):
+            ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    ks.sort()
+    starts = [t0 for t0, _, n in ks if "k_march_train_count" in n]
+    if len(starts) < steps + 1:
+        return None
+    b0 = starts[-steps]
+    groups, top = {}, {}
+    for t0, t1, n in ks:
+        if t0 < b0:
+            continue
+        g = next((grp for frag, grp in MODULE_GROUPS if frag in n), "other")
+        groups[g] = groups.get(g, 0.0) + (t1 - t0) / 1e3 / steps
+        short = n.split("(")[0][:60]
+        top[short] = top.get(short, 0.0) + (t1 - t0) / 1e3 / steps
+    tot = sum(groups.values())
+    return {"kernel_us_per_step": round(tot, 1),
+            "groups_us_per_step": {k: round(v, 1) for k, v in
+                                   sorted(groups.items(), key=lambda kv: -kv[1])},
+            "top_kernels_us_per_step": {k: round(v, 1) for k, v in
+                                        sorted(top.items(), key=lambda kv: -kv[1])[:12]}}
+
+
 def module_path_leg(args, timeout=300):
-    """The C2 step through the reference-API modules one by one — grid
-    encoder, MLP and compositing as separate autograd nodes on the
-    `_gridencoder` / `_raymarching` kernels (DFHIP_FUSED_FIELD=0), autograd
-    body instead of the native step (DFHIP_NATIVE_STEP=0), still HIP-graph
-    replayed: the path the reference's own nerf/network_grid.py takes on this
-    package.  A child bench (the switches are read at import)."""
+    """The C2 step through the reference-API modules one by one — GridEncoder,
+    the sigma_net MLP, trunc_exp / sigmoid, composite_rays_train and the ray
+    head as separate autograd nodes, the Trainer's autograd backward — in the
+    reference's own launch structure: eager launches and the host-count march
+    (`step_counter[0].item()`, raymarching.py:224), the samples sliced to the
+    align-rounded count.  The path the reference's nerf/network_grid.py takes
+    on this package.  A child bench times it; a second child runs under
+    rocprofv3 --kernel-trace for the per-kernel breakdown of its last steps."""
+    import shutil
     import subprocess
+    import tempfile
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
-    env.update(DFHIP_NATIVE_STEP="0", DFHIP_FUSED_FIELD="0")
+    env["TMPDIR"] = "/tmp"
     cmd = [sys.executable, str(Path(__file__).resolve()), "--steps", str(min(args.steps, 20)),
-           "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-kernel-timing",
-           "--no-alt-backward", "--no-shading", "--no-infer", "--no-traffic", "--no-c5",
-           "--no-module-path"]
+           "--warmup", str(args.warmup), "--eager", "--module-path-child", "--no-cpu-baseline",
+           "--no-kernel-timing", "--no-alt-backward", "--no-shading", "--no-infer",
+           "--no-traffic", "--no-c5", "--no-module-path"]
     try:
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
         d = json.loads(line)
     except (subprocess.TimeoutExpired, IndexError, ValueError) as e:
         return {"error": f"{type(e).__name__}"}
-    return {"ms_per_step": d["ms_per_step"], "value": d["value"], "unit": d["unit"],
-            "mean_samples_per_step": d["config"]["mean_samples_per_step"],
-            "note": "DFHIP_FUSED_FIELD=0 DFHIP_NATIVE_STEP=0: encoder, MLP and compositing "
-                    "as separate autograd nodes (reference-API modules), graph-replayed"}
+    res = {"ms_per_step": d["ms_per_step"], "value": d["value"], "unit": d["unit"],
+           "mean_samples_per_step": d["config"]["mean_samples_per_step"],
+           "launch": "eager autograd, host-count march (raymarching.py:224 sync), samples "
+                     "sliced to the align-rounded count",
+           "note": "reference-API modules as separate autograd nodes: GridEncoder (binned "
+                   "embedding backward), sigma_net MLP (dfhip_mlp_forward / _backward), "
+                   "trunc_exp / gaussian / sigmoid in torch, composite_rays_train, ray head"}
+    rp = shutil.which("rocprofv3")
+    if rp is None or args.no_traffic:
+        return res
+    tmp = tempfile.mkdtemp(prefix="dfhip_module_", dir="/tmp")
+    try:
+        pcmd = [rp, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o", "run", "--",
+                *cmd]
+        r = subprocess.run(pcmd, env=env, capture_output=True, text=True, timeout=timeout)
+        if r.returncode == 0:
+            bd = _module_breakdown(list(Path(tmp).rglob("*kernel_trace.csv")), 16)
+            if bd:
+                res["breakdown"] = dict(bd, source="rocprofv3 --kernel-trace of the same child "
+                                        "command, its last 16 steps (one density refresh)")
+    except subprocess.TimeoutExpired:
+        res["breakdown_error"] = "rocprofv3 pass timed out"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return res
 
 
 def shading_roofline(trainer, args):
@@ -688,6 +830,9 @@ def main():
     _dfhip.load()
     trainer, data = make_trainer(args.res, args.seed, rank, world, not args.two_pass_backward,
                                  graph=not args.eager, mock_sds=args.mock_sds)
+    if args.module_path_child:
+        trainer.native_step = False
+        trainer.model.fused_field = False
     if args.shade != "albedo":
         trainer.pick_shading = (lambda k: (lambda: (k, 0.1)))(args.shade)
 
@@ -721,6 +866,9 @@ def main():
     last = min(16, args.steps)
     rows = [(trainer.model.local_step - 1 - i) % 16 for i in range(last)]
     samples = float(trainer.model.step_counter[rows, 0].float().mean().item())
+    # the replicas after the timed region (every rank must hold the same
+    # model: DDP's contract), and each rank's own samples per step
+    identical, per_rank = replica_check(trainer, samples, world)
     kernels, timing = {}, None
     if not args.no_kernel_timing:
         kernels, timing = kernel_timing_pass(trainer, step, min(args.steps, 20))
@@ -755,10 +903,13 @@ def main():
                    "launch": "eager" if not trainer.graph_step else "hip-graph replay",
                    "mean_samples_per_step": round(samples, 1)},
         "steps_per_sec": round(steps_per_sec, 3),
+        "replicas_identical": identical,
+        "samples_per_step_per_rank": per_rank,
         "host_issue_ms_per_step": round(host_issue / args.steps * 1e3, 3),
         "host_cost_ms_per_step": round(host_cost * 1e3, 3),
     }
     g0 = next(iter(trainer._graphs.values()), None)
+    result["config"]["grad_exchange"] = "none (one rank)"
     if g0 is not None:
         result["config"]["optimizer_in_graph"] = bool(g0.optimizer_in_graph)
         nat0 = getattr(g0, "native", None)
@@ -769,6 +920,13 @@ def main():
                 "rccl all-reduce inside the replayed step graph"
                 if nat0 is not None and nat0.dp_world is not None
                 else "eager all-reduce after the replay")
+    elif world > 1:
+        result["config"]["grad_exchange"] = "eager flat all-reduce (rccl)"
+    if "grad_allreduce" in kernels:
+        # the exchange's time per step: HIP events around the same all-reduce +
+        # 1/world launches in the eager twin of the replayed step (every rank
+        # issues it; rank 0's events)
+        result["grad_allreduce_us"] = kernels["grad_allreduce"]["avg_us"]
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         kd = kernels[dom]

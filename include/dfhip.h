@@ -51,6 +51,11 @@ enum dfhip_status {
     DFHIP_ENOMEM = 4      /* stream-ordered scratch allocation failed */
 };
 
+/* ABI version: a hash of this header's text taken at build time
+ * (dfhip_build.py passes it as DFHIP_ABI_HASH).  The Python binding hashes
+ * the header it was written against the same way and refuses a library whose
+ * value differs, so a stale library fails to load instead of being called
+ * with another signature. */
 int dfhip_abi_version(void);
 const char *dfhip_last_error(void);
 
@@ -284,6 +289,17 @@ int dfhip_grid_encode_forward_blc(int dtype, const float *inputs,
                                   uint32_t L, float S, uint32_t H, void *dy_dx,
                                   uint32_t gridtype, int align_corners,
                                   dfhip_stream_t stream);
+/* dfhip_grid_encode_forward_blc over a capacity-sized batch (GridEncoder.forward
+ * on the capacity-sized samples of the device-count march, grid.py:138-154):
+ * rows [0, *m_dev) are encoded (all B rows when m_dev is NULL), rows
+ * [*m_dev, B) are written as zeros (and their dy_dx rows); with bound > 0
+ * `inputs` are raw positions in [-bound, bound], mapped to [0, 1] as
+ * grid.py:142 does ((x + bound) / (2 bound), bit-identical to that torch op). */
+int dfhip_grid_encode_forward_dyn(int dtype, const float *inputs, float bound,
+                                  const void *embeddings, const int32_t *offsets,
+                                  void *outputs, uint32_t B, const int32_t *m_dev, uint32_t D,
+                                  uint32_t C, uint32_t L, float S, uint32_t H, void *dy_dx,
+                                  uint32_t gridtype, int align_corners, dfhip_stream_t stream);
 /* grad_dtype: dtype of `grad` ([B, L*C]); acc_dtype: dtype of grad_embeddings
  * (F32 accumulation is allowed with F16 grads: more accurate than the
  * reference's half2 atomics, same request count). */
@@ -322,7 +338,7 @@ int dfhip_grid_encode_backward_sliced_dyn(int grad_dtype, int out_dtype, const v
  * Replaces gridencoder.cu:226-313 on the native path. */
 /* [B, L*C] -> [L, B, C] copy of the native encoder gradient into the layout
  * the sliced backward walks (the reference forms the same layout with a torch
- * permute, grid.py:70).  dtype F16/F32/F64; C * sizeof(dtype) in {2,4,8,16}. */
+ * permute, grid.py:70).  dtype F16/BF16/F32/F64; C * sizeof(dtype) in {2,4,8,16}. */
 int dfhip_grid_grad_blc_to_lbc(int dtype, const void *src, void *dst, uint32_t B, uint32_t L,
                                uint32_t C, dfhip_stream_t stream);
 uint32_t dfhip_grid_backward_default_parts(uint32_t total_rows, uint32_t C);
@@ -380,6 +396,28 @@ int dfhip_field_mlp_backward(const void *enc, const float *xyz, const float *w1,
                              uint32_t M, void *d_enc_lbc, float *partial, uint32_t parts,
                              float *gw1, float *gb1, float *gw2, float *gb2, float *gw3,
                              float *gb3, int accumulate, dfhip_stream_t stream);
+
+/* The MLP module alone (nerf/network_grid.py:13-32, the reference's sigma_net
+ * = 3 nn.Linear + ReLU under autocast; the reference runs 3 hipBLASLt GEMMs +
+ * ~20 elementwise / reduction kernels forward and backward): elem DFHIP_F16
+ * (fp16 autocast) or DFHIP_BF16; x [cap, 32] and h [cap, 4] in elem, f16 /
+ * bf16 GEMM operands with f32 accumulation, elem activations (autocast's
+ * numerics), parameters as in dfhip_field_mlp_forward.  With m_dev (device
+ * int32 live-row count, e.g. the march's counter[0]) rows [0, *m_dev) are
+ * computed and rows [*m_dev, cap) of h (backward: of dx) written as zeros.
+ * Backward: dh [cap, 4] elem -> dx [cap, 32] elem (natural layout) and the
+ * f32 weight gradients (overwritten, or added into with accumulate);
+ * partial: parts * dfhip_field_mlp_params() floats of scratch with parts =
+ * dfhip_field_mlp_backward_parts(cap).  Deterministic. */
+int dfhip_mlp_forward(int elem, const void *x, const float *w1, const float *b1, const float *w2,
+                      const float *b2, const float *w3, const float *b3, void *h, uint32_t cap,
+                      const int32_t *m_dev, dfhip_stream_t stream);
+int dfhip_mlp_backward(int elem, const void *x, const float *w1, const float *b1,
+                       const float *w2, const float *b2, const float *w3, const float *b3,
+                       const void *dh, uint32_t cap, const int32_t *m_dev, void *dx,
+                       float *partial, uint32_t parts, float *gw1, float *gb1, float *gw2,
+                       float *gb2, float *gw3, float *gb3, int accumulate,
+                       dfhip_stream_t stream);
 
 /* Fused grid field (native path of nerf/field.py): tiled-grid encoding
  * (gridencoder.cu:75-178 arithmetic, f16 table) + the MLP/heads above in ONE
@@ -527,11 +565,8 @@ int dfhip_grid_encode_backward_binned_stencil(int phase, int grad_dtype, const v
  * (or 0 where noted) keeps the default; NULL options = all defaults. */
 typedef struct dfhip_binned_opts {
     int32_t walk_mode;          /* -1 default: per-segment walk for single samples, flat walk
-                                   for stencil groups; 0 per-segment, 1 flat, 2 flat
-                                   per-wave pieces (mask-form layouts); 3 the resolved
-                                   stream for single samples (16-byte entries binned with
-                                   their fractions and gradient, streamed by the walk;
-                                   f16 / bf16, C = 2, align_corners = 0, else flat) */
+                                   for stencil groups; 0 per-segment, 1 flat (mask-form
+                                   layouts) */
     int32_t fast_bin;           /* -1 / 1: mask-form fast binning where it applies; 0 the
                                    generic binning kernel */
     int32_t walk_groups_per_cu; /* 0 default (3); 1..16 walk workgroups per CU (changes the
@@ -544,12 +579,11 @@ typedef struct dfhip_binned_opts {
 } dfhip_binned_opts;
 /* dfhip_grid_backward_binned_scratch / dfhip_grid_encode_backward_binned_stencil
  * with per-call options (group 1 = single samples, eps ignored; group 7 =
- * stencil groups).  The scratch depends on the layout (S, H, gridtype,
- * align_corners as the launch), the group and the options: size it with the
- * values the launches will use. */
+ * stencil groups; any other group is DFHIP_EINVAL).  The partial scratch
+ * depends on the options (walk_groups_per_cu): size it with the opts the
+ * launches will use.  Host only (no device work, no device pointers). */
 int dfhip_grid_backward_binned_scratch_opts(uint32_t cap, const int32_t *offsets_host,
-                                            uint32_t L, uint32_t C, float S, uint32_t H,
-                                            uint32_t gridtype, int align_corners, uint32_t group,
+                                            uint32_t L, uint32_t C, uint32_t group,
                                             const dfhip_binned_opts *opts, uint64_t *entries_u32,
                                             uint64_t *counts_u32, uint64_t *partial_f32);
 /* Samples per binning tile (the id slots of one (tile, slice) segment of the

@@ -63,6 +63,8 @@ _SIGS = {
                                   _vp, _u32, _i32, _vp],
     "dfhip_grid_encode_forward_blc": [_i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _f32,
                                       _u32, _vp, _u32, _i32, _vp],
+    "dfhip_grid_encode_forward_dyn": [_i32, _vp, _f32, _vp, _vp, _vp, _u32, _vp, _u32, _u32,
+                                      _u32, _f32, _u32, _vp, _u32, _i32, _vp],
     "dfhip_grid_encode_backward": [_i32, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _f32,
                                    _u32, _vp, _vp, _u32, _i32, _vp],
     "dfhip_grid_encode_backward_blc": [_i32, _i32, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32,
@@ -82,8 +84,8 @@ _SIGS = {
     "dfhip_grid_encode_backward_binned_stencil": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp,
                                                   _u32, _vp, _u32, _u32, _u32, _f32, _u32, _u32,
                                                   _i32, _u32, _f32, _vp, _vp, _vp, _i32, _vp],
-    "dfhip_grid_backward_binned_scratch_opts": [_u32, _vp, _u32, _u32, _f32, _u32, _u32,
-                                                _i32, _u32, _vp, _vp, _vp, _vp],
+    "dfhip_grid_backward_binned_scratch_opts": [_u32, _vp, _u32, _u32, _u32, _vp, _vp, _vp,
+                                                _vp],
     "dfhip_grid_encode_backward_binned_opts": [_i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _u32,
                                                _vp, _u32, _u32, _u32, _f32, _u32, _u32, _i32,
                                                _u32, _f32, _vp, _vp, _vp, _i32, _vp, _vp],
@@ -91,6 +93,9 @@ _SIGS = {
     "dfhip_field_mlp_forward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp],
     "dfhip_field_mlp_backward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp,
                                  _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dfhip_mlp_forward": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp],
+    "dfhip_mlp_backward": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp,
+                           _u32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dfhip_grid_field_forward": [_vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32, _vp, _vp, _vp,
                                  _vp, _vp, _vp, _vp, _vp, _vp, _i32, _u32, _vp, _vp],
     "dfhip_grid_field_backward": [_vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
@@ -177,6 +182,16 @@ def load() -> ctypes.CDLL:
     lib = ctypes.CDLL(str(LIB_PATH))
     lib.dfhip_last_error.restype = ctypes.c_char_p
     lib.dfhip_abi_version.restype = ctypes.c_int
+    # the library must be built from the header these signatures follow: a
+    # stale one would be called with other argument lists (and crash)
+    from dfhip_build import HEADER, abi_hash
+    if not HEADER.exists():
+        raise ImportError(f"{HEADER} not found: cannot check the ABI of {LIB_PATH}")
+    want, got = abi_hash(HEADER), int(lib.dfhip_abi_version())
+    if got != want:
+        raise ImportError(
+            f"{LIB_PATH} was built from another include/dfhip.h (ABI {got:#x}, header "
+            f"{want:#x}); rebuild it: python -c 'import __graft_entry__ as g; g.build()'")
     lib.dfhip_march_rays_train_scratch_ints.restype = _u32
     lib.dfhip_march_rays_train_scratch_ints.argtypes = [_u32]
     lib.dfhip_grid_backward_default_parts.restype = _u32

@@ -65,6 +65,44 @@ def field_mlp_backward(enc, xyz, weights, grad_sigma, grad_rgb, d_enc_lbc, parti
          backward_parts(M) if M else 1, *gp, int(bool(accumulate)), stream())
 
 
+# ---- the MLP module alone (network_grid.py:13-32), no heads
+
+def mlp_forward(x, weights, out, m_dev=None):
+    """x [cap, 32] f16 / bf16 -> out [cap, 4] (same dtype): the sigma_net
+    MLP under autocast on MFMA.  Rows [m_dev[0], cap) of out are zeros when
+    m_dev (int32 device live-row count) is given."""
+    checked(x, "x")
+    checked(out, "out")
+    if x.dtype not in (torch.float16, torch.bfloat16) or x.dim() != 2 or x.shape[1] != IN:
+        raise RuntimeError("x must be a [M, 32] float16 / bfloat16 tensor")
+    if out.dtype != x.dtype or tuple(out.shape) != (x.shape[0], OUT):
+        raise RuntimeError("out must be [M, 4] of x's dtype")
+    if m_dev is not None:
+        checked(m_dev, "m_dev", "int")
+    call("dfhip_mlp_forward", _d.dtype_code(x, "x"), ptr(x), *_weights(weights), ptr(out),
+         x.shape[0], ptr(m_dev), stream())
+
+
+def mlp_backward(x, weights, dh, dx, partial, grads, m_dev=None, accumulate=False):
+    """dh [cap, 4] (x's dtype) -> dx [cap, 32] (rows past m_dev[0] zero) and the
+    six f32 weight gradients (overwritten, or added into with accumulate);
+    partial: backward_parts(cap) * params_count() f32 scratch."""
+    cap = x.shape[0]
+    for t, n in ((x, "x"), (dh, "dh"), (dx, "dx")):
+        checked(t, n)
+        if t.dtype != x.dtype:
+            raise RuntimeError(f"{n} must have x's dtype")
+    if tuple(dh.shape) != (cap, OUT) or tuple(dx.shape) != (cap, IN):
+        raise RuntimeError("dh must be [M, 4] and dx [M, 32]")
+    _f32(partial, "partial")
+    if m_dev is not None:
+        checked(m_dev, "m_dev", "int")
+    gp = _weights(grads)
+    call("dfhip_mlp_backward", _d.dtype_code(x, "x"), ptr(x), *_weights(weights), ptr(dh), cap,
+         ptr(m_dev), ptr(dx), ptr(partial), backward_parts(cap) if cap else 1, *gp,
+         int(bool(accumulate)), stream())
+
+
 # ---- fused grid field (encoding + MLP in one kernel; device-side sample count)
 
 def grid_quads(embeddings, offsets, S, H, gridtype, align_corners, table, quads):

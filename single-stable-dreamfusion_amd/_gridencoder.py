@@ -28,9 +28,31 @@ def grid_encode_forward(inputs, embeddings, offsets, outputs, B, D, C, L, S, H, 
 
 def grid_encode_backward(grad, inputs, embeddings, offsets, grad_embeddings, B, D, C, L, S, H,
                          dy_dx, grad_inputs, gridtype, align_corners):
+    """gridencoder.cu:449-479: ADDS d(outputs)/d(embeddings) . grad into
+    grad_embeddings (the caller zero-fills it, grid.py:72), grad [L, B, C].
+    Without an input gradient (dy_dx None, the NeRF path) the sum comes from
+    the binned owner-computes walk (exact f64 sums rounded to f32 once, then
+    added into grad_embeddings in its dtype: f16 under autocast, where the
+    reference rounds every atomic add to half); with dy_dx, or a shape the
+    walk does not take, from the reference's atomic scatter."""
+    import torch
+    from gridencoder.grid import binned_eligible, binned_embedding_grad, host_offsets
     dt = _common(inputs, embeddings, offsets)
     checked(grad, "grad")
     checked(grad_embeddings, "grad_embeddings")
+    if (dy_dx is None and grad_inputs is None and binned_eligible(D, C, grad.dtype)
+            and grad.dtype == embeddings.dtype and grad_embeddings.dtype in (torch.float16,
+                                                                            torch.float32)):
+        if B == 0:
+            return
+        offs_h = host_offsets(offsets)
+        f32 = grad_embeddings.dtype == torch.float32
+        out = binned_embedding_grad(grad, inputs, 0.0, offsets, offs_h, B, None, C, L, S, H,
+                                    gridtype, align_corners,
+                                    out=grad_embeddings if f32 else None, accumulate=f32)
+        if not f32:
+            grad_embeddings.add_(out.to(grad_embeddings.dtype))
+        return
     call("dfhip_grid_encode_backward", dt, ptr(grad), ptr(inputs), ptr(embeddings), ptr(offsets),
          ptr(grad_embeddings), B, D, C, L, S, H, ptr(dy_dx), ptr(grad_inputs), gridtype,
          int(bool(align_corners)), stream())
@@ -42,6 +64,19 @@ def grid_encode_forward_blc(inputs, embeddings, offsets, outputs, B, D, C, L, S,
     checked(outputs, "outputs")
     call("dfhip_grid_encode_forward_blc", dt, ptr(inputs), ptr(embeddings), ptr(offsets),
          ptr(outputs), B, D, C, L, S, H, ptr(dy_dx), gridtype, int(bool(align_corners)), stream())
+
+
+def grid_encode_forward_dyn(inputs, bound, embeddings, offsets, outputs, B, m_dev, D, C, L, S, H,
+                            dy_dx, gridtype, align_corners):
+    """grid_encode_forward_blc over a capacity-sized batch: rows [0, m_dev[0])
+    encoded, the rest zero; raw inputs in [-bound, bound] when bound > 0."""
+    dt = _common(inputs, embeddings, offsets)
+    checked(outputs, "outputs")
+    if m_dev is not None:
+        checked(m_dev, "m_dev", "int")
+    call("dfhip_grid_encode_forward_dyn", dt, ptr(inputs), float(bound), ptr(embeddings),
+         ptr(offsets), ptr(outputs), B, ptr(m_dev), D, C, L, S, H, ptr(dy_dx), gridtype,
+         int(bool(align_corners)), stream())
 
 
 def grid_encode_backward_blc(grad, inputs, offsets, grad_embeddings, B, D, C, L, S, H, dy_dx,
@@ -130,19 +165,15 @@ def grid_backward_binned_tile(opts=None, group=1):
     return int(_d.load().dfhip_grid_backward_binned_tile(int(group), _opts_ref(opts)))
 
 
-def grid_backward_binned_scratch(cap, offsets_host, L, C, opts=None, group=1, S=0.0, H=1,
-                                 gridtype=1, align_corners=False):
+def grid_backward_binned_scratch(cap, offsets_host, L, C, opts=None, group=1):
     """(entries u32, counts u32, partial f32) element counts for capacity cap
     (samples, or stencil groups with group=7; opts: the BinnedOpts the
-    launches will use; S, H, gridtype, align_corners: the launches' layout,
-    which sizes the resolved stream's pool)."""
-    import ctypes
+    launches will use).  Host only."""
     import numpy as np
     off = np.ascontiguousarray(offsets_host, dtype=np.int32)
     e, c, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
     call("dfhip_grid_backward_binned_scratch_opts", int(cap), off.ctypes.data, int(L), int(C),
-         float(S), int(H), int(gridtype), int(bool(align_corners)), int(group), _opts_ref(opts),
-         ctypes.byref(e), ctypes.byref(c), ctypes.byref(p))
+         int(group), _opts_ref(opts), ctypes.byref(e), ctypes.byref(c), ctypes.byref(p))
     return int(e.value), int(c.value), int(p.value)
 
 

@@ -80,5 +80,9 @@ uint32_t resident_blocks(const void *kernel, int threads, int fallback_per_cu) {
 
 }  // namespace dfhip
 
-extern "C" int dfhip_abi_version(void) { return 1; }
+// A hash of include/dfhip.h, passed by the build (dfhip_build.abi_hash).
+#ifndef DFHIP_ABI_HASH
+#error "build with -DDFHIP_ABI_HASH=<hash of include/dfhip.h> (dfhip_build.py)"
+#endif
+extern "C" int dfhip_abi_version(void) { return DFHIP_ABI_HASH; }
 extern "C" const char *dfhip_last_error(void) { return dfhip::g_last_error; }

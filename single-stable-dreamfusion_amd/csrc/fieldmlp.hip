@@ -139,6 +139,41 @@ __global__ __launch_bounds__(256) void k_field_fwd(const half_t *__restrict__ en
     }
 }
 
+// The MLP alone (network_grid.py:13-32: the reference's sigma_net module, no
+// heads): h [cap, 4] in E, output h of sample c on lane group h as autocast's
+// f16 (bf16) linear output.  Rows [M, cap) of a capacity-sized batch (M =
+// *m_dev) are written as zeros, so whatever reads the whole batch stays finite.
+template <typename E>
+__global__ __launch_bounds__(256) void k_mlp_fwd(const E *__restrict__ x, const float *w1,
+                                                 const float *b1, const float *w2,
+                                                 const float *b2, const float *w3,
+                                                 const float *b3, E *__restrict__ out,
+                                                 uint32_t cap, const int32_t *__restrict__ m_dev) {
+    typedef typename Elem<E>::v8 v8;
+    __shared__ WeightsG<E> W;
+    load_weights<false>(W, nullptr, w1, b1, w2, b2, w3, b3);
+    __syncthreads();
+    const uint32_t M = active_count(m_dev, cap);
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t tiles = ceil_div(M, 16u);
+    const uint32_t tile0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    v8 xb = tile0 < tiles ? load_x(x, tile0 * 16 + c, M, h) : v8{};
+    for (uint32_t tile = tile0; tile < tiles; tile += waves) {
+        const uint32_t sample = tile * 16 + c;
+        const v8 xn = tile + waves < tiles ? load_x(x, (tile + waves) * 16 + c, M, h) : v8{};
+        FwdG<E> F;
+        forward_tile(W, xb, c, h, F);
+        xb = xn;
+        if (sample < M) out[(size_t)sample * kOut + h] = (E)F.o[0];
+    }
+    // the rows past the live count: zeros (8 bytes per row)
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    for (size_t r = (size_t)M + (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < cap;
+         r += (size_t)gridDim.x * blockDim.x)
+        *reinterpret_cast<u2 *>(out + r * kOut) = u2{0u, 0u};
+}
+
 // ------------------------------------------------------------------ backward
 // Workgroup = 4 waves, two workgroups per CU (76 KB of LDS each), persistent
 // over rounds.  Per round each wave takes one 16-sample tile: recomputes the
@@ -231,12 +266,20 @@ struct TileIn {
     rgb_t grgb;
 };
 
-template <typename E, typename rgb_t>
+// MLP_ONLY (the plain MLP, k_mlp_fwd's backward): grad_rgb is dh [M, 4] and
+// lane group h takes output h's gradient.
+template <typename E, typename rgb_t, bool MLP_ONLY = false>
 __device__ __forceinline__ void load_tile(TileIn<E, rgb_t> &g, uint32_t tile, const E *enc,
                                           const float *xyz, const float *grad_sigma,
                                           const rgb_t *grad_rgb, uint32_t M, int c, int h) {
     const uint32_t sample = tile * 16 + c;
     g.xb = load_x(enc, sample, M, h);
+    if constexpr (MLP_ONLY) {
+        g.gs = 0.0f;
+        g.xyz[0] = g.xyz[1] = g.xyz[2] = 0.0f;
+        g.grgb = sample < M ? grad_rgb[(size_t)sample * kOut + h] : (rgb_t)0.0f;
+        return;
+    }
     const bool v = (h == 0) && sample < M;
 #pragma unroll
     for (int d = 0; d < 3; ++d) g.xyz[d] = v ? xyz[(size_t)sample * 3 + d] : 0.0f;
@@ -246,8 +289,10 @@ __device__ __forceinline__ void load_tile(TileIn<E, rgb_t> &g, uint32_t tile, co
 
 // PERM: enc holds the fused forward's permuted feature order (k_field_fwd_fused);
 // otherwise the natural [M, 32] encoder output.  M = *m_dev (clamped to cap)
-// when m_dev is given; d_enc is [16, cap, 2].
-template <typename E, typename rgb_t, bool PERM>
+// when m_dev is given; d_enc is [16, cap, 2].  MLP_ONLY: the plain MLP's
+// backward (k_mlp_fwd): grad_rgb is dh [cap, 4] in E, no heads, and d_enc is
+// the natural [cap, 32] feature gradient (rows [M, cap) written as zeros).
+template <typename E, typename rgb_t, bool PERM, bool MLP_ONLY = false>
 __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
     const E *__restrict__ enc, const float *__restrict__ xyz, const float *w1,
     const float *b1, const float *w2, const float *b2, const float *w3, const float *b3,
@@ -305,7 +350,9 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
         // dL/d(output h), in E as autocast's backward produces it: lane group h
         // holds output h (F.o[0]) and its incoming gradient
         E dOh = (E)0.0f;
-        if (valid) {
+        if (MLP_ONLY) {
+            dOh = valid ? (E)cur.grgb : (E)0.0f;
+        } else if (valid) {
             if (h == 0) {
                 const float y = (float)(E)F.o[0] + gaussian(cur.xyz);
                 // trunc_exp backward (activation.py:14-18): g * exp(clamp(y, -15, 15))
@@ -370,7 +417,11 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
             for (int s2 = 0; s2 < 2; ++s2)
                 d = mfma((kBwdWreg & 2) ? w1top[f][s2] : a_perm(T.w1t, kLd64, 16 * f + c, s2, h),
                          b_from_tiles(dz1, s2), d);
-            if (valid) {
+            if (MLP_ONLY && valid) {
+                // natural [cap, 32]: features 16f + 4h .. 16f + 4h + 3 of the sample
+                *reinterpret_cast<v4 *>(d_enc + (size_t)sample * kIn + 16 * f + 4 * h) =
+                    v4{(E)d[0], (E)d[1], (E)d[2], (E)d[3]};
+            } else if (valid) {
                 // features 16f + 4h + r = level 8f + 2h + (r >> 1), channel r & 1
                 const uint32_t lv = 8 * f + 2 * h;
                 typedef E e2v __attribute__((ext_vector_type(2)));
@@ -457,14 +508,21 @@ __global__ __launch_bounds__(64 * kBwdWaves, 2) void k_field_bwd(
     }
 #else
     TileIn<E, rgb_t> cur;
-    load_tile<E, rgb_t>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+    load_tile<E, rgb_t, MLP_ONLY>(cur, tile, enc, xyz, grad_sigma, grad_rgb, M, c, h);
     for (uint32_t round = 0; round < rounds; ++round, tile += per_round) {
         TileIn<E, rgb_t> nxt;  // the next round's inputs, loaded while this one runs
-        load_tile<E, rgb_t>(nxt, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c, h);
+        load_tile<E, rgb_t, MLP_ONLY>(nxt, tile + per_round, enc, xyz, grad_sigma, grad_rgb, M, c,
+                                      h);
         round_of(cur, tile);
         cur = nxt;
     }
 #endif
+    if constexpr (MLP_ONLY) {
+        // feature-gradient rows past the live count: zeros (64 bytes per row)
+        for (size_t i = (size_t)M * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+             i < (size_t)cap * 4; i += (size_t)gridDim.x * blockDim.x)
+            reinterpret_cast<u32x4 *>(d_enc)[i] = u32x4{0u, 0u, 0u, 0u};
+    }
 
     // ---- this workgroup's partial: every entry written by exactly one lane.
     // Accumulator element r of lane (c, h): row 4h + r, column c of the tile.
@@ -633,6 +691,81 @@ extern "C" int dfhip_field_mlp_backward(const void *enc, const float *xyz, const
             set_error("%s: grad_rgb dtype must be f32 or f16", name);
             return DFHIP_EDTYPE;
         }
+    } else {
+        parts = 1;
+        (void)hipMemsetAsync(partial, 0, kParams * sizeof(float), s);
+    }
+    k_field_wgrad_sum<<<ceil_div((uint32_t)kParams, 64u), 1024, 0, s>>>(
+        partial, parts, gw1, gb1, gw2, gb2, gw3, gb3, accumulate);
+    return check_launch(name);
+}
+
+template <typename E>
+static int mlp_launch(const char *name, const void *x, const float *w1, const float *b1,
+                      const float *w2, const float *b2, const float *w3, const float *b3, void *h,
+                      uint32_t cap, const int32_t *m_dev, hipStream_t s) {
+    const uint32_t tiles = ceil_div(cap, 16u);
+    const uint32_t blocks = ceil_div(tiles, 4u) < 2048u ? ceil_div(tiles, 4u) : 2048u;
+    k_mlp_fwd<E><<<blocks, 256, 0, s>>>((const E *)x, w1, b1, w2, b2, w3, b3, (E *)h, cap, m_dev);
+    return check_launch(name);
+}
+
+extern "C" int dfhip_mlp_forward(int elem, const void *x, const float *w1, const float *b1,
+                                 const float *w2, const float *b2, const float *w3,
+                                 const float *b3, void *h, uint32_t cap, const int32_t *m_dev,
+                                 dfhip_stream_t stream) {
+    const char *name = "mlp_forward";
+    if (cap == 0) return DFHIP_OK;
+    if (!x || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !h) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    if (elem == DFHIP_F16)
+        return mlp_launch<half_t>(name, x, w1, b1, w2, b2, w3, b3, h, cap, m_dev,
+                                  as_stream(stream));
+    if (elem == DFHIP_BF16)
+        return mlp_launch<bf16_t>(name, x, w1, b1, w2, b2, w3, b3, h, cap, m_dev,
+                                  as_stream(stream));
+    set_error("%s: elem must be f16 or bf16", name);
+    return DFHIP_EDTYPE;
+}
+
+extern "C" int dfhip_mlp_backward(int elem, const void *x, const float *w1, const float *b1,
+                                  const float *w2, const float *b2, const float *w3,
+                                  const float *b3, const void *dh, uint32_t cap,
+                                  const int32_t *m_dev, void *dx, float *partial, uint32_t parts,
+                                  float *gw1, float *gb1, float *gw2, float *gb2, float *gw3,
+                                  float *gb3, int accumulate, dfhip_stream_t stream) {
+    const char *name = "mlp_backward";
+    if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !gw1 || !gb1 || !gw2 || !gb2 || !gw3 || !gb3 ||
+        !partial) {
+        set_error("%s: null pointer", name);
+        return DFHIP_EINVAL;
+    }
+    if (elem != DFHIP_F16 && elem != DFHIP_BF16) {
+        set_error("%s: elem must be f16 or bf16", name);
+        return DFHIP_EDTYPE;
+    }
+    hipStream_t s = as_stream(stream);
+    if (cap > 0) {
+        if (!x || !dh || !dx) {
+            set_error("%s: null pointer", name);
+            return DFHIP_EINVAL;
+        }
+        if (parts != bwd_parts(cap)) {
+            set_error("%s: parts must be dfhip_field_mlp_backward_parts(cap) = %u (got %u)", name,
+                      bwd_parts(cap), parts);
+            return DFHIP_EINVAL;
+        }
+        const uint32_t nblk = bwd_blocks(cap);
+        if (elem == DFHIP_F16)
+            k_field_bwd<half_t, half_t, false, true><<<nblk, 256, 0, s>>>(
+                (const half_t *)x, nullptr, w1, b1, w2, b2, w3, b3, nullptr, (const half_t *)dh,
+                cap, m_dev, (half_t *)dx, partial);
+        else
+            k_field_bwd<bf16_t, bf16_t, false, true><<<nblk, 256, 0, s>>>(
+                (const bf16_t *)x, nullptr, w1, b1, w2, b2, w3, b3, nullptr, (const bf16_t *)dh,
+                cap, m_dev, (bf16_t *)dx, partial);
     } else {
         parts = 1;
         (void)hipMemsetAsync(partial, 0, kParams * sizeof(float), s);

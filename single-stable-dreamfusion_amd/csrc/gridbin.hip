@@ -48,18 +48,6 @@ using ge::SliceDyn;
 typedef unsigned long long u64;
 
 constexpr uint32_t kTile = 1024;              // samples per binning tile (ids per segment)
-// Samples per binning tile for single samples (the albedo step; stencil
-// groups keep kTile: their entries carry a 6-bit point mask above 10 id
-// bits).  Longer tiles make longer (tile, slice) segments: the per-segment
-// walk pays one dependent count -> ids -> data round trip per segment, and at
-// the fine levels a 1,024-sample tile leaves ~40 entries per segment, less
-// than one per lane.
-#ifndef DFHIP_TILE1
-#define DFHIP_TILE1 1024
-#endif
-constexpr uint32_t kTile1 = DFHIP_TILE1;
-static_assert(kTile1 >= kTile && kTile1 <= 65536 && (kTile1 & (kTile1 - 1)) == 0,
-              "DFHIP_TILE1: a power of two in [1024, 65536] (u16 tile-relative ids)");
 constexpr uint32_t kMaxBins = 4096;
 constexpr uint32_t kMaxSlices = 128;          // slices per level (k_bin's 128-bit masks)
 constexpr uint32_t kSliceBytes = 128 * 1024;  // f64 accumulators of one walk workgroup
@@ -90,7 +78,7 @@ struct BinInfo {
     uint32_t tile;                       // samples per tile = id slots per segment
     uint32_t G;                          // walk workgroups
     uint32_t lane_perm;                  // walk: bit-reversed lane -> run map (1) or identity
-    uint32_t o_roff, o_totals, o_plan;   // word offsets into `counts` (layout below)
+    uint32_t o_totals, o_plan;           // word offsets into `counts` (layout below)
     uint32_t bin0[ge::kMaxLevels + 1];   // first bin of level l (bin0[L] = nbins)
     uint32_t base[ge::kMaxLevels];       // first row of level l
     uint32_t rows[ge::kMaxLevels];       // rows of level l
@@ -125,8 +113,8 @@ static bool resolve_opts(const dfhip_binned_opts *o, Opts &r) {
     r.lane_perm = 1;
     r.trace = nullptr;
     if (!o) return true;
-    if (o->walk_mode < -1 || o->walk_mode > 3) {
-        set_error("binned backward: walk_mode must be -1, 0, 1, 2 or 3 (got %d)",
+    if (o->walk_mode < -1 || o->walk_mode > 1) {
+        set_error("binned backward: walk_mode must be -1, 0 or 1 (got %d)",
                   (int)o->walk_mode);
         return false;
     }
@@ -151,8 +139,6 @@ static uint32_t slice_shift(uint32_t C) {
 
 // scratch layout (u32 words of `counts`):
 //   [tcap][nbins]  per-(tile, bin) counts          (k_bin)
-//   [tcap][nbins]  per-(tile, bin) segment offsets in the tile's pool region
-//                  (k_rbin, the resolved stream only)
 //   [nbins][16]    totals, as 16 partial sums      (k_bin; zeroed before it)
 //   [nbins][2]     first image slot, parts         (k_walk; zeroed before k_bin)
 // Host: bins and layout from the HOST copy of the offsets.
@@ -163,9 +149,7 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     bi.L = L;
     bi.trace = op.trace;
     bi.shift = slice_shift(C);
-    // single samples bin into kTile1-sample tiles (not the resolved stream,
-    // whose k_rbin runs one thread per sample of a kTile tile)
-    bi.tile = (group == 1 && flat_walk_mode(1, op) != 3) ? kTile1 : kTile;
+    bi.tile = kTile;
     bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, bi.tile);
     bi.G = op.walk_g * device_cus();
     bi.lane_perm = op.lane_perm;
@@ -187,9 +171,8 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     // so the per-call clear is ONE aligned fill (an unaligned one took two
     // fill launches)
     const uint64_t tot = ((uint64_t)nb * bi.tcap + 3ull) & ~3ull;
-    if (2ull * tot + (kTotSplit + 2ull) * nb + 4ull >= (1ull << 32)) return false;
-    bi.o_roff = (uint32_t)tot;
-    bi.o_totals = (uint32_t)(2ull * tot);
+    if (tot + (kTotSplit + 2ull) * nb + 4ull >= (1ull << 32)) return false;
+    bi.o_totals = (uint32_t)tot;
     bi.o_plan = bi.o_totals + nb * kTotSplit;
     return true;
 }
@@ -676,22 +659,9 @@ static bool make_fast_levels(const int32_t *offsets_host, const Levels &lv, cons
 }
 
 // ---------------------------------------------------------------- 2. walk
-// Timing probes of the slice-image adds (variant libraries only; results are
-// wrong): 1 = the same number of ds_add_f64 on bank-distinct rows (lane-indexed
-// inside the row's 512-row block), 2 = no LDS adds (the value kept alive by a
-// never-taken store).
-#ifndef DFHIP_PROBE_ADDS
-#define DFHIP_PROBE_ADDS 0
-#endif
 __device__ __forceinline__ void lds_add(double *acc, uint32_t idx, double v, uint32_t k) {
-    if constexpr (DFHIP_PROBE_ADDS == 1) {
-        atomicAdd(acc + ((idx & ~511u) | ((threadIdx.x & 63u) + 64u * (k & 7u))), v);
-    } else if constexpr (DFHIP_PROBE_ADDS == 2) {
-        if (__builtin_expect(v == 1.0e300, 0)) acc[idx] = v;
-    } else {
-        (void)k;
-        atomicAdd(acc + idx, v);
-    }
+    (void)k;
+    atomicAdd(acc + idx, v);
 }
 
 // Flush one cell's merged corner contributions into the LDS slice [r0, r1).
@@ -1369,47 +1339,18 @@ __device__ __forceinline__ void walk_entry(FlatCell<C> &cell, const EntryIn<grad
     }
 }
 
-// A lane's entries [ea, eb) of one piece of a tile segment (entries at seg),
-// RB loads in flight per batch (clamped slots: every load is issued before
-// the first use).
-template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RB,
-          bool SAT>
-__device__ __forceinline__ void flat_piece(FlatCell<C> &cell, const grad_t *__restrict__ gl,
-                                           const float *__restrict__ inputs,
-                                           const uint16_t *__restrict__ seg, uint32_t tbase,
-                                           uint32_t ea, uint32_t eb, double *acc, uint32_t srows,
-                                           uint32_t lo, uint32_t n, float sc, float half,
-                                           uint32_t m1, uint32_t m2, uint32_t wm,
-                                           const SliceDyn &dyn, float inv, const Stencil &st) {
-    for (uint32_t x = ea; x < eb; x += RB) {
-        const uint32_t m = min(eb - x, RB);
-        uint32_t v[RB];
-#pragma unroll
-        for (uint32_t i = 0; i < RB; ++i) v[i] = seg[x + min(i, m - 1)];
-        EntryIn<grad_t, C, GROUP, SAT> in[RB];
-#pragma unroll
-        for (uint32_t i = 0; i < RB; ++i) load_entry(in[i], gl, inputs, tbase, v[i]);
-#pragma unroll
-        for (uint32_t i = 0; i < RB; ++i)
-            if (i < m)
-                walk_entry<grad_t, C, POW2, GROUP, LEAD, SAT>(cell, in[i], gl, tbase, v[i], acc,
-                                                              srows, lo, n, sc, half, m1, m2, wm,
-                                                              dyn, inv, st);
-    }
-}
-
 // One phase of a part's walk over a chunk of nc tiles (part + (cb + i) P):
 // the centre entries (front of each segment; every entry for GROUP 1) or the
 // satellite entries (back of each segment, stencil groups only).
 template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RUN,
-          uint32_t WMODE, bool SAT>
+          bool SAT>
 __device__ __forceinline__ void flat_walk_chunk(
     FlatCell<C> &cell, const grad_t *__restrict__ gl, const float *__restrict__ inputs,
     const uint32_t *counts, const uint16_t *__restrict__ entries, double *acc, uint32_t *pre,
     uint32_t *wsum, uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t cb,
     uint32_t nc, uint32_t srows, uint32_t lo, uint32_t n, float sc, float half, uint32_t m1,
     uint32_t m2, uint32_t wm, const SliceDyn &dyn, float inv, const Stencil &st,
-    uint32_t *entries_seen, uint32_t tile1) {
+    uint32_t *entries_seen) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t waves = blockDim.x >> 6, nthr = blockDim.x;
     // the chunk's segments end to end: exclusive scan of the counts
@@ -1435,53 +1376,13 @@ __device__ __forceinline__ void flat_walk_chunk(
     const uint32_t E = pre[nc];
     if (tid == 0) *entries_seen += E;  // the debug trace's entry count
     // entries of chunk tile ti: front slots [0, cnt) or back slots [kTile - cnt, kTile)
-    const uint32_t T = GROUP == 1 ? tile1 : kTile;
+    constexpr uint32_t T = kTile;
     auto seg_of = [&](uint32_t ti) {
         const uint32_t t = part + (cb + ti) * P;
         const uint16_t *sg = entries + ((size_t)t * nb + b) * T;
         return SAT ? sg + (T - (pre[ti + 1] - pre[ti])) : sg;
     };
-    if constexpr (WMODE == 2) {
-        // per-wave pieces: wave w takes entries [E w / waves, E (w+1) / waves)
-        // and walks them segment piece by segment piece, the 64 lanes of the
-        // wave on one piece at a time (runs of ceil(piece / 64), bit-reversed),
-        // as k_walk does per whole segment
-        const uint32_t w0 = (uint32_t)((uint64_t)E * wave / waves);
-        const uint32_t w1 = (uint32_t)((uint64_t)E * (wave + 1) / waves);
-        if (w0 < w1) {
-            uint32_t a = 0, z = nc;  // pre[a] <= w0 < pre[z]
-            while (z - a > 1) {
-                const uint32_t mid = (a + z) >> 1;
-                if (pre[mid] <= w0) a = mid;
-                else z = mid;
-            }
-            const uint32_t rl = __builtin_bitreverse32(lane) >> 26;
-            uint32_t ti = a, e = w0;
-            while (e < w1) {
-                const uint32_t pe = min(pre[ti + 1], w1);
-                const uint32_t cnt = pe - e;
-                const uint32_t t = part + (cb + ti) * P;
-                const uint16_t *seg = seg_of(ti) + (e - pre[ti]);
-                const uint32_t Qp = (cnt + 63u) >> 6;
-                const uint32_t ea = min(rl * Qp, cnt), eb = min(ea + Qp, cnt);
-                if (GROUP > 1 || Qp <= 1)
-                    flat_piece<grad_t, C, POW2, GROUP, LEAD, 1, SAT>(
-                        cell, gl, inputs, seg, t * T, ea, eb, acc, srows, lo, n, sc,
-                        half, m1, m2, wm, dyn, inv, st);
-                else if (Qp <= 4)
-                    flat_piece<grad_t, C, POW2, GROUP, LEAD, 4, SAT>(
-                        cell, gl, inputs, seg, t * T, ea, eb, acc, srows, lo, n, sc,
-                        half, m1, m2, wm, dyn, inv, st);
-                else
-                    flat_piece<grad_t, C, POW2, GROUP, LEAD, 8, SAT>(
-                        cell, gl, inputs, seg, t * T, ea, eb, acc, srows, lo, n, sc,
-                        half, m1, m2, wm, dyn, inv, st);
-                e = pe;
-                ++ti;
-                while (e < w1 && pre[ti + 1] == e) ++ti;  // empty segments
-            }
-        }
-    } else {
+    {
         const uint32_t Q = ceil_div(E, nthr);
         // wave w takes the w-th 1/waves of the chunk, so its lanes stay on
         // neighbouring samples (one or two tile segments: positions and
@@ -1558,31 +1459,31 @@ __device__ __forceinline__ void flat_walk_chunk(
 }
 
 template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t LEAD, uint32_t RUN,
-          uint32_t RUN_SAT, uint32_t WMODE>
+          uint32_t RUN_SAT>
 __device__ __forceinline__ void flat_walk_level(
     const grad_t *__restrict__ gl, const float *__restrict__ inputs, const uint32_t *counts,
     const uint16_t *__restrict__ entries, double *acc, uint32_t *pre, uint32_t *wsum,
     uint32_t nb, uint32_t b, uint32_t part, uint32_t P, uint32_t ntiles, uint32_t srows,
     uint32_t lo, uint32_t n, float sc, float half, uint32_t m1, uint32_t m2, uint32_t wm,
-    const SliceDyn &dyn, float inv, const Stencil &st, uint32_t *entries_seen, uint32_t tile1) {
+    const SliceDyn &dyn, float inv, const Stencil &st, uint32_t *entries_seen) {
     const uint32_t nt = ntiles > part ? ceil_div(ntiles - part, P) : 0u;
     FlatCell<C> cell;
     cell.have = false;
     cell.i0 = 0;
     for (uint32_t cb = 0; cb < nt; cb += kChunkTiles) {
         const uint32_t nc = min(nt - cb, kChunkTiles);
-        flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN, WMODE, false>(
+        flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN, false>(
             cell, gl, inputs, counts, entries, acc, pre, wsum, nb, b, part, P, cb, nc, srows, lo,
-            n, sc, half, m1, m2, wm, dyn, inv, st, entries_seen, tile1);
+            n, sc, half, m1, m2, wm, dyn, inv, st, entries_seen);
         if constexpr (GROUP > 1)
-            flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN_SAT, WMODE, true>(
+            flat_walk_chunk<grad_t, C, POW2, GROUP, LEAD, RUN_SAT, true>(
                 cell, gl, inputs, counts, entries, acc, pre, wsum, nb, b, part, P, cb, nc, srows,
-                lo, n, sc, half, m1, m2, wm, dyn, inv, st, entries_seen, tile1);
+                lo, n, sc, half, m1, m2, wm, dyn, inv, st, entries_seen);
     }
     flat_flush<C, LEAD>(cell, acc, srows, lo, n, m1, m2, wm);
 }
 
-template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP, uint32_t WMODE>
+template <typename grad_t, uint32_t C, bool POW2, uint32_t GROUP>
 __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ grad,  // [L, GROUP B, C]
                                                     const float *__restrict__ inputs,
                                                     FastLevels fl, BinInfo bi, int align_corners,
@@ -1610,7 +1511,7 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     const uint32_t n = min(srows, bi.rows[l] - lo);
     const uint64_t tr1 = bi.trace ? wall_clock64() : 0;
     const uint32_t M = ge::dyn_count(dyn, B);
-    const uint32_t ntiles = ceil_div(M, GROUP == 1 ? bi.tile : kTile);
+    const uint32_t ntiles = ceil_div(M, kTile);
     const grad_t *gl = grad + (size_t)l * GROUP * B * C;
     const float sc = fl.scale[l], half = align_corners ? 0.0f : 0.5f;
     const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
@@ -1619,10 +1520,10 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     constexpr uint32_t RUN = GROUP > 1 ? (uint32_t)DFHIP_WALK_RUN7 : (uint32_t)DFHIP_WALK_RUN;
     constexpr uint32_t RUN_SAT = DFHIP_WALK_RUN_SAT;
 #define DFHIP_FLAT(LD)                                                                         \
-    flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN, RUN_SAT, WMODE>(gl, inputs, counts, entries, acc, pre, \
-                                                     wsum, nb, b, part, P, ntiles, srows, lo, \
-                                                     n, sc, half, m1, m2, wm, dyn, inv, st, \
-                                                     &sh_entries, bi.tile)
+    flat_walk_level<grad_t, C, POW2, GROUP, LD, RUN, RUN_SAT>(gl, inputs, counts, entries, acc,  \
+                                                            pre, wsum, nb, b, part, P, ntiles,   \
+                                                            srows, lo, n, sc, half, m1, m2, wm,  \
+                                                            dyn, inv, st, &sh_entries)
     if (lead >= 3) DFHIP_FLAT(3);
     else if (lead == 2) DFHIP_FLAT(2);
     else DFHIP_FLAT(1);
@@ -1641,376 +1542,6 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
         r[5] = tr1;
         r[6] = part;
         r[7] = wall_clock64();
-    }
-}
-
-// ---------------------------------------------------------------- 4. resolved stream
-// Single samples (the albedo step) with f16 / bf16 gradients on a mask-form
-// layout: the binning resolves every (sample, level, slice) entry once, so
-// the walk streams its bin instead of gathering.
-//
-//   k_rbin (one workgroup per tile of kTile samples, one thread per sample):
-//     pass A: each level's cell, fractions and slice mask (kept in registers);
-//       per (level, slice) a wave ballot counts the wave's entries (no LDS
-//       atomics: the one-slice coarse levels put every lane of a wave on one
-//       counter); a workgroup scan gives every (wave, bin) its base inside
-//       the tile's segment and every bin its segment offset in the tile's
-//       region of the pool;
-//     pass B: per level the sample's gradient row (coalesced: [L, B, 2]) and,
-//       per slice, its 16-byte entry at base + ballot rank.
-//   An entry is {g (2 x 16 bit), fx | i0 lo << 24, fy | i0 hi << 24, fz}: the
-//   level-relative tiled index of the cell (masked by the level's wrap, < 2^16
-//   rows) and the three fractions as exact 24-bit fixed point (p = x * scale
-//   + 0.5 >= 0.5, so frac = p - floor(p) is a multiple of ulp(p) >= 2^-24).
-//   Entries of a segment are in sample order (wave-major, then lane order),
-//   i.e. in ray order: a lane's run of consecutive entries follows a ray.
-//   k_rwalk: the flat walk's plan and part layout over the pool's segments;
-//     per entry one 16-byte load of the lane's own run (prefetched one batch
-//     ahead), no id -> position / gradient gathers and no cell location.
-constexpr uint32_t kRMaxBins = 256;    // bins of a resolved layout (k_rbin LDS: 16 x 256 counts)
-constexpr uint32_t kRMaxSlices = 32;   // slices per level (u32 slice masks)
-constexpr uint32_t kRWaves = kTile / 64;
-constexpr uint32_t kRBatch = 4;        // entries per lane per walk batch
-
-__device__ __forceinline__ uint32_t frac24(float f) {
-    return (uint32_t)(f * 16777216.0f);  // exact: f is a multiple of 2^-24 in [0, 1)
-}
-
-template <bool POW2>
-__global__ __launch_bounds__(1024) void k_rbin(const float *__restrict__ inputs,
-                                              const uint32_t *__restrict__ grad,  // [L, B] rows
-                                              FastLevels fl, BinInfo bi, SliceDyn dyn, float inv,
-                                              uint32_t B, uint32_t tile_entries,
-                                              uint32_t *__restrict__ counts,
-                                              uint4 *__restrict__ pool) {
-    __shared__ uint32_t cw[kRWaves][kRMaxBins];  // the wave's count, then its base
-    __shared__ uint32_t toff[kRMaxBins];
-    __shared__ uint32_t wtot[kRWaves];
-    const uint32_t M = ge::dyn_count(dyn, B);
-    const uint32_t ntiles = ceil_div(M, kTile);
-    const uint32_t nb = bi.nbins, L = bi.L, shift = bi.shift, smask = (1u << bi.shift) - 1u;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint32_t s = tile * kTile + threadIdx.x;
-        float x[3] = {0.0f, 0.0f, 0.0f};
-        const bool in = s < M && load_pos<3, POW2>(inputs, dyn, inv, s, x);
-        uint32_t mk[kFastLevels], px[kFastLevels], py[kFastLevels], pz[kFastLevels];
-#pragma unroll
-        for (uint32_t l = 0; l < kFastLevels; ++l) {
-            mk[l] = px[l] = py[l] = pz[l] = 0;
-            if (l >= L) continue;  // uniform
-            const float sc = fl.scale[l];
-            const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
-            uint32_t c[3], fq[3];
-#pragma unroll
-            for (uint32_t d = 0; d < 3; ++d) {
-                const float p = fmaf(x[d], sc, 0.5f);
-                const float fl0 = floorf(p);
-                c[d] = (uint32_t)fl0;
-                fq[d] = frac24(p - fl0);
-            }
-            const uint32_t i0 = c[0] + c[1] * m1 + c[2] * m2;
-            uint32_t mask = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {  // x-neighbour pairs, as k_bin_fast
-                if (q >= (1u << (lead - 1u))) break;  // uniform
-                const uint32_t o = ((q & 1u) ? m1 : 0u) + ((q & 2u) ? m2 : 0u);
-                const uint32_t r = (i0 + o) & wm;
-                mask |= 1u << (r >> shift);
-                if ((r & smask) == smask) mask |= 1u << (((r + 1u) & wm) >> shift);
-            }
-            const uint32_t im = i0 & wm;
-            mk[l] = in ? mask : 0u;
-            px[l] = fq[0] | (im << 24);
-            py[l] = fq[1] | ((im >> 8) << 24);
-            pz[l] = fq[2];
-            const uint32_t b0 = fl.bin0[l], ns = bi.bin0[l + 1] - b0;
-            for (uint32_t k = 0; k < ns; ++k) {  // uniform
-                const u64 bal = __ballot((mk[l] >> k) & 1u);
-                if (lane == 0) cw[wave][b0 + k] = (uint32_t)__popcll(bal);
-            }
-        }
-        __syncthreads();
-        // per bin: the waves' bases inside the segment and the tile's count;
-        // then the segments' offsets in the tile region (exclusive scan)
-        const uint32_t b = threadIdx.x;
-        uint32_t tc = 0;
-        if (b < nb) {
-#pragma unroll
-            for (uint32_t w = 0; w < kRWaves; ++w) {
-                const uint32_t v = cw[w][b];
-                cw[w][b] = tc;
-                tc += v;
-            }
-        }
-        uint32_t inc = tc;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += u;
-        }
-        if (lane == 63) wtot[wave] = inc;
-        __syncthreads();
-        uint32_t wofs = 0;
-        for (uint32_t w = 0; w < wave; ++w) wofs += wtot[w];
-        if (b < nb) {
-            const uint32_t off = wofs + inc - tc;
-            toff[b] = off;
-            counts[(size_t)tile * nb + b] = tc;
-            counts[bi.o_roff + (size_t)tile * nb + b] = off;
-            if (tc)
-                atomicAdd(&counts[bi.o_totals + b * kTotSplit + tile % kTotSplit],
-                          tc + (uint32_t)DFHIP_SEG_COST);
-        }
-        __syncthreads();
-        // pass B: the entries
-        uint4 *tp = pool + (size_t)tile * tile_entries;
-#pragma unroll
-        for (uint32_t l = 0; l < kFastLevels; ++l) {
-            if (l >= L) continue;  // uniform
-            const uint32_t g = in ? grad[(size_t)l * B + s] : 0u;
-            const uint32_t b0 = fl.bin0[l], ns = bi.bin0[l + 1] - b0;
-            for (uint32_t k = 0; k < ns; ++k) {  // uniform
-                const bool mine = (mk[l] >> k) & 1u;
-                const u64 bal = __ballot(mine);
-                if (mine) {
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                        (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    const uint32_t bb = b0 + k;
-                    tp[toff[bb] + cw[wave][bb] + rank] = make_uint4(g, px[l], py[l], pz[l]);
-                }
-            }
-        }
-        __syncthreads();  // cw / toff are rewritten by the next tile
-    }
-}
-
-// One resolved entry into the lane's cell state (flat_take_at's arithmetic:
-// the same trailing-dimension factor and per-corner weight products).
-template <typename grad_t, uint32_t LEAD>
-__device__ __forceinline__ void rtake(FlatCell<2> &st, double *acc, uint32_t srows, uint32_t lo,
-                                      uint32_t n, uint32_t m1, uint32_t m2, uint32_t wm,
-                                      const uint4 v) {
-    const uint32_t i0 = (v.y >> 24) | ((v.z >> 16) & 0xFF00u);
-    float fr[3];
-    fr[0] = (float)(v.y & 0xFFFFFFu) * 5.9604644775390625e-8f;  // 2^-24, exact
-    fr[1] = (float)(v.z & 0xFFFFFFu) * 5.9604644775390625e-8f;
-    fr[2] = (float)(v.w & 0xFFFFFFu) * 5.9604644775390625e-8f;
-    float g[2];
-    {
-        grad_t lo16, hi16;
-        const uint16_t a = (uint16_t)(v.x & 0xFFFFu), b = (uint16_t)(v.x >> 16);
-        __builtin_memcpy(&lo16, &a, 2);
-        __builtin_memcpy(&hi16, &b, 2);
-        g[0] = (float)lo16;
-        g[1] = (float)hi16;
-    }
-    float tw = 1.0f;  // trailing dims dropped from the index: their corners coincide
-#pragma unroll
-    for (uint32_t d = LEAD; d < 3; ++d) tw *= (1.0f - fr[d]) + fr[d];
-    const double gd0 = (double)g[0], gd1 = (double)g[1];
-    if (!(st.have && i0 == st.i0)) {
-        if (st.have) {
-#pragma unroll
-            for (uint32_t k = 0; k < (1u << LEAD); ++k) {
-                const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
-                const uint32_t rel = ((st.i0 + o) & wm) - lo;
-                if (rel < n) {
-                    lds_add(acc, rel, st.cw[k][0], k);
-                    lds_add(acc, srows + rel, st.cw[k][1], k);
-                }
-            }
-        }
-        st.i0 = i0;
-        st.have = true;
-#pragma unroll
-        for (uint32_t k = 0; k < (1u << LEAD); ++k) st.cw[k][0] = st.cw[k][1] = 0.0;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < (1u << LEAD); ++k) {
-        float w = tw;
-#pragma unroll
-        for (uint32_t d = 0; d < LEAD; ++d) w *= (k & (1u << d)) ? fr[d] : 1.0f - fr[d];
-        const double wd = (double)w;
-        st.cw[k][0] = fma(wd, gd0, st.cw[k][0]);
-        st.cw[k][1] = fma(wd, gd1, st.cw[k][1]);
-    }
-}
-
-// A part's walk at one level lead: its tiles (part, part + P, ...) in chunks
-// of up to kChunkTiles; each chunk's segments laid end to end (scan of the
-// counts), cut into 1024 equal runs (wave w the w-th sixteenth, lanes
-// bit-reversed); a lane's run may cross segments.  Entries are loaded one
-// batch ahead of their use.
-template <typename grad_t, uint32_t LEAD>
-__device__ __forceinline__ void rwalk_level(const uint4 *__restrict__ pool, const uint32_t *counts,
-                                            const BinInfo &bi, uint32_t tile_entries,
-                                            double *acc, uint32_t *pre, uint32_t *sbase,
-                                            uint32_t *wsum, uint32_t b, uint32_t part, uint32_t P,
-                                            uint32_t ntiles, uint32_t srows, uint32_t lo,
-                                            uint32_t n, uint32_t m1, uint32_t m2, uint32_t wm,
-                                            uint32_t *entries_seen) {
-    const uint32_t nb = bi.nbins;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t waves = blockDim.x >> 6, nthr = blockDim.x;
-    const uint32_t nt = ntiles > part ? ceil_div(ntiles - part, P) : 0u;
-    FlatCell<2> cell;
-    cell.have = false;
-    cell.i0 = 0;
-    for (uint32_t cb = 0; cb < nt; cb += kChunkTiles) {
-        const uint32_t nc = min(nt - cb, kChunkTiles);
-        uint32_t v = 0;
-        if (tid < nc) {
-            const uint32_t t = part + (cb + tid) * P;
-            v = counts[(size_t)t * nb + b];
-            sbase[tid] = t * tile_entries + counts[bi.o_roff + (size_t)t * nb + b];
-        }
-        uint32_t inc = v;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += u;
-        }
-        if (lane == 63) wsum[wave] = inc;
-        __syncthreads();
-        uint32_t wofs = 0;
-        for (uint32_t w = 0; w < wave; ++w) wofs += wsum[w];
-        if (tid < nc) pre[tid] = wofs + inc - v;
-        if (tid == 0) {
-            uint32_t tot = 0;
-            for (uint32_t w = 0; w < waves; ++w) tot += wsum[w];
-            pre[nc] = tot;
-        }
-        __syncthreads();
-        const uint32_t E = pre[nc];
-        if (tid == 0) *entries_seen += E;  // debug trace only
-        const uint32_t Q = ceil_div(E, nthr);
-        const uint32_t r = wave * 64u + (__builtin_bitreverse32(lane) >> 26);
-        uint32_t e = min(r * Q, E);
-        const uint32_t e1 = min(e + Q, E);
-        if (e < e1) {
-            uint32_t a = 0, z = nc;  // segment of entry e: pre[a] <= e < pre[z]
-            while (z - a > 1) {
-                const uint32_t mid = (a + z) >> 1;
-                if (pre[mid] <= e) a = mid;
-                else z = mid;
-            }
-            uint32_t ti = a, tend = pre[a + 1], addr = sbase[a] + (e - pre[a]);
-            // one entry on: the next pool index (into the next non-empty
-            // segment at a segment's end)
-            auto advance = [&]() {
-                ++addr;
-                ++e;
-                if (e < e1 && e == tend) {
-                    do {
-                        ++ti;
-                        tend = pre[ti + 1];
-                    } while (tend == e);
-                    addr = sbase[ti];
-                }
-            };
-            // the pool indices of the next m <= kRBatch entries (the rest
-            // clamped to the last: every load is issued before the first use)
-            auto next_batch = [&](uint32_t (&ix)[kRBatch], uint32_t &m) {
-                m = min(kRBatch, e1 - e);
-#pragma unroll
-                for (uint32_t i = 0; i < kRBatch; ++i) {
-                    if (i < m) {
-                        ix[i] = addr;
-                        advance();
-                    } else {
-                        ix[i] = ix[i ? i - 1 : 0];
-                    }
-                }
-            };
-            uint32_t ix[kRBatch], m;
-            next_batch(ix, m);
-            uint4 cur[kRBatch];
-#pragma unroll
-            for (uint32_t i = 0; i < kRBatch; ++i) cur[i] = pool[ix[i]];
-            while (true) {
-                const bool more = e < e1;
-                uint32_t nm = 0;
-                uint4 nxt[kRBatch];
-                if (more) {
-                    next_batch(ix, nm);
-#pragma unroll
-                    for (uint32_t i = 0; i < kRBatch; ++i) nxt[i] = pool[ix[i]];
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < kRBatch; ++i)
-                    if (i < m) rtake<grad_t, LEAD>(cell, acc, srows, lo, n, m1, m2, wm, cur[i]);
-                if (!more) break;
-                m = nm;
-#pragma unroll
-                for (uint32_t i = 0; i < kRBatch; ++i) cur[i] = nxt[i];
-            }
-        }
-        __syncthreads();  // pre / sbase / wsum are rewritten by the next chunk
-    }
-    if (cell.have) {
-#pragma unroll
-        for (uint32_t k = 0; k < (1u << LEAD); ++k) {
-            const uint32_t o = (k & 1u) + ((k & 2u) ? m1 : 0u) + ((k & 4u) ? m2 : 0u);
-            const uint32_t rel = ((cell.i0 + o) & wm) - lo;
-            if (rel < n) {
-                lds_add(acc, rel, cell.cw[k][0], k);
-                lds_add(acc, srows + rel, cell.cw[k][1], k);
-            }
-        }
-    }
-}
-
-template <typename grad_t>
-__global__ __launch_bounds__(1024) void k_rwalk(const uint4 *__restrict__ pool, FastLevels fl,
-                                               BinInfo bi, SliceDyn dyn, uint32_t B,
-                                               uint32_t tile_entries, uint32_t *counts,
-                                               float *__restrict__ partial) {
-    extern __shared__ double acc[];
-    __shared__ uint32_t pre[kChunkTiles + 1];
-    __shared__ uint32_t sbase[kChunkTiles];
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t sh_b, sh_j, sh_p, sh_entries;
-    __shared__ uint32_t tot_s[kMaxBins];
-    const uint64_t tr0 = bi.trace ? wall_clock64() : 0;
-    const uint32_t srows = 1u << bi.shift;
-    for (uint32_t i = threadIdx.x; i < srows * 2; i += blockDim.x) acc[i] = 0.0;
-    if (threadIdx.x == 0) sh_entries = 0;
-    walk_plan(bi, counts, tot_s, sh_b, sh_j, sh_p);  // (its barriers cover the zeroing)
-    const uint32_t P = sh_p;
-    if (P == 0) return;  // uniform
-    const uint32_t b = sh_b, part = sh_j;
-    uint32_t l = 0;
-    while (l + 1 < bi.L && bi.bin0[l + 1] <= b) ++l;
-    const uint32_t lo = (b - bi.bin0[l]) << bi.shift;  // slice start, relative to the level
-    const uint32_t n = min(srows, bi.rows[l] - lo);
-    const uint64_t tr1 = bi.trace ? wall_clock64() : 0;
-    const uint32_t ntiles = ceil_div(ge::dyn_count(dyn, B), kTile);
-    const uint32_t m1 = fl.m1[l], m2 = fl.m2[l], wm = fl.wmask[l], lead = fl.lead[l];
-#define DFHIP_RW(LD)                                                                            \
-    rwalk_level<grad_t, LD>(pool, counts, bi, tile_entries, acc, pre, sbase, wsum, b, part, P, \
-                            ntiles, srows, lo, n, m1, m2, wm, &sh_entries)
-    if (lead >= 3) DFHIP_RW(3);
-    else if (lead == 2) DFHIP_RW(2);
-    else DFHIP_RW(1);
-#undef DFHIP_RW
-    __syncthreads();
-    float *out = partial + (size_t)blockIdx.x * ((size_t)srows * 2);
-    for (uint32_t i = threadIdx.x; i < n * 2; i += blockDim.x)
-        out[i] = (float)acc[(i & 1u) * srows + (i >> 1)];
-    if (bi.trace) {  // debug timeline (dfhip_binned_opts.trace), as k_walk's
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint64_t *r = bi.trace + (size_t)blockIdx.x * 8;
-            r[0] = b;
-            r[1] = b + 1;
-            r[2] = P;
-            r[3] = sh_entries;
-            r[4] = tr0;
-            r[5] = tr1;
-            r[6] = part;
-            r[7] = wall_clock64();
-        }
     }
 }
 
@@ -2095,25 +1626,6 @@ __global__ __launch_bounds__(256) void k_sum2(const float *__restrict__ partial,
     }
 }
 
-// The resolved stream (k_rbin + k_rwalk) fits the layout: at most kRMaxBins
-// bins, kRMaxSlices slices and 2^16 rows per level (16-bit cell index), and
-// the pool index below 2^32.  tile_entries: the pool region of one tile, the
-// bound kTile x sum over levels of min(2^lead, slices) (a cell's corners lie
-// in at most that many slices).
-static bool resolved_layout(const FastLevels &fl, const BinInfo &bi, uint32_t &tile_entries) {
-    if (bi.nbins > kRMaxBins || bi.L > kFastLevels) return false;
-    uint64_t per = 0;
-    for (uint32_t l = 0; l < bi.L; ++l) {
-        const uint32_t ns = bi.bin0[l + 1] - bi.bin0[l];
-        if (ns > kRMaxSlices || bi.rows[l] > 65536u) return false;
-        per += std::min<uint32_t>(1u << fl.lead[l], ns);
-    }
-    const uint64_t te = per * kTile;
-    if (te * bi.tcap >= (1ull << 32)) return false;
-    tile_entries = (uint32_t)te;
-    return true;
-}
-
 // Corner-row wrap mode shared by every level (0 mask, 1 modulo, 2 hash; the
 // host restatement of ge::level_ctx / level_rows / row_mode), or kModeAny.
 static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t L, uint32_t D,
@@ -2140,11 +1652,10 @@ static int uniform_mode(const int32_t *offsets_host, const Levels &lv, uint32_t 
 }
 
 // Walk form for mask-form layouts (dfhip_binned_opts.walk_mode: 0 the
-// per-segment k_walk, 1 the flat k_walk_flat, 2 its per-wave pieces; A/B
-// runs, tests).  Default: flat for stencil groups (textureless step, rocprof:
-// walk 1307 -> 1051 us), per-segment for single samples (albedo step: 189 us
-// against 197 per-wave pieces and 269 flat — one entry's work is too short to
-// pay for lanes spread over a part's tiles).
+// per-segment k_walk, 1 the flat k_walk_flat; A/B runs, tests).  Default:
+// flat for stencil groups (textureless step, rocprof: walk 1307 -> 1051 us),
+// per-segment for single samples (albedo step: 189 us against 269 flat — one
+// entry's work is too short to pay for lanes spread over a part's tiles).
 static int flat_walk_mode(uint32_t group, const Opts &op) {
     if (op.walk_mode >= 0) return op.walk_mode;
     return group > 1 ? 1 : 0;
@@ -2163,11 +1674,8 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
         typedef void (*flat_fn)(const grad_t *, const float *, FastLevels, BinInfo, int,
                                 SliceDyn, float, uint32_t, uint32_t *, const uint16_t *,
                                 float *, Stencil);
-        const int wmode = flat_walk_mode(GROUP, op);
-        const flat_fn kf = wmode == 2 ? (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 2>
-                                              : k_walk_flat<grad_t, C, false, GROUP, 2>)
-                                      : (pow2 ? k_walk_flat<grad_t, C, true, GROUP, 1>
-                                              : k_walk_flat<grad_t, C, false, GROUP, 1>);
+        const flat_fn kf = pow2 ? k_walk_flat<grad_t, C, true, GROUP>
+                                : k_walk_flat<grad_t, C, false, GROUP>;
         ensure_dynamic_lds((const void *)kf, (int)kSliceBytes);
         kf<<<bi.G, 1024, lds, s>>>(grad, inputs, *fl, bi, align, dyn, inv, B, counts, entries,
                                    partial, st);
@@ -2198,34 +1706,25 @@ static void launch_walk(hipStream_t s, size_t lds, const grad_t *grad, const flo
 using namespace dfhip;
 
 extern "C" int dfhip_grid_backward_binned_scratch_opts(
-    uint32_t cap, const int32_t *offsets_host, uint32_t L, uint32_t C, float S, uint32_t H,
-    uint32_t gridtype, int align_corners, uint32_t group, const dfhip_binned_opts *opts,
-    uint64_t *entries_u32, uint64_t *counts_u32, uint64_t *partial_f32) {
+    uint32_t cap, const int32_t *offsets_host, uint32_t L, uint32_t C, uint32_t group,
+    const dfhip_binned_opts *opts, uint64_t *entries_u32, uint64_t *counts_u32,
+    uint64_t *partial_f32) {
     gb::Opts op;
     if (!gb::resolve_opts(opts, op)) return DFHIP_EINVAL;
-    gb::BinInfo bi, bo;
-    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, group, op, bi) ||
-        !gb::make_bins(offsets_host, L, C, cap, group == 1 ? 7u : 1u, op, bo)) {
+    if (group != 1 && group != 7) {
+        set_error("grid_backward_binned_scratch: group must be 1 or 7 (got %u)", group);
+        return DFHIP_EINVAL;
+    }
+    gb::BinInfo bi;
+    if (!offsets_host || !gb::make_bins(offsets_host, L, C, cap, group, op, bi)) {
         set_error("grid_backward_binned_scratch: unsupported level layout");
         return DFHIP_EINVAL;
     }
-    // sized for both groups' tile layouts (single samples and stencil groups
-    // tile differently), so a scratch sized for one group is never short for
-    // the other
-    // tile-relative sample ids, u16 (kTile <= 65536), counted in u32 words;
-    // the resolved stream's pool (16-byte entries) where it may run
-    uint64_t ew = std::max<uint64_t>(((uint64_t)bi.tcap * bi.nbins * bi.tile + 1) / 2,
-                                      ((uint64_t)bo.tcap * bo.nbins * bo.tile + 1) / 2);
-    if (group == 1 && C == 2 && gb::flat_walk_mode(1, op) == 3 && L <= ge::kMaxLevels) {
-        const ge::Levels lv = ge::make_levels(L, S, H);
-        gb::FastLevels fl;
-        uint32_t te = 0;
-        if (gb::make_fast_levels(offsets_host, lv, bi, gridtype, align_corners != 0, fl) &&
-            gb::resolved_layout(fl, bi, te))
-            ew = std::max<uint64_t>(ew, (uint64_t)bi.tcap * te * 4ull);
-    }
-    if (entries_u32) *entries_u32 = ew;
-    if (counts_u32) *counts_u32 = std::max(gb::counts_words(bi), gb::counts_words(bo));
+    // single samples and stencil groups tile alike (kTile ids per segment),
+    // so one scratch serves both; tile-relative sample ids are u16, counted
+    // in u32 words
+    if (entries_u32) *entries_u32 = ((uint64_t)bi.tcap * bi.nbins * bi.tile + 1) / 2;
+    if (counts_u32) *counts_u32 = gb::counts_words(bi);
     if (partial_f32) *partial_f32 = gb::partial_floats(bi, C);
     return DFHIP_OK;
 }
@@ -2234,16 +1733,15 @@ extern "C" int dfhip_grid_backward_binned_scratch_opts(
 // with this group and these options (tests read segments with it).
 extern "C" uint32_t dfhip_grid_backward_binned_tile(uint32_t group, const dfhip_binned_opts *opts) {
     gb::Opts op;
-    if (!gb::resolve_opts(opts, op)) return 0;
-    return (group == 1 && gb::flat_walk_mode(1, op) != 3) ? gb::kTile1 : gb::kTile;
+    if ((group != 1 && group != 7) || !gb::resolve_opts(opts, op)) return 0;
+    return gb::kTile;
 }
 
 extern "C" int dfhip_grid_backward_binned_scratch(uint32_t cap, const int32_t *offsets_host,
                                                   uint32_t L, uint32_t C, uint64_t *entries_u32,
                                                   uint64_t *counts_u32, uint64_t *partial_f32) {
-    return dfhip_grid_backward_binned_scratch_opts(cap, offsets_host, L, C, 0.0f, 1, 1, 0, 1,
-                                                   nullptr, entries_u32, counts_u32,
-                                                   partial_f32);
+    return dfhip_grid_backward_binned_scratch_opts(cap, offsets_host, L, C, 1, nullptr,
+                                                   entries_u32, counts_u32, partial_f32);
 }
 
 static int binned_backward(const char *name, int phase, int grad_dtype, const void *grad_lbc,
@@ -2293,12 +1791,6 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
         }
     }
     const gb::Stencil st{eps, bound};
-    // the resolved stream: single samples, 2 channels of f16 / bf16 gradients,
-    // a mask-form layout, half-cell origin (frac exact in 24 bits)
-    uint32_t r_tile = 0;
-    const bool rs = group == 1 && C == 2 && fast && align_corners == 0 &&
-                    grad_dtype != DFHIP_F32 && gb::flat_walk_mode(1, op) == 3 &&
-                    gb::resolved_layout(fl, bi, r_tile);
     if (phase & 1) {
         // totals (k_bin adds) and the plan (k_walk sets; P = 0: no images)
         (void)hipMemsetAsync(counts + bi.o_totals, 0,
@@ -2307,16 +1799,7 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
             const uint32_t gbin = bi.tcap < 4096u ? bi.tcap : 4096u;
             const bool pow2 = ge::dyn_pow2(dyn.bound);
             const float inv = pow2 ? 1.0f / (2.0f * dyn.bound) : 0.0f;
-            if (rs) {
-                if (pow2)
-                    gb::k_rbin<true><<<gbin, 1024, 0, s>>>(inputs, (const uint32_t *)grad_lbc, fl,
-                                                           bi, dyn, inv, B, r_tile, counts,
-                                                           (uint4 *)entries);
-                else
-                    gb::k_rbin<false><<<gbin, 1024, 0, s>>>(inputs, (const uint32_t *)grad_lbc,
-                                                            fl, bi, dyn, inv, B, r_tile, counts,
-                                                            (uint4 *)entries);
-            } else if (group == 7) {
+            if (group == 7) {
                 if (pow2)
                     gb::k_bin_fast<true, 7><<<gbin, 1024, 0, s>>>(inputs, fl, bi, align_corners,
                                                                    dyn, inv, B, counts,
@@ -2357,12 +1840,7 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
     gb::launch_walk<GT, 2, 7>(s, lds, (const GT *)grad_lbc, inputs, offsets, offsets_host, lv, \
                               bi, gridtype, align_corners, dyn, B, counts,                   \
                               (const uint16_t *)entries, partial, flp, op, st)
-        if (rs) {
-            auto kr = grad_dtype == DFHIP_F16 ? gb::k_rwalk<half_t> : gb::k_rwalk<bf16_t>;
-            ensure_dynamic_lds((const void *)kr, (int)gb::kSliceBytes);
-            kr<<<bi.G, 1024, lds, s>>>((const uint4 *)entries, fl, bi, dyn, B, r_tile, counts,
-                                       partial);
-        } else if (group == 7) {
+        if (group == 7) {
             if (grad_dtype == DFHIP_F16) DFHIP_WALK7(half_t);
             else DFHIP_WALK7(bf16_t);
         } else if (grad_dtype == DFHIP_F16) {

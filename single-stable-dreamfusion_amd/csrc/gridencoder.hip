@@ -29,6 +29,10 @@ namespace ge {
 // ------------------------------------------------------------ forward
 
 // gridencoder.cu:75-223.  BLC: outputs [B, L*C] (native) else [L, B, C].
+// dyn (grid_common.h SliceDyn): with a device count, rows [*m_dev, B) of a
+// capacity-sized batch are written as zeros (their features stay finite for
+// whatever reads the whole batch) and no table row is gathered for them; with
+// bound > 0 the inputs are raw positions mapped as grid.py:142 does.
 template <typename scalar_t, uint32_t D, uint32_t C, bool BLC>
 __global__ __launch_bounds__(256) void k_grid_fwd(const float *__restrict__ inputs,
                                                   const scalar_t *__restrict__ grid,
@@ -36,16 +40,19 @@ __global__ __launch_bounds__(256) void k_grid_fwd(const float *__restrict__ inpu
                                                   scalar_t *__restrict__ outputs, uint32_t B,
                                                   uint32_t L, Levels lv,
                                                   scalar_t *__restrict__ dy_dx,
-                                                  uint32_t gridtype, int align_corners) {
+                                                  uint32_t gridtype, int align_corners,
+                                                  SliceDyn dyn) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const bool align = align_corners != 0;
 
     float x[D];
-    bool oob = false;
+    // a row past the live count reads no input and comes out as zeros, like
+    // an out-of-bounds sample
+    bool oob = b >= dyn_count(dyn, B);
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) {
-        x[d] = inputs[(size_t)b * D + d];
+        x[d] = oob ? 0.0f : dyn_map(dyn, inputs[(size_t)b * D + d]);
         if (x[d] < 0.0f || x[d] > 1.0f) oob = true;
     }
 
@@ -569,25 +576,27 @@ __global__ __launch_bounds__(256) void k_blc_to_lbc(const word_t *__restrict__ s
 template <typename scalar_t, uint32_t D, bool BLC>
 static void launch_fwd_c(uint32_t C, dim3 g, dim3 blk, hipStream_t s, const float *in,
                          const scalar_t *emb, const int32_t *off, scalar_t *out, uint32_t B,
-                         uint32_t L, const Levels &lv, scalar_t *dy, uint32_t gt, int ac) {
+                         uint32_t L, const Levels &lv, scalar_t *dy, uint32_t gt, int ac,
+                         SliceDyn dn) {
     switch (C) {
-    case 1: k_grid_fwd<scalar_t, D, 1, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
-    case 2: k_grid_fwd<scalar_t, D, 2, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
-    case 4: k_grid_fwd<scalar_t, D, 4, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
-    case 8: k_grid_fwd<scalar_t, D, 8, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 1: k_grid_fwd<scalar_t, D, 1, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
+    case 2: k_grid_fwd<scalar_t, D, 2, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
+    case 4: k_grid_fwd<scalar_t, D, 4, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
+    case 8: k_grid_fwd<scalar_t, D, 8, BLC><<<g, blk, 0, s>>>(in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
     }
 }
 
 template <typename scalar_t, bool BLC>
 static void launch_fwd(uint32_t D, uint32_t C, dim3 g, dim3 blk, hipStream_t s, const float *in,
                        const scalar_t *emb, const int32_t *off, scalar_t *out, uint32_t B,
-                       uint32_t L, const Levels &lv, scalar_t *dy, uint32_t gt, int ac) {
+                       uint32_t L, const Levels &lv, scalar_t *dy, uint32_t gt, int ac,
+                       SliceDyn dn) {
     switch (D) {
-    case 1: launch_fwd_c<scalar_t, 1, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
-    case 2: launch_fwd_c<scalar_t, 2, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
-    case 3: launch_fwd_c<scalar_t, 3, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
-    case 4: launch_fwd_c<scalar_t, 4, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
-    case 5: launch_fwd_c<scalar_t, 5, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac); break;
+    case 1: launch_fwd_c<scalar_t, 1, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
+    case 2: launch_fwd_c<scalar_t, 2, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
+    case 3: launch_fwd_c<scalar_t, 3, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
+    case 4: launch_fwd_c<scalar_t, 4, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
+    case 5: launch_fwd_c<scalar_t, 5, BLC>(C, g, blk, s, in, emb, off, out, B, L, lv, dy, gt, ac, dn); break;
     }
 }
 
@@ -715,7 +724,7 @@ static int grid_fwd_impl(const char *name, int dtype, const float *inputs,
                          const void *embeddings, const int32_t *offsets, void *outputs,
                          uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
                          void *dy_dx, uint32_t gridtype, int align_corners,
-                         dfhip_stream_t stream) {
+                         dfhip_stream_t stream, SliceDyn dyn = SliceDyn{nullptr, 0.0f}) {
     if (!check_dc(name, D, C, L)) return DFHIP_EINVAL;
     if (B == 0 || L == 0) return DFHIP_OK;
     const Levels lv = make_levels(L, S, H);
@@ -723,7 +732,7 @@ static int grid_fwd_impl(const char *name, int dtype, const float *inputs,
     DFHIP_DISPATCH(dtype, name,
         launch_fwd<scalar_t, BLC>(D, C, g, blk, as_stream(stream), inputs,
                                   (const scalar_t *)embeddings, offsets, (scalar_t *)outputs, B,
-                                  L, lv, (scalar_t *)dy_dx, gridtype, align_corners));
+                                  L, lv, (scalar_t *)dy_dx, gridtype, align_corners, dyn));
     return check_launch(name);
 }
 
@@ -746,6 +755,21 @@ extern "C" int dfhip_grid_encode_forward_blc(int dtype, const float *inputs,
     return grid_fwd_impl<true>("grid_encode_forward_blc", dtype, inputs, embeddings, offsets,
                                outputs, B, D, C, L, S, H, dy_dx, gridtype, align_corners,
                                stream);
+}
+
+extern "C" int dfhip_grid_encode_forward_dyn(int dtype, const float *inputs, float bound,
+                                             const void *embeddings, const int32_t *offsets,
+                                             void *outputs, uint32_t B, const int32_t *m_dev,
+                                             uint32_t D, uint32_t C, uint32_t L, float S,
+                                             uint32_t H, void *dy_dx, uint32_t gridtype,
+                                             int align_corners, dfhip_stream_t stream) {
+    if (!(bound >= 0.0f)) {
+        set_error("grid_encode_forward_dyn: bound must be >= 0");
+        return DFHIP_EINVAL;
+    }
+    return grid_fwd_impl<true>("grid_encode_forward_dyn", dtype, inputs, embeddings, offsets,
+                               outputs, B, D, C, L, S, H, dy_dx, gridtype, align_corners, stream,
+                               SliceDyn{m_dev, bound});
 }
 
 template <bool BLC>
@@ -905,7 +929,8 @@ extern "C" int dfhip_grid_encode_backward_sliced(int grad_dtype, int out_dtype, 
 extern "C" int dfhip_grid_grad_blc_to_lbc(int dtype, const void *src, void *dst, uint32_t B,
                                           uint32_t L, uint32_t C, dfhip_stream_t stream) {
     const char *name = "grid_grad_blc_to_lbc";
-    size_t esz = dtype == DFHIP_F16 ? 2 : dtype == DFHIP_F32 ? 4 : dtype == DFHIP_F64 ? 8 : 0;
+    size_t esz = (dtype == DFHIP_F16 || dtype == DFHIP_BF16) ? 2
+                 : dtype == DFHIP_F32 ? 4 : dtype == DFHIP_F64 ? 8 : 0;
     if (esz == 0) {
         set_error("%s: unsupported dtype %d", name, dtype);
         return DFHIP_EDTYPE;

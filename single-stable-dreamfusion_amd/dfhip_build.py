@@ -19,8 +19,19 @@ CSRC = PKG / "csrc"
 OBJ = PKG / "build"
 LIB = PKG / "lib" / "libdfhip.so"
 
+HEADER = ROOT / "include" / "dfhip.h"
+
 ARCH = os.environ.get("DFHIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+
+def abi_hash(header: Path = HEADER) -> int:
+    """dfhip_abi_version() of a library built from `header`: the first 28 bits
+    of the SHA-256 of its bytes.  _dfhip.load() recomputes it from the header
+    the Python binding was written against and refuses a library that differs
+    (a stale library would otherwise be called with another signature)."""
+    import hashlib
+    return int(hashlib.sha256(header.read_bytes()).hexdigest()[:7], 16)
+
 
 # -ffp-contract=off: only the explicit fmaf() calls (the reference's nvcc
 # contraction sites) fuse; see DESIGN.md "Numerics".
@@ -28,6 +39,7 @@ CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
     "-fno-gpu-rdc", "-mcode-object-version=5", "-Wall", "-Wno-unused-function",
     "-fhip-fp32-correctly-rounded-divide-sqrt", f"-I{ROOT / 'include'}",
+    f"-DDFHIP_ABI_HASH={abi_hash():#x}",
     *os.environ.get("DFHIP_EXTRA_CFLAGS", "").split(),  # A/B probe builds (tools only)
 ]
 

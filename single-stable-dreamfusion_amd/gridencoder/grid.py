@@ -7,15 +7,21 @@ align_corners)` with the same parameter layout (`offsets`, `embeddings`,
 grid.py:91-133) and the same autocast rule (half embeddings when C is even,
 grid.py:38-39).
 
-GPU-side differences (invisible to callers): outputs are produced directly in
-the [B, L*C] layout the caller consumes (no [L, B, C] buffer + permute copy,
-grid.py:42,52,70), and the backward reads the [B, L*C] gradient as is.
-`DFHIP_GRID_GRAD_ACC=float` accumulates the embedding gradient in f32 instead
-of the reference's half2 atomics (same atomic request count, no fp16 rounding
-of partial sums); the default keeps the reference's half accumulation.
-"""
-import os
+GPU-side differences (invisible to callers):
 
+* outputs are produced directly in the [B, L*C] layout the caller consumes
+  (no [L, B, C] buffer + permute copy, grid.py:42,52,70);
+* the embedding backward is the binned owner-computes walk
+  (csrc/gridbin.hip: exact f64 sums, no global atomics, deterministic) in
+  place of the reference's half2 atomics (gridencoder.cu:226-313); the
+  reference's atomic scatter stays available as `GridEncoder.backward_mode =
+  "atomic"` and is taken when the input gradient is requested (dy_dx);
+* capacity-sized batches: inputs that carry a device live-row count
+  (`raymarching.live_rows`, the device-count march) are encoded up to that
+  count only — rows past it come out as zeros — and the backward walks only
+  those rows; GridEncoder passes the raw positions and `bound` to the kernels
+  (the map (x + bound) / (2 bound) of grid.py:142 is done there, bit for bit).
+"""
 import numpy as np
 import torch
 import torch.nn as nn
@@ -27,18 +33,10 @@ import _gridencoder as _backend
 
 _gridtype_to_id = {"hash": 0, "tiled": 1}
 
+# attribute name of the device live-row count on capacity-sized tensors
+# (raymarching.march_rays_train_dev sets it; raymarching.live_rows reads it)
+_LIVE_ROWS_ATTR = "_dfhip_live_rows"
 
-def _grad_acc_dtype(emb_dtype):
-    mode = os.environ.get("DFHIP_GRID_GRAD_ACC", "native").lower()
-    if mode == "float" and emb_dtype == torch.float16:
-        return torch.float32
-    return emb_dtype
-
-
-# Embedding backward: "sliced" (default; LDS-privatised owner slices, f32
-# sums, no global atomics) or "atomic" (the reference's scatter of half2 /
-# f32 atomics, kept for A/B and the reference-form ABI).
-_BWD_MODE = os.environ.get("DFHIP_GRID_BWD", "sliced").lower()
 _parts_cache = {}
 
 
@@ -49,13 +47,64 @@ def _parts(total_rows, C):
     return _parts_cache[key]
 
 
+_host_offsets_cache = {}
+
+
+def host_offsets(offsets):
+    """Host copy of a level-offset tensor (the binned backward plans its slices
+    on the host).  Cached per (storage, version): a copy per new tensor only."""
+    key = (offsets.data_ptr(), offsets._version, offsets.numel(), str(offsets.device))
+    got = _host_offsets_cache.get(key)
+    if got is None:
+        got = offsets.detach().to("cpu", torch.int32).numpy().copy()
+        if len(_host_offsets_cache) > 64:
+            _host_offsets_cache.clear()
+        _host_offsets_cache[key] = got
+    return got
+
+
+def binned_eligible(D, C, grad_dtype):
+    """The binned walk handles this shape / gradient dtype (gridbin.hip)."""
+    if D != 3 or C not in (1, 2, 4):
+        return False
+    if grad_dtype == torch.bfloat16:
+        return C == 2
+    return grad_dtype in (torch.float16, torch.float32)
+
+
+def binned_embedding_grad(grad_lbc, inputs, bound, offsets, offsets_host, B, m_dev, C, L, S, H,
+                          gridtype, align_corners, out=None, accumulate=False):
+    """grad_embeddings (f32 [rows, C]) of grad_lbc [L, B, C] through the binned
+    owner-computes walk (scratch allocated here, from the caching allocator).
+    inputs [B, 3]: raw positions when bound > 0, else in [0, 1]; rows
+    [0, m_dev[0]) when m_dev is given."""
+    rows = int(offsets_host[-1])
+    dev = grad_lbc.device
+    ne, nc, npf = _backend.grid_backward_binned_scratch(B, offsets_host, L, C)
+    ent = torch.empty(ne, dtype=torch.int32, device=dev)
+    cnt = torch.empty(nc, dtype=torch.int32, device=dev)
+    part = torch.empty(npf, dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty(rows, C, dtype=torch.float32, device=dev)
+    _backend.grid_encode_backward_binned(grad_lbc, inputs, float(bound), offsets, offsets_host,
+                                         out, B, m_dev, 3, C, L, S, H, gridtype,
+                                         bool(align_corners), ent, cnt, part, accumulate)
+    return out
+
+
 class _grid_encode(Function):
     @staticmethod
     @custom_fwd(device_type="cuda")
     def forward(ctx, inputs, embeddings, offsets, per_level_scale, base_resolution,
-                calc_grad_inputs=False, gridtype=0, align_corners=False):
+                calc_grad_inputs=False, gridtype=0, align_corners=False, offsets_host=None,
+                bound=0.0, m_dev=None, backward_mode="binned"):
         """inputs [B, D] in [0, 1] (f32), embeddings [sum_l rows_l, C],
-        offsets [L+1] int32 -> [B, L*C] (half under autocast when C is even)."""
+        offsets [L+1] int32 -> [B, L*C] (half under autocast when C is even).
+        Past the reference's arguments (all optional): offsets_host (host
+        copy of offsets), bound > 0 (inputs are raw positions in [-bound,
+        bound]), m_dev (int32 device live-row count of a capacity-sized batch:
+        rows past it come out zero and get no gradient), backward_mode
+        ("binned" or the reference's "atomic")."""
         inputs = inputs.contiguous()
         B, D = inputs.shape
         L = offsets.shape[0] - 1
@@ -69,57 +118,78 @@ class _grid_encode(Function):
         outputs = torch.empty(B, L * C, device=inputs.device, dtype=table.dtype)
         dy_dx = (torch.empty(B, L * D * C, device=inputs.device, dtype=table.dtype)
                  if calc_grad_inputs else None)
+        es = table.element_size()
         # algorithmic bytes: inputs + outputs per sample, table once
-        nbytes = B * (4 * D + L * C * table.element_size()) + table.numel() * table.element_size()
-        with _dfhip.timed("grid_encode_forward", nbytes):
-            _backend.grid_encode_forward_blc(inputs, table, offsets, outputs, B, D, C, L, S, H,
-                                             dy_dx, gridtype, align_corners)
+        if m_dev is not None or bound > 0:
+            with _dfhip.timed("grid_encode_forward", table.numel() * es, m_dev,
+                              4 * D + L * C * es):
+                _backend.grid_encode_forward_dyn(inputs, float(bound), table, offsets, outputs,
+                                                 B, m_dev, D, C, L, S, H, dy_dx, gridtype,
+                                                 align_corners)
+        else:
+            with _dfhip.timed("grid_encode_forward", B * (4 * D + L * C * es) + table.numel() * es):
+                _backend.grid_encode_forward_blc(inputs, table, offsets, outputs, B, D, C, L, S,
+                                                 H, dy_dx, gridtype, align_corners)
         ctx.save_for_backward(inputs, offsets, dy_dx)
-        ctx.dims = (B, D, C, L, S, H, gridtype, bool(align_corners))
-        ctx.table_meta = (table.shape[0], table.dtype)
+        # the live count is read by the backward's kernels at run time (not a
+        # saved tensor: the march rewrites its counter row every 16 steps)
+        ctx.m_dev = m_dev
+        ctx.dims = (B, D, C, L, S, H, gridtype, bool(align_corners), float(bound))
+        ctx.table_meta = (table.shape[0], table.dtype, embeddings.dtype)
+        ctx.offsets_host = offsets_host
+        ctx.backward_mode = backward_mode
         return outputs
 
     @staticmethod
     @custom_bwd(device_type="cuda")
     def backward(ctx, grad):
         inputs, offsets, dy_dx = ctx.saved_tensors
-        B, D, C, L, S, H, gridtype, align_corners = ctx.dims
-        rows, table_dtype = ctx.table_meta
-        grad = grad.to(table_dtype)
-        if dy_dx is None and _BWD_MODE == "sliced" and grad.dtype in (torch.float16,
-                                                                       torch.float32):
-            # [B, L*C] -> the level-major [L, B, C] the slices stream through
-            grad = grad.contiguous()
+        m_dev = ctx.m_dev
+        B, D, C, L, S, H, gridtype, align_corners, bound = ctx.dims
+        rows, table_dtype, emb_dtype = ctx.table_meta
+        nones = (None,) * 10
+        grad = grad.to(table_dtype).contiguous()
+        if dy_dx is None and ctx.backward_mode == "binned" and binned_eligible(D, C, grad.dtype):
+            # [B, L*C] -> the level-major [L, B, C] the walk streams per level
             grad_lbc = torch.empty(L, B, C, dtype=grad.dtype, device=grad.device)
             _backend.grid_grad_blc_to_lbc(grad, grad_lbc, B, L, C)
-            parts = _parts(rows, C)
-            partial = torch.empty(_backend.grid_backward_partial_floats(rows, C, parts),
-                                  dtype=torch.float32, device=grad.device)
-            # f32 sums returned as the f32 parameter's gradient directly
-            grad_embeddings = torch.empty(rows, C, device=grad.device, dtype=torch.float32)
-            # algorithmic bytes: inputs + grads once, the f32 table gradient written once
-            nbytes = B * (4 * D + L * C * grad.element_size()) + 4 * rows * C
-            with _dfhip.timed("grid_encode_backward", nbytes):
-                _backend.grid_encode_backward_sliced(grad_lbc, inputs, offsets, grad_embeddings,
-                                                     rows, B, D, C, L, S, H, gridtype,
-                                                     align_corners, partial, parts)
-            return None, grad_embeddings, None, None, None, None, None, None
-
-        grad = grad.contiguous()  # [B, L*C], no permute
-        grad_embeddings = torch.zeros(rows, C, device=grad.device,
-                                      dtype=_grad_acc_dtype(table_dtype))
+            offs_h = ctx.offsets_host if ctx.offsets_host is not None else host_offsets(offsets)
+            # algorithmic bytes: inputs + grads of the live rows once, the f32
+            # table gradient written once
+            per = 4 * D + L * C * grad.element_size()
+            with _dfhip.timed("grid_encode_backward", 4 * rows * C + (0 if m_dev is not None
+                                                                      else B * per),
+                              m_dev, per):
+                gemb = binned_embedding_grad(grad_lbc, inputs, bound, offsets, offs_h, B, m_dev,
+                                             C, L, S, H, gridtype, align_corners)
+            return (None, gemb.to(emb_dtype)) + nones
+        # the reference's scatter of half2 / f32 atomics (gridencoder.cu:226-313)
+        if m_dev is not None:  # the atomic kernels take no device count
+            m = int(m_dev[0].item())
+            grad, inputs = grad[:m], inputs[:m]
+            if dy_dx is not None:
+                dy_dx = dy_dx[:m]
+            B = m
+        x01 = inputs if bound <= 0 else (inputs + bound) / (2 * bound)
+        grad_embeddings = torch.zeros(rows, C, device=grad.device, dtype=table_dtype)
         grad_inputs = None
         if dy_dx is not None:
             grad_inputs = torch.empty(B, D, device=grad.device, dtype=table_dtype)
         # HBM algorithmic bytes: grad + inputs per sample (the 2^D*L*C atomic
         # adds per sample are L2/atomic-unit traffic, accounted separately)
-        nbytes = B * (4 * D + L * C * grad.element_size())
-        with _dfhip.timed("grid_encode_backward", nbytes):
-            _backend.grid_encode_backward_blc(grad, inputs, offsets, grad_embeddings, B, D, C, L, S,
-                                              H, dy_dx, grad_inputs, gridtype, align_corners)
+        with _dfhip.timed("grid_encode_backward", B * (4 * D + L * C * grad.element_size())):
+            _backend.grid_encode_backward_blc(grad, x01.contiguous(), offsets, grad_embeddings, B,
+                                              D, C, L, S, H, dy_dx, grad_inputs, gridtype,
+                                              align_corners)
         if grad_inputs is not None:
             grad_inputs = grad_inputs.to(inputs.dtype)
-        return grad_inputs, grad_embeddings, None, None, None, None, None, None
+            if bound > 0:
+                grad_inputs = grad_inputs / (2 * bound)
+            if grad_inputs.shape[0] < ctx.dims[0]:  # rows past the live count: no gradient
+                full = torch.zeros(ctx.dims[0], D, device=grad.device, dtype=grad_inputs.dtype)
+                full[:grad_inputs.shape[0]] = grad_inputs
+                grad_inputs = full
+        return (grad_inputs, grad_embeddings.to(emb_dtype)) + nones
 
 
 grid_encode = _grid_encode.apply
@@ -161,6 +231,9 @@ class GridEncoder(nn.Module):
         self.gridtype_id = _gridtype_to_id[gridtype]
         self.align_corners = align_corners
         self.max_params = 2 ** log2_hashmap_size
+        # embedding backward: "binned" (owner-computes walk, csrc/gridbin.hip)
+        # or "atomic" (the reference's scatter, gridencoder.cu:226-313)
+        self.backward_mode = "binned"
 
         offsets = level_offsets(num_levels, level_dim, input_dim, base_resolution,
                                 per_level_scale, log2_hashmap_size, align_corners)
@@ -182,11 +255,32 @@ class GridEncoder(nn.Module):
                 f"gridtype={self.gridtype} align_corners={self.align_corners}")
 
     def forward(self, inputs, bound=1):
-        """inputs [..., input_dim] in [-bound, bound] -> [..., num_levels*level_dim]."""
-        x = (inputs + bound) / (2 * bound)
-        lead = list(x.shape[:-1])
-        x = x.view(-1, self.input_dim)
-        out = grid_encode(x, self.embeddings, self.offsets, self.per_level_scale,
-                          self.base_resolution, x.requires_grad, self.gridtype_id,
-                          self.align_corners)
-        return out.view(lead + [self.output_dim])
+        """inputs [..., input_dim] in [-bound, bound] -> [..., num_levels*level_dim].
+        Capacity-sized inputs carrying a device live-row count (the
+        device-count march) are encoded up to that count; the rest of the rows
+        come out as zeros."""
+        lead = list(inputs.shape[:-1])
+        m_dev = getattr(inputs, _LIVE_ROWS_ATTR, None)
+        raw = (inputs.is_cuda and inputs.dtype == torch.float32 and bound > 0
+               and not inputs.requires_grad)
+        if raw or m_dev is not None:
+            # the kernels map (x + bound) / (2 bound) themselves (grid.py:142)
+            x = inputs.reshape(-1, self.input_dim)
+            if not raw:
+                x = ((x + bound) / (2 * bound)).float()
+            out = grid_encode(x, self.embeddings, self.offsets, self.per_level_scale,
+                              self.base_resolution, x.requires_grad, self.gridtype_id,
+                              self.align_corners, self.offsets_host, float(bound) if raw else 0.0,
+                              m_dev, self.backward_mode)
+        else:
+            x = (inputs + bound) / (2 * bound)
+            x = x.view(-1, self.input_dim)
+            out = grid_encode(x, self.embeddings, self.offsets, self.per_level_scale,
+                              self.base_resolution, x.requires_grad, self.gridtype_id,
+                              self.align_corners, self.offsets_host, 0.0, None,
+                              self.backward_mode)
+        out = out.view(lead + [self.output_dim])
+        if m_dev is not None:
+            # the features of the capacity-sized batch: the same live rows
+            setattr(out, _LIVE_ROWS_ATTR, m_dev)
+        return out

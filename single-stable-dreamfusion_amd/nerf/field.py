@@ -15,8 +15,6 @@ autocast (the C5 option: the table, features and activations in bf16, the
 embedding gradient by the binned backward); anything else runs the unfused
 modules.
 """
-import os
-
 import numpy as np
 import torch
 from torch.autograd import Function
@@ -26,10 +24,6 @@ import _fieldmlp
 import _gridencoder
 from gridencoder.grid import _parts
 
-
-# Embedding backward: binned owner-computes (csrc/gridbin.hip, default) or the
-# LDS-sliced walk (DFHIP_GRID_BWD=sliced)
-_BINNED = os.environ.get("DFHIP_GRID_BWD", "binned") != "sliced"
 
 # When a list, _GridField.backward appends (launch, grad_buffer) instead of
 # launching the embedding backward (see defer_embedding_backward).
@@ -60,7 +54,7 @@ def eligible(encoder, layers, x):
     if torch.get_autocast_dtype("cuda") not in (torch.float16, torch.bfloat16):
         return False
     if torch.get_autocast_dtype("cuda") == torch.bfloat16 and (
-            not _BINNED or getattr(encoder, "offsets_host", None) is None):
+            getattr(encoder, "offsets_host", None) is None):
         return False  # bf16 feature gradients: binned embedding backward only
     if encoder.num_levels != 16 or encoder.level_dim != 2 or encoder.input_dim != 3:
         return False
@@ -115,12 +109,11 @@ class _GridField(Function):
         grads = [torch.empty_like(w) for w in ws]
         grad_emb = gpartial = None
         gparts = _parts(rows, C)
-        binned = _BINNED and offsets_host is not None
+        binned = offsets_host is not None
         if ctx.needs_input_grad[2]:
             grad_emb = torch.empty(rows, C, device=dev, dtype=torch.float32)
             if binned:
-                ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
-                    cap, offsets_host, L, C, S=S, H=H, gridtype=gridtype, align_corners=align)
+                ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offsets_host, L, C)
                 scratch = (torch.empty(ne, device=dev, dtype=torch.int32),
                            torch.empty(nc, device=dev, dtype=torch.int32),
                            torch.empty(npf, device=dev))

@@ -31,16 +31,11 @@ steps (finite-difference normals, csrc/shade.hip) only as the native step.  RNG 
 direction, timestep, SDS noise) use torch's graph-safe Philox offsets, so
 every replay draws fresh numbers.
 """
-import os
-
 import torch
 
 import _dfhip
 from . import field as _field
 from . import native_step as _native
-
-# DFHIP_NATIVE_STEP=0 keeps the autograd body even where the native step applies
-_NATIVE = os.environ.get("DFHIP_NATIVE_STEP", "1") != "0"
 
 
 class GraphedTrainStep:
@@ -50,7 +45,7 @@ class GraphedTrainStep:
         self.H, self.W = data["H"], data["W"]
         # the albedo step as native launches without autograd (nerf/native_step.py)
         self.native = None
-        if (_NATIVE and allow_native and "pose" in data and "intrinsics" in data
+        if (trainer.native_step and allow_native and "pose" in data and "intrinsics" in data
                 and _native.eligible(trainer, shading)):
             self.native = _native.NativeAlbedoStep(trainer, self.H, self.W, shading,
                                                    ambient_ratio)
@@ -97,10 +92,6 @@ class GraphedTrainStep:
                     self.optimizer_in_graph = True
             self.load(data, self.text_z)
             self.stream.wait_stream(torch.cuda.current_stream())
-            # graph branches (quad build and binning on a side stream) only
-            # under DFHIP_STEP_FORK=1 (native_step._FORK, off by default: the
-            # branches overlap but slow the kernels beside them as much)
-            nat.fork = True
             with torch.cuda.stream(self.stream):
                 # dry run (first-use setup outside the capture); neither the
                 # optimizer nor the all-reduce runs.  The communicator is
@@ -120,7 +111,6 @@ class GraphedTrainStep:
                     nat.optimizer_tail()
             torch.cuda.current_stream().wait_stream(self.stream)
         finally:
-            nat.fork = False
             _dfhip.set_kernel_timer(timer)
         model.local_step += 1  # as run_cuda's step in the autograd capture
         model.last_counter = nat.counter

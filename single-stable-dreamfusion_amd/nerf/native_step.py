@@ -59,17 +59,6 @@ import _raymarching
 from _dfhip import call, ptr, stream
 
 
-import os
-
-_STENCIL_BIN = os.environ.get("DFHIP_STENCIL_BIN", "1") != "0"
-# DFHIP_STEP_FORK=1: the captured step runs the corner-quad build and the
-# embedding backward's binning on a second stream, as graph branches beside
-# the march / the field forward.  The branches do overlap (rocprofv3 trace,
-# tools/trace_overlap.py) but slow the kernels beside them by as much as they
-# hide (k_bin 47 -> 118 us beside a field forward 78 -> 100 us): 0.663 ms/step
-# both ways, so one stream is the default.
-_FORK = os.environ.get("DFHIP_STEP_FORK", "0") != "0"
-
 # shading -> dfhip_shading code (csrc/shade.hip); albedo needs no shading kernel
 SHADINGS = {"albedo": 0, "textureless": 1, "lambertian": 2}
 FD_EPS = 1e-2  # network_grid.py:90 finite_difference_normal epsilon
@@ -211,13 +200,12 @@ class NativeAlbedoStep:
         self.mlp_partial = torch.empty(_fieldmlp.backward_parts(fcap) * _fieldmlp.params_count(),
                                        **f32)
         # shaded steps: the embedding backward bins and walks each sample's
-        # 7-point stencil as one group (DFHIP_STENCIL_BIN=0: the 7 M rows one by one)
-        self.stencil_bin = bool(self.shade_code) and _STENCIL_BIN
-        S_, Hb_, gridtype_, align_, _ = self.meta
+        # 7-point stencil as one group (trainer.stencil_bin False: the 7 M rows
+        # one by one)
+        self.stencil_bin = bool(self.shade_code) and bool(getattr(trainer, "stencil_bin", True))
         ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
             cap if self.stencil_bin else fcap, enc.offsets_host, self.L, self.C,
-            group=7 if self.stencil_bin else 1, S=S_, H=Hb_, gridtype=gridtype_,
-            align_corners=align_)
+            group=7 if self.stencil_bin else 1)
         self.bin_scratch = (torch.empty(ne, **i32), torch.empty(nc, **i32),
                             torch.empty(npf, **f32))
         sc = trainer.scaler
@@ -243,14 +231,9 @@ class NativeAlbedoStep:
         self.params = [p for p in m.parameters() if p.requires_grad]
         self.grads = [(p, p.grad) for p in self.params]
         self._emb_launch = None
-        self._emb_bin = self._emb_walk = None
         # dfhip_binned_opts of the embedding backward (tools: a walk trace of
         # the eager twin; None = the library defaults the scratch is sized for)
         self.binned_opts = None
-        # graph branches (set by the capture; the eager twin runs one stream)
-        self.fork = False
-        self._side = None
-        self._bin_forked = False
         # optimizer inside the graph (attach_optimizer): the learning rates
         # live on the device, written by the prologue launch every step
         self.lr_dev = torch.zeros(8, **f32)
@@ -326,16 +309,6 @@ class NativeAlbedoStep:
             with T("grid_quads", rc * (4 + hb) + 16 * self.rows):
                 _fieldmlp.grid_quads(self.encoder.embeddings.detach(), self.encoder.offsets, S,
                                      Hb, gridtype, align, self.table, self.quads)
-        fork = self.fork and _FORK
-        if fork:
-            # the quads depend on the parameters only: a branch beside the march
-            main = torch.cuda.current_stream()
-            if self._side is None:
-                self._side = torch.cuda.Stream()
-            side = self._side
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                quads()
         # march (raymarching.py:161-235, device count): rays + near/far +
         # noise + bitfield in, (ray, offset, count) + one 20-B stage row per
         # sample out; the emit copies the stage into xyz / dir / delta rows
@@ -351,22 +324,11 @@ class NativeAlbedoStep:
         # field (grid.py:38-39 autocast table, network_grid.py:76-87); with a
         # shading, the six finite-difference stencil points of every sample are
         # field rows too (network_grid.py:90-114)
-        if not fork:
-            quads()
+        quads()
         if self.shade_code:
             with T("shading_stencil", 0, md, 12 + 84):
                 call("dfhip_shading_stencil", ptr(self.xyzs), ptr(self.m_dev), cap, FD_EPS,
                      float(m.bound), ptr(self.xyz_field), ptr(self.m7), stream())
-        self._bin_forked = False
-        if fork:
-            main.wait_stream(side)  # the quads
-            if not self.two_pass:
-                # the binning needs only the field rows' positions and count
-                self._emb_launchers()
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    self._emb_bin()
-                self._bin_forked = True
         with T("grid_field_forward", rc * hb, mf, 12 + self.L * self.C * hb + 4 + 3 * hb):
             _fieldmlp.grid_field_forward(self.xyz_field, m.bound, self.table,
                                          self.encoder.offsets, S, Hb, gridtype, align, self.mlp,
@@ -479,13 +441,8 @@ class NativeAlbedoStep:
             live, per = self.m_dev, 12 + 7 * self.L * self.C * 2
         else:
             live, per = self.m_field, 12 + self.L * self.C * 2
-        if self._bin_forked:  # binned on the side stream (body): join, then walk + sum
-            torch.cuda.current_stream().wait_stream(self._side)
-            self._bin_forked = False
-            self._emb_walk()
-        else:
-            with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, live, per):
-                self._emb_launch()
+        with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, live, per):
+            self._emb_launch()
         if self.two_pass and self.lam > 0:
             if self._emb_launch2 is None:
                 m = self.trainer.model
@@ -498,8 +455,7 @@ class NativeAlbedoStep:
                 self._emb_launch2()
 
     def _emb_launchers(self):
-        """The binned embedding backward's launchers: whole (phase 3), and
-        bin (phase 1) / walk + sum (phase 2) for the forked graph."""
+        """The binned embedding backward's launcher (bin, walk and sum)."""
         if self._emb_launch is not None:
             return
         m = self.trainer.model
@@ -517,8 +473,6 @@ class NativeAlbedoStep:
         if self.binned_opts is not None:
             kw["opts"] = self.binned_opts
         self._emb_launch = _gridencoder.binned_launcher(*args, **kw)
-        self._emb_bin = _gridencoder.binned_launcher(*args, phase=1, **kw)
-        self._emb_walk = _gridencoder.binned_launcher(*args, phase=2, **kw)
 
     def time_field(self, reps=5):
         """Eager re-launches of the last step's fused field forward and MLP

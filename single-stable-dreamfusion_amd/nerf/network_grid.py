@@ -7,12 +7,11 @@ background MLP 39 -> 64 -> 3.  Module names, parameter shapes and creation
 order (hence seeded initialisation and state_dict keys) match the reference
 (network_grid.py:35-181).  Its forward goes through the same reference-API
 modules (GridEncoder, FreqEncoder, trunc_exp, raymarching.*) that the
-reference file calls; with DFHIP_FUSED_FIELD=0 and DFHIP_NATIVE_STEP=0 they
-run one by one as separate autograd nodes — the path the reference file
-takes on this package — and bench.py times that path as `module_path`.
+reference file calls; with `fused_field = False` (and the Trainer's
+`native_step = False`) they run one by one as separate autograd nodes — the
+path the reference file takes on this package — and bench.py times that path
+as `module_path`.
 """
-import os
-
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -50,9 +49,6 @@ class MLP(nn.Module):
         return x
 
 
-# DFHIP_FUSED_FIELD=0 runs the encoder and the MLP as separate nodes
-_FUSED_FIELD = os.environ.get("DFHIP_FUSED_FIELD", "1") != "0"
-
 # unit offsets of the central-difference stencil (+x, -x, +y, -y, +z, -z)
 _STENCIL = ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1))
 
@@ -65,6 +61,9 @@ class NeRFNetwork(NeRFRenderer):
         self.encoder, self.in_dim = get_encoder("tiledgrid", input_dim=3, log2_hashmap_size=16,
                                                 desired_resolution=2048 * self.bound)
         self.sigma_net = MLP(self.in_dim, 4, hidden_dim, num_layers, bias=True)
+        # encoder + MLP + heads as one native node (nerf/field.py) where it
+        # applies; False: GridEncoder -> MLP -> trunc_exp / sigmoid one by one
+        self.fused_field = True
         if self.bg_radius > 0:
             self.num_layers_bg = num_layers_bg
             self.hidden_dim_bg = hidden_dim_bg
@@ -79,7 +78,7 @@ class NeRFNetwork(NeRFRenderer):
 
     def common_forward(self, x):
         """x [N, 3] in [-bound, bound] -> sigma [N] (f32), albedo [N, 3]."""
-        if _FUSED_FIELD and _field.eligible(self.encoder, self.sigma_net.net, x):
+        if self.fused_field and _field.eligible(self.encoder, self.sigma_net.net, x):
             # encoder + MLP + heads as one native node (nerf/field.py)
             # capacity-sized samples of the device-count march carry their live count
             return _field.grid_field(x, self.bound, self.encoder, self.sigma_net.net,
@@ -126,7 +125,7 @@ class NeRFNetwork(NeRFRenderer):
         return {"sigma": sigma, "albedo": albedo}
 
     def native_infer_field(self, shading, x):
-        if shading != "albedo" or not _FUSED_FIELD:
+        if shading != "albedo" or not self.fused_field:
             return None
         if not _field.eligible(self.encoder, self.sigma_net.net, x):
             return None

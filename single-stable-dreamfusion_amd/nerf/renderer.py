@@ -10,23 +10,12 @@ against the reference (e.g. its nerf/network_grid.py) subclasses it unchanged.
 The ray-marching ops it calls are the gfx950 kernels behind `raymarching`.
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
 
 import raymarching
 from .utils import custom_meshgrid, safe_normalize
-
-# the fused inference renderer gathers through the corner-quad table
-# (DFHIP_INFER_QUADS=0: 8-byte corner-pair gathers from the f16 table)
-_INFER_QUADS = os.environ.get("DFHIP_INFER_QUADS", "1") != "0"
-# Queue order of the fused inference render (DFHIP_INFER_ORDER=0: pixel
-# order): chunks of 2^_INFER_CHUNK_LOG2 consecutive rays, those passing
-# closest to the scene centre first (1, dfhip_render_ray_order) or those
-# meeting the most occupied cells first (2, dfhip_render_ray_order_occ)
-_INFER_ORDER = int(os.environ.get("DFHIP_INFER_ORDER", "1"))
-_INFER_CHUNK_LOG2 = int(os.environ.get("DFHIP_INFER_CHUNK_LOG2", "6"))
 
 
 def sample_pdf(bins, weights, n_samples, det=False):
@@ -92,6 +81,15 @@ class NeRFRenderer(nn.Module):
         # fused persistent inference render when the field allows it (False: the
         # reference's march / field / composite host loop)
         self.native_infer = True
+        # the fused renderer's gathers: through the corner-quad table (False:
+        # 8-byte corner-pair gathers from the f16 table)
+        self.infer_quads = True
+        # its queue order: chunks of 2^infer_chunk_log2 consecutive rays, those
+        # passing closest to the scene centre first (1, dfhip_render_ray_order),
+        # those meeting the most occupied cells first (2,
+        # dfhip_render_ray_order_occ), or pixel order (0)
+        self.infer_order = 1
+        self.infer_chunk_log2 = 6
         # generator of the density-grid jitter (None: torch's default)
         self.grid_generator = None
 
@@ -372,7 +370,7 @@ class NeRFRenderer(nn.Module):
                 weights += [lin.weight.detach().float().contiguous(),
                             lin.bias.detach().float().contiguous()]
             emb = encoder.embeddings.detach()
-            if _INFER_QUADS:
+            if self.infer_quads:
                 # the f16 cast and its corner quads in one launch (the field's
                 # gathers then take two 16-byte loads per level)
                 table = torch.empty(emb.shape, dtype=torch.half, device=dev)
@@ -393,15 +391,15 @@ class NeRFRenderer(nn.Module):
         # queue order: the chunks of 64 consecutive rays crossing the most of
         # the scene first (their rays do not then finish alone after the queue
         # ran dry: 0.38 -> 0.64 of the frame before it does)
-        cl = _INFER_CHUNK_LOG2
+        cl = int(self.infer_chunk_log2)
         while (N + (1 << cl) - 1) >> cl > 16384:  # the order kernel's chunk limit
             cl += 1
         occ = ((nears.float().contiguous(), fars.float().contiguous(), self.density_bitfield,
                 self.bound, self.cascade, self.grid_size, max_steps)
-               if _INFER_ORDER == 2 else None)
+               if self.infer_order == 2 else None)
         order = (_fieldmlp.render_ray_order(rays_o.float().contiguous(),
                                             rays_d.float().contiguous(), cl, occ=occ)
-                 if _INFER_ORDER and N > 0 else None)
+                 if self.infer_order and N > 0 else None)
         with _dfhip.timed("render_rays_infer", nbytes):
             _fieldmlp.render_rays_infer(
                 rays_o.float().contiguous(), rays_d.float().contiguous(),

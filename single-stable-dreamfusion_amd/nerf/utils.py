@@ -119,8 +119,10 @@ def get_rays_host_pose(poses, intrinsics, H, W, device, out=None):
 
 
 def seed_everything(seed):
+    """utils.py seed_everything, minus PYTHONHASHSEED: the hash seed is fixed
+    when the interpreter starts, so setting it here only reaches child
+    interpreters (none on this path)."""
     random.seed(seed)
-    os.environ["PYTHONHASHSEED"] = str(seed)
     np.random.seed(seed)
     torch.manual_seed(seed)
     torch.cuda.manual_seed(seed)
@@ -274,11 +276,17 @@ class Trainer(object):
         self.dp_in_graph = None
         self._graphs = {}
         # GradScaler + Adam as one native call (nerf/optim.py) when eligible
-        self.native_optimizer = os.environ.get("DFHIP_NATIVE_ADAM", "1") != "0"
+        self.native_optimizer = True
+        # the albedo / shaded steps as the native launch sequence
+        # (nerf/native_step.py) where it applies; False: the autograd body
+        self.native_step = True
+        # shaded native steps: the embedding backward bins and walks each
+        # sample's 7-point finite-difference stencil as one group (False: the
+        # 7 M rows one by one)
+        self.stencil_bin = True
         # entropy regulariser as one native kernel each way (nerf/head.py)
         self.native_losses = True
         self._native_opt = None
-        self._capture_stream = None
         # bench.py kernel timing: called with the GraphedTrainStep in place of
         # its replay (runs the eager twin of the captured launches)
         self.step_hook = None
@@ -292,12 +300,19 @@ class Trainer(object):
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
                     dist.broadcast(t.data, src=0)
+        self._capture_stream = None
         if (self.device.type == "cuda" and dist.is_available() and dist.is_initialized()
                 and dist.get_backend() == "nccl"):
             # the communicator's first collective, issued by every rank here
             # (not inside a step): the graph capture's dry run issues none, so
-            # a capturing step and a replaying step both issue exactly one
-            dist.all_reduce(torch.zeros(1, device=self.device))
+            # a capturing step and a replaying step both issue exactly one.
+            # It runs on the stream the step graphs are captured on, so the
+            # first collective that stream sees is not the captured one.
+            self._capture_stream = torch.cuda.Stream(device=self.device)
+            self._capture_stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._capture_stream):
+                dist.all_reduce(torch.zeros(1, device=self.device))
+            torch.cuda.current_stream().wait_stream(self._capture_stream)
         if getattr(model, "cuda_ray", False) and self.device.type == "cuda":
             # the density-grid jitter draws the same numbers on every rank, so
             # the occupancy grids stay identical without a collective
@@ -527,9 +542,8 @@ class Trainer(object):
         if not self.fused_backward or shading != "albedo" or self.bf16:
             # the two-pass backward and the normal-shaded steps are graphed only
             # as the native step
-            from . import graph as _graph
             from . import native_step as _native
-            return _graph._NATIVE and _native.eligible(self, shading)
+            return self.native_step and _native.eligible(self, shading)
         return (self.graph_step and self.fp16 and self.model.cuda_ray and shading == "albedo"
                 and self.fused_backward and hasattr(self.guidance, "sds_grad")
                 and self.device.type == "cuda")

@@ -146,23 +146,3 @@ def test_graph_training_runs(gpu):
     for a, b in zip(after, before):
         assert torch.isfinite(a).all()
         assert not torch.equal(a, b)
-
-
-def test_graph_branches_match_one_stream(gpu, monkeypatch):
-    """DFHIP_STEP_FORK's graph branches (quad build and binning on a side
-    stream) train bit-identically to the one-stream capture."""
-    import bench
-    from nerf import native_step
-
-    def train(fork):
-        monkeypatch.setattr(native_step, "_FORK", fork)
-        trainer, data = bench.make_trainer(64, 11, 0, 1, True, graph=True)
-        losses = [float(trainer.train_iteration(data.collate([i % 4]))) for i in range(6)]
-        torch.cuda.synchronize()
-        return losses, [p.detach().clone() for p in trainer.model.parameters()]
-
-    l0, p0 = train(False)
-    l1, p1 = train(True)
-    assert l0 == l1
-    for a, b in zip(p0, p1):
-        assert torch.equal(a, b)

@@ -135,3 +135,64 @@ def test_rccl_all_reduce_captured_in_step_graph(gpu):
     assert res["b_plain"], res
     assert res["moved"], res
     assert res["params_equal"] and res["state_equal"] and res["scale_equal"], res
+
+
+def _worker_two_gpus(rank, world, port, out):
+    """One rank per GPU over RCCL, as bench.py --gpus N runs them: the
+    in-graph data-parallel native step (all-reduce + 1/world + Adam captured
+    in the step graph, replayed every step), per-rank cameras; afterwards
+    every rank holds the same replica (bench.replica_check)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "single-stable-dreamfusion_amd")]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dev = torch.device("cuda", rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    import bench
+    tr, data = bench.make_trainer(64, 7, rank, world, True, graph=True)
+    start = [p.detach().clone() for p in tr.model.parameters()]
+    for i in range(12):
+        tr.train_iteration(data.collate([i % 4]))
+    torch.cuda.synchronize()
+    g = next(iter(tr._graphs.values()))
+    rows = [(tr.model.local_step - 1 - i) % 16 for i in range(8)]
+    samples = float(tr.model.step_counter[rows, 0].float().mean().item())
+    identical, per_rank = bench.replica_check(tr, samples, world)
+    res = {"in_graph": g.native is not None and g.native.dp_world == world,
+           "opt_in_graph": bool(g.optimizer_in_graph), "identical": identical,
+           "per_rank": per_rank,
+           "moved": not all(bool(torch.equal(a, b)) for a, b in
+                            zip(start, tr.model.parameters()))}
+    dist.destroy_process_group()
+    if rank == 0:
+        out.put(res)
+
+
+def test_two_gpu_in_graph_nccl_step(gpu):
+    """bench.py --gpus 2's exchange on two devices (skipped on a one-GPU box):
+    every rank replays ONE graph per step holding the RCCL all-reduce, and the
+    replicas stay bit-identical while the ranks render different cameras."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker_two_gpus, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = q.get(timeout=300)
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs)
+    assert res["in_graph"] and res["opt_in_graph"], res
+    assert res["moved"] and res["identical"], res
+    assert len(res["per_rank"]) == 2 and res["per_rank"][0] != res["per_rank"][1], res

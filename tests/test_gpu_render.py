@@ -235,7 +235,6 @@ def test_ray_order_and_ordered_queue(gpu, monkeypatch):
     and N not a multiple of the chunk (the partial chunk anywhere in the
     order)."""
     import _fieldmlp
-    import nerf.renderer as rr
     m = _model(gpu, 8, 1.0, "grid")
     rays_o, rays_d = _rays(gpu, 37, 29, 8)  # N = 1073
     n = rays_o.shape[0]
@@ -259,8 +258,7 @@ def test_ray_order_and_ordered_queue(gpu, monkeypatch):
         assert np.all(np.diff(order)[same] > 0)
     outs = []
     for flag, cl in ((0, 6), (1, 0), (1, 3), (1, 6), (2, 3), (2, 6)):
-        monkeypatch.setattr(rr, "_INFER_ORDER", flag)
-        monkeypatch.setattr(rr, "_INFER_CHUNK_LOG2", cl)
+        m.infer_order, m.infer_chunk_log2 = flag, cl
         (fw, fd, fi), _ = _both(m, rays_o, rays_d, 1)
         outs.append((fw, fd, fi))
     assert (outs[0][0] > 0).sum() > 100

@@ -52,8 +52,7 @@ def main():
             opts = _gridencoder.BinnedOpts(walk_mode=mode)
             gemb = torch.empty(rows, 2, device=dev)
             Hr = int(round(H))  # H rounded: representative cell sizes
-            ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts, S=S,
-                                                                     H=Hr)
+            ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts)
             ent = torch.empty(ne_, dtype=torch.int32, device=dev)
             cnt = torch.empty(nc, dtype=torch.int32, device=dev)
             part = torch.empty(npf, device=dev)

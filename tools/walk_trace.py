@@ -46,7 +46,7 @@ def main():
     gemb = torch.empty(int(offs[-1]), 2, device=dev)
     trace = torch.zeros(8 * 8192, dtype=torch.int64, device=dev)
     opts = _gridencoder.BinnedOpts(walk_mode=args.mode, trace=trace)
-    ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts, S=S, H=16)
+    ne_, nc, npf = _gridencoder.grid_backward_binned_scratch(B, offs, L, 2, opts)
     ent = torch.empty(ne_, dtype=torch.int32, device=dev)
     cnt = torch.empty(nc, dtype=torch.int32, device=dev)
     part = torch.empty(npf, device=dev)
