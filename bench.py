@@ -82,7 +82,8 @@ def env_options(model=None, trainer=None):
     """A/B switches of tools/ scripts, read from the environment here only (the
     package itself takes them as explicit options): DFHIP_NATIVE_STEP,
     DFHIP_NATIVE_ADAM, DFHIP_STENCIL_BIN (Trainer), DFHIP_FUSED_FIELD,
-    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2 (renderer),
+    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2,
+    DFHIP_INFER_HANDOFF (renderer),
     DFHIP_GRID_BWD=atomic (GridEncoder)."""
     env = os.environ
     if trainer is not None:
@@ -101,6 +102,8 @@ def env_options(model=None, trainer=None):
             model.infer_order = int(env["DFHIP_INFER_ORDER"])
         if "DFHIP_INFER_CHUNK_LOG2" in env:
             model.infer_chunk_log2 = int(env["DFHIP_INFER_CHUNK_LOG2"])
+        if "DFHIP_INFER_HANDOFF" in env:
+            model.infer_handoff = int(env["DFHIP_INFER_HANDOFF"])
         enc = getattr(model, "encoder", None)
         if env.get("DFHIP_GRID_BWD") == "atomic" and hasattr(enc, "backward_mode"):
             enc.backward_mode = "atomic"
@@ -287,7 +290,9 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1,
     _dfhip.set_kernel_timer(timer)
     fused_s = timed_frames(frames)
     _dfhip.set_kernel_timer(None)
-    kern = summarize_kernels(timer.records).get("render_rays_infer", {})
+    kall = summarize_kernels(timer.records)
+    kern = kall.get("render_rays_infer", {})
+    korder = kall.get("render_ray_order", {})
     work = model.last_infer_work.cpu().numpy().view(np.uint32)
     samples = int(work[1]) + (int(work[2]) << 32)
     occ = ("occupancy from update_extra_state of a seeded U(-0.5,0.5) grid network (R0)"
@@ -296,7 +301,13 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1,
                        f"T_thresh 1e-4), test-view camera, {occ}",
            "rays_per_frame": n, "ms_per_frame": round(fused_s * 1e3, 3),
            "rays_per_sec": round(n / fused_s, 1), "samples_per_frame": samples,
-           "launch": "one persistent kernel (render_rays_infer)"}
+           "rays_handed_off": int(work[3]),
+           "launch": ("queue order (k_chunk_cost + k_chunk_order, render_ray_order) then the "
+                      "persistent k_render_infer and its straggler pass (rays handed off by "
+                      "waves down to <= %d live lanes once the queue is dry)"
+                      % int(model.infer_handoff))}
+    if korder:
+        out["order_avg_us"] = korder["avg_us"]
     if kern:
         t = kern["avg_us"] * 1e-6
         flops = 12800.0 * samples  # sigma MLP forward, SURVEY §8d

@@ -39,6 +39,14 @@ uint32_t resident_blocks(const void *kernel, int threads, int fallback_per_cu);
 
 inline hipStream_t as_stream(dfhip_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// GridEncoder forward on the fused field's tile gather (csrc/fieldmlp.hip) for
+// D = 3, C = 2, L = 16 with an f16 table and no dy_dx ([B, 32] output, rows
+// [*m_dev, B) zero, raw positions when bound > 0); false when L does not fit.
+bool grid_forward_tiles_f16(const float *inputs, float bound, const void *table,
+                            const int32_t *offsets, uint32_t L, float S, uint32_t H,
+                            uint32_t gridtype, int align_corners, void *outputs, uint32_t B,
+                            const int32_t *m_dev, hipStream_t s);
+
 template <typename T>
 __host__ __device__ inline T ceil_div(T a, T b) { return (a + b - 1) / b; }
 

@@ -775,6 +775,76 @@ extern "C" int dfhip_mlp_backward(int elem, const void *x, const float *w1, cons
     return check_launch(name);
 }
 
+// ------------------------------------------------------------------ grid encoding
+// GridEncoder's forward for the reference's grid shape (16 levels x 2
+// channels, D = 3, f16 table; gridencoder.cu:75-178) on the fused field's
+// gather: a wave takes 16 samples, lane group h gathers levels h, h + 4,
+// h + 8, h + 12 of its sample with the paired-corner loads (50 gathers per
+// sample instead of k_grid_fwd's 128 scalar ones, every level chain of a lane
+// independent), and the features are stored in the natural [B, 32] order —
+// the same half arithmetic, so the same bits.  Rows [M, B) of a
+// capacity-sized batch (M = *m_dev) are written as zeros; bound > 0: raw
+// positions mapped as grid.py:142.
+__global__ __launch_bounds__(256) void k_grid_fwd_tiles(const float *__restrict__ inputs,
+                                                       float bound, const half_t *__restrict__ table,
+                                                       const int32_t *__restrict__ offsets,
+                                                       ge::Levels lv, uint32_t gridtype,
+                                                       int align_corners,
+                                                       half_t *__restrict__ out, uint32_t B,
+                                                       const int32_t *__restrict__ m_dev) {
+    __shared__ LevelK LK[kLevels];
+    stage_levels(LK, offsets, lv, gridtype, align_corners != 0);
+    __syncthreads();
+    const uint32_t M = active_count(m_dev, B);
+    const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t tiles = ceil_div(B, 16u);
+    const float ext = 2.0f * bound;
+    for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles;
+         tile += waves) {
+        const uint32_t sample = tile * 16 + c;
+        if (sample >= B) continue;
+        half8 f{};
+        if (sample < M) {
+            float x[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const float v = inputs[(size_t)sample * 3 + d];
+                x[d] = bound > 0.0f ? (v + bound) / ext : v;
+            }
+            f = grid_features<half_t>(table, LK, align_corners != 0, x, h);
+        }
+        // level 4 q + h, channel ch -> column 2 (4 q + h) + ch
+        uint32_t *row = reinterpret_cast<uint32_t *>(out + (size_t)sample * 32);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            half2v v = half2v{f[2 * q], f[2 * q + 1]};
+            uint32_t w;
+            __builtin_memcpy(&w, &v, 4);
+            row[4 * q + h] = w;
+        }
+    }
+}
+
+namespace dfhip {
+// GridEncoder forward on the tile gather (k_grid_fwd_tiles) for the shapes it
+// takes (gridencoder.hip dispatches here): D = 3, C = 2, L = 16, f16 table,
+// no dy_dx, [B, L C] output.  Returns false when it does not apply.
+bool grid_forward_tiles_f16(const float *inputs, float bound, const void *table,
+                            const int32_t *offsets, uint32_t L, float S, uint32_t H,
+                            uint32_t gridtype, int align_corners, void *outputs, uint32_t B,
+                            const int32_t *m_dev, hipStream_t s) {
+    if (L != (uint32_t)kLevels || B == 0) return false;
+    const ge::Levels lv = ge::make_levels(L, S, H);
+    const uint32_t tiles = ceil_div(B, 16u);
+    const uint32_t want = ceil_div(tiles, 4u);
+    const uint32_t blocks = want < 8192u ? want : 8192u;
+    k_grid_fwd_tiles<<<blocks, 256, 0, s>>>(inputs, bound, (const half_t *)table, offsets, lv,
+                                            gridtype, align_corners, (half_t *)outputs, B, m_dev);
+    return true;
+}
+}  // namespace dfhip
+
 // ------------------------------------------------------------------ fused grid field
 static bool check_field_grid(const char *name, uint32_t L) {
     if (L != 16) {

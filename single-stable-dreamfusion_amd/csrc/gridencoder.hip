@@ -727,6 +727,11 @@ static int grid_fwd_impl(const char *name, int dtype, const float *inputs,
                          dfhip_stream_t stream, SliceDyn dyn = SliceDyn{nullptr, 0.0f}) {
     if (!check_dc(name, D, C, L)) return DFHIP_EINVAL;
     if (B == 0 || L == 0) return DFHIP_OK;
+    // the reference grid's shape under autocast: the tile gather (same bits)
+    if (BLC && dtype == DFHIP_F16 && D == 3 && C == 2 && dy_dx == nullptr &&
+        grid_forward_tiles_f16(inputs, dyn.bound, embeddings, offsets, L, S, H, gridtype,
+                               align_corners, outputs, B, dyn.m_dev, as_stream(stream)))
+        return check_launch(name);
     const Levels lv = make_levels(L, S, H);
     const dim3 g(ceil_div(B, 256u)), blk(256);
     DFHIP_DISPATCH(dtype, name,

@@ -90,6 +90,9 @@ class NeRFRenderer(nn.Module):
         # dfhip_render_ray_order_occ), or pixel order (0)
         self.infer_order = 1
         self.infer_chunk_log2 = 6
+        # with a queue order: once the queue is dry, waves down to this many
+        # live rays hand them to a second launch (csrc/render.hip; 0: off)
+        self.infer_handoff = 16
         # generator of the density-grid jitter (None: torch's default)
         self.grid_generator = None
 
@@ -352,7 +355,7 @@ class NeRFRenderer(nn.Module):
         weights_sum = torch.empty(N, dtype=torch.float32, device=dev)
         depth = torch.empty(N, dtype=torch.float32, device=dev)
         image = torch.empty(N, 3, dtype=torch.float32, device=dev)
-        work = torch.empty(4, dtype=torch.int32, device=dev)
+        work = torch.empty(8, dtype=torch.int32, device=dev)
         noises = torch.rand(N, device=dev) if perturb else None
         # the field's launch operands (f32 weights, the f16 table and its corner
         # quads) are rebuilt only when a parameter changed: consecutive eval
@@ -397,9 +400,22 @@ class NeRFRenderer(nn.Module):
         occ = ((nears.float().contiguous(), fars.float().contiguous(), self.density_bitfield,
                 self.bound, self.cascade, self.grid_size, max_steps)
                if self.infer_order == 2 else None)
-        order = (_fieldmlp.render_ray_order(rays_o.float().contiguous(),
-                                            rays_d.float().contiguous(), cl, occ=occ)
-                 if self.infer_order and N > 0 else None)
+        order = None
+        if self.infer_order and N > 0:
+            # rays in, one cost and one order entry per chunk out
+            with _dfhip.timed("render_ray_order", N * 24 + 8 * ((N >> cl) + 1)):
+                order = _fieldmlp.render_ray_order(rays_o.float().contiguous(),
+                                                   rays_d.float().contiguous(), cl, occ=occ)
+        handoff = int(self.infer_handoff) if order is not None else 0
+        stash = None
+        if handoff:
+            # at most every resident wave's handoff lanes; the kernel keeps a
+            # ray whose slot does not fit
+            cap = min(N, 1 << 18)
+            stash = self.__dict__.get("_infer_stash")
+            if stash is None or stash.shape[0] < cap or stash.device != dev:
+                stash = torch.empty(cap, 12, dtype=torch.int32, device=dev)
+                self.__dict__["_infer_stash"] = stash
         with _dfhip.timed("render_rays_infer", nbytes):
             _fieldmlp.render_rays_infer(
                 rays_o.float().contiguous(), rays_d.float().contiguous(),
@@ -407,7 +423,8 @@ class NeRFRenderer(nn.Module):
                 dt_gamma, max_steps, self.cascade, self.grid_size, self.density_bitfield,
                 T_thresh, table, encoder.offsets, float(np.log2(encoder.per_level_scale)),
                 int(encoder.base_resolution), encoder.gridtype_id, bool(encoder.align_corners),
-                weights, weights_sum, depth, image, work, quads, order=order, chunk_log2=cl)
+                weights, weights_sum, depth, image, work, quads, order=order, chunk_log2=cl,
+                stash=stash, handoff_lanes=handoff)
         self.last_infer_work = work  # work[1] (+ 2^32 work[2]) = samples evaluated
         return weights_sum, depth, image
 

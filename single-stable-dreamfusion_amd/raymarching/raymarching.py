@@ -182,15 +182,29 @@ class _march_rays_train(Function):
 
         # per ray: o, d, near, far, noise in; (id, offset, count) out; bitfield once
         ray_bytes = n * (4 * 9 + 12) + density_bitfield.numel()
+        # exact form: the count pass keeps every sample in a stage buffer and
+        # the emit only copies it into ray order (no second march)
+        stage = (torch.empty(_backend.march_rays_train_stage_floats(n, max_steps), dtype=dt,
+                             device=dev) if exact and dt == torch.float32 else None)
         with _dfhip.timed("march_rays_train_count", ray_bytes):
-            _backend.march_rays_train_count(rays_o, rays_d, density_bitfield, bound, dt_gamma,
-                                            max_steps, n, C, H, nears, fars, rays, step_counter,
-                                            noises, block_sums)
+            if stage is not None:
+                _backend.march_rays_train_count_staged(rays_o, rays_d, density_bitfield, bound,
+                                                       dt_gamma, max_steps, n, C, H, nears, fars,
+                                                       rays, step_counter, noises, block_sums,
+                                                       stage)
+            else:
+                _backend.march_rays_train_count(rays_o, rays_d, density_bitfield, bound,
+                                                dt_gamma, max_steps, n, C, H, nears, fars, rays,
+                                                step_counter, noises, block_sums)
         emit_region = _dfhip.timed("march_rays_train_emit", ray_bytes)
         with emit_region:  # + 32 B per written sample, added below once known
-            _backend.march_rays_train_emit(rays_o, rays_d, density_bitfield, bound, dt_gamma,
-                                           max_steps, n, C, H, cap, nears, fars, xyzs, dirs, deltas,
-                                           rays, noises, block_sums, zero_tail)
+            if stage is not None:
+                _backend.march_rays_train_emit_staged(rays_d, max_steps, n, cap, xyzs, dirs,
+                                                      deltas, rays, block_sums, zero_tail, stage)
+            else:
+                _backend.march_rays_train_emit(rays_o, rays_d, density_bitfield, bound, dt_gamma,
+                                               max_steps, n, C, H, cap, nears, fars, xyzs, dirs,
+                                               deltas, rays, noises, block_sums, zero_tail)
         if exact:
             m = _align_up(int(step_counter[0].item()), align)  # D2H sync (as the reference)
             xyzs, dirs, deltas = xyzs[:m], dirs[:m], deltas[:m]

@@ -1,6 +1,7 @@
 """Host-side cost of the graph-replayed C2 train step: cProfile over K steps
 of bench.py's loop (no sync inside), top functions by own time and by
-cumulative time.  Usage: python tools/host_profile.py [K]"""
+cumulative time.  Usage: python tools/host_profile.py [K] [--module]
+(--module: the eager reference-API module path, bench.py --module-path-child)"""
 import cProfile
 import pstats
 import sys
@@ -16,8 +17,13 @@ import bench  # noqa: E402
 
 
 def main():
-    k = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    tr, data = bench.make_trainer(128, 0, 0, 1, True, graph=True)
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    module = "--module" in sys.argv
+    k = int(args[0]) if args else 200
+    tr, data = bench.make_trainer(128, 0, 0, 1, True, graph=not module)
+    if module:
+        tr.native_step = False
+        tr.model.fused_field = False
 
     def step():
         tr.train_iteration(data.collate([0]))
