@@ -82,8 +82,7 @@ def env_options(model=None, trainer=None):
     """A/B switches of tools/ scripts, read from the environment here only (the
     package itself takes them as explicit options): DFHIP_NATIVE_STEP,
     DFHIP_NATIVE_ADAM, DFHIP_STENCIL_BIN (Trainer), DFHIP_FUSED_FIELD,
-    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2,
-    DFHIP_INFER_HANDOFF (renderer),
+    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2 (renderer),
     DFHIP_GRID_BWD=atomic (GridEncoder)."""
     env = os.environ
     if trainer is not None:
@@ -102,8 +101,7 @@ def env_options(model=None, trainer=None):
             model.infer_order = int(env["DFHIP_INFER_ORDER"])
         if "DFHIP_INFER_CHUNK_LOG2" in env:
             model.infer_chunk_log2 = int(env["DFHIP_INFER_CHUNK_LOG2"])
-        if "DFHIP_INFER_HANDOFF" in env:
-            model.infer_handoff = int(env["DFHIP_INFER_HANDOFF"])
+
         enc = getattr(model, "encoder", None)
         if env.get("DFHIP_GRID_BWD") == "atomic" and hasattr(enc, "backward_mode"):
             enc.backward_mode = "atomic"
@@ -301,11 +299,8 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1,
                        f"T_thresh 1e-4), test-view camera, {occ}",
            "rays_per_frame": n, "ms_per_frame": round(fused_s * 1e3, 3),
            "rays_per_sec": round(n / fused_s, 1), "samples_per_frame": samples,
-           "rays_handed_off": int(work[3]),
-           "launch": ("queue order (k_chunk_cost + k_chunk_order, render_ray_order) then the "
-                      "persistent k_render_infer and its straggler pass (rays handed off by "
-                      "waves down to <= %d live lanes once the queue is dry)"
-                      % int(model.infer_handoff))}
+           "launch": "queue order (k_chunk_cost + k_chunk_order: render_ray_order, "
+                     "order_avg_us) then ONE persistent kernel (k_render_infer, kernel_avg_us)"}
     if korder:
         out["order_avg_us"] = korder["avg_us"]
     if kern:
@@ -686,12 +681,15 @@ def _module_breakdown(csv_files, steps):
 def module_path_leg(args, timeout=300):
     """The C2 step through the reference-API modules one by one — GridEncoder,
     the sigma_net MLP, trunc_exp / sigmoid, composite_rays_train and the ray
-    head as separate autograd nodes, the Trainer's autograd backward — in the
-    reference's own launch structure: eager launches and the host-count march
-    (`step_counter[0].item()`, raymarching.py:224), the samples sliced to the
-    align-rounded count.  The path the reference's nerf/network_grid.py takes
-    on this package.  A child bench times it; a second child runs under
-    rocprofv3 --kernel-trace for the per-kernel breakdown of its last steps."""
+    head as separate autograd nodes, the Trainer's autograd backward — with
+    the reference's host-count march (`step_counter[0].item()`,
+    raymarching.py:224) and the rest of the step replayed from a graph per
+    sample-count bucket (nerf/graph.py BucketedModuleStep).  The path the
+    reference's nerf/network_grid.py takes on this package.  A child bench
+    times it, a second child the same modules launched eagerly op by op
+    (`eager_ms_per_step`, the reference's launch structure exactly), and a
+    third runs under rocprofv3 --kernel-trace for the per-kernel breakdown of
+    the graph-replayed child's last steps."""
     import shutil
     import subprocess
     import tempfile
@@ -699,7 +697,7 @@ def module_path_leg(args, timeout=300):
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
     env["TMPDIR"] = "/tmp"
     cmd = [sys.executable, str(Path(__file__).resolve()), "--steps", str(min(args.steps, 20)),
-           "--warmup", str(args.warmup), "--eager", "--module-path-child", "--no-cpu-baseline",
+           "--warmup", str(args.warmup), "--module-path-child", "--no-cpu-baseline",
            "--no-kernel-timing", "--no-alt-backward", "--no-shading", "--no-infer",
            "--no-traffic", "--no-c5", "--no-module-path"]
     try:
@@ -710,11 +708,20 @@ def module_path_leg(args, timeout=300):
         return {"error": f"{type(e).__name__}"}
     res = {"ms_per_step": d["ms_per_step"], "value": d["value"], "unit": d["unit"],
            "mean_samples_per_step": d["config"]["mean_samples_per_step"],
-           "launch": "eager autograd, host-count march (raymarching.py:224 sync), samples "
-                     "sliced to the align-rounded count",
+           "launch": "host-count march (the reference's raymarching.py:224 sync) run eagerly, "
+                     "then the rest of the step (field modules -> compositing -> head -> loss "
+                     "-> autograd backward) replayed from a HIP graph captured per sample-count "
+                     "bucket (<= 1.25 x the count; nerf/graph.py BucketedModuleStep)",
            "note": "reference-API modules as separate autograd nodes: GridEncoder (binned "
                    "embedding backward), sigma_net MLP (dfhip_mlp_forward / _backward), "
                    "trunc_exp / gaussian / sigmoid in torch, composite_rays_train, ray head"}
+    try:
+        out = subprocess.run(cmd + ["--eager"], env=env, capture_output=True, text=True,
+                             timeout=timeout)
+        line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+        res["eager_ms_per_step"] = json.loads(line)["ms_per_step"]
+    except (subprocess.TimeoutExpired, IndexError, ValueError) as e:
+        res["eager_ms_per_step"] = f"error: {type(e).__name__}"
     rp = shutil.which("rocprofv3")
     if rp is None or args.no_traffic:
         return res
@@ -852,6 +859,15 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if args.module_path_child:
+        # every sample-count bucket's graph captured now, none inside the
+        # timed region (BucketedModuleStep)
+        from nerf.graph import BucketedModuleStep
+        seen = int(trainer.model.step_counter[:, 0].max().item())
+        for g in trainer._graphs.values():
+            if isinstance(g, BucketedModuleStep):
+                g.precapture(2 * seen)
+        torch.cuda.synchronize()
 
     def barrier():
         if world > 1:

@@ -737,9 +737,8 @@ int dfhip_train_step_prologue_lr(const float *pose, float fx, float fy, float cx
  * Out: weights_sum [N], depth [N] (sum of w * t with t measured from the
  *      near plane's rays_t, as composite_rays leaves it), image [N,3] f32 —
  *      every ray written once (no zero-fill needed).
- * work: [8] u32 caller scratch, zeroed here; after the launch work[1] +
- *      2^32 work[2] = number of samples evaluated (work[3]: rays handed off
- *      to the straggler pass, dfhip_render_rays_infer_ordered).
+ * work: [4] u32 caller scratch, zeroed here; after the launch work[1] +
+ *      2^32 work[2] = number of samples evaluated.
  * quads: the table's corner quads [rows, 4] u32 (dfhip_grid_quads of the
  *      same table) or NULL: with them the field gathers each level's corners
  *      0-3 / 4-7 as two 16-byte loads (bit-identical features). */
@@ -778,13 +777,7 @@ int dfhip_render_rays_infer_prof(uint32_t N, const float *rays_o, const float *r
  * first (dfhip_render_ray_order); whole chunks keep a wave's refills on
  * neighbouring pixels.  Outputs are per ray: any order gives the same
  * results; ids >= N (the partial last chunk) and order entries that are not
- * chunk indices are skipped.
- * Straggler hand-off (handoff_lanes > 0): once the queue is dry, a wave down
- * to <= handoff_lanes live rays at a round boundary writes their state
- * (12 u32 each) to stash [stash_cap * 12] u32 (DEVICE, 16-byte aligned
- * scratch) and exits; a second launch continues them with full waves.  The
- * same samples and sums: outputs unchanged bit for bit.  handoff_lanes 0 =
- * one launch (stash unused, may be NULL). */
+ * chunk indices are skipped. */
 int dfhip_render_rays_infer_ordered(uint32_t N, const float *rays_o, const float *rays_d,
                                     const float *nears, const float *fars, const float *noises,
                                     float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
@@ -795,8 +788,7 @@ int dfhip_render_rays_infer_ordered(uint32_t N, const float *rays_o, const float
                                     const float *w2, const float *b2, const float *w3,
                                     const float *b3, float *weights_sum, float *depth,
                                     float *image, uint32_t *work, const void *quads,
-                                    const int32_t *order, uint32_t chunk_log2, uint32_t *stash,
-                                    uint32_t stash_cap, uint32_t handoff_lanes, uint64_t *prof,
+                                    const int32_t *order, uint32_t chunk_log2, uint64_t *prof,
                                     dfhip_stream_t stream);
 /* The queue order for dfhip_render_rays_infer_ordered: the chunks of
  * 2^chunk_log2 consecutive rays (rays_o / rays_d [N, 3] f32) by ascending

@@ -157,7 +157,7 @@ _SIGS = {
     "dfhip_render_rays_infer_ordered": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32,
                                         _u32, _vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                        _u32, _vp, _u32, _u32, _vp, _vp],
+                                        _u32, _vp, _vp],
     "dfhip_render_ray_order": [_vp, _vp, _u32, _u32, _vp, _vp, _vp],
     "dfhip_render_ray_order_occ": [_vp, _vp, _vp, _vp, _vp, _f32, _u32, _u32, _u32, _u32, _u32,
                                    _vp, _vp, _vp],

@@ -249,23 +249,19 @@ def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None, occ=No
 def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                       bitfield, T_thresh, table, offsets, S, base_res, gridtype, align_corners,
                       weights, weights_sum, depth, image, work, quads=None, prof=None,
-                      order=None, chunk_log2=6, stash=None, handoff_lanes=0):
+                      order=None, chunk_log2=6):
     """Inference render of N rays in one launch (csrc/render.hip; reference
     nerf/renderer.py:496-532).  rays_o/rays_d [N, 3] f32, nears/fars [N] f32,
     noises [N] f32 or None, bitfield u8, table [rows, 2] f16, offsets int32.
-    Writes weights_sum [N], depth [N], image [N, 3] f32; work: [8] int32
-    scratch whose words 1, 2 hold the evaluated sample count afterwards
-    (word 3: the rays handed off to the straggler pass);
+    Writes weights_sum [N], depth [N], image [N, 3] f32; work: [4] int32
+    scratch whose words 1, 2 hold the evaluated sample count afterwards;
     quads: the table's corner quads ([rows, 4] int32, grid_quads) or None.
     prof: [10] int64 device tensor receiving the kernel's per-wave phase
     cycles and its wall-clock drain profile (dfhip_render_rays_infer_prof:
     [6], [7] set to -1, the rest to 0 by the caller; tools only) or None.
     order: [ceil(N / 2^chunk_log2)] int32 device permutation of the chunks
     of 2^chunk_log2 consecutive rays, the queue's order (render_ray_order;
-    outputs are per ray, so identical), or None for pixel order.
-    stash / handoff_lanes (with an order): once the queue is dry, waves down to
-    <= handoff_lanes live rays hand them to a second launch through stash
-    ([cap, 12] int32; outputs unchanged)."""
+    outputs are per ray, so identical), or None for pixel order."""
     n = rays_o.shape[0]
     for t, what in ((rays_o, "rays_o"), (rays_d, "rays_d"), (nears, "nears"), (fars, "fars"),
                     (weights_sum, "weights_sum"), (depth, "depth"), (image, "image")):
@@ -289,8 +285,8 @@ def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_
         raise RuntimeError("table must be a [rows, 2] float16 tensor")
     checked(offsets, "offsets", "int")
     checked(work, "work", "int")
-    if work.numel() < 8:
-        raise RuntimeError("work must hold 8 int32")
+    if work.numel() < 4:
+        raise RuntimeError("work must hold 4 int32")
     if quads is not None:
         checked(quads, "quads", "int")
         if tuple(quads.shape) != (table.shape[0], 4):
@@ -308,14 +304,7 @@ def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_
         checked(order, "order", "int")
         if tuple(order.shape) != (-(-n // (1 << chunk_log2)),):
             raise RuntimeError("order must be [ceil(N / 2^chunk_log2)] int32")
-        cap = 0
-        if handoff_lanes:
-            checked(stash, "stash", "int")
-            if stash.dim() != 2 or stash.shape[1] != 12:
-                raise RuntimeError("stash must be [cap, 12] int32")
-            cap = stash.shape[0]
-        call("dfhip_render_rays_infer_ordered", *args, ptr(order), int(chunk_log2),
-             ptr(stash) if handoff_lanes else None, cap, int(handoff_lanes), ptr(prof),
+        call("dfhip_render_rays_infer_ordered", *args, ptr(order), int(chunk_log2), ptr(prof),
              stream())
     elif prof is None:
         call("dfhip_render_rays_infer", *args, stream())

@@ -50,17 +50,8 @@
 //    terminated takes the next ray id (ballot / mbcnt), so there is no host
 //    loop, no compaction, no per-iteration sync, and the xyzs / dirs /
 //    deltas / sigma / rgb intermediates never touch HBM.  Every ray id
-//    taken is finished before its wave exits (or handed off, below), so each
-//    output is written exactly once (no zero-fill).
-//  * straggler hand-off: once the queue is dry the waves drain the rays they
-//    hold, fewer and fewer live lanes each (0.35-0.4 of the kernel's span,
-//    profiled in round 5).  A wave down to <= handoff_lanes live rays at a
-//    round boundary (every staged sample composited, so a ray's whole state
-//    is its march position and its running sums) writes those rays' state to
-//    a stash (48 bytes each) and exits; a second launch of the same kernel
-//    takes the stash as its queue with every lane busy again.  The restored
-//    state continues the same sample sequence, so the outputs are unchanged
-//    bit for bit.
+//    taken is finished before its wave exits, so each output is written
+//    exactly once (no zero-fill).
 #include "march_common.h"
 #include <type_traits>
 #include "field_common.h"
@@ -137,8 +128,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     const float *b3, float *__restrict__ weights_sum, float *__restrict__ depth,
     float *__restrict__ image, uint32_t *__restrict__ work,
     const fm::u32x4 *__restrict__ quads, uint64_t *prof, const int32_t *__restrict__ order,
-    uint32_t chunk_log2, uint32_t *__restrict__ stash, uint32_t stash_cap,
-    uint32_t handoff_lanes, int pass) {
+    uint32_t chunk_log2) {
     __shared__ fm::Weights W;
     __shared__ fm::LevelK LK[fm::kLevels];
     __shared__ Stage stages[kWaves];
@@ -150,12 +140,9 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     Stage &S = stages[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const float inv_extent = 1.0f / (2.0f * k.bound);
-    // queue positions: N, or whole chunks of the order; the straggler pass
-    // (pass 1): the stash entries the first pass wrote (work[3])
+    // queue positions: N, or whole chunks of the order
     const uint32_t nchunks = ceil_div(N, 1u << chunk_log2);
-    const uint32_t Nq = pass ? min(work[3], stash_cap)
-                             : (order ? nchunks << chunk_log2 : N);
-    uint32_t *const qctr = pass ? &work[4] : &work[0];
+    const uint32_t Nq = order ? nchunks << chunk_log2 : N;
 
     int ray = -1;
     bool exhausted = false;
@@ -185,7 +172,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
         if (needm) {
             const int leader = __ffsll((unsigned long long)needm) - 1;
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(qctr, (uint32_t)__popcll(needm));
+            if (lane == leader) base = atomicAdd(&work[0], (uint32_t)__popcll(needm));
             base = __shfl(base, leader);
             if (need) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -195,9 +182,10 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 // (chunks of 2^cl consecutive rays, the costly ones first, so
                 // that they do not finish alone after the queue ran dry); an id
                 // >= N (the partial last chunk, or an order entry that is not a
-                // chunk index) is skipped, never read or written
+                // chunk index: checked before the shift, which could wrap it
+                // onto a valid chunk) is skipped, never read or written
                 uint32_t id = N;
-                if (q < Nq && !pass) {
+                if (q < Nq) {
                     if (order) {
                         const uint32_t ch = (uint32_t)order[q >> chunk_log2];
                         if (ch < nchunks)
@@ -208,25 +196,6 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 }
                 if (q >= Nq) {
                     exhausted = true;
-                } else if (pass) {
-                    // a ray the first pass handed off: its state as it left it
-                    const uint4 *e = reinterpret_cast<const uint4 *>(stash + 12 * (size_t)q);
-                    const uint4 a = e[0], b = e[1], cc = e[2];
-                    ray = (int)a.x;
-                    r = rm::load_ray(rays_o + 3 * (size_t)a.x, rays_d + 3 * (size_t)a.x);
-                    far = fars[a.x];
-                    t = __uint_as_float(a.y);
-                    last_t = __uint_as_float(a.z);
-                    tc = __uint_as_float(a.w);
-                    marched = b.x;
-                    ws = __uint_as_float(b.y);
-                    dp = __uint_as_float(b.z);
-                    cr = __uint_as_float(b.w);
-                    cg = __uint_as_float(cc.x);
-                    cb = __uint_as_float(cc.y);
-                    taken = cc.z;
-                    at_far = false;
-                    finished = false;
                 } else if (id < N) {
                     ray = (int)id;
                     r = rm::load_ray(rays_o + 3 * (size_t)id, rays_d + 3 * (size_t)id);
@@ -249,36 +218,6 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 dry = true;
                 if (lane == 0)
                     atomicMin((unsigned long long *)&prof[7], (unsigned long long)wall_clock64());
-            }
-        }
-        // hand-off: the queue is dry (a lane of this wave found it so) and at
-        // most handoff_lanes rays are left: their state to the stash, the wave
-        // exits; the straggler pass continues them (pass 0 only)
-        if (!pass && handoff_lanes && __ballot(exhausted)) {
-            const uint64_t live = __ballot(ray >= 0);
-            const uint32_t nl = (uint32_t)__popcll(live);
-            if (nl <= handoff_lanes) {  // uniform
-                if (nl) {
-                    const int leader = __ffsll((unsigned long long)live) - 1;
-                    uint32_t base = 0;
-                    if (lane == leader) base = atomicAdd(&work[3], nl);
-                    base = __shfl(base, leader);
-                    if (ray >= 0) {
-                        const uint32_t q = base + __builtin_amdgcn_mbcnt_hi(
-                                                      (uint32_t)(live >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-                        if (q < stash_cap) {  // a full stash: the ray stays here
-                            uint4 *e = reinterpret_cast<uint4 *>(stash + 12 * (size_t)q);
-                            e[0] = make_uint4((uint32_t)ray, __float_as_uint(t),
-                                              __float_as_uint(last_t), __float_as_uint(tc));
-                            e[1] = make_uint4(marched, __float_as_uint(ws), __float_as_uint(dp),
-                                              __float_as_uint(cr));
-                            e[2] = make_uint4(__float_as_uint(cg), __float_as_uint(cb), taken, 0u);
-                            ray = -1;
-                        }
-                    }
-                }
-                exhausted = true;  // the queue is dry for every lane
             }
         }
         // done when no lane holds a ray and the queue is dry for all (a lane
@@ -464,13 +403,8 @@ static int render_infer(
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
     const void *quads, uint64_t *prof, const int32_t *order, uint32_t chunk_log2,
-    uint32_t *stash, uint32_t stash_cap, uint32_t handoff_lanes, dfhip_stream_t stream) {
+    dfhip_stream_t stream) {
     const char *name = "render_rays_infer";
-    if (handoff_lanes > 64 || (handoff_lanes && (!stash || stash_cap == 0))) {
-        set_error("%s: handoff_lanes must be <= 64 and needs a stash (got %u lanes, cap %u)",
-                  name, handoff_lanes, stash_cap);
-        return DFHIP_EINVAL;
-    }
     if (order && (chunk_log2 > 16 || N > 0xFFFFFFFFu - (1u << chunk_log2))) {
         set_error("%s: chunk_log2 must be <= 16 and N + 2^chunk_log2 < 2^32 (got %u, N=%u)",
                   name, chunk_log2, N);
@@ -492,7 +426,7 @@ static int render_infer(
         return DFHIP_EINVAL;
     }
     hipStream_t s = as_stream(stream);
-    if (hipMemsetAsync(work, 0, 8 * sizeof(uint32_t), s) != hipSuccess) return check_launch(name);
+    if (hipMemsetAsync(work, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return check_launch(name);
     if (N == 0) return DFHIP_OK;
     const rm::MarchConsts k = rm::make_consts(bound, dt_gamma, max_steps, C, H);
     const ge::Levels lv = ge::make_levels(L, S, base_res);
@@ -502,12 +436,10 @@ static int render_infer(
         resident_blocks((const void *)rd::k_render_infer, 64 * rd::kWaves, 2);
     const uint32_t want = ceil_div(N, 64u * rd::kWaves);
     const uint32_t blocks = want < resident ? want : resident;
-    for (int pass = 0; pass < (handoff_lanes ? 2 : 1); ++pass)
-        rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
-            N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
-            (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
-            weights_sum, depth, image, work, (const fm::u32x4 *)quads, prof, order, chunk_log2,
-            stash, stash_cap, handoff_lanes, pass);
+    rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
+        N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
+        (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
+        weights_sum, depth, image, work, (const fm::u32x4 *)quads, prof, order, chunk_log2);
     return check_launch(name);
 }
 
@@ -522,7 +454,7 @@ extern "C" int dfhip_render_rays_infer(
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, nullptr,
-                        nullptr, 0, nullptr, 0, 0, stream);
+                        nullptr, 0, stream);
 }
 
 extern "C" int dfhip_render_rays_infer_prof(
@@ -536,7 +468,7 @@ extern "C" int dfhip_render_rays_infer_prof(
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, prof,
-                        nullptr, 0, nullptr, 0, 0, stream);
+                        nullptr, 0, stream);
 }
 
 extern "C" int dfhip_render_rays_infer_ordered(
@@ -546,12 +478,12 @@ extern "C" int dfhip_render_rays_infer_ordered(
     uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
-    const void *quads, const int32_t *order, uint32_t chunk_log2, uint32_t *stash,
-    uint32_t stash_cap, uint32_t handoff_lanes, uint64_t *prof, dfhip_stream_t stream) {
+    const void *quads, const int32_t *order, uint32_t chunk_log2, uint64_t *prof,
+    dfhip_stream_t stream) {
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, prof,
-                        order, chunk_log2, stash, stash_cap, handoff_lanes, stream);
+                        order, chunk_log2, stream);
 }
 
 // ---------------------------------------------------------------- queue order

@@ -212,3 +212,195 @@ class GraphedTrainStep:
             nat.optimizer_tail()
         for p, g in self.grads:
             p.grad = g
+
+
+class BucketedModuleStep:
+    """The train step through the reference-API modules (GridEncoder, the MLP
+    module, trunc_exp / sigmoid, composite_rays_train, the ray head: the
+    Trainer's autograd body with `model.fused_field = False`) in the
+    reference's own structure — the march counts its samples and the host
+    reads the count (`step_counter[0].item()`, raymarching.py:224) — with the
+    rest of the step replayed from a HIP graph instead of launched op by op.
+
+    Per step: the camera rays, near / far, march noise and the staged march
+    (count + emit into persistent buffers) run eagerly; the host reads the
+    sample count M, as the reference does, and picks the smallest row bucket
+    Mb >= M (geometric, ratio 1.25, multiples of 4096); rows [M, Mb) of the
+    samples are zeroed, and the graph captured for Mb replays field ->
+    compositing -> head -> loss -> backward on the [0, Mb) views.  Every
+    per-sample op therefore runs on Mb rows (<= 1.25 M) instead of the
+    capacity N * max_steps, and the modules that honour the device live-row
+    count (GridEncoder, the MLP kernels, the compositing) stop at M.  The
+    gradients are copied into one flat bucket at the end of the graph, so the
+    optimizer sees the same gradient buffers whatever the bucket.  A graph is
+    captured per bucket on first use (a few over a run)."""
+
+    RATIO = 1.25
+    MIN_ROWS = 1 << 16
+    ALIGN = 4096
+
+    def __init__(self, trainer, H, W, shading, ambient_ratio, stream):
+        import _raymarching
+        from .utils import flat_grad_bucket_
+        t = trainer
+        m = t.model
+        dev = t.device
+        self.trainer, self.shading, self.ambient_ratio = t, shading, ambient_ratio
+        self.H, self.W = int(H), int(W)
+        N = self.N = self.H * self.W
+        self.max_steps = int(t.opt.max_steps)
+        cap = self.cap = N * self.max_steps
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.rays_o = torch.empty(1, N, 3, **f32)
+        self.rays_d = torch.empty(1, N, 3, **f32)
+        self.nears = torch.empty(N, **f32)
+        self.fars = torch.empty(N, **f32)
+        self.noises = torch.empty(N, **f32)
+        self.rays = torch.empty(N, 3, device=dev, dtype=torch.int32)
+        self.counter = torch.zeros(2, device=dev, dtype=torch.int32)
+        self.block_sums = torch.empty(_raymarching.march_rays_train_scratch_ints(N), device=dev,
+                                      dtype=torch.int32)
+        self.stage = torch.empty(_raymarching.march_rays_train_stage_floats(N, self.max_steps),
+                                 **f32)
+        self.xyzs = torch.empty(cap, 3, **f32)
+        self.dirs = torch.empty(cap, 3, **f32)
+        self.deltas = torch.empty(cap, 2, **f32)
+        self.params = [p for p in m.parameters() if p.requires_grad]
+        self.grad_bucket = flat_grad_bucket_(self.params)
+        self.grad_views = [p.grad for p in self.params]
+        self.stream = stream
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs = {}  # bucket rows -> (graph, loss)
+        self.text_z = None
+        self._text_src = None
+        self.last_rows = None
+        # (GraphedTrainStep's attributes bench.py reads)
+        self.native = None
+        self.optimizer_in_graph = False
+
+    def bucket(self, m):
+        b = self.MIN_ROWS
+        while b < m:
+            b = -(-int(b * self.RATIO) // self.ALIGN) * self.ALIGN
+        return min(b, self.cap)
+
+    def march(self, data):
+        """The eager part: rays, near / far, noise, the staged march; returns
+        the sample count read on the host (the reference's sync)."""
+        import raymarching
+        import _raymarching
+        from .utils import get_rays_host_pose
+        m = self.trainer.model
+        if "pose" in data and "rays_o" not in data:
+            get_rays_host_pose(data["pose"], data["intrinsics"], self.H, self.W, None,
+                               out=(self.rays_o, self.rays_d))
+        else:
+            self.rays_o.copy_(data["rays_o"], non_blocking=True)
+            self.rays_d.copy_(data["rays_d"], non_blocking=True)
+        ro, rd = self.rays_o.view(-1, 3), self.rays_d.view(-1, 3)
+        # the train path passes no min_near -> the op's default 0.2 (renderer.py:458)
+        _raymarching.near_far_from_aabb(ro, rd, m.aabb_train, self.N, 0.2, self.nears,
+                                        self.fars)
+        torch.rand(self.N, out=self.noises)  # perturb=True in train_step
+        self.counter.zero_()
+        dt_gamma = float(self.trainer.opt.dt_gamma)
+        _raymarching.march_rays_train_count_staged(
+            ro, rd, m.density_bitfield, m.bound, dt_gamma, self.max_steps, self.N, m.cascade,
+            m.grid_size, self.nears, self.fars, self.rays, self.counter, self.noises,
+            self.block_sums, self.stage)
+        _raymarching.march_rays_train_emit_staged(
+            rd, self.max_steps, self.N, self.cap, self.xyzs, self.dirs, self.deltas, self.rays,
+            self.block_sums, 0, self.stage)
+        del raymarching
+        return int(self.counter[0].item())  # D2H sync (raymarching.py:224)
+
+    def _premarched(self, rows):
+        """The march outputs as run_cuda consumes them: [0, rows) views that
+        carry the device live-row count; rays ray-ordered."""
+        from raymarching.raymarching import LIVE_ROWS_ATTR, _ORDERED_ATTR
+        xyzs, dirs, deltas = self.xyzs[:rows], self.dirs[:rows], self.deltas[:rows]
+        for v in (xyzs, dirs, deltas, self.rays):
+            setattr(v, LIVE_ROWS_ATTR, self.counter[:1])
+        setattr(self.rays, _ORDERED_ATTR, True)
+        return (self.nears, self.fars, xyzs, dirs, deltas, self.rays)
+
+    def _body(self, rows):
+        t = self.trainer
+        model = t.model
+        static = {"H": self.H, "W": self.W, "rays_o": self.rays_o, "rays_d": self.rays_d,
+                  "dir": None}
+        model.premarched = self._premarched(rows)
+        try:
+            with torch.autocast("cuda", enabled=t.amp, dtype=t.amp_dtype):
+                _, _, loss = t.train_step(static, shading=self.shading,
+                                          ambient_ratio=self.ambient_ratio, text_z=self.text_z)
+            t.backward_only(loss)
+        finally:
+            model.premarched = None
+        # the gradients into the flat bucket the optimizer steps
+        for p, v in zip(self.params, self.grad_views):
+            if p.grad is not None and p.grad is not v:
+                v.copy_(p.grad)
+        return loss
+
+    def _capture(self, rows):
+        t = self.trainer
+        timer = _dfhip.set_kernel_timer(None)  # no event records inside the graph
+        try:
+            self.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                # dry run: library first-use setup outside the capture
+                for p in self.params:
+                    p.grad = None
+                self._body(rows)
+            for p in self.params:
+                p.grad = None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream, pool=self.pool):
+                loss = self._body(rows).detach()
+            torch.cuda.current_stream().wait_stream(self.stream)
+        finally:
+            _dfhip.set_kernel_timer(timer)
+            for p, v in zip(self.params, self.grad_views):
+                p.grad = v
+        self.graphs[rows] = (g, loss)
+        return self.graphs[rows]
+
+    def step(self, data, text_z):
+        """One step: the eager march, the count, the bucket's graph.  Leaves
+        every parameter's .grad a view of the flat bucket.  Returns the loss."""
+        if self.text_z is None:
+            self.text_z = text_z.detach().clone()
+            self._text_src = text_z.data_ptr()
+        elif text_z.data_ptr() != self._text_src:
+            self.text_z.copy_(text_z, non_blocking=True)
+            self._text_src = text_z.data_ptr()
+        M = self.march(data)
+        rows = self.bucket(max(M, 1))
+        self.last_rows = (M, rows)
+        # rows past the count: zeros (finite inputs for the per-row torch ops)
+        if rows > M:
+            self.xyzs[M:rows].zero_()
+            self.dirs[M:rows].zero_()
+            self.deltas[M:rows].zero_()
+        g = self.graphs.get(rows)
+        if g is None:
+            g = self._capture(rows)
+        g[0].replay()
+        for p, v in zip(self.params, self.grad_views):
+            p.grad = v
+        return g[1]
+
+    def precapture(self, max_rows):
+        """Capture the graphs of every bucket up to bucket(max_rows) now (the
+        bench does this after its warm-up, so no capture lands in a timed
+        region).  The dry runs use the last step's march; their gradients are
+        overwritten by the next replay."""
+        b = self.MIN_ROWS
+        top = self.bucket(max_rows)
+        while True:
+            if b not in self.graphs:
+                self._capture(b)
+            if b >= top:
+                break
+            b = self.bucket(b + 1)

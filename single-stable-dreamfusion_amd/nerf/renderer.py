@@ -90,11 +90,11 @@ class NeRFRenderer(nn.Module):
         # dfhip_render_ray_order_occ), or pixel order (0)
         self.infer_order = 1
         self.infer_chunk_log2 = 6
-        # with a queue order: once the queue is dry, waves down to this many
-        # live rays hand them to a second launch (csrc/render.hip; 0: off)
-        self.infer_handoff = 16
         # generator of the density-grid jitter (None: torch's default)
         self.grid_generator = None
+        # (nears, fars, xyzs, dirs, deltas, rays) of a march already run for
+        # this train step (nerf/graph.py BucketedModuleStep), else None
+        self.premarched = None
 
     # mean_density / mean_count: the sync-free grid refresh leaves them on the
     # device; they are read to the host only when somebody asks (checkpoint,
@@ -248,9 +248,13 @@ class NeRFRenderer(nn.Module):
         N = rays_o.shape[0]
         device = rays_o.device
 
-        # the train path passes no min_near -> the op's default 0.2 (renderer.py:458)
-        nears, fars = raymarching.near_far_from_aabb(
-            rays_o, rays_d, self.aabb_train if self.training else self.aabb_infer)
+        pre = self.premarched if self.training else None
+        if pre is not None:
+            nears, fars = pre[0], pre[1]
+        else:
+            # the train path passes no min_near -> the op's default 0.2 (renderer.py:458)
+            nears, fars = raymarching.near_far_from_aabb(
+                rays_o, rays_d, self.aabb_train if self.training else self.aabb_infer)
         if light_d is None and shading != "albedo":
             # the albedo field never reads the light; the reference draws it
             # anyway (renderer.py:466), which here would be seven tiny launches
@@ -258,11 +262,16 @@ class NeRFRenderer(nn.Module):
 
         results = {}
         if self.training:
-            counter = self.step_counter[self.local_step % 16]
-            counter.zero_()
-            self.local_step += 1
-            self.last_counter = counter
-            if self.device_count_march and force_all_rays and shading == "albedo":
+            if pre is None:
+                counter = self.step_counter[self.local_step % 16]
+                counter.zero_()
+                self.local_step += 1
+                self.last_counter = counter
+            if pre is not None:
+                # the march ran already (its count read on the host by the
+                # caller, which keeps step_counter and local_step)
+                xyzs, dirs, deltas, rays = pre[2:]
+            elif self.device_count_march and force_all_rays and shading == "albedo":
                 # no host sync: capacity-sized samples + device-side count (the
                 # graph-captured train step); only the albedo path, whose
                 # per-sample consumers all stop at the live count
@@ -355,7 +364,7 @@ class NeRFRenderer(nn.Module):
         weights_sum = torch.empty(N, dtype=torch.float32, device=dev)
         depth = torch.empty(N, dtype=torch.float32, device=dev)
         image = torch.empty(N, 3, dtype=torch.float32, device=dev)
-        work = torch.empty(8, dtype=torch.int32, device=dev)
+        work = torch.empty(4, dtype=torch.int32, device=dev)
         noises = torch.rand(N, device=dev) if perturb else None
         # the field's launch operands (f32 weights, the f16 table and its corner
         # quads) are rebuilt only when a parameter changed: consecutive eval
@@ -406,16 +415,6 @@ class NeRFRenderer(nn.Module):
             with _dfhip.timed("render_ray_order", N * 24 + 8 * ((N >> cl) + 1)):
                 order = _fieldmlp.render_ray_order(rays_o.float().contiguous(),
                                                    rays_d.float().contiguous(), cl, occ=occ)
-        handoff = int(self.infer_handoff) if order is not None else 0
-        stash = None
-        if handoff:
-            # at most every resident wave's handoff lanes; the kernel keeps a
-            # ray whose slot does not fit
-            cap = min(N, 1 << 18)
-            stash = self.__dict__.get("_infer_stash")
-            if stash is None or stash.shape[0] < cap or stash.device != dev:
-                stash = torch.empty(cap, 12, dtype=torch.int32, device=dev)
-                self.__dict__["_infer_stash"] = stash
         with _dfhip.timed("render_rays_infer", nbytes):
             _fieldmlp.render_rays_infer(
                 rays_o.float().contiguous(), rays_d.float().contiguous(),
@@ -423,8 +422,7 @@ class NeRFRenderer(nn.Module):
                 dt_gamma, max_steps, self.cascade, self.grid_size, self.density_bitfield,
                 T_thresh, table, encoder.offsets, float(np.log2(encoder.per_level_scale)),
                 int(encoder.base_resolution), encoder.gridtype_id, bool(encoder.align_corners),
-                weights, weights_sum, depth, image, work, quads, order=order, chunk_log2=cl,
-                stash=stash, handoff_lanes=handoff)
+                weights, weights_sum, depth, image, work, quads, order=order, chunk_log2=cl)
         self.last_infer_work = work  # work[1] (+ 2^32 work[2]) = samples evaluated
         return weights_sum, depth, image
 

@@ -284,6 +284,10 @@ class Trainer(object):
         # sample's 7-point finite-difference stencil as one group (False: the
         # 7 M rows one by one)
         self.stencil_bin = True
+        # graph-replayed steps through the reference-API modules (no native
+        # step, model.fused_field False): the host-count march, then a graph
+        # per sample-count bucket (nerf/graph.py BucketedModuleStep)
+        self.module_buckets = True
         # entropy regulariser as one native kernel each way (nerf/head.py)
         self.native_losses = True
         self._native_opt = None
@@ -548,15 +552,36 @@ class Trainer(object):
                 and self.fused_backward and hasattr(self.guidance, "sds_grad")
                 and self.device.type == "cuda")
 
+    def _bucketed(self, shading):
+        """The step runs as BucketedModuleStep: the module path (unfused field)
+        where no native step applies."""
+        from . import native_step as _native
+        if not self.module_buckets or getattr(self.model, "fused_field", True):
+            return False
+        return not (self.native_step and _native.eligible(self, shading))
+
     def _graph_iteration(self, data, shading, ambient_ratio):
         """The step as a HIP-graph replay (nerf/graph.py): captured on the first
         eligible step of each (shading, resolution), replayed afterwards."""
-        from .graph import GraphedTrainStep
+        from .graph import BucketedModuleStep, GraphedTrainStep
         model = self.model
         if self._capture_stream is None:
             self._capture_stream = torch.cuda.Stream(device=self.device)
         key = (shading, ambient_ratio, data["H"], data["W"])
         g = self._graphs.get(key)
+        if g is None and self._bucketed(shading):
+            g = BucketedModuleStep(self, data["H"], data["W"], shading, ambient_ratio,
+                                   self._capture_stream)
+            self._graphs[key] = g
+        if isinstance(g, BucketedModuleStep):
+            text_z = self.text_z[data["dir"]] if self.opt.dir_text else self.text_z
+            row = model.local_step % 16
+            model.local_step += 1
+            loss = g.step(data, text_z)
+            model.step_counter[row].copy_(g.counter)
+            model.last_counter = g.counter
+            self.optimizer_step()
+            return loss
         # the prompt embedding of the view class: an index op whose CPU index is
         # copied from pageable memory (which waits for the stream); the native
         # step's synthetic guidance does not read it

@@ -215,3 +215,67 @@ def test_module_field_matches_fused_field(gpu):
     for a, b in zip(g1, g0):
         rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
         assert rel < 2e-2, rel
+
+
+def _module_trainer(seed=3, res=64):
+    import bench
+    tr, data = bench.make_trainer(res, seed, 0, 1, True, graph=True)
+    tr.native_step = False
+    tr.model.fused_field = False
+    return tr, data
+
+
+def test_bucketed_module_step_rows_do_not_matter(gpu):
+    """BucketedModuleStep's body on the exact sample count M and on the padded
+    bucket (rows [M, Mb) zero, the device live count on the views): the same
+    draws give the same parameter gradients (the dead rows contribute
+    nothing; only the MLP weight-gradient part split differs, f32 order)."""
+    from nerf.graph import BucketedModuleStep
+    tr, data = _module_trainer()
+    for i in range(3):  # a few steps: the occupancy grid and samples move
+        tr.train_iteration(data.collate([i]))
+    g = next(iter(tr._graphs.values()))
+    assert isinstance(g, BucketedModuleStep) and g.graphs
+    batch = data.collate([5])
+    text_z = tr.text_z[batch["dir"]]
+    g.text_z = text_z.detach().clone()
+    M = g.march(batch)
+    Mb = g.bucket(M)
+    assert Mb > M
+    g.xyzs[M:Mb].zero_()
+    g.dirs[M:Mb].zero_()
+    g.deltas[M:Mb].zero_()
+    grads = []
+    for rows in (M, Mb):
+        torch.manual_seed(11)
+        g._body(rows)
+        torch.cuda.synchronize()
+        grads.append([p.grad.detach().clone() for p in g.params])
+        for p, v in zip(g.params, g.grad_views):
+            p.grad = v
+    for a, b in zip(*grads):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-7)
+    assert any(a.abs().sum() > 0 for a in grads[0])
+
+
+def test_bucketed_module_training(gpu):
+    """Graph-replayed module-path steps: captured per bucket, finite losses,
+    the parameters move, every gradient is a view of the flat bucket the
+    optimizer steps, step_counter holds every step's count."""
+    from nerf.graph import BucketedModuleStep
+    tr, data = _module_trainer(seed=4)
+    start = [p.detach().clone() for p in tr.model.parameters()]
+    losses = [float(tr.train_iteration(data.collate([i % 4]))) for i in range(10)]
+    torch.cuda.synchronize()
+    g = next(iter(tr._graphs.values()))
+    assert isinstance(g, BucketedModuleStep) and len(g.graphs) >= 1
+    M, rows = g.last_rows
+    assert M <= rows < 1.25 * max(M, g.MIN_ROWS) + g.ALIGN
+    assert all(np.isfinite(losses))
+    assert int(tr.model.step_counter[:, 0].min()) > 0
+    moved = [not torch.equal(a, b) for a, b in zip(start, tr.model.parameters())]
+    assert all(moved)
+    flat = g.grad_bucket
+    for p, v in zip(g.params, g.grad_views):
+        assert p.grad is v and torch.isfinite(v).all()
+    assert flat.abs().sum() > 0
