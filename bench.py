@@ -650,8 +650,11 @@ MODULE_GROUPS = (  # rocprofv3 kernel name fragment -> breakdown group
 
 
 def _module_breakdown(csv_files, steps):
-    """Kernel time per step by group over the child's last `steps` steps (a
-    step starts at its march count launch) from rocprofv3 kernel traces."""
+    """Kernel time per step by group over `steps` whole steps of the child —
+    from the march count launch `steps + 1` launches before its last one up
+    to that last one (a step starts at its march count launch), so neither
+    the child's final step nor its post-run checks are counted — from
+    rocprofv3 kernel traces."""
     import csv
     ks = []
     for f in csv_files:
@@ -661,10 +664,10 @@ def _module_breakdown(csv_files, steps):
     starts = [t0 for t0, _, n in ks if "k_march_train_count" in n]
     if len(starts) < steps + 1:
         return None
-    b0 = starts[-steps]
+    b0, b1 = starts[-steps - 1], starts[-1]
     groups, top = {}, {}
     for t0, t1, n in ks:
-        if t0 < b0:
+        if t0 < b0 or t0 >= b1:
             continue
         g = next((grp for frag, grp in MODULE_GROUPS if frag in n), "other")
         groups[g] = groups.get(g, 0.0) + (t1 - t0) / 1e3 / steps
@@ -734,7 +737,8 @@ def module_path_leg(args, timeout=300):
             bd = _module_breakdown(list(Path(tmp).rglob("*kernel_trace.csv")), 16)
             if bd:
                 res["breakdown"] = dict(bd, source="rocprofv3 --kernel-trace of the same child "
-                                        "command, its last 16 steps (one density refresh)")
+                                        "command, 16 whole steps before its last (one density "
+                                        "refresh)")
     except subprocess.TimeoutExpired:
         res["breakdown_error"] = "rocprofv3 pass timed out"
     finally:

@@ -215,3 +215,28 @@ def test_native_adam_unit_scale_only_for_bf16():
     off = torch.amp.GradScaler("cuda", enabled=False)
     assert not eligible(opt, off)
     assert not eligible(opt, None, unit_scale=True)
+
+
+def test_module_breakdown_counts_whole_steps(tmp_path):
+    """bench._module_breakdown: per-step kernel time over whole steps between
+    march count launches; the last step and anything after it are ignored."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "single-stable-dreamfusion_amd")]
+    import bench
+    rows = ["Kernel_Name,Start_Timestamp,End_Timestamp"]
+    t = 0
+    for step in range(5):
+        for name, dur in (("void dfhip::rm::k_march_train_count<float, true>()", 50_000),
+                          ("void dfhip::gb::k_bin_fast<true, 1u>()", 40_000),
+                          ("__amd_rocclr_copyBuffer", 5_000)):
+            rows.append(f"\"{name}\",{t},{t + dur}")
+            t += dur + 1_000
+    rows.append(f"\"at::native::reduce_kernel\",{t},{t + 900_000}")  # a post-run check
+    f = tmp_path / "run_kernel_trace.csv"
+    f.write_text("\n".join(rows) + "\n")
+    bd = bench._module_breakdown([f], 3)
+    assert bd["kernel_us_per_step"] == 95.0
+    g = bd["groups_us_per_step"]
+    assert g["march_rays_train"] == 50.0 and g["grid_encode_backward"] == 40.0
+    assert g["runtime_copies_and_fills"] == 5.0 and "torch_elementwise_and_reductions" not in g
+    assert bench._module_breakdown([f], 5) is None
