@@ -573,6 +573,12 @@ typedef struct dfhip_binned_opts {
                                    partial scratch size: pass the same opts to the scratch call) */
     int32_t lane_perm;          /* -1 default (1): per-segment walk lanes take runs in
                                    bit-reversed order (1) or in lane order (0) */
+    int32_t kept_clean;         /* <= 0 default: the call clears the counts scratch's totals /
+                                   plan words with a fill launch; 1: no fill launch — the
+                                   counts scratch is freshly zeroed or was last used by a
+                                   completed binned call with the same B and group (every
+                                   call leaves its totals zero and the walk rewrites every
+                                   bin's plan; the totals' place depends on B) */
     uint64_t *trace;            /* debug: per-workgroup walk timeline, 8 u64 per walk
                                    workgroup {bin, bin + 1, parts, entries, t0, t0, part, t1}
                                    (every walk form); NULL = off */
@@ -629,7 +635,6 @@ int dfhip_adam_amp_step_lr_dev(int count, float *const *params, const float *con
                                float *scale, int32_t *growth_tracker, float *found_inf,
                                float growth_factor, float backoff_factor, int growth_interval,
                                dfhip_stream_t stream);
-
 /* Per-ray tail of run_cuda (nerf/renderer.py:536-551, csrc/head.hip).
  * Forward: bg = sigmoid(W2 relu(W1 freq6(rays_d) + b1) + b2) with the
  * reference's fp16 autocast rounding (w1 != NULL: W1 [64, 39], b1 [64], W2

@@ -148,12 +148,12 @@ class BinnedOpts(ctypes.Structure):
     backward (fields < 0 keep the library default; see include/dfhip.h)."""
     _fields_ = [("walk_mode", ctypes.c_int32), ("fast_bin", ctypes.c_int32),
                 ("walk_groups_per_cu", ctypes.c_int32), ("lane_perm", ctypes.c_int32),
-                ("trace", ctypes.c_void_p)]
+                ("kept_clean", ctypes.c_int32), ("trace", ctypes.c_void_p)]
 
     def __init__(self, walk_mode=-1, fast_bin=-1, walk_groups_per_cu=0, lane_perm=-1,
-                 trace=None):
+                 trace=None, kept_clean=0):
         super().__init__(int(walk_mode), int(fast_bin), int(walk_groups_per_cu), int(lane_perm),
-                         None if trace is None else ptr(trace))
+                         int(kept_clean), None if trace is None else ptr(trace))
 
 
 def _opts_ref(opts):

@@ -79,6 +79,7 @@ struct BinInfo {
     uint32_t G;                          // walk workgroups
     uint32_t lane_perm;                  // walk: bit-reversed lane -> run map (1) or identity
     uint32_t o_totals, o_plan;           // word offsets into `counts` (layout below)
+    uint32_t clear_totals;               // k_sum zeroes the totals after use (kept-clean scratch)
     uint32_t bin0[ge::kMaxLevels + 1];   // first bin of level l (bin0[L] = nbins)
     uint32_t base[ge::kMaxLevels];       // first row of level l
     uint32_t rows[ge::kMaxLevels];       // rows of level l
@@ -103,6 +104,7 @@ struct Opts {
     bool fast_bin;        // mask-form fast binning where it applies
     uint32_t walk_g;      // walk workgroups per CU
     uint32_t lane_perm;   // per-segment walk: bit-reversed lane -> run map
+    bool clean;           // the counts scratch's totals / plan words are zero on entry
     uint64_t *trace;      // debug walk timeline or null
 };
 
@@ -111,6 +113,7 @@ static bool resolve_opts(const dfhip_binned_opts *o, Opts &r) {
     r.fast_bin = true;
     r.walk_g = DFHIP_WALK_G_DEFAULT;
     r.lane_perm = 1;
+    r.clean = false;
     r.trace = nullptr;
     if (!o) return true;
     if (o->walk_mode < -1 || o->walk_mode > 1) {
@@ -127,6 +130,7 @@ static bool resolve_opts(const dfhip_binned_opts *o, Opts &r) {
     r.fast_bin = o->fast_bin != 0;
     if (o->walk_groups_per_cu > 0) r.walk_g = (uint32_t)o->walk_groups_per_cu;
     if (o->lane_perm >= 0) r.lane_perm = o->lane_perm != 0;
+    r.clean = o->kept_clean > 0;
     r.trace = o->trace;
     return true;
 }
@@ -148,6 +152,7 @@ static bool make_bins(const int32_t *offsets_host, uint32_t L, uint32_t C, uint3
     if (L == 0 || L > ge::kMaxLevels || C == 0) return false;
     bi.L = L;
     bi.trace = op.trace;
+    bi.clear_totals = 0;
     bi.shift = slice_shift(C);
     bi.tile = kTile;
     bi.tcap = ceil_div<uint32_t>(cap ? cap : 1u, bi.tile);
@@ -813,6 +818,11 @@ __device__ __forceinline__ void walk_plan(const BinInfo &bi, uint32_t *counts, u
             if (b < nb && p && slot == s) {
                 counts[bi.o_plan + 2 * b] = s;
                 counts[bi.o_plan + 2 * b + 1] = p;
+            } else if (b < nb && !p && slot == 0) {
+                // an empty bin's plan is written too, so the plan needs no
+                // clearing launch (kept-clean scratch)
+                counts[bi.o_plan + 2 * b] = 0;
+                counts[bi.o_plan + 2 * b + 1] = 0;
             }
             carry += (uint32_t)tot;
         }
@@ -1546,13 +1556,25 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
 }
 
 // ---------------------------------------------------------------- 3. sum
+// Every call leaves its counts scratch clean: the bin totals, read last by
+// the walk plan, are zeroed here (k_sum reads only the plan, which the walk
+// rewrites for every bin), so a call with dfhip_binned_opts.kept_clean needs
+// no clearing launch before its binning.
+__device__ __forceinline__ void clear_totals(const BinInfo &bi, uint32_t *counts) {
+    if (!bi.clear_totals) return;
+    const uint32_t n = bi.nbins * kTotSplit;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        counts[bi.o_totals + i] = 0u;
+}
+
 // Every (row, channel) of the table sums its bin's P_b images (slots
 // S_b .. S_b + P_b - 1, recorded by k_walk) in order.
 template <typename out_t>
 __global__ __launch_bounds__(256) void k_sum(const float *__restrict__ partial, BinInfo bi,
                                              uint32_t C, uint32_t total_rows,
-                                             const uint32_t *__restrict__ counts,
+                                             uint32_t *__restrict__ counts,
                                              out_t *__restrict__ out, int accumulate) {
+    clear_totals(bi, counts);
     const uint32_t srows = 1u << bi.shift;
     const size_t img = (size_t)srows * C;
     const uint64_t n = (uint64_t)total_rows * C;
@@ -1585,8 +1607,9 @@ __global__ __launch_bounds__(256) void k_sum(const float *__restrict__ partial, 
 template <typename out_t>
 __global__ __launch_bounds__(256) void k_sum2(const float *__restrict__ partial, BinInfo bi,
                                               uint32_t total_rows,
-                                              const uint32_t *__restrict__ counts,
+                                              uint32_t *__restrict__ counts,
                                               out_t *__restrict__ out, int accumulate) {
+    clear_totals(bi, counts);
     const uint32_t srows = 1u << bi.shift;
     const size_t img = (size_t)srows * 2;
     for (uint32_t row = blockIdx.x * blockDim.x + threadIdx.x; row < total_rows;
@@ -1791,10 +1814,15 @@ static int binned_backward(const char *name, int phase, int grad_dtype, const vo
         }
     }
     const gb::Stencil st{eps, bound};
+    bi.clear_totals = 1u;  // every call leaves the totals zero (see clear_totals)
     if (phase & 1) {
-        // totals (k_bin adds) and the plan (k_walk sets; P = 0: no images)
-        (void)hipMemsetAsync(counts + bi.o_totals, 0,
-                             (size_t)(gb::counts_words(bi) - bi.o_totals) * sizeof(uint32_t), s);
+        // totals (k_bin adds) and the plan (k_walk sets): cleared here, or
+        // kept clean by the previous call's k_sum (the walk writes every
+        // bin's plan; with B = 0 no walk runs, so clear anyway)
+        if (!op.clean || B == 0)
+            (void)hipMemsetAsync(counts + bi.o_totals, 0,
+                                 (size_t)(gb::counts_words(bi) - bi.o_totals) * sizeof(uint32_t),
+                                 s);
         if (B > 0) {
             const uint32_t gbin = bi.tcap < 4096u ? bi.tcap : 4096u;
             const bool pow2 = ge::dyn_pow2(dyn.bound);

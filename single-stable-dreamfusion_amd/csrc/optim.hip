@@ -56,12 +56,13 @@ struct Batch {
     uint8_t lr_slot[kMaxTensors];
 };
 
-// The tensor of this (wave-uniform) block: a scalar scan of the block table.
-__device__ __forceinline__ int block_tensor(const Batch &B) {
+// The tensor of (wave-uniform) chunk blk: a scalar scan of the block table.
+__device__ __forceinline__ int chunk_tensor(const Batch &B, uint32_t blk) {
     int k = 0;
-    while (k + 1 < B.count && B.t[k + 1].block0 <= blockIdx.x) ++k;
+    while (k + 1 < B.count && B.t[k + 1].block0 <= blk) ++k;
     return k;
 }
+__device__ __forceinline__ int block_tensor(const Batch &B) { return chunk_tensor(B, blockIdx.x); }
 
 // Elements [e0, e0 + kPerBlock) of tensor t: vectorised when the tensor's
 // base is 16-byte aligned and the chunk is whole, else element by element.
@@ -107,16 +108,15 @@ __device__ __forceinline__ float adam1(const Tensor &t, const AdamK &k, float g,
     return p;
 }
 
-__global__ __launch_bounds__(kThreads) void k_adam(Batch B, const float *scale,
-                                                   const float *found_inf) {
-    if (*found_inf != 0.0f) return;
-    const int ti = block_tensor(B);
+// The Adam update of chunk blk (kPerBlock elements of one tensor).
+__device__ __forceinline__ void adam_chunk(const Batch &B, uint32_t blk, float scale) {
+    const int ti = chunk_tensor(B, blk);
     const Tensor &t = B.t[ti];
-    const uint64_t e0 = (uint64_t)(blockIdx.x - t.block0) * kPerBlock;
+    const uint64_t e0 = (uint64_t)(blk - t.block0) * kPerBlock;
     // per-tensor constants (the same f32 expressions torch evaluates per element)
     const float step = *t.step + 1.0f;
     AdamK k;
-    k.s = *scale;
+    k.s = scale;
     const float lr = B.lr_dev ? B.lr_dev[B.lr_slot[ti]] : t.lr;
     k.step_size = lr / (1.0f - powf(t.b1, step));
     k.bc2s = sqrtf(1.0f - powf(t.b2, step));
@@ -144,15 +144,20 @@ __global__ __launch_bounds__(kThreads) void k_adam(Batch B, const float *scale,
         });
 }
 
+__global__ __launch_bounds__(kThreads) void k_adam(Batch B, const float *scale,
+                                                   const float *found_inf) {
+    if (*found_inf != 0.0f) return;
+    adam_chunk(B, blockIdx.x, *scale);
+}
+
 // One wave: lane k bumps tensor k's step (independent RMWs in parallel, not
 // one thread's serial chain of dependent global round trips), lane 0 updates
 // the scale.
-__global__ __launch_bounds__(64) void k_finalize(Batch B, float *scale, int32_t *growth_tracker,
-                                                 float *found_inf, float growth_factor,
-                                                 float backoff_factor, int growth_interval) {
-    if (blockIdx.x != 0) return;
-    const int k = (int)threadIdx.x;
-    const bool inf = *found_inf != 0.0f;
+__device__ __forceinline__ void finalize_wave(const Batch &B, bool inf, float *scale,
+                                              int32_t *growth_tracker, float *found_inf,
+                                              float growth_factor, float backoff_factor,
+                                              int growth_interval) {
+    const int k = (int)(threadIdx.x & 63);
     if (!inf && k < B.count) *B.t[k].step += 1.0f;
     if (k != 0) return;
     // ATen amp_update_scale_cuda_kernel
@@ -170,6 +175,14 @@ __global__ __launch_bounds__(64) void k_finalize(Batch B, float *scale, int32_t 
         }
     }
     *found_inf = 0.0f;  // every lane read it above; the wave runs in lock step
+}
+
+__global__ __launch_bounds__(64) void k_finalize(Batch B, float *scale, int32_t *growth_tracker,
+                                                 float *found_inf, float growth_factor,
+                                                 float backoff_factor, int growth_interval) {
+    if (blockIdx.x != 0) return;
+    finalize_wave(B, *found_inf != 0.0f, scale, growth_tracker, found_inf, growth_factor,
+                  backoff_factor, growth_interval);
 }
 
 }  // namespace opt

@@ -337,10 +337,16 @@ class BucketedModuleStep:
             t.backward_only(loss)
         finally:
             model.premarched = None
-        # the gradients into the flat bucket the optimizer steps
+        # the gradients into the flat bucket the optimizer steps: one
+        # multi-tensor copy launch (per-tensor copies were 12 blit launches,
+        # ~58 us per step)
+        dst, src = [], []
         for p, v in zip(self.params, self.grad_views):
             if p.grad is not None and p.grad is not v:
-                v.copy_(p.grad)
+                dst.append(v)
+                src.append(p.grad)
+        if dst:
+            torch._foreach_copy_(dst, src)
         return loss
 
     def _capture(self, rows):

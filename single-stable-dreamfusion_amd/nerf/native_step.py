@@ -206,7 +206,9 @@ class NativeAlbedoStep:
         ne, nc, npf = _gridencoder.grid_backward_binned_scratch(
             cap if self.stencil_bin else fcap, enc.offsets_host, self.L, self.C,
             group=7 if self.stencil_bin else 1)
-        self.bin_scratch = (torch.empty(ne, **i32), torch.empty(nc, **i32),
+        # counts zeroed once: every binned call leaves them clean, so the
+        # step's calls skip the clearing launch (BinnedOpts.kept_clean)
+        self.bin_scratch = (torch.empty(ne, **i32), torch.zeros(nc, **i32),
                             torch.empty(npf, **f32))
         sc = trainer.scaler
         if sc.is_enabled() and sc._scale is None:
@@ -450,7 +452,8 @@ class NativeAlbedoStep:
                 self._emb_launch2 = _gridencoder.binned_launcher(
                     self.d_enc2, self.xyzs, m.bound, self.encoder.offsets, offsets_host,
                     self.encoder.embeddings.grad, self.cap, self.m_dev, 3, self.C, self.L, S,
-                    Hb, gridtype, align, *self.bin_scratch, accumulate=True)
+                    Hb, gridtype, align, *self.bin_scratch, accumulate=True,
+                    opts=self._kept_clean_opts())
             with _dfhip.timed("grid_encode_backward", 4 * self.rows * self.C, self.m_dev, per):
                 self._emb_launch2()
 
@@ -470,9 +473,15 @@ class NativeAlbedoStep:
                     self.encoder.embeddings.grad, self.fcap, self.m_field, 3, self.C, self.L, S,
                     Hb, gridtype, align, *self.bin_scratch)
             kw = {}
-        if self.binned_opts is not None:
-            kw["opts"] = self.binned_opts
+        kw["opts"] = self._kept_clean_opts()
         self._emb_launch = _gridencoder.binned_launcher(*args, **kw)
+
+    def _kept_clean_opts(self):
+        """The call's BinnedOpts (self.binned_opts or the defaults) with
+        kept_clean set: the persistent counts scratch needs no fill launch."""
+        o = self.binned_opts if self.binned_opts is not None else _gridencoder.BinnedOpts()
+        o.kept_clean = 1 if getattr(self.trainer, "kept_clean_scratch", True) else 0
+        return o
 
     def time_field(self, reps=5):
         """Eager re-launches of the last step's fused field forward and MLP

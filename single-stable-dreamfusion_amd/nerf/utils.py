@@ -284,6 +284,9 @@ class Trainer(object):
         # sample's 7-point finite-difference stencil as one group (False: the
         # 7 M rows one by one)
         self.stencil_bin = True
+        # native steps: the embedding backward's counts scratch is kept clean
+        # by every call (no clearing launch per step; BinnedOpts.kept_clean)
+        self.kept_clean_scratch = True
         # graph-replayed steps through the reference-API modules (no native
         # step, model.fused_field False): the host-count march, then a graph
         # per sample-count bucket (nerf/graph.py BucketedModuleStep)

@@ -578,3 +578,50 @@ def test_grid_backward_walk_forms(gpu, mode):
     want = oracle.grid_encode_backward(gl, x01, offs, 2, S, 16, gridtype=1, blc=False)
     np.testing.assert_allclose(gemb.double().cpu().numpy(), want, rtol=1e-5,
                                atol=1e-7 * np.abs(want).max())
+
+
+def test_grid_backward_kept_clean_scratch(gpu):
+    """BinnedOpts.kept_clean (no clearing launch; the native step's form):
+    a run of calls on ONE counts scratch of one capacity B, zeroed once —
+    changing live counts (down to zero), a phase-split call and a default
+    call in between — equals fresh-scratch default calls bit for bit, and the
+    bin totals are zero after every call; the same for stencil groups."""
+    import _gridencoder
+    offs, S, _ = _grid_consts()
+    rows = int(offs[-1])
+    tsz = _gridencoder.grid_backward_binned_tile()
+    nb = int(sum(-(-int(offs[l + 1] - offs[l]) // 8192) for l in range(16)))
+    clean = _gridencoder.BinnedOpts(kept_clean=1)
+    for group, cap, seq in ((1, 30000, ((30000, clean, (3,)), (12345, clean, (3,)),
+                                        (0, clean, (3,)), (29993, clean, (1, 2)),
+                                        (20000, None, (3,)), (29999, clean, (3,)))),
+                            (7, 4000, ((4000, clean, (3,)), (1234, clean, (1, 2)),
+                                       (0, clean, (3,)), (3999, clean, (3,))))):
+        x01 = _samples(cap, 71 + group, edge=False)
+        xr = T(x01 * 2 - 1, gpu)
+        g = (np.random.default_rng(72).normal(size=(group * cap, 32)) * 0.1).astype(np.float16)
+        glbc = T(g, gpu).view(group * cap, 16, 2).transpose(0, 1).contiguous()
+        ne, nc, npf = _gridencoder.grid_backward_binned_scratch(cap, offs, 16, 2, group=group)
+        scratch = (torch.empty(ne, dtype=torch.int32, device=gpu),
+                   torch.zeros(nc, dtype=torch.int32, device=gpu), torch.empty(npf, device=gpu))
+        kw = {} if group == 1 else {"stencil_eps": 1e-2}
+
+        def call(m, opts, phases, sc):
+            m_dev = torch.tensor([m], dtype=torch.int32, device=gpu)
+            out = torch.empty(rows, 2, device=gpu)
+            for ph in phases:
+                _gridencoder.binned_launcher(glbc, xr, 1.0, T(offs, gpu), offs, out, cap, m_dev,
+                                             3, 2, 16, S, 16, 1, False, *sc, phase=ph,
+                                             opts=opts, **kw)()
+            torch.cuda.synchronize()
+            return out.cpu().numpy()
+
+        tiles = -(-cap // tsz)
+        for m, opts, phases in seq:
+            got = call(m, opts, phases, scratch)
+            fresh = (torch.empty(ne, dtype=torch.int32, device=gpu),
+                     torch.empty(nc, dtype=torch.int32, device=gpu).fill_(-1),
+                     torch.empty(npf, device=gpu))
+            assert np.array_equal(got, call(m, None, (3,), fresh)), (group, m, phases)
+            totals = scratch[1][tiles * nb:tiles * nb + nb * 16]
+            assert int(totals.abs().sum()) == 0, (group, m, phases)

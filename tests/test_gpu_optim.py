@@ -51,3 +51,4 @@ def test_native_adam_amp_matches_torch(gpu):
                                        atol=1e-6 * sq)
     # the inf step was skipped (7 updates) and the scale backed off then grew
     assert float(oa.state[pa[0]]["step"]) == 7.0
+
