@@ -81,7 +81,8 @@ def parse():
 def env_options(model=None, trainer=None):
     """A/B switches of tools/ scripts, read from the environment here only (the
     package itself takes them as explicit options): DFHIP_NATIVE_STEP,
-    DFHIP_NATIVE_ADAM, DFHIP_KEPT_CLEAN, DFHIP_STENCIL_BIN (Trainer), DFHIP_FUSED_FIELD,
+    DFHIP_NATIVE_ADAM, DFHIP_KEPT_CLEAN, DFHIP_COMBINED_HEAD, DFHIP_STENCIL_BIN
+    (Trainer), DFHIP_FUSED_FIELD,
     DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2 (renderer),
     DFHIP_GRID_BWD=atomic (GridEncoder)."""
     env = os.environ
@@ -89,6 +90,7 @@ def env_options(model=None, trainer=None):
         for name, attr in (("DFHIP_NATIVE_STEP", "native_step"),
                            ("DFHIP_NATIVE_ADAM", "native_optimizer"),
                            ("DFHIP_KEPT_CLEAN", "kept_clean_scratch"),
+                           ("DFHIP_COMBINED_HEAD", "combined_head"),
                            ("DFHIP_STENCIL_BIN", "stencil_bin")):
             if name in env:
                 setattr(trainer, attr, env[name] != "0")

@@ -680,6 +680,17 @@ int dfhip_ray_head_backward_entropy_loss(uint32_t N, const float *g_image, const
                                          float *gw1, float *gb1, float *gw2, float *gb2,
                                          const float *grad_loss, float lambda, float *loss,
                                          dfhip_stream_t stream);
+/* dfhip_ray_head_forward followed by dfhip_ray_head_backward_entropy_loss, in
+ * two launches instead of three (the backward's recomputed background is the
+ * forward's: outputs bit-identical), for an upstream g_image that does not
+ * depend on out_image (the native step's injected SDS gradient).  Background
+ * network only (w1 != NULL); no bg_color / grad_bg. */
+int dfhip_ray_head_forward_backward_entropy_loss(
+    uint32_t N, const float *ws, const float *depth, const float *image, const float *rays_d,
+    const float *nears, const float *fars, const float *w1, const float *b1, const float *w2,
+    const float *b2, float *out_image, float *out_depth, uint8_t *mask, const float *g_image,
+    float *grad_image, float *grad_ws, float *partial, float *gw1, float *gb1, float *gw2,
+    float *gb2, const float *grad_loss, float lambda, float *loss, dfhip_stream_t stream);
 
 /* nerf/utils.py:386-391 entropy regulariser: loss[0] = lambda * mean(-a log2 a
  * - (1 - a) log2(1 - a)), a = clamp(ws, 1e-5, 1 - 1e-5) (f64 sum); backward

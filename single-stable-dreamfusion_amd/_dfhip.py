@@ -135,6 +135,7 @@ _SIGS = {
                                 _vp, _vp, _vp, _vp, _vp],
     "dfhip_ray_head_backward_entropy": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp],
+    "dfhip_ray_head_forward_backward_entropy_loss": [_u32] + [_vp] * 22 + [_f32, _vp, _vp],
     "dfhip_ray_head_backward_entropy_loss": [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                              _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp,
                                              _vp],

@@ -236,15 +236,28 @@ __device__ __forceinline__ float entropy_grad(uint32_t N, float a, const float *
     return (a >= kLo && a <= kHi) ? scale * (log2f(1.0f - a) - log2f(a)) : 0.0f;
 }
 
+// The forward's operands and outputs for the combined launch (FWD).
+struct FwdIO {
+    const float *depth, *image, *nears, *fars;
+    float *out_image, *out_depth;
+    uint8_t *mask;
+};
+
 // Network backward: the forward is recomputed (four lanes per ray), then the
 // sigmoid and the two f16 Linear layers are run backward and this block's
 // weight-gradient partials (f32 sums over its 64 rays of f16 products) formed
-// from LDS images of the activations.
+// from LDS images of the activations.  FWD: the recomputed forward is also the
+// forward's output (k_head_fwd_net's values bit for bit: the same mlp_part,
+// sigmoid and mix), so a step whose upstream gradient does not depend on
+// pred_rgb (the native step's injected SDS gradient) runs the head as ONE
+// launch instead of two.
+template <bool FWD>
 __global__ __launch_bounds__(kThreads) void k_head_bwd_net(
     uint32_t N, const float *__restrict__ g_image /* [3, N] */, const float *__restrict__ ws,
     const float *__restrict__ rays_d, const float *w1, const float *b1, const float *w2,
     const float *b2, float *__restrict__ grad_image, float *__restrict__ grad_ws,
-    float *__restrict__ partial, const float *__restrict__ ent_grad_loss, float ent_lambda) {
+    float *__restrict__ partial, const float *__restrict__ ent_grad_loss, float ent_lambda,
+    FwdIO io) {
     __shared__ W w;
     __shared__ alignas(16) float s_x[kRays][kIn + 1];
     __shared__ half_t s_dh[kRays][kHid];  // relu-masked hidden grads (f16 values)
@@ -267,6 +280,16 @@ __global__ __launch_bounds__(kThreads) void k_head_bwd_net(
         for (int k = 0; k < 3; ++k) g[k] = g_image[(size_t)k * N + n];
 #pragma unroll
     for (int k = 0; k < 3; ++k) bg[k] = sigmoid16(o[k]);
+    if (FWD && live && q == 0) {  // write_outputs on the recomputed background
+        const float t = 1.0f - ws[n];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            io.out_image[(size_t)k * N + n] = io.image[3 * (size_t)n + k] + t * bg[k];
+        const float nr = io.nears[n], fr = io.fars[n];
+        const float dd = io.depth[n] - nr;
+        io.out_depth[n] = (dd < 0.0f ? 0.0f : dd) / (fr - nr);
+        io.mask[n] = nr < fr ? 1 : 0;
+    }
     if (live && q == 0) {
         // ((1 - ws) * bg) backward: d ws = -(sum_c g_c * bg_c)
         float sw = 0.0f;
@@ -459,7 +482,8 @@ static int ray_head_backward(uint32_t N, const float *g_image, const float *ws,
                              float *grad_image, float *grad_ws, float *grad_bg, float *partial,
                              float *gw1, float *gb1, float *gw2, float *gb2,
                              const float *ent_grad_loss, float ent_lambda,
-                             dfhip_stream_t stream, float *ent_loss = nullptr) {
+                             dfhip_stream_t stream, float *ent_loss = nullptr,
+                             const hd::FwdIO *fwd = nullptr) {
     const char *name = "ray_head_backward";
     if (N == 0) return DFHIP_OK;
     if (!g_image || !ws || !grad_image || !grad_ws) {
@@ -475,9 +499,14 @@ static int ray_head_backward(uint32_t N, const float *g_image, const float *ws,
     hipStream_t s = as_stream(stream);
     if (net) {
         const uint32_t blocks = ceil_div(N, (uint32_t)hd::kRays);
-        hd::k_head_bwd_net<<<blocks, hd::kThreads, 0, s>>>(N, g_image, ws, rays_d, w1, b1, w2, b2,
-                                                  grad_image, grad_ws, partial, ent_grad_loss,
-                                                  ent_lambda);
+        if (fwd)
+            hd::k_head_bwd_net<true><<<blocks, hd::kThreads, 0, s>>>(
+                N, g_image, ws, rays_d, w1, b1, w2, b2, grad_image, grad_ws, partial,
+                ent_grad_loss, ent_lambda, *fwd);
+        else
+            hd::k_head_bwd_net<false><<<blocks, hd::kThreads, 0, s>>>(
+                N, g_image, ws, rays_d, w1, b1, w2, b2, grad_image, grad_ws, partial,
+                ent_grad_loss, ent_lambda, hd::FwdIO{});
         hd::k_head_wsum<<<ceil_div((uint32_t)hd::kParams, 64u) + (ent_loss ? 1u : 0u), 1024, 0,
                           s>>>(partial, blocks, gw1, gb1, gw2, gb2, ws, N, ent_lambda,
                                ent_loss);
@@ -536,6 +565,32 @@ extern "C" int dfhip_ray_head_backward_entropy_loss(
     return ray_head_backward(N, g_image, ws, rays_d, w1, b1, w2, b2, bg_color, grad_image,
                              grad_ws, grad_bg, partial, gw1, gb1, gw2, gb2, grad_loss, lambda,
                              stream, loss);
+}
+
+// dfhip_ray_head_forward + dfhip_ray_head_backward_entropy_loss in two
+// launches instead of three, for an upstream gradient that does not depend on
+// the forward's outputs (background network only).
+extern "C" int dfhip_ray_head_forward_backward_entropy_loss(
+    uint32_t N, const float *ws, const float *depth, const float *image, const float *rays_d,
+    const float *nears, const float *fars, const float *w1, const float *b1, const float *w2,
+    const float *b2, float *out_image, float *out_depth, uint8_t *mask, const float *g_image,
+    float *grad_image, float *grad_ws, float *partial, float *gw1, float *gb1, float *gw2,
+    float *gb2, const float *grad_loss, float lambda, float *loss, dfhip_stream_t stream) {
+    const char *name = "ray_head_forward_backward_entropy_loss";
+    if (!loss) {
+        set_error("%s: null loss", name);
+        return DFHIP_EINVAL;
+    }
+    if (N == 0) return dfhip_entropy_forward(N, ws, lambda, loss, stream);
+    if (!w1 || !depth || !image || !nears || !fars || !out_image || !out_depth || !mask ||
+        !grad_loss) {
+        set_error("%s: null pointer (the combined launch needs the background network)", name);
+        return DFHIP_EINVAL;
+    }
+    const hd::FwdIO io{depth, image, nears, fars, out_image, out_depth, mask};
+    return ray_head_backward(N, g_image, ws, rays_d, w1, b1, w2, b2, nullptr, grad_image,
+                             grad_ws, nullptr, partial, gw1, gb1, gw2, gb2, grad_loss, lambda,
+                             stream, loss, &io);
 }
 
 extern "C" int dfhip_entropy_forward(uint32_t N, const float *ws, float lambda, float *loss,

@@ -353,11 +353,17 @@ class NativeAlbedoStep:
                 self.image)
         # ray head (renderer.py:536-551) and the entropy regulariser (utils.py:386-391)
         bw = self._bg_weights()
-        with T("ray_head_forward", 60 * N):
-            call("dfhip_ray_head_forward", N, ptr(self.ws), ptr(self.depth), ptr(self.image),
-                 ptr(self.rays_d), ptr(self.nears), ptr(self.fars), *[ptr(w) for w in bw],
-                 ptr(self.bg_color), ptr(self.out_image), ptr(self.out_depth), ptr(self.mask),
-                 stream())
+        # the injected SDS gradient does not depend on pred_rgb: with the
+        # background network and the entropy term, the head's forward comes out
+        # of its backward launch (the recomputed background, bit-identical)
+        combined = (not self.two_pass and self.lam > 0 and bw[0] is not None
+                    and bool(getattr(self.trainer, "combined_head", True)))
+        if not combined:
+            with T("ray_head_forward", 60 * N):
+                call("dfhip_ray_head_forward", N, ptr(self.ws), ptr(self.depth), ptr(self.image),
+                     ptr(self.rays_d), ptr(self.nears), ptr(self.fars), *[ptr(w) for w in bw],
+                     ptr(self.bg_color), ptr(self.out_image), ptr(self.out_depth),
+                     ptr(self.mask), stream())
         if self.two_pass:
             if self.lam > 0:
                 call("dfhip_entropy_forward", N, ptr(self.ws), self.lam, ptr(self.loss),
@@ -370,8 +376,15 @@ class NativeAlbedoStep:
         head_args = (N, ptr(self.g_image), ptr(self.ws), ptr(self.rays_d), *[ptr(w) for w in bw],
                      ptr(self.bg_color), ptr(self.grad_image), ptr(self.grad_ws), None,
                      ptr(self.head_partial), *[ptr(g) for g in gbw])
-        with T("ray_head_backward", 60 * N):
-            if self.lam > 0:
+        with T("ray_head_backward", 60 * N if not combined else 120 * N):
+            if combined:
+                call("dfhip_ray_head_forward_backward_entropy_loss", N, ptr(self.ws),
+                     ptr(self.depth), ptr(self.image), ptr(self.rays_d), ptr(self.nears),
+                     ptr(self.fars), *[ptr(w) for w in bw], ptr(self.out_image),
+                     ptr(self.out_depth), ptr(self.mask), ptr(self.g_image), ptr(self.grad_image),
+                     ptr(self.grad_ws), ptr(self.head_partial), *[ptr(g) for g in gbw],
+                     ptr(scale), self.lam, ptr(self.loss), stream())
+            elif self.lam > 0:
                 # head backward + the entropy term's gradient (upstream: the
                 # scale); the entropy loss itself (utils.py:386-391) comes out
                 # of the same launches (dfhip_entropy_forward's value)

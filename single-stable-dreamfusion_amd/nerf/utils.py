@@ -287,6 +287,9 @@ class Trainer(object):
         # native steps: the embedding backward's counts scratch is kept clean
         # by every call (no clearing launch per step; BinnedOpts.kept_clean)
         self.kept_clean_scratch = True
+        # native steps with the injected SDS gradient: the ray head's forward
+        # and backward as one launch (dfhip_ray_head_forward_backward_entropy_loss)
+        self.combined_head = True
         # graph-replayed steps through the reference-API modules (no native
         # step, model.fused_field False): the host-count march, then a graph
         # per sample-count bucket (nerf/graph.py BucketedModuleStep)

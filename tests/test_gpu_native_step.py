@@ -78,6 +78,7 @@ def test_native_step_matches_autograd_step(gpu, fused):
     got = [p.grad.detach().clone() for p in params]
     got_count = nat.counter.clone()
     got_loss = nat.loss.clone()
+    got_rgb = nat.out_image.clone()  # pred_rgb, channel-major [3, N]
     assert int(got_count[0]) > 0
 
     # the autograd step on the same inputs
@@ -94,7 +95,7 @@ def test_native_step_matches_autograd_step(gpu, fused):
     text_z = trainer.text_z[batch["dir"]]
     try:
         with torch.autocast("cuda", dtype=torch.float16):
-            loss = trainer.train_step(eager, "albedo", 1.0, text_z)[2]
+            pred_rgb, _, loss = trainer.train_step(eager, "albedo", 1.0, text_z)
         trainer.backward_only(loss)
     finally:
         model.device_count_march = False
@@ -103,6 +104,8 @@ def test_native_step_matches_autograd_step(gpu, fused):
     torch.cuda.synchronize()
     assert torch.equal(model.last_counter, got_count)
     assert torch.equal(loss.detach().float(), got_loss)
+    # the forward's output (with fused: from the head's combined launch)
+    assert torch.equal(pred_rgb.detach().float().reshape(-1), got_rgb.reshape(-1))
     for p, g in zip(params, got):
         assert p.grad is not None
         assert torch.equal(p.grad, g), (tuple(p.shape), float((p.grad - g).abs().max()))

@@ -265,3 +265,70 @@ def test_ray_order_and_ordered_queue(gpu, monkeypatch):
     for got in outs[1:]:
         for a, b in zip(outs[0], got):
             np.testing.assert_array_equal(a, b)
+
+
+def _f32(x):
+    return np.float32(x)
+
+
+def _fma32(a, b, c):
+    """f32 fmaf restated in f64 (the f32 x f32 product is exact in f64)."""
+    return np.float32(np.float64(a) * np.float64(b) + np.float64(c))
+
+
+def test_ray_order_occupancy_cost_vs_numpy(gpu):
+    """dfhip_render_ray_order_occ (the infer_order = 2 option): each chunk's
+    cost is minus the occupied cells at 16 evenly spaced points of its rays'
+    [near, far), restated in numpy on a hand-built bitfield (one cascade,
+    H = 128, an occupied ball, Morton order via oracle.morton3D); the order is
+    a stable sort of the chunks by 64 cost buckets."""
+    import _fieldmlp
+    import oracle
+    H, bound, cl = 128, 1.0, 6
+    rng = np.random.default_rng(5)
+    cells = np.stack(np.meshgrid(np.arange(H), np.arange(H), np.arange(H), indexing="ij"),
+                     -1).reshape(-1, 3).astype(np.int32)
+    centre = (cells + 0.5) / H * 2 - 1
+    occ = (np.linalg.norm(centre - np.array([0.2, -0.1, 0.0]), axis=1) < 0.55)
+    occ |= rng.random(occ.shape[0]) < 0.02  # scattered occupied cells too
+    bits = np.zeros(H ** 3, np.uint8)
+    bits[oracle.morton3D(cells)] = occ
+    bitfield = np.packbits(bits.reshape(-1, 8), axis=1, bitorder="little").reshape(-1)
+    N = 64 * 40
+    ro = (rng.normal(size=(N, 3)) * 0.1 + np.array([0.0, 0.0, 2.5])).astype(np.float32)
+    tgt = (rng.random((N, 3)) * 1.6 - 0.8).astype(np.float32)
+    rd = tgt - ro
+    rd = (rd / np.linalg.norm(rd, axis=1, keepdims=True)).astype(np.float32)
+    nears = (rng.random(N) * 0.5 + 1.2).astype(np.float32)
+    fars = (nears + rng.random(N) * 2.0).astype(np.float32)
+    fars[::97] = nears[::97]  # rays missing the box: no probes
+    dev = dict(device=gpu)
+    cost = torch.empty(N >> cl, dtype=torch.float32, **dev)
+    order = _fieldmlp.render_ray_order(
+        torch.from_numpy(ro).to(gpu), torch.from_numpy(rd).to(gpu), cl, cost=cost,
+        occ=(torch.from_numpy(nears).to(gpu), torch.from_numpy(fars).to(gpu),
+             torch.from_numpy(bitfield).to(gpu), bound, 1, H, 1024))
+    torch.cuda.synchronize()
+    # numpy restatement of k_chunk_cost_occ (render.hip) for C = 1, H = 128
+    want = np.zeros(N >> cl, np.float64)
+    for r in range(N):
+        n0, f0 = nears[r], fars[r]
+        if not f0 > n0:
+            continue
+        step = _f32(f0 - n0) / _f32(16)
+        for i in range(16):
+            t = _fma32(_f32(i) + _f32(0.5), step, n0)
+            p = [min(max(_fma32(t, rd[r, d], ro[r, d]), _f32(-bound)), _f32(bound))
+                 for d in range(3)]
+            c = [int(min(max(_fma32(p[d], _f32(1.0), _f32(1.0)) * _f32(H / 2), 0.0), H - 1))
+                 for d in range(3)]
+            want[r >> cl] -= float(bits[oracle.morton3D(np.array([c], np.int32))[0]])
+    np.testing.assert_array_equal(cost.cpu().numpy(), want.astype(np.float32))
+    o = order.cpu().numpy()
+    assert sorted(o.tolist()) == list(range(N >> cl))
+    c = want[o]
+    span = c.max() - c.min()
+    b = np.minimum(((c - c.min()) * (64 / span)).astype(np.int64), 63) if span > 0 else 0 * c
+    assert np.all(np.diff(b) >= 0)  # bucket order
+    for k in np.unique(b):  # stable inside a bucket
+        assert np.all(np.diff(o[b == k]) > 0)
