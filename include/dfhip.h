@@ -580,8 +580,9 @@ typedef struct dfhip_binned_opts {
                                    call leaves its totals zero and the walk rewrites every
                                    bin's plan; the totals' place depends on B) */
     uint64_t *trace;            /* debug: per-workgroup walk timeline, 8 u64 per walk
-                                   workgroup {bin, bin + 1, parts, entries, t0, t0, part, t1}
-                                   (every walk form); NULL = off */
+                                   workgroup {bin, XCC id << 32 | HW_ID, parts, entries,
+                                   t0 (start), t1 (plan done), part, t2 (end)} (every walk
+                                   form, wall clock at 100 MHz); NULL = off */
 } dfhip_binned_opts;
 /* dfhip_grid_backward_binned_scratch / dfhip_grid_encode_backward_binned_stencil
  * with per-call options (group 1 = single samples, eps ignored; group 7 =

@@ -86,6 +86,15 @@ struct BinInfo {
     uint64_t *trace;                     // debug: per-workgroup walk timeline (null: off)
 };
 
+// Debug walk timeline: where a workgroup ran — XCC id in the high word, the
+// HW_ID register (CU / SH / SE ids) in the low word.
+__device__ __forceinline__ uint64_t trace_hw_id() {
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    return ((uint64_t)xcc << 32) | hw;
+}
+
 // Walk workgroups per CU (default 3: walk + sum 216.5 -> 208.4 us per C2
 // step against 4; 2 and 5-6 slower).  A/B: dfhip_binned_opts.walk_groups_per_cu.
 #ifndef DFHIP_WALK_G_DEFAULT
@@ -1029,7 +1038,7 @@ __global__ __launch_bounds__(1024) void k_walk(const grad_t *__restrict__ grad, 
         if (threadIdx.x == 0) {
             uint64_t *r = bi.trace + (size_t)blockIdx.x * 8;
             r[0] = b;
-            r[1] = b + 1;
+            r[1] = trace_hw_id();
             r[2] = P;
             r[3] = n_seen;
             r[4] = tr0;
@@ -1545,7 +1554,7 @@ __global__ __launch_bounds__(1024) void k_walk_flat(const grad_t *__restrict__ g
     if (bi.trace && threadIdx.x == 0) {  // debug timeline (dfhip_binned_opts.trace)
         uint64_t *r = bi.trace + (size_t)blockIdx.x * 8;
         r[0] = b;
-        r[1] = b + 1;
+        r[1] = trace_hw_id();
         r[2] = P;
         r[3] = sh_entries;
         r[4] = tr0;

@@ -70,12 +70,20 @@ def report(trace, B, L, offs=None, shift=13):
     print(f"B={B} walk workgroups={len(tr)} span={span:.1f} us")
     print(f"workgroup duration mean {dur.mean():.1f} max {dur.max():.1f} min {dur.min():.1f} us; "
           f"plan mean {plan.mean():.2f} us; start max {us(tr[:, 4]).max():.1f} us")
-    print(f"entries/workgroup mean {tr[:, 3].mean():.0f} max {tr[:, 3].max()}; "
-          f"bins/workgroup mean {(tr[:, 1] - tr[:, 0]).mean():.2f}")
+    print(f"entries/workgroup mean {tr[:, 3].mean():.0f} max {tr[:, 3].max()}")
+    # where the workgroups ran (trace column 1: XCC id << 32 | HW_ID)
+    xcc = (tr[:, 1] >> 32).astype(np.int64)
+    hw = (tr[:, 1] & 0xFFFFFFFF).astype(np.int64)
+    cu = ((hw >> 8) & 0xF) | (((hw >> 12) & 0x1) << 4) | (((hw >> 13) & 0x7) << 5)
+    print("per XCC: workgroups / busy us (sum of durations) / last end us / CUs used")
+    for x in np.unique(xcc):
+        sel = xcc == x
+        print(f"  xcc {x}: {int(sel.sum())} / {dur[sel].sum():.0f} / {us(tr[sel, 7]).max():.1f} / "
+              f"{len(np.unique(cu[sel]))}")
     order = np.argsort(-dur)[:16]
     for i in order:
-        print(f"  slow wg: bins {tr[i, 0]}..{tr[i, 1] - 1} xcd {tr[i, 2]} entries {tr[i, 3]} "
-              f"dur {dur[i]:.1f} us")
+        print(f"  slow wg: bin {tr[i, 0]} parts {tr[i, 2]} xcc {tr[i, 1] >> 32} entries "
+              f"{tr[i, 3]} dur {dur[i]:.1f} us start {us(tr[i, 4]):.1f}")
     ends = np.sort(us(tr[:, 7]))
     print("end-time quantiles (us):", [round(float(np.quantile(ends, q)), 1)
                                       for q in (0.1, 0.25, 0.5, 0.75, 0.9, 1.0)])
@@ -92,7 +100,7 @@ def report(trace, B, L, offs=None, shift=13):
             rows = int(offs[lv + 1] - offs[lv])
             bin0.append(bin0[-1] + ((rows - 1) >> shift) + 1)
         lvl = np.searchsorted(np.array(bin0), tr[:, 0], side="right") - 1
-        one = (tr[:, 1] - tr[:, 0]) == 1
+        one = np.ones(len(tr), bool)  # every workgroup walks one bin
         print("level: entries/us per workgroup (single-bin workgroups); max duration us")
         print("  " + "  ".join(f"{lv}:{(tr[one & (lvl == lv), 3] / dur[one & (lvl == lv)]).mean():.0f}"
                                for lv in range(L) if (one & (lvl == lv)).any()))
