@@ -161,7 +161,8 @@ int dfhip_march_rays_train_emit(int dtype, const void *rays_o, const void *rays_
  * (dfhip_march_rays_train_stage_floats(N, max_steps) floats), and the emit
  * pass copies those rows to the ray-ordered outputs (same conversions to
  * `dtype`, dirs = rays_d) instead of marching each ray a second time.  Same
- * outputs, zero_tail and block_sums contract as the pair above. */
+ * outputs, zero_tail and block_sums contract as the pair above; dirs may be
+ * NULL (not written: a caller that reads rays_d per ray). */
 uint64_t dfhip_march_rays_train_stage_floats(uint32_t N, uint32_t max_steps);
 int dfhip_march_rays_train_count_staged(int dtype, const void *rays_o, const void *rays_d,
                                         const uint8_t *grid, float bound, float dt_gamma,

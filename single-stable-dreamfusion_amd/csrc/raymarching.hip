@@ -197,7 +197,9 @@ __device__ __forceinline__ void zero_rows(scalar_t *xyzs, scalar_t *dirs, scalar
     const scalar_t zero = from_f<scalar_t>(0.0f);
     for (uint64_t row = begin + first; row < end; row += stride) {
         xyzs[3 * row] = zero; xyzs[3 * row + 1] = zero; xyzs[3 * row + 2] = zero;
-        dirs[3 * row] = zero; dirs[3 * row + 1] = zero; dirs[3 * row + 2] = zero;
+        if (dirs) {
+            dirs[3 * row] = zero; dirs[3 * row + 1] = zero; dirs[3 * row + 2] = zero;
+        }
         deltas[2 * row] = zero; deltas[2 * row + 1] = zero;
     }
 }
@@ -248,9 +250,11 @@ __global__ __launch_bounds__(64 * kMarchRaysPerBlock) void k_march_train_emit(
                 xyzs[3 * o + 0] = from_f<scalar_t>(row[0]);
                 xyzs[3 * o + 1] = from_f<scalar_t>(row[1]);
                 xyzs[3 * o + 2] = from_f<scalar_t>(row[2]);
-                dirs[3 * o + 0] = d0;
-                dirs[3 * o + 1] = d1;
-                dirs[3 * o + 2] = d2;
+                if (dirs) {  // uniform: NULL when the caller reads rays_d per ray instead
+                    dirs[3 * o + 0] = d0;
+                    dirs[3 * o + 1] = d1;
+                    dirs[3 * o + 2] = d2;
+                }
                 deltas[2 * o + 0] = from_f<scalar_t>(row[3]);
                 deltas[2 * o + 1] = from_f<scalar_t>(row[4]);
             }
@@ -865,7 +869,7 @@ extern "C" int dfhip_march_rays_train_emit_staged(
         return DFHIP_EINVAL;
     }
     if (N == 0) return DFHIP_OK;
-    if (!stage || !rays_d || !rays || !block_sums) {
+    if (!stage || !rays_d || !rays || !block_sums || !xyzs || !deltas) {
         set_error("march_rays_train_emit_staged: null pointer");
         return DFHIP_EINVAL;
     }
