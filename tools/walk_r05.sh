@@ -2,6 +2,8 @@
 # Round-5 walk study: per-workgroup timelines of the per-segment walk (mode 0)
 # and the resolved stream (mode 3), then SQ counters of both walks and bins,
 # then the binning A/B against lib/libdfhip_${VAR:-ballot4}.so.
+# Record of round 5 only: walk mode 3 and the binning variants it drives were
+# removed from the library in round 6.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
