@@ -83,7 +83,7 @@ def env_options(model=None, trainer=None):
     package itself takes them as explicit options): DFHIP_NATIVE_STEP,
     DFHIP_NATIVE_ADAM, DFHIP_KEPT_CLEAN, DFHIP_COMBINED_HEAD, DFHIP_STENCIL_BIN
     (Trainer), DFHIP_FUSED_FIELD,
-    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2 (renderer),
+    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2, DFHIP_INFER_TILES=0 (renderer),
     DFHIP_GRID_BWD=atomic (GridEncoder)."""
     env = os.environ
     if trainer is not None:
@@ -104,6 +104,8 @@ def env_options(model=None, trainer=None):
             model.infer_order = int(env["DFHIP_INFER_ORDER"])
         if "DFHIP_INFER_CHUNK_LOG2" in env:
             model.infer_chunk_log2 = int(env["DFHIP_INFER_CHUNK_LOG2"])
+        if env.get("DFHIP_INFER_TILES") == "0":  # 64-ray row strips as queue chunks
+            model.infer_tile_w = 0
 
         enc = getattr(model, "encoder", None)
         if env.get("DFHIP_GRID_BWD") == "atomic" and hasattr(enc, "backward_mode"):
@@ -257,6 +259,7 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1,
     opt = main.parse_opt(["--text", "a hamburger", "-O", "--h", str(res), "--w", str(res)])
     torch.manual_seed(seed)
     model = NeRFNetwork(opt).to(device)
+    model.infer_tile_w = res  # the frame's rays are one res x res image: 8 x 8 tile chunks
     env_options(model=model)
     with torch.no_grad():
         model.encoder.embeddings.uniform_(-0.5, 0.5)

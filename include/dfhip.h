@@ -769,13 +769,19 @@ int dfhip_render_rays_infer(uint32_t N, const float *rays_o, const float *rays_d
                             const float *b1, const float *w2, const float *b2, const float *w3,
                             const float *b3, float *weights_sum, float *depth, float *image,
                             uint32_t *work, const void *quads, dfhip_stream_t stream);
-/* The same with a debug profile of this call: prof (DEVICE u64 [10]; caller
- * sets [6] and [7] to UINT64_MAX, the others to 0) receives the per-wave
+/* The same with a debug profile of this call: prof (DEVICE u64 [16 + 16 W];
+ * caller sets [6] and [7] to UINT64_MAX, [10] to W >= 0 and the others to 0)
+ * receives the per-wave
  * phase cycles of the persistent kernel summed {refill, march, field,
  * composite, rounds, field tiles}, then wall-clock ticks (100 MHz): [6] the
  * first wave's start, [7] the first time a wave found the ray queue empty,
  * [8] the last wave's end, [9] the waves' lifetimes summed (the drain after
- * the queue ran dry and the mean resident waves).  NULL = the call above.
+ * the queue ran dry and the mean resident waves), and for the first W waves
+ * of the grid a record at [16 + 16 w]: {start, the time it first found the
+ * queue empty (0: never), end, rounds << 32 | rounds then << 8 | rays held
+ * then, the most samples one of its rays marched, its samples composited,
+ * the most one of its rays composited, its rays retired, its phase cycles
+ * [0..5] as above, 0, 0}.  NULL = the call above.
  * Used by tools/infer_case.py. */
 int dfhip_render_rays_infer_prof(uint32_t N, const float *rays_o, const float *rays_d,
                                  const float *nears, const float *fars, const float *noises,
@@ -790,12 +796,18 @@ int dfhip_render_rays_infer_prof(uint32_t N, const float *rays_o, const float *r
 /* dfhip_render_rays_infer[_prof] taking rays from the queue chunk by chunk:
  * order[0 .. ceil(N / 2^chunk_log2)) (DEVICE int32, a permutation of the
  * chunk indices; NULL = pixel order) names the chunks of 2^chunk_log2
- * consecutive rays in queue order.  The persistent kernel's tail is the rays
- * still marching after the queue ran dry, so a caller puts the costly chunks
- * first (dfhip_render_ray_order); whole chunks keep a wave's refills on
- * neighbouring pixels.  Outputs are per ray: any order gives the same
- * results; ids >= N (the partial last chunk) and order entries that are not
- * chunk indices are skipped. */
+ * consecutive rays in queue order (tile_w > 0: chunk c is the 8 x 8 pixel
+ * tile c of a row-major image tile_w pixels wide, tiles row-major; needs
+ * chunk_log2 6 and N a multiple of 8 tile_w).  The persistent kernel's tail
+ * is the rays still marching after the queue ran dry, so a caller puts the
+ * costly chunks first (dfhip_render_ray_order); whole chunks keep a wave's
+ * refills on neighbouring pixels.  The queue takes the order in blocks of G
+ * positions (G = the launch's resident waves, so every wave's first grab is
+ * in the first block): grab g of a block takes the first half of chunk g and
+ * the second half of chunk G-1-g, so no wave starts on two halves of the
+ * costliest chunks (chunk_log2 >= 1).  Outputs are per ray: any order gives
+ * the same results; ids >= N (the partial last chunk) and order entries that
+ * are not chunk indices are skipped. */
 int dfhip_render_rays_infer_ordered(uint32_t N, const float *rays_o, const float *rays_d,
                                     const float *nears, const float *fars, const float *noises,
                                     float bound, float dt_gamma, uint32_t max_steps, uint32_t C,
@@ -806,8 +818,8 @@ int dfhip_render_rays_infer_ordered(uint32_t N, const float *rays_o, const float
                                     const float *w2, const float *b2, const float *w3,
                                     const float *b3, float *weights_sum, float *depth,
                                     float *image, uint32_t *work, const void *quads,
-                                    const int32_t *order, uint32_t chunk_log2, uint64_t *prof,
-                                    dfhip_stream_t stream);
+                                    const int32_t *order, uint32_t chunk_log2, uint32_t tile_w,
+                                    uint64_t *prof, dfhip_stream_t stream);
 /* The queue order for dfhip_render_rays_infer_ordered: the chunks of
  * 2^chunk_log2 consecutive rays (rays_o / rays_d [N, 3] f32) by ascending
  * summed squared distance of their rays' lines from the scene centre (the
@@ -815,10 +827,12 @@ int dfhip_render_rays_infer_ordered(uint32_t N, const float *rays_o, const float
  * scene first — the cost quantised to 64 levels between its min and max,
  * ties in chunk order (a stable counting sort).  cost: [nchunks] f32
  * scratch (the per-chunk cost, a partial last chunk scaled to a whole one);
- * order: [nchunks] int32 out; nchunks = ceil(N / 2^chunk_log2) <= 16384.
- * Two launches, deterministic. */
+ * order: [nchunks] int32 out; nchunks = ceil(N / 2^chunk_log2) <= 16384;
+ * tile_w: the chunks are 8 x 8 pixel tiles as in
+ * dfhip_render_rays_infer_ordered (0: consecutive rays).  Two launches,
+ * deterministic. */
 int dfhip_render_ray_order(const float *rays_o, const float *rays_d, uint32_t N,
-                           uint32_t chunk_log2, float *cost, int32_t *order,
+                           uint32_t chunk_log2, uint32_t tile_w, float *cost, int32_t *order,
                            dfhip_stream_t stream);
 /* The same order from the occupancy grid (grid: the march's bitfield, C
  * cascades of H^3; nears / fars [N] f32): a chunk's cost is minus the occupied
@@ -827,7 +841,8 @@ int dfhip_render_ray_order(const float *rays_o, const float *rays_d, uint32_t N,
 int dfhip_render_ray_order_occ(const float *rays_o, const float *rays_d, const float *nears,
                                const float *fars, const uint8_t *grid, float bound, uint32_t C,
                                uint32_t H, uint32_t max_steps, uint32_t N, uint32_t chunk_log2,
-                               float *cost, int32_t *order, dfhip_stream_t stream);
+                               uint32_t tile_w, float *cost, int32_t *order,
+                               dfhip_stream_t stream);
 
 /* ---- non-albedo shading of the train step (csrc/shade.hip) ------------------
  * Replaces, for the `textureless` / `lambertian` steps, network_grid.py:90-144

@@ -158,10 +158,10 @@ _SIGS = {
     "dfhip_render_rays_infer_ordered": [_u32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _u32, _u32,
                                         _u32, _vp, _f32, _vp, _vp, _u32, _f32, _u32, _u32, _i32,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                        _u32, _vp, _vp],
-    "dfhip_render_ray_order": [_vp, _vp, _u32, _u32, _vp, _vp, _vp],
+                                        _u32, _u32, _vp, _vp],
+    "dfhip_render_ray_order": [_vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp],
     "dfhip_render_ray_order_occ": [_vp, _vp, _vp, _vp, _vp, _f32, _u32, _u32, _u32, _u32, _u32,
-                                   _vp, _vp, _vp],
+                                   _u32, _vp, _vp, _vp],
     "dfhip_freq_encode_forward": [_vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_freq_encode_backward": [_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp],
     "dfhip_sh_encode_forward": [_i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp],

@@ -207,9 +207,10 @@ def grid_field_backward(enc, xyz, bound, weights, grad_sigma, grad_rgb, d_enc_lb
 
 # ---- fused inference render (march + field + composite, persistent queue)
 
-def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None, occ=None):
+def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None, occ=None, tile_w=0):
     """Queue order of the fused render (csrc/render.hip k_chunk_cost +
-    k_chunk_sort): the chunks of 2^chunk_log2 consecutive rays by ascending
+    k_chunk_sort): the chunks of 2^chunk_log2 consecutive rays (tile_w > 0:
+    8 x 8 pixel tiles of a row-major image tile_w wide) by ascending
     summed squared distance of their lines from the origin.  Returns the
     [ceil(N / 2^chunk_log2)] int32 order (cost: f32 scratch of that size).
     occ = (nears, fars, bitfield, bound, C, H, max_steps): cost from the
@@ -229,7 +230,8 @@ def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None, occ=No
     if cost.numel() < nc or order.numel() < nc:
         raise RuntimeError("cost / order must hold ceil(N / 2^chunk_log2) values")
     if occ is None:
-        call("dfhip_render_ray_order", ptr(rays_o), ptr(rays_d), n, int(chunk_log2), ptr(cost),
+        call("dfhip_render_ray_order", ptr(rays_o), ptr(rays_d), n, int(chunk_log2), int(tile_w),
+             ptr(cost),
              ptr(order), stream())
     else:  # (nears, fars, bitfield, bound, C, H, max_steps): occupancy cost
         nears, fars, bitfield, bound, C, H, max_steps = occ
@@ -242,6 +244,7 @@ def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None, occ=No
             raise RuntimeError("bitfield is smaller than C * H^3 / 8 bytes")
         call("dfhip_render_ray_order_occ", ptr(rays_o), ptr(rays_d), ptr(nears), ptr(fars),
              ptr(bitfield), float(bound), int(C), int(H), int(max_steps), n, int(chunk_log2),
+             int(tile_w),
              ptr(cost), ptr(order), stream())
     return order
 
@@ -249,19 +252,22 @@ def render_ray_order(rays_o, rays_d, chunk_log2=6, cost=None, order=None, occ=No
 def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                       bitfield, T_thresh, table, offsets, S, base_res, gridtype, align_corners,
                       weights, weights_sum, depth, image, work, quads=None, prof=None,
-                      order=None, chunk_log2=6):
+                      order=None, chunk_log2=6, tile_w=0):
     """Inference render of N rays in one launch (csrc/render.hip; reference
     nerf/renderer.py:496-532).  rays_o/rays_d [N, 3] f32, nears/fars [N] f32,
     noises [N] f32 or None, bitfield u8, table [rows, 2] f16, offsets int32.
     Writes weights_sum [N], depth [N], image [N, 3] f32; work: [4] int32
     scratch whose words 1, 2 hold the evaluated sample count afterwards;
     quads: the table's corner quads ([rows, 4] int32, grid_quads) or None.
-    prof: [10] int64 device tensor receiving the kernel's per-wave phase
+    prof: [16 + 16 W] int64 device tensor receiving the kernel's per-wave phase
     cycles and its wall-clock drain profile (dfhip_render_rays_infer_prof:
     [6], [7] set to -1, the rest to 0 by the caller; tools only) or None.
     order: [ceil(N / 2^chunk_log2)] int32 device permutation of the chunks
-    of 2^chunk_log2 consecutive rays, the queue's order (render_ray_order;
-    outputs are per ray, so identical), or None for pixel order."""
+    of 2^chunk_log2 consecutive rays (tile_w > 0: 8 x 8 pixel tiles of a
+    row-major image tile_w wide, as given to render_ray_order), the queue's
+    order (render_ray_order; taken in mirrored halves, see
+    dfhip_render_rays_infer_ordered; outputs are per ray, so identical), or
+    None for pixel order."""
     n = rays_o.shape[0]
     for t, what in ((rays_o, "rays_o"), (rays_d, "rays_d"), (nears, "nears"), (fars, "fars"),
                     (weights_sum, "weights_sum"), (depth, "depth"), (image, "image")):
@@ -298,14 +304,14 @@ def render_rays_infer(rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_
             ptr(depth), ptr(image), ptr(work), ptr(quads))
     if prof is not None:
         checked(prof, "prof", "i64")
-        if prof.numel() < 10:
-            raise RuntimeError("prof must hold 10 int64 values")
+        if prof.numel() < 16 or prof.numel() < 16 + 16 * int(prof[10]):
+            raise RuntimeError("prof must hold 16 + 16 prof[10] int64 values")
     if order is not None:
         checked(order, "order", "int")
         if tuple(order.shape) != (-(-n // (1 << chunk_log2)),):
             raise RuntimeError("order must be [ceil(N / 2^chunk_log2)] int32")
-        call("dfhip_render_rays_infer_ordered", *args, ptr(order), int(chunk_log2), ptr(prof),
-             stream())
+        call("dfhip_render_rays_infer_ordered", *args, ptr(order), int(chunk_log2), int(tile_w),
+             ptr(prof), stream())
     elif prof is None:
         call("dfhip_render_rays_infer", *args, stream())
     else:

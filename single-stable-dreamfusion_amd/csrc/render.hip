@@ -97,6 +97,17 @@ struct Stage {
     float tc[kSlots];  // rays_t after the sample (the depth weight's t)
 };
 
+// Ray j of queue chunk ch: 2^cl consecutive ray ids, or with tile_w (the
+// width of a row-major image; cl = 6) pixel (j / 8, j % 8) of the image's
+// 8 x 8 tile ch (tiles row-major).  A tile's rays stay closer in 3-D than a
+// 64-pixel row strip's, so a wave's field gathers share more cache lines.
+__device__ __forceinline__ uint32_t chunk_ray(uint32_t ch, uint32_t j, uint32_t cl,
+                                              uint32_t tile_w) {
+    if (!tile_w) return (ch << cl) + j;
+    const uint32_t tw = tile_w >> 3, ty = ch / tw, tx = ch - ty * tw;
+    return ((ty << 3) + (j >> 3)) * tile_w + (tx << 3) + (j & 7u);
+}
+
 __device__ __forceinline__ uint32_t pack_h2(half_t a, half_t b) {
     uint16_t ua, ub;
     __builtin_memcpy(&ua, &a, 2);
@@ -128,7 +139,7 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     const float *b3, float *__restrict__ weights_sum, float *__restrict__ depth,
     float *__restrict__ image, uint32_t *__restrict__ work,
     const fm::u32x4 *__restrict__ quads, uint64_t *prof, const int32_t *__restrict__ order,
-    uint32_t chunk_log2) {
+    uint32_t chunk_log2, uint32_t tile_w) {
     __shared__ fm::Weights W;
     __shared__ fm::LevelK LK[fm::kLevels];
     __shared__ Stage stages[kWaves];
@@ -143,6 +154,11 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     // queue positions: N, or whole chunks of the order
     const uint32_t nchunks = ceil_div(N, 1u << chunk_log2);
     const uint32_t Nq = order ? nchunks << chunk_log2 : N;
+    // mirrored halves: in blocks of G chunk positions (G = the grid's waves,
+    // so that the first grab of every wave falls in the first block), grab g
+    // takes the first half of chunk g and the second half of chunk G-1-g
+    // (none for single-ray chunks)
+    const uint32_t G = order && chunk_log2 ? gridDim.x * kWaves : 0u;
 
     int ray = -1;
     bool exhausted = false;
@@ -164,6 +180,9 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     uint64_t c0 = prof ? clock64() : 0;
     const uint64_t w0 = prof ? wall_clock64() : 0;
     bool dry = false;  // this wave has seen the queue empty (prof)
+    uint64_t wdry = 0;     // ... since (wall clock), holding held_dry rays
+    uint32_t held_dry = 0;
+    uint32_t max_marched = 0, max_taken = 0, retired = 0;  // prof records
 
     while (true) {
         // ---- refill lanes without a ray from the global queue
@@ -187,9 +206,14 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 uint32_t id = N;
                 if (q < Nq) {
                     if (order) {
-                        const uint32_t ch = (uint32_t)order[q >> chunk_log2];
-                        if (ch < nchunks)
-                            id = (ch << chunk_log2) + (q & ((1u << chunk_log2) - 1u));
+                        const uint32_t j = q & ((1u << chunk_log2) - 1u);
+                        uint32_t pos = q >> chunk_log2;
+                        if (G && (j >> (chunk_log2 - 1))) {
+                            const uint32_t base = pos / G * G;
+                            pos = base + min(G, nchunks - base) - 1u - (pos - base);
+                        }
+                        const uint32_t ch = (uint32_t)order[pos];
+                        if (ch < nchunks) id = chunk_ray(ch, j, chunk_log2, tile_w);
                     } else {
                         id = q;
                     }
@@ -216,8 +240,9 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
             }
             if (prof && !dry && __ballot(exhausted)) {  // uniform
                 dry = true;
-                if (lane == 0)
-                    atomicMin((unsigned long long *)&prof[7], (unsigned long long)wall_clock64());
+                wdry = wall_clock64();
+                held_dry = (uint32_t)__popcll(__ballot(ray >= 0)) | (uint32_t)(pc[4] << 8);
+                if (lane == 0) atomicMin((unsigned long long *)&prof[7], (unsigned long long)wdry);
             }
         }
         // done when no lane holds a ray and the queue is dry for all (a lane
@@ -363,6 +388,11 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
                 image[3 * (size_t)ray + 1] = cg;
                 image[3 * (size_t)ray + 2] = cb;
                 ray = -1;
+                if (prof) {
+                    max_marched = max(max_marched, marched);
+                    max_taken = max(max_taken, taken);
+                    ++retired;
+                }
             }
         }
         fm::wave_lds_sync();
@@ -372,6 +402,17 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
             c0 = c1;
         }
     }
+    uint32_t tot = samples;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
+    if (prof) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            max_marched = max(max_marched, (uint32_t)__shfl_xor(max_marched, off));
+            max_taken = max(max_taken, (uint32_t)__shfl_xor(max_taken, off));
+            retired += __shfl_xor(retired, off);
+        }
+    }
     if (prof && lane == 0) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) atomicAdd((unsigned long long *)&prof[i], pc[i]);
@@ -379,11 +420,22 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
         atomicMin((unsigned long long *)&prof[6], (unsigned long long)w0);
         atomicMax((unsigned long long *)&prof[8], (unsigned long long)w1);
         atomicAdd((unsigned long long *)&prof[9], (unsigned long long)(w1 - w0));
+        // the per-wave record (prof[10] = records wanted)
+        const uint64_t gw = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        if (gw < prof[10]) {
+            uint64_t *rec = prof + 16 + 16 * gw;
+            rec[0] = w0;
+            rec[1] = wdry;
+            rec[2] = w1;
+            rec[3] = (pc[4] << 32) | held_dry;
+            rec[4] = max_marched;
+            rec[5] = tot;
+            rec[6] = max_taken;
+            rec[7] = retired;
+            for (int i = 0; i < 6; ++i) rec[8 + i] = pc[i];
+        }
     }
     // stats: composited samples (64-bit, low / high words)
-    uint32_t tot = samples;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
     if (lane == 0 && tot) {
         const uint32_t old = atomicAdd(&work[1], tot);
         if (old + tot < old) atomicAdd(&work[2], 1u);
@@ -403,8 +455,13 @@ static int render_infer(
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
     const void *quads, uint64_t *prof, const int32_t *order, uint32_t chunk_log2,
-    dfhip_stream_t stream) {
+    uint32_t tile_w, dfhip_stream_t stream) {
     const char *name = "render_rays_infer";
+    if (order && tile_w && (chunk_log2 != 6 || tile_w % 8 || N % (8 * tile_w))) {
+        set_error("%s: tile chunks need chunk_log2 6, tile_w a multiple of 8 and N of 8 tile_w "
+                  "(got chunk_log2 %u, tile_w %u, N %u)", name, chunk_log2, tile_w, N);
+        return DFHIP_EINVAL;
+    }
     if (order && (chunk_log2 > 16 || N > 0xFFFFFFFFu - (1u << chunk_log2))) {
         set_error("%s: chunk_log2 must be <= 16 and N + 2^chunk_log2 < 2^32 (got %u, N=%u)",
                   name, chunk_log2, N);
@@ -439,7 +496,8 @@ static int render_infer(
     rd::k_render_infer<<<blocks, 64 * rd::kWaves, 0, s>>>(
         N, rays_o, rays_d, nears, fars, noises, k, grid, max_steps, T_thresh,
         (const half_t *)table, offsets, lv, gridtype, align_corners, w1, b1, w2, b2, w3, b3,
-        weights_sum, depth, image, work, (const fm::u32x4 *)quads, prof, order, chunk_log2);
+        weights_sum, depth, image, work, (const fm::u32x4 *)quads, prof, order, chunk_log2,
+        tile_w);
     return check_launch(name);
 }
 
@@ -454,7 +512,7 @@ extern "C" int dfhip_render_rays_infer(
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, nullptr,
-                        nullptr, 0, stream);
+                        nullptr, 0, 0, stream);
 }
 
 extern "C" int dfhip_render_rays_infer_prof(
@@ -468,7 +526,7 @@ extern "C" int dfhip_render_rays_infer_prof(
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, prof,
-                        nullptr, 0, stream);
+                        nullptr, 0, 0, stream);
 }
 
 extern "C" int dfhip_render_rays_infer_ordered(
@@ -478,12 +536,12 @@ extern "C" int dfhip_render_rays_infer_ordered(
     uint32_t L, float S, uint32_t base_res, uint32_t gridtype, int align_corners,
     const float *w1, const float *b1, const float *w2, const float *b2, const float *w3,
     const float *b3, float *weights_sum, float *depth, float *image, uint32_t *work,
-    const void *quads, const int32_t *order, uint32_t chunk_log2, uint64_t *prof,
-    dfhip_stream_t stream) {
+    const void *quads, const int32_t *order, uint32_t chunk_log2, uint32_t tile_w,
+    uint64_t *prof, dfhip_stream_t stream) {
     return render_infer(N, rays_o, rays_d, nears, fars, noises, bound, dt_gamma, max_steps, C, H,
                         grid, T_thresh, table, offsets, L, S, base_res, gridtype, align_corners,
                         w1, b1, w2, b2, w3, b3, weights_sum, depth, image, work, quads, prof,
-                        order, chunk_log2, stream);
+                        order, chunk_log2, tile_w, stream);
 }
 
 // ---------------------------------------------------------------- queue order
@@ -498,13 +556,14 @@ constexpr uint32_t kMaxOrderChunks = 16384;  // one workgroup's counting sort (6
 __global__ __launch_bounds__(256) void k_chunk_cost(const float *__restrict__ rays_o,
                                                     const float *__restrict__ rays_d, uint32_t N,
                                                     uint32_t cl, uint32_t nchunks,
-                                                    float *__restrict__ cost) {
+                                                    float *__restrict__ cost, uint32_t tile_w) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (ch >= nchunks) return;  // uniform per wave
     const uint32_t r0 = ch << cl, r1 = min(N, (ch + 1) << cl);
     float acc = 0.0f;
-    for (uint32_t r = r0 + lane; r < r1; r += 64) {
+    for (uint32_t j = lane; j < r1 - r0; j += 64) {
+        const uint32_t r = chunk_ray(ch, j, cl, tile_w);
         const float ox = rays_o[3 * (size_t)r], oy = rays_o[3 * (size_t)r + 1],
                     oz = rays_o[3 * (size_t)r + 2];
         const float dx = rays_d[3 * (size_t)r], dy = rays_d[3 * (size_t)r + 1],
@@ -529,13 +588,14 @@ __global__ __launch_bounds__(256) void k_chunk_cost_occ(
     const float *__restrict__ rays_o, const float *__restrict__ rays_d,
     const float *__restrict__ nears, const float *__restrict__ fars,
     const uint8_t *__restrict__ grid, rm::MarchConsts k, uint32_t N, uint32_t cl,
-    uint32_t nchunks, float *__restrict__ cost) {
+    uint32_t nchunks, float *__restrict__ cost, uint32_t tile_w) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (ch >= nchunks) return;  // uniform per wave
     const uint32_t r0 = ch << cl, r1 = min(N, (ch + 1) << cl);
     uint32_t occ = 0;
-    for (uint32_t r = r0 + lane; r < r1; r += 64) {
+    for (uint32_t j = lane; j < r1 - r0; j += 64) {
+        const uint32_t r = chunk_ray(ch, j, cl, tile_w);
         const float n0 = nears[r], f0 = fars[r];
         if (!(f0 > n0)) continue;  // a ray missing the box
         const float ox = rays_o[3 * (size_t)r], oy = rays_o[3 * (size_t)r + 1],
@@ -652,9 +712,14 @@ extern "C" int dfhip_render_ray_order_occ(const float *rays_o, const float *rays
                                           const float *nears, const float *fars,
                                           const uint8_t *grid, float bound, uint32_t C,
                                           uint32_t H, uint32_t max_steps, uint32_t N,
-                                          uint32_t chunk_log2, float *cost, int32_t *order,
-                                          dfhip_stream_t stream) {
+                                          uint32_t chunk_log2, uint32_t tile_w, float *cost,
+                                          int32_t *order, dfhip_stream_t stream) {
     const char *name = "render_ray_order_occ";
+    if (tile_w && (chunk_log2 != 6 || tile_w % 8 || N % (8 * tile_w))) {
+        set_error("%s: tile chunks need chunk_log2 6, tile_w a multiple of 8 and N of 8 tile_w "
+                  "(got chunk_log2 %u, tile_w %u, N %u)", name, chunk_log2, tile_w, N);
+        return DFHIP_EINVAL;
+    }
     if (chunk_log2 > 16 || C < 1 || C > 16 || H < 2 || H > 1024 || max_steps == 0 ||
         !(bound > 0.0f)) {
         set_error("%s: invalid chunk_log2=%u C=%u H=%u max_steps=%u bound=%g", name,
@@ -675,15 +740,21 @@ extern "C" int dfhip_render_ray_order_occ(const float *rays_o, const float *rays
     hipStream_t s = as_stream(stream);
     const rm::MarchConsts k = rm::make_consts(bound, 0.0f, max_steps, C, H);
     rd::k_chunk_cost_occ<<<ceil_div(nchunks, 4u), 256, 0, s>>>(rays_o, rays_d, nears, fars, grid,
-                                                               k, N, chunk_log2, nchunks, cost);
+                                                               k, N, chunk_log2, nchunks, cost,
+                                                               tile_w);
     rd::k_chunk_order<<<1, rd::kOrderThreads, 0, s>>>(cost, nchunks, order);
     return check_launch(name);
 }
 
 extern "C" int dfhip_render_ray_order(const float *rays_o, const float *rays_d, uint32_t N,
-                                      uint32_t chunk_log2, float *cost, int32_t *order,
-                                      dfhip_stream_t stream) {
+                                      uint32_t chunk_log2, uint32_t tile_w, float *cost,
+                                      int32_t *order, dfhip_stream_t stream) {
     const char *name = "render_ray_order";
+    if (tile_w && (chunk_log2 != 6 || tile_w % 8 || N % (8 * tile_w))) {
+        set_error("%s: tile chunks need chunk_log2 6, tile_w a multiple of 8 and N of 8 tile_w "
+                  "(got chunk_log2 %u, tile_w %u, N %u)", name, chunk_log2, tile_w, N);
+        return DFHIP_EINVAL;
+    }
     if (chunk_log2 > 16) {
         set_error("%s: chunk_log2 must be <= 16 (got %u)", name, chunk_log2);
         return DFHIP_EINVAL;
@@ -701,7 +772,7 @@ extern "C" int dfhip_render_ray_order(const float *rays_o, const float *rays_d, 
     }
     hipStream_t s = as_stream(stream);
     rd::k_chunk_cost<<<ceil_div(nchunks, 4u), 256, 0, s>>>(rays_o, rays_d, N, chunk_log2,
-                                                           nchunks, cost);
+                                                           nchunks, cost, tile_w);
     rd::k_chunk_order<<<1, rd::kOrderThreads, 0, s>>>(cost, nchunks, order);
     return check_launch(name);
 }

@@ -90,6 +90,10 @@ class NeRFRenderer(nn.Module):
         # dfhip_render_ray_order_occ), or pixel order (0)
         self.infer_order = 1
         self.infer_chunk_log2 = 6
+        # the image width of the rays (row-major H x W, one or more images),
+        # set by the caller: the queue's chunks are then 8 x 8 pixel tiles
+        # (when 64-ray chunks apply and H is a multiple of 8), else 0: strips
+        self.infer_tile_w = 0
         # generator of the density-grid jitter (None: torch's default)
         self.grid_generator = None
         # (nears, fars, xyzs, dirs, deltas, rays) of a march already run for
@@ -406,6 +410,8 @@ class NeRFRenderer(nn.Module):
         cl = int(self.infer_chunk_log2)
         while (N + (1 << cl) - 1) >> cl > 16384:  # the order kernel's chunk limit
             cl += 1
+        tw = int(self.infer_tile_w)
+        tile_w = tw if cl == 6 and tw > 0 and tw % 8 == 0 and N % (8 * tw) == 0 else 0
         occ = ((nears.float().contiguous(), fars.float().contiguous(), self.density_bitfield,
                 self.bound, self.cascade, self.grid_size, max_steps)
                if self.infer_order == 2 else None)
@@ -414,7 +420,8 @@ class NeRFRenderer(nn.Module):
             # rays in, one cost and one order entry per chunk out
             with _dfhip.timed("render_ray_order", N * 24 + 8 * ((N >> cl) + 1)):
                 order = _fieldmlp.render_ray_order(rays_o.float().contiguous(),
-                                                   rays_d.float().contiguous(), cl, occ=occ)
+                                                   rays_d.float().contiguous(), cl, occ=occ,
+                                                   tile_w=tile_w)
         with _dfhip.timed("render_rays_infer", nbytes):
             _fieldmlp.render_rays_infer(
                 rays_o.float().contiguous(), rays_d.float().contiguous(),
@@ -422,7 +429,8 @@ class NeRFRenderer(nn.Module):
                 dt_gamma, max_steps, self.cascade, self.grid_size, self.density_bitfield,
                 T_thresh, table, encoder.offsets, float(np.log2(encoder.per_level_scale)),
                 int(encoder.base_resolution), encoder.gridtype_id, bool(encoder.align_corners),
-                weights, weights_sum, depth, image, work, quads, order=order, chunk_log2=cl)
+                weights, weights_sum, depth, image, work, quads, order=order, chunk_log2=cl,
+                tile_w=tile_w)
         self.last_infer_work = work  # work[1] (+ 2^32 work[2]) = samples evaluated
         return weights_sum, depth, image
 

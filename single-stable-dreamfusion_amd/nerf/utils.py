@@ -644,6 +644,8 @@ class Trainer(object):
         rays_o, rays_d = data["rays_o"], data["rays_d"]
         B, N = rays_o.shape[:2]
         H, W = data["H"], data["W"]
+        if H * W == N:  # row-major images: the fused renderer's queue takes 8 x 8 tiles
+            self.model.infer_tile_w = W
         out = self.model.render(rays_o, rays_d, staged=True, perturb=perturb, light_d=None,
                                 ambient_ratio=1.0, shading="albedo", force_all_rays=True,
                                 bg_color=bg_color, **vars(self.opt))

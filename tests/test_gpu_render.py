@@ -267,6 +267,46 @@ def test_ray_order_and_ordered_queue(gpu, monkeypatch):
             np.testing.assert_array_equal(a, b)
 
 
+def test_ordered_queue_mirror_and_tiles(gpu):
+    """The queue's chunk layouts render bit-identically to pixel order with
+    the same sample count (every ray taken exactly once): mirrored halves
+    over several blocks of G chunk positions and a partial one (cl 3), one
+    partial block (cl 6), 8 x 8 tile chunks (the tile cost is the tile rays'
+    mean squared line distance x 64, restated in numpy), and a tile width
+    the renderer does not apply (strips)."""
+    import _fieldmlp
+    m = _model(gpu, 3, 1.0, "grid")
+    h, w = 40, 48
+    rays_o, rays_d = _rays(gpu, h, w, 3)
+    n = rays_o.shape[0]
+    o, d = rays_o.cpu().double().numpy(), rays_d.cpu().double().numpy()
+    t = -(o * d).sum(1) / (d * d).sum(1)
+    dist = ((o + t[:, None] * d) ** 2).sum(1).reshape(h // 8, 8, w // 8, 8)
+    cost = torch.empty(n // 64, device=gpu)
+    order = _fieldmlp.render_ray_order(rays_o, rays_d, 6, cost=cost, tile_w=w).cpu().numpy()
+    assert sorted(order.tolist()) == list(range(n // 64))
+    want = dist.transpose(0, 2, 1, 3).reshape(-1, 64).mean(1) * 64
+    np.testing.assert_allclose(cost.cpu().numpy(), want, rtol=1e-4, atol=1e-6 * want.max())
+    with pytest.raises(RuntimeError, match="tile chunks"):
+        _fieldmlp.render_ray_order(rays_o, rays_d, 6, tile_w=w + 8)  # N not 8 rows of it
+    with pytest.raises(RuntimeError, match="tile chunks"):
+        _fieldmlp.render_ray_order(rays_o, rays_d, 3, tile_w=w)  # tiles are 64-ray chunks
+    runs = []
+    variants = [(0, 6, 0), (1, 0, 0), (1, 3, 0), (1, 6, 0), (1, 6, w), (2, 6, w), (1, 3, w),
+                (1, 6, w + 8)]
+    for flag, cl, tile in variants:
+        m.infer_order, m.infer_chunk_log2, m.infer_tile_w = flag, cl, tile
+        (fw, fd, fi), _ = _both(m, rays_o, rays_d, 1)
+        runs.append(((fw, fd, fi), m.last_infer_work.cpu().numpy()[:3].copy()))
+    m.infer_tile_w = 0
+    (ref, ref_work) = runs[0]
+    assert (ref[0] > 0).sum() > 100
+    for (got, work), v in zip(runs[1:], variants[1:]):
+        for a, b in zip(ref, got):
+            np.testing.assert_array_equal(a, b, err_msg=str(v))
+        np.testing.assert_array_equal(work[1:3], ref_work[1:3], err_msg=str(v))
+
+
 def _f32(x):
     return np.float32(x)
 
