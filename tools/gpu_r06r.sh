@@ -1,5 +1,5 @@
-# Train march count: ray groups dispatched centre-out (a -DDFHIP_MARCH_CENTER=1 build, since removed,
-# -DDFHIP_MARCH_CENTER=1) vs in ray order; rocprofv3 of the C2 child, alternating
+# Train march count: ray groups dispatched centre-out (a -DDFHIP_MARCH_CENTER=1 build,
+# since removed) vs in ray order; rocprofv3 of the C2 child, alternating
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
