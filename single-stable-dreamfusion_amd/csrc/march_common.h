@@ -308,6 +308,71 @@ __device__ __forceinline__ int march_step(const MarchConsts &k, const Ray &r, Oc
     return 0;
 }
 
+// Up to K iterations of march_step in one call, for empty space: the skip
+// target of a cell does not depend on its occupancy bit, so the K candidate
+// points the loop would visit if every cell were empty (each the first t of
+// the dt sequence at or past the previous cell's far face) are computed
+// first and their K bitfield bytes loaded together; the first occupied
+// candidate is then taken as march_step takes it, and the candidates after it
+// are dropped.  Returns 1 with the sample, 0 after K empty cells (t at the
+// last one's skip target), 2 when t reached far before an occupied cell (t
+// at that skip target).  The same t sequence, samples and deltas as K calls
+// of march_step; one load latency per K cells instead of K.
+template <int K>
+__device__ __forceinline__ int march_step_ahead(const MarchConsts &k, const Ray &r,
+                                                const uint8_t *__restrict__ grid, float &t,
+                                                float &last_t, float far, float (&xyz)[3],
+                                                float &dt_out, float &dl_out) {
+    if (!(t < far)) return 2;
+    float tc[K];
+    uint32_t idx[K];
+    int n = 0;
+    float tn = t;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        if (i > 0 && !(tn < far)) break;
+        tc[i] = tn;
+        const float x = clampf(fmaf(tn, r.dx, r.ox), -k.bound, k.bound);
+        const float y = clampf(fmaf(tn, r.dy, r.oy), -k.bound, k.bound);
+        const float z = clampf(fmaf(tn, r.dz, r.oz), -k.bound, k.bound);
+        const float dt = clampf(tn * k.dt_gamma, k.dt_min, k.dt_max);
+        const Mip mp = mip_of(k, x, y, z, dt);
+        const int nx = cell_of(k, x, mp.rbound);
+        const int ny = cell_of(k, y, mp.rbound);
+        const int nz = cell_of(k, z, mp.rbound);
+        idx[i] = grid_index(k, mp.level, nx, ny, nz);
+        n = i + 1;
+        const float tx = face_dist(k, nx, r.dx, r.rdx, x, mp.bound);
+        const float ty = face_dist(k, ny, r.dy, r.rdy, y, mp.bound);
+        const float tz = face_dist(k, nz, r.dz, r.rdz, z, mp.bound);
+        const float tt = tn + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+        do {
+            tn += clampf(tn * k.dt_gamma, k.dt_min, k.dt_max);
+        } while (tn < tt);
+    }
+    uint32_t bits[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        bits[i] = i < n ? ((uint32_t)grid[idx[i] >> 3] >> (idx[i] & 7u)) & 1u : 0u;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        if (bits[i]) {
+            const float ts = tc[i];
+            xyz[0] = clampf(fmaf(ts, r.dx, r.ox), -k.bound, k.bound);
+            xyz[1] = clampf(fmaf(ts, r.dy, r.oy), -k.bound, k.bound);
+            xyz[2] = clampf(fmaf(ts, r.dz, r.oz), -k.bound, k.bound);
+            const float dt = clampf(ts * k.dt_gamma, k.dt_min, k.dt_max);
+            t = ts + dt;
+            dt_out = dt;
+            dl_out = t - last_t;
+            last_t = t;
+            return 1;
+        }
+    }
+    t = tn;
+    return n < K ? 2 : 0;
+}
+
 template <typename Occ>
 __device__ __forceinline__ bool march_next_f(const MarchConsts &k, const Ray &r, Occ occupied,
                                              float &t, float &last_t, float far,

@@ -31,8 +31,9 @@
 //
 // MI355X design:
 //  * one lane owns one ray; a wave runs 64 rays.  The march runs AHEAD of the
-//    field: every iteration each lane takes one march step (one grid cell,
-//    rm::march_step) and stages the sample it finds in a per-wave LDS batch
+//    field: every iteration each lane takes one march step (up to kAhead
+//    grid cells, their occupancy bytes loaded together,
+//    rm::march_step_ahead) and stages the sample it finds in a per-wave LDS batch
 //    (slot = ballot / mbcnt, no atomics), up to kK (8) pending samples per
 //    ray, until the batch holds kBatch (64) samples or no lane may march
 //    (kK 4 -> 8: 2.86 -> 2.73 ms per frame; batches of 48-128 the same).  Lanes
@@ -72,6 +73,14 @@ constexpr int kBatch = DFHIP_RENDER_BATCH;  // a batch closes at >= kBatch stage
 #define DFHIP_RENDER_TPP 2
 #endif
 constexpr int kTPP = DFHIP_RENDER_TPP;  // field tiles per pass
+// empty cells a lane checks per march iteration (rm::march_step_ahead): their
+// occupancy bytes load together.  K = 2: 1.830 -> 1.776 ms per frame (R0),
+// 2.005 -> 1.963 (R1); K = 3 / 4 lose to the discarded candidates' work in
+// occupied space (profiles/r06/c4_march_ahead_ab.txt)
+#ifndef DFHIP_RENDER_AHEAD
+#define DFHIP_RENDER_AHEAD 2
+#endif
+constexpr int kAhead = DFHIP_RENDER_AHEAD;
 // pending slots, 8 bits each: one u64 holds 8, a second one up to 16
 static_assert(kK >= 1 && kK <= 16, "kK: 1..16 pending samples");
 struct PendSlots {
@@ -147,7 +156,6 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
     fm::load_weights<true>(W, nullptr, w1, b1, w2, b2, w3, b3);
     fm::stage_levels(LK, offsets, lv, gridtype, align);
     __syncthreads();
-    auto occupied = [&](uint32_t idx) { return ((grid[idx >> 3] >> (idx & 7)) & 1) != 0; };
     Stage &S = stages[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63, c = lane & 15, h = lane >> 4;
     const float inv_extent = 1.0f / (2.0f * k.bound);
@@ -272,7 +280,8 @@ __global__ __launch_bounds__(256, 3) void k_render_infer(
             bool emit = false;
             float px[3], pdt = 0.0f, dl = 0.0f;
             if (can) {
-                const int st = rm::march_step(k, r, occupied, t, last_t, far, px, pdt, dl);
+                const int st =
+                    rm::march_step_ahead<kAhead>(k, r, grid, t, last_t, far, px, pdt, dl);
                 if (st == 2) {
                     at_far = true;
                 } else if (st == 1) {
