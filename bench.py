@@ -83,7 +83,8 @@ def env_options(model=None, trainer=None):
     package itself takes them as explicit options): DFHIP_NATIVE_STEP,
     DFHIP_NATIVE_ADAM, DFHIP_KEPT_CLEAN, DFHIP_COMBINED_HEAD, DFHIP_STENCIL_BIN
     (Trainer), DFHIP_FUSED_FIELD,
-    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2, DFHIP_INFER_TILES=0 (renderer),
+    DFHIP_INFER_QUADS, DFHIP_INFER_ORDER, DFHIP_INFER_CHUNK_LOG2, DFHIP_INFER_TILES=0,
+    DFHIP_INFER_OVERLAP_BG=0 (renderer),
     DFHIP_GRID_BWD=atomic (GridEncoder)."""
     env = os.environ
     if trainer is not None:
@@ -106,6 +107,8 @@ def env_options(model=None, trainer=None):
             model.infer_chunk_log2 = int(env["DFHIP_INFER_CHUNK_LOG2"])
         if env.get("DFHIP_INFER_TILES") == "0":  # 64-ray row strips as queue chunks
             model.infer_tile_w = 0
+        if env.get("DFHIP_INFER_OVERLAP_BG") == "0":  # background net after the render
+            model.infer_overlap_bg = False
 
         enc = getattr(model, "encoder", None)
         if env.get("DFHIP_GRID_BWD") == "atomic" and hasattr(enc, "backward_mode"):
@@ -306,7 +309,9 @@ def bench_inference(device, res=800, frames=10, warmup=3, loop_frames=2, seed=1,
            "rays_per_frame": n, "ms_per_frame": round(fused_s * 1e3, 3),
            "rays_per_sec": round(n / fused_s, 1), "samples_per_frame": samples,
            "launch": "queue order (k_chunk_cost + k_chunk_order: render_ray_order, "
-                     "order_avg_us) then ONE persistent kernel (k_render_infer, kernel_avg_us)"}
+                     "order_avg_us) then ONE persistent kernel (k_render_infer, kernel_avg_us) "
+                     "with the background net (k_head_fwd_net) on a side stream beside it, "
+                     "then the mix (k_head_fwd_plain)"}
     if korder:
         out["order_avg_us"] = korder["avg_us"]
     if kern:

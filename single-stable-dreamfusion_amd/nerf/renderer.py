@@ -94,6 +94,9 @@ class NeRFRenderer(nn.Module):
         # set by the caller: the queue's chunks are then 8 x 8 pixel tiles
         # (when 64-ray chunks apply and H is a multiple of 8), else 0: strips
         self.infer_tile_w = 0
+        # eval frames: the background net runs on a side stream beside the
+        # fused render (bit-identical; False: after it, in the head)
+        self.infer_overlap_bg = True
         # generator of the density-grid jitter (None: torch's default)
         self.grid_generator = None
         # (nears, fars, xyzs, dirs, deltas, rays) of a march already run for
@@ -265,6 +268,7 @@ class NeRFRenderer(nn.Module):
             light_d = safe_normalize(rays_o[0] + torch.randn(3, device=device, dtype=torch.float))
 
         results = {}
+        bg_net = None  # [N, 3] background colours computed ahead (eval, fused render)
         if self.training:
             if pre is None:
                 counter = self.step_counter[self.local_step % 16]
@@ -302,25 +306,70 @@ class NeRFRenderer(nn.Module):
         else:
             field = self.native_infer_field(shading, rays_o) if self.native_infer else None
             if field is not None:
+                bg = self._background_async(rays_d, nears, fars, prefix, bg_color)
                 weights_sum, depth, image = self._infer_fused(rays_o, rays_d, nears, fars, field,
                                                               perturb, dt_gamma, max_steps,
                                                               T_thresh)
+                if bg is not None:  # the background net ran beside the render
+                    torch.cuda.current_stream().wait_event(bg[1])
+                    bg[0].record_stream(torch.cuda.current_stream())
+                    bg_net = bg[0].t().contiguous()
             else:
                 weights_sum, depth, image = self._infer_loop(rays_o, rays_d, nears, fars, light_d,
                                                              ambient_ratio, shading, perturb,
                                                              dt_gamma, max_steps, T_thresh)
 
         results.update(self._compose(rays_d, nears, fars, weights_sum, depth, image, bg_color,
-                                     prefix))
+                                     prefix, bg_net))
         return results
 
-    def _compose(self, rays_d, nears, fars, weights_sum, depth, image, bg_color, prefix):
+    def _background_async(self, rays_d, nears, fars, prefix, bg_color):
+        """The background MLP of the eval frame (network_grid.py:158-167) on a
+        side stream, so it runs beside the fused render kernel instead of after
+        it: dfhip_ray_head_forward with ws = 0 and image = 0 writes exactly
+        bg = sigmoid(net(rays_d)) ([3, N]); _compose then mixes it in with the
+        plain head (image + (1 - ws) * bg, the same f32 expression as the net
+        head, so the frame is bit-identical).  Returns (bg, event) or None
+        when the native head would not take the background net."""
+        from . import head as _head
+        if self.bg_radius <= 0 or not self.native_head or not self.infer_overlap_bg:
+            return None
+        if not (len(prefix) == 2 and prefix[0] == 1) or torch.is_grad_enabled():
+            return None
+        layers = self.native_background_layers()
+        N = rays_d.shape[0]
+        dev = rays_d.device
+        if layers is None or not _head.head_eligible(nears, layers) or N == 0:
+            return None
+        z = self.__dict__.get("_bg_zeros")
+        if z is None or z.numel() < 5 * N or z.device != dev:
+            z = torch.zeros(5 * N, device=dev)  # ws, depth, image [N, 3]: zeros, kept
+            self.__dict__["_bg_zeros"] = z
+        main = torch.cuda.current_stream()
+        side = self.__dict__.get("_bg_stream")
+        if side is None or side.device != dev:
+            side = torch.cuda.Stream(device=dev)
+            self.__dict__["_bg_stream"] = side
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            out, _, _ = _head.ray_head(z[:N], z[N:2 * N], z[2 * N:5 * N].view(N, 3), rays_d,
+                                       nears, fars, None, layers)
+            done = torch.cuda.Event()
+            done.record(side)
+        for t in (rays_d, nears, fars, z):
+            t.record_stream(side)
+        return out, done
+
+    def _compose(self, rays_d, nears, fars, weights_sum, depth, image, bg_color, prefix,
+                 bg_net=None):
         """Background mix, depth normalisation, mask (renderer.py:536-551); on the
         GPU as the native ray head (nerf/head.py) when the shapes allow."""
         from . import head as _head
-        net = self.bg_radius > 0
+        net = self.bg_radius > 0 and bg_net is None
         layers = self.native_background_layers() if net else None
-        bgc = None if net else bg_color
+        bgc = bg_net if bg_net is not None else (None if net else bg_color)
         ok = (self.native_head and len(prefix) == 2 and prefix[0] == 1
               and (layers is not None if net else
                    (bgc is None or (torch.is_tensor(bgc) and bgc.shape == image.shape)))

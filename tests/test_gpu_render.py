@@ -122,6 +122,29 @@ def test_fused_infer_sample_count_and_render_api(gpu):
     assert work[1] > 0 and work[2] == 0
 
 
+def test_eval_background_beside_render(gpu):
+    """The eval frame's background net on a side stream beside the fused
+    render (renderer._background_async, then the plain head's mix) gives the
+    frame of the fused net head after the render, bit for bit."""
+    m = _model(gpu, 5, 1.0, "grid")
+    assert m.bg_radius > 0 and m.native_background_layers() is not None
+    rays_o, rays_d = _rays(gpu, 32, 40, 5)
+    outs = []
+    for overlap in (True, False):
+        m.infer_overlap_bg = overlap
+        m.__dict__.pop("_bg_stream", None)
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            out = m.render(rays_o[None], rays_d[None], staged=True, perturb=False,
+                           max_steps=512)
+        torch.cuda.synchronize()
+        assert ("_bg_stream" in m.__dict__) == overlap
+        outs.append({k: out[k].float().cpu().numpy() for k in ("image", "depth", "weights_sum")})
+    m.infer_overlap_bg = True
+    assert (outs[1]["weights_sum"] < 0.99).sum() > 100  # the background shows
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
 def _oracle_render(m, rays_o, rays_d, nears, fars, max_steps=512, T_thresh=1e-4):
     """The reference's inference loop (renderer.py:496-532) at n_step = 1 on
     the CPU oracle: oracle.march_rays -> oracle/field.py (f16 autocast

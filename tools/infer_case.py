@@ -20,6 +20,8 @@ def main():
                     help="per-wave phase cycles of k_render_infer (dfhip_render_rays_infer_prof)")
     ap.add_argument("--strips", action="store_true",
                     help="64-ray row strips as queue chunks (default: 8 x 8 tiles, renderer.infer_tile_w)")
+    ap.add_argument("--serial-bg", action="store_true",
+                    help="background net after the render (renderer.infer_overlap_bg = False)")
     ap.add_argument("--dump", default="", help="save the per-wave records (.npy; last row: prof[:16])")
     ap.add_argument("--sphere", action="store_true", help="analytic sphere occupancy (R1)")
     args = ap.parse_args()
@@ -41,6 +43,7 @@ def main():
     model.eval()
     model.native_infer = True
     model.infer_tile_w = 0 if args.strips else args.res
+    model.infer_overlap_bg = not args.serial_bg
     data = NeRFDataset(opt, device=dev, type="test", H=args.res, W=args.res, size=8).collate([1])
 
     def frame():
