@@ -557,7 +557,7 @@ extern "C" int dfhip_render_rays_infer_ordered(
 namespace dfhip {
 namespace rd {
 
-constexpr uint32_t kMaxOrderChunks = 16384;  // one workgroup's counting sort (64 x 256 slots)
+constexpr uint32_t kMaxOrderChunks = 16384;  // one workgroup's counting sort (256 blocks of 64)
 
 // Cost of each chunk of 2^cl consecutive rays: the summed squared distance
 // of the rays' lines from the scene centre (the origin of the reference's
@@ -632,23 +632,30 @@ __global__ __launch_bounds__(256) void k_chunk_cost_occ(
 
 // The chunks by ascending cost, quantised to kOrderBuckets levels between the
 // costs' min and max (NaN last), ties by chunk index: a stable counting sort
-// in one workgroup.  Thread t takes the chunks [t per, (t + 1) per) and counts
-// them per bucket in its own LDS column; an exclusive scan over (bucket,
-// thread) gives every thread its first slot per bucket; each thread then
-// places its chunks in index order.  (A full bitonic sort of 16 k keys in one
-// workgroup took 229 us per frame; a queue order needs only the coarse rank.)
+// in one workgroup of 16 waves.  The chunks are taken in blocks of 64, one per
+// lane: six ballots over the bucket's bits give every lane the lanes of its
+// block with the same bucket, hence its rank among them and the block's count
+// per bucket (no LDS atomics, no serial per-thread ranges); the counts are
+// scanned over blocks by 16 parts of 64 threads (one per bucket), the bucket
+// totals over buckets by one wave, and each lane writes its chunk at bucket
+// base + block offset + rank.  (The previous form: 256 threads with a serial
+// 256-step scan per bucket, 25 us per frame; a full bitonic sort of 16 k keys
+// in one workgroup took 229 us; a queue order needs only the coarse rank.)
 constexpr uint32_t kOrderBuckets = 64;
-constexpr uint32_t kOrderThreads = 256;
-constexpr uint32_t kOrderRow = kOrderThreads + 1;  // padded row: thread b's scan row, and
-                                                  // thread t's column, hit distinct banks
+constexpr uint32_t kOrderThreads = 1024;
+constexpr uint32_t kOrderWaves = kOrderThreads / 64;
+constexpr uint32_t kOrderBlocks = kMaxOrderChunks / 64;  // 64-chunk blocks
+static_assert(kOrderBuckets == 64, "the ballot rank takes six bucket bits");
 __global__ __launch_bounds__(kOrderThreads) void k_chunk_order(const float *__restrict__ cost,
                                                                uint32_t nchunks,
                                                                int32_t *__restrict__ order) {
-    __shared__ uint16_t slot[kOrderBuckets * kOrderRow];  // [bucket][thread] (<= 16 k chunks)
-    __shared__ uint8_t bk[kMaxOrderChunks];                // each chunk's bucket
-    __shared__ float rmin[kOrderThreads], rmax[kOrderThreads];
-    __shared__ uint32_t rsum[kOrderBuckets];
-    const uint32_t t = threadIdx.x;
+    __shared__ uint8_t bk[kMaxOrderChunks];                     // each chunk's bucket
+    __shared__ uint16_t cnt[kOrderBlocks * kOrderBuckets];      // [block][bucket]: count, then offset
+    __shared__ uint32_t part[kOrderWaves * kOrderBuckets];      // [part][bucket] sums, then offsets
+    __shared__ uint32_t base[kOrderBuckets];
+    __shared__ float rmin[kOrderWaves], rmax[kOrderWaves];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t nblk = ceil_div(nchunks, 64u);
     // the costs once, coalesced: range, then every chunk's bucket into LDS
     float lo = INFINITY, hi = -INFINITY;
     for (uint32_t c = t; c < nchunks; c += kOrderThreads) {
@@ -658,18 +665,23 @@ __global__ __launch_bounds__(kOrderThreads) void k_chunk_order(const float *__re
             hi = fmaxf(hi, v);
         }
     }
-    rmin[t] = lo;
-    rmax[t] = hi;
-    for (uint32_t b = 0; b < kOrderBuckets; ++b) slot[b * kOrderRow + t] = 0;
-    __syncthreads();
-    for (uint32_t o = kOrderThreads / 2; o > 0; o >>= 1) {
-        if (t < o) {
-            rmin[t] = fminf(rmin[t], rmin[t + o]);
-            rmax[t] = fmaxf(rmax[t], rmax[t + o]);
-        }
-        __syncthreads();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o));
+        hi = fmaxf(hi, __shfl_xor(hi, o));
     }
-    const float cmin = rmin[0], span = rmax[0] - rmin[0];
+    if (lane == 0) {
+        rmin[wave] = lo;
+        rmax[wave] = hi;
+    }
+    __syncthreads();
+    lo = rmin[0];
+    hi = rmax[0];
+    for (uint32_t w = 1; w < kOrderWaves; ++w) {
+        lo = fminf(lo, rmin[w]);
+        hi = fmaxf(hi, rmax[w]);
+    }
+    const float cmin = lo, span = hi - lo;
     const float scale = span > 0.0f ? (float)kOrderBuckets / span : 0.0f;
     for (uint32_t c = t; c < nchunks; c += kOrderThreads) {
         const float v = cost[c];
@@ -681,36 +693,69 @@ __global__ __launch_bounds__(kOrderThreads) void k_chunk_order(const float *__re
         bk[c] = (uint8_t)b;
     }
     __syncthreads();
-    // thread t's chunks: the contiguous range [c0, c1), counted per bucket in
-    // its own column
-    const uint32_t per = ceil_div(nchunks, kOrderThreads);
-    const uint32_t c0 = min(nchunks, t * per), c1 = min(nchunks, c0 + per);
-    for (uint32_t c = c0; c < c1; ++c) ++slot[bk[c] * kOrderRow + t];
-    __syncthreads();
-    // exclusive scan of the bucket-major [bucket][thread] counts: thread b
-    // scans bucket b's row, then the row sums are scanned and added
-    if (t < kOrderBuckets) {
-        uint32_t sum = 0;
-        for (uint32_t u = 0; u < kOrderThreads; ++u) {
-            const uint32_t v = slot[t * kOrderRow + u];
-            slot[t * kOrderRow + u] = (uint16_t)sum;
-            sum += v;
+    // per 64-chunk block: each lane's rank among the block's chunks of its
+    // bucket (lanes below it with the same six bits) and the block's counts
+    auto same_bucket = [&](uint32_t b, bool valid) {
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const uint64_t bal = __ballot(valid && ((b >> i) & 1u));
+            m &= ((b >> i) & 1u) ? bal : ~bal;
         }
-        rsum[t] = sum;
+        return m;
+    };
+    for (uint32_t k = wave; k < nblk; k += kOrderWaves) {
+        cnt[k * kOrderBuckets + lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t c = k * 64 + lane;
+        const bool valid = c < nchunks;
+        const uint32_t b = valid ? bk[c] : 0u;
+        const uint64_t m = same_bucket(b, valid);
+        if (valid && (m & ((1ull << lane) - 1ull)) == 0)  // the bucket's first lane
+            cnt[k * kOrderBuckets + b] = (uint16_t)__popcll(m);
     }
     __syncthreads();
-    if (t == 0) {
+    // exclusive scan over blocks per bucket: part w (one wave) sums its blocks
+    // [w per, (w + 1) per) for bucket = lane, then the parts are scanned
+    const uint32_t per = ceil_div(nblk, kOrderWaves);
+    const uint32_t k0 = min(nblk, wave * per), k1 = min(nblk, k0 + per);
+    uint32_t sum = 0;
+    for (uint32_t k = k0; k < k1; ++k) sum += cnt[k * kOrderBuckets + lane];
+    part[wave * kOrderBuckets + lane] = sum;
+    __syncthreads();
+    if (wave == 0) {
         uint32_t acc = 0;
-        for (uint32_t b = 0; b < kOrderBuckets; ++b) {
-            const uint32_t v = rsum[b];
-            rsum[b] = acc;
+        for (uint32_t w = 0; w < kOrderWaves; ++w) {
+            const uint32_t v = part[w * kOrderBuckets + lane];
+            part[w * kOrderBuckets + lane] = acc;
             acc += v;
         }
+        // the bucket totals (lane = bucket), exclusive over buckets
+        uint32_t x = acc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        base[lane] = x - acc;
     }
     __syncthreads();
-    for (uint32_t c = c0; c < c1; ++c) {
-        const uint32_t b = bk[c];
-        order[rsum[b] + slot[b * kOrderRow + t]++] = (int32_t)c;
+    uint32_t off = part[wave * kOrderBuckets + lane];
+    for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t v = cnt[k * kOrderBuckets + lane];
+        cnt[k * kOrderBuckets + lane] = (uint16_t)off;
+        off += v;
+    }
+    __syncthreads();
+    for (uint32_t k = wave; k < nblk; k += kOrderWaves) {
+        const uint32_t c = k * 64 + lane;
+        const bool valid = c < nchunks;
+        const uint32_t b = valid ? bk[c] : 0u;
+        const uint64_t m = same_bucket(b, valid);
+        if (valid) {
+            const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            order[base[b] + cnt[k * kOrderBuckets + b] + rank] = (int32_t)c;
+        }
     }
 }
 
