@@ -22,6 +22,8 @@ def main():
                     help="64-ray row strips as queue chunks (default: 8 x 8 tiles, renderer.infer_tile_w)")
     ap.add_argument("--serial-bg", action="store_true",
                     help="background net after the render (renderer.infer_overlap_bg = False)")
+    ap.add_argument("--order", type=int, default=1,
+                    help="queue order: 0 pixel, 1 line distance, 2 occupied cells (renderer.infer_order)")
     ap.add_argument("--dump", default="", help="save the per-wave records (.npy; last row: prof[:16])")
     ap.add_argument("--sphere", action="store_true", help="analytic sphere occupancy (R1)")
     args = ap.parse_args()
@@ -44,6 +46,7 @@ def main():
     model.native_infer = True
     model.infer_tile_w = 0 if args.strips else args.res
     model.infer_overlap_bg = not args.serial_bg
+    model.infer_order = args.order
     data = NeRFDataset(opt, device=dev, type="test", H=args.res, W=args.res, size=8).collate([1])
 
     def frame():
