@@ -240,3 +240,30 @@ def test_module_breakdown_counts_whole_steps(tmp_path):
     assert g["march_rays_train"] == 50.0 and g["grid_encode_backward"] == 40.0
     assert g["runtime_copies_and_fills"] == 5.0 and "torch_elementwise_and_reductions" not in g
     assert bench._module_breakdown([f], 5) is None
+
+
+def test_eval_background_side_stream_gating():
+    """NeRFRenderer._background_async (the eval frame's background net beside
+    the fused render) applies only to no-grad eval frames of one image on the
+    GPU with the native head: here (CPU tensors, or grad enabled, or the
+    option off, or no background net) it declines before any GPU call."""
+    import main
+    from nerf.network_grid import NeRFNetwork
+    opt = main.parse_opt(["--text", "x", "-O"])
+    torch.manual_seed(0)
+    net = NeRFNetwork(opt).eval()
+    assert net.bg_radius > 0 and net.infer_overlap_bg
+    rays_d = torch.nn.functional.normalize(torch.randn(64, 3), dim=-1)
+    nears, fars = torch.full((64,), 0.1), torch.full((64,), 2.0)
+    with torch.no_grad():
+        assert net._background_async(rays_d, nears, fars, (1, 64), None) is None  # CPU
+        assert net._background_async(rays_d, nears, fars, (2, 32), None) is None  # two images
+        net.infer_overlap_bg = False
+        assert net._background_async(rays_d, nears, fars, (1, 64), None) is None
+        net.infer_overlap_bg = True
+        r = net.bg_radius
+        net.bg_radius = 0.0
+        assert net._background_async(rays_d, nears, fars, (1, 64), None) is None
+        net.bg_radius = r
+    assert net._background_async(rays_d, nears, fars, (1, 64), None) is None  # grad enabled
+    assert "_bg_stream" not in net.__dict__ and "_bg_zeros" not in net.__dict__
