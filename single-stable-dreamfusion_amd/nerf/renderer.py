@@ -306,11 +306,12 @@ class NeRFRenderer(nn.Module):
         else:
             field = self.native_infer_field(shading, rays_o) if self.native_infer else None
             if field is not None:
-                bg = self._background_async(rays_d, nears, fars, prefix, bg_color)
-                weights_sum, depth, image = self._infer_fused(rays_o, rays_d, nears, fars, field,
-                                                              perturb, dt_gamma, max_steps,
-                                                              T_thresh)
-                if bg is not None:  # the background net ran beside the render
+                launch_bg = self._background_async(rays_d, nears, fars, prefix, bg_color)
+                bg = launch_bg() if launch_bg else None
+                weights_sum, depth, image = self._infer_fused(
+                    rays_o, rays_d, nears, fars, field, perturb, dt_gamma, max_steps, T_thresh,
+                    render_stream=self.__dict__["_bg_streams"][0] if launch_bg else None)
+                if bg:  # the background net ran beside the render
                     torch.cuda.current_stream().wait_event(bg[1])
                     bg[0].record_stream(torch.cuda.current_stream())
                     bg_net = bg[0].t().contiguous()
@@ -329,8 +330,10 @@ class NeRFRenderer(nn.Module):
         it: dfhip_ray_head_forward with ws = 0 and image = 0 writes exactly
         bg = sigmoid(net(rays_d)) ([3, N]); _compose then mixes it in with the
         plain head (image + (1 - ws) * bg, the same f32 expression as the net
-        head, so the frame is bit-identical).  Returns (bg, event) or None
-        when the native head would not take the background net."""
+        head, so the frame is bit-identical).  Returns a launcher (called
+        before the queue order, the net then runs beside the order and the
+        render) that returns (bg, event); or None when the native head would
+        not take the background net."""
         from . import head as _head
         if self.bg_radius <= 0 or not self.native_head or not self.infer_overlap_bg:
             return None
@@ -345,22 +348,30 @@ class NeRFRenderer(nn.Module):
         if z is None or z.numel() < 5 * N or z.device != dev:
             z = torch.zeros(5 * N, device=dev)  # ws, depth, image [N, 3]: zeros, kept
             self.__dict__["_bg_zeros"] = z
-        main = torch.cuda.current_stream()
-        side = self.__dict__.get("_bg_stream")
-        if side is None or side.device != dev:
-            side = torch.cuda.Stream(device=dev)
-            self.__dict__["_bg_stream"] = side
-        ready = torch.cuda.Event()
-        ready.record(main)
-        with torch.cuda.stream(side):
-            side.wait_event(ready)
-            out, _, _ = _head.ray_head(z[:N], z[N:2 * N], z[2 * N:5 * N].view(N, 3), rays_d,
-                                       nears, fars, None, layers)
-            done = torch.cuda.Event()
-            done.record(side)
-        for t in (rays_d, nears, fars, z):
-            t.record_stream(side)
-        return out, done
+        pair = self.__dict__.get("_bg_streams")
+        if pair is None or pair[0].device != dev:
+            # two streams taken from torch's pool one after the other, the
+            # render's and the net's: consecutive pool streams sit on
+            # different hardware queues, so the net runs beside the render
+            # (a stream that shares the render's queue runs after it)
+            pair = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+            self.__dict__["_bg_streams"] = pair
+            self.__dict__["_bg_stream"] = pair[1]
+        side = pair[1]
+
+        def launch():
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                out, _, _ = _head.ray_head(z[:N], z[N:2 * N], z[2 * N:5 * N].view(N, 3), rays_d,
+                                           nears, fars, None, layers)
+                done = torch.cuda.Event()
+                done.record(side)
+            for t in (rays_d, nears, fars, z):
+                t.record_stream(side)
+            return out, done
+        return launch
 
     def _compose(self, rays_d, nears, fars, weights_sum, depth, image, bg_color, prefix,
                  bg_net=None):
@@ -405,7 +416,7 @@ class NeRFRenderer(nn.Module):
         self.__dict__.pop("_infer_operands", None)
 
     def _infer_fused(self, rays_o, rays_d, nears, fars, field, perturb, dt_gamma, max_steps,
-                     T_thresh):
+                     T_thresh, before_render=None, render_stream=None):
         """The inference loop below as ONE persistent launch (csrc/render.hip):
         march, grid field and compositing per ray with a device work queue, no
         host sync and no per-sample intermediates in HBM."""
@@ -471,15 +482,28 @@ class NeRFRenderer(nn.Module):
                 order = _fieldmlp.render_ray_order(rays_o.float().contiguous(),
                                                    rays_d.float().contiguous(), cl, occ=occ,
                                                    tile_w=tile_w)
-        with _dfhip.timed("render_rays_infer", nbytes):
+        if before_render is not None:  # e.g. the background net on its side stream
+            before_render()
+        operands = (rays_o.float().contiguous(), rays_d.float().contiguous(),
+                    nears.float().contiguous(), fars.float().contiguous())
+        main = torch.cuda.current_stream()
+        rs = render_stream if render_stream is not None else main
+        if rs is not main:  # the render on its own stream (beside a side-stream job)
+            rs.wait_stream(main)
+        with torch.cuda.stream(rs), _dfhip.timed("render_rays_infer", nbytes):
             _fieldmlp.render_rays_infer(
-                rays_o.float().contiguous(), rays_d.float().contiguous(),
-                nears.float().contiguous(), fars.float().contiguous(), noises, self.bound,
+                *operands, noises, self.bound,
                 dt_gamma, max_steps, self.cascade, self.grid_size, self.density_bitfield,
                 T_thresh, table, encoder.offsets, float(np.log2(encoder.per_level_scale)),
                 int(encoder.base_resolution), encoder.gridtype_id, bool(encoder.align_corners),
                 weights, weights_sum, depth, image, work, quads, order=order, chunk_log2=cl,
                 tile_w=tile_w)
+        if rs is not main:
+            main.wait_stream(rs)
+            for t in (*operands, weights_sum, depth, image, work, order, noises, table, quads,
+                      *weights):
+                if torch.is_tensor(t):
+                    t.record_stream(rs)
         self.last_infer_work = work  # work[1] (+ 2^32 work[2]) = samples evaluated
         return weights_sum, depth, image
 
