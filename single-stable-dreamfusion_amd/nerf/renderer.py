@@ -306,11 +306,10 @@ class NeRFRenderer(nn.Module):
         else:
             field = self.native_infer_field(shading, rays_o) if self.native_infer else None
             if field is not None:
-                launch_bg = self._background_async(rays_d, nears, fars, prefix, bg_color)
-                bg = launch_bg() if launch_bg else None
+                bg = self._background_async(rays_d, nears, fars, prefix, bg_color)
                 weights_sum, depth, image = self._infer_fused(
                     rays_o, rays_d, nears, fars, field, perturb, dt_gamma, max_steps, T_thresh,
-                    render_stream=self.__dict__["_bg_streams"][0] if launch_bg else None)
+                    render_stream=bg[2] if bg else None)
                 if bg:  # the background net ran beside the render
                     torch.cuda.current_stream().wait_event(bg[1])
                     bg[0].record_stream(torch.cuda.current_stream())
@@ -330,10 +329,10 @@ class NeRFRenderer(nn.Module):
         it: dfhip_ray_head_forward with ws = 0 and image = 0 writes exactly
         bg = sigmoid(net(rays_d)) ([3, N]); _compose then mixes it in with the
         plain head (image + (1 - ws) * bg, the same f32 expression as the net
-        head, so the frame is bit-identical).  Returns a launcher (called
-        before the queue order, the net then runs beside the order and the
-        render) that returns (bg, event); or None when the native head would
-        not take the background net."""
+        head, so the frame is bit-identical).  Launched before the queue
+        order, the net runs beside the order and the render.  Returns (bg,
+        event, the render's stream), or None when the native head would not
+        take the background net."""
         from . import head as _head
         if self.bg_radius <= 0 or not self.native_head or not self.infer_overlap_bg:
             return None
@@ -358,20 +357,17 @@ class NeRFRenderer(nn.Module):
             self.__dict__["_bg_streams"] = pair
             self.__dict__["_bg_stream"] = pair[1]
         side = pair[1]
-
-        def launch():
-            ready = torch.cuda.Event()
-            ready.record(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                side.wait_event(ready)
-                out, _, _ = _head.ray_head(z[:N], z[N:2 * N], z[2 * N:5 * N].view(N, 3), rays_d,
-                                           nears, fars, None, layers)
-                done = torch.cuda.Event()
-                done.record(side)
-            for t in (rays_d, nears, fars, z):
-                t.record_stream(side)
-            return out, done
-        return launch
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            out, _, _ = _head.ray_head(z[:N], z[N:2 * N], z[2 * N:5 * N].view(N, 3), rays_d,
+                                       nears, fars, None, layers)
+            done = torch.cuda.Event()
+            done.record(side)
+        for t in (rays_d, nears, fars, z):
+            t.record_stream(side)
+        return out, done, pair[0]
 
     def _compose(self, rays_d, nears, fars, weights_sum, depth, image, bg_color, prefix,
                  bg_net=None):
@@ -416,7 +412,7 @@ class NeRFRenderer(nn.Module):
         self.__dict__.pop("_infer_operands", None)
 
     def _infer_fused(self, rays_o, rays_d, nears, fars, field, perturb, dt_gamma, max_steps,
-                     T_thresh, before_render=None, render_stream=None):
+                     T_thresh, render_stream=None):
         """The inference loop below as ONE persistent launch (csrc/render.hip):
         march, grid field and compositing per ray with a device work queue, no
         host sync and no per-sample intermediates in HBM."""
@@ -482,8 +478,6 @@ class NeRFRenderer(nn.Module):
                 order = _fieldmlp.render_ray_order(rays_o.float().contiguous(),
                                                    rays_d.float().contiguous(), cl, occ=occ,
                                                    tile_w=tile_w)
-        if before_render is not None:  # e.g. the background net on its side stream
-            before_render()
         operands = (rays_o.float().contiguous(), rays_d.float().contiguous(),
                     nears.float().contiguous(), fars.float().contiguous())
         main = torch.cuda.current_stream()
